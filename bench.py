@@ -1,0 +1,176 @@
+"""Headline benchmark: activations/sec of a Pythia-70m residual-stream SAE ensemble.
+
+BASELINE.json config 2/3: an 8-way L1 sweep (l1 = logspace(-4, -2, 8)) of untied
+SAEs on d_model = 512 activations with dict_ratio 4 (n = 2048), bf16 MFMA compute
+with fp32 master weights and fp32 Adam, trained on synthetic Pythia-70m-shaped
+activations (sparse mixture of 4096 unit-norm features, held in an HBM ring
+buffer; no network, so no real harvest).  Every timed step does the full work:
+device-side random batch gather, encoder/decoder forward, backward, Adam on all
+8 models.  With N > 1 GPUs it is data parallel (per-GPU batch fixed, i.e. weak
+scaling) with RCCL gradient all-reduce overlapped with the encoder wgrad/Adam.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      torchrun --nproc-per-node N bench.py --gpus N ...
+Prints one JSON line (rank 0).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+# the reference's untied 8-model d=512 n=2048 step (its own math,
+# vmap(grad)+Adam) -- the only measured throughput for this exact config (no GPU number
+# is published, BASELINE.json "published": {}).
+BASELINE_ACT_PER_S = 1.86e3
+METRIC = "activations/sec (ensemble train) + FVU@L0, Pythia-70m resid SAE at 1/2/4/8 GPU"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=2048, help="rows per GPU per step")
+    ap.add_argument("--d", type=int, default=512)
+    ap.add_argument("--ratio", type=int, default=4)
+    ap.add_argument("--models", type=int, default=8)
+    ap.add_argument("--kind", choices=["untied", "tied"], default="untied")
+    ap.add_argument("--engine", choices=["fused", "eager"], default="fused")
+    ap.add_argument("--ring-rows", type=int, default=1 << 21)
+    ap.add_argument("--eval-rows", type=int, default=16384)
+    ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--no-eval", action="store_true")
+    return ap.parse_args(argv)
+
+
+def build_ring(args, device):
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.data.synthetic import RandomDatasetGenerator
+
+    gen = RandomDatasetGenerator(activation_dim=args.d, n_ground_truth_components=8 * args.d,
+                                 batch_size=65536, feature_num_nonzero=32, feature_prob_decay=0.999,
+                                 correlated=False, device=device, seed=1234)
+    ring = DeviceRing(args.ring_rows, args.d, device=device, seed=4321)
+    ring.fill(lambda: gen.send(None))
+    held_out = gen.send(None)[: args.eval_rows]
+    return ring, held_out
+
+
+def fvu_l0(dicts, x):
+    from sparse_coding__amd.eval.metrics import fraction_variance_unexplained, mean_l0
+
+    return [(float(mean_l0(ld, x)), float(fraction_variance_unexplained(ld, x))) for ld in dicts]
+
+
+def main(argv=None):
+    args = parse(argv)
+    from sparse_coding__amd.parallel.dist import all_reduce_max, barrier, init_distributed, shutdown
+
+    info = init_distributed()
+    if not torch.cuda.is_available():
+        print("bench.py needs an MI355X (torch.cuda.is_available() is False)", file=sys.stderr)
+        return 2
+    device = info.device
+    torch.manual_seed(0)
+    from sparse_coding__amd.models.signatures import FunctionalSAE, FunctionalTiedSAE
+
+    sig = FunctionalSAE if args.kind == "untied" else FunctionalTiedSAE
+    n = args.d * args.ratio
+    l1s = np.logspace(-4, -2, args.models)
+    models = [sig.init(args.d, n, float(l1), device=device) for l1 in l1s]
+    ring, held_out = build_ring(args, device)
+    B = args.batch
+
+    if args.engine == "fused":
+        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+        from sparse_coding__amd.parallel.data_parallel import DataParallelFused
+
+        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
+        trainer = DataParallelFused(eng, info, torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
+        xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
+
+        def step():
+            trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf))
+
+        def dicts():
+            return eng.to_learned_dicts(device)
+    else:
+        from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
+        from sparse_coding__amd.engine.optim import adam
+        from sparse_coding__amd.parallel.data_parallel import DataParallelEnsemble
+
+        ens = FunctionalEnsemble(models, sig, adam, {"lr": 1e-3}, device=device)
+        trainer = DataParallelEnsemble(ens, info)
+
+        def step():
+            trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size).float())
+
+        def dicts():
+            return ens.to_learned_dicts(device)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(info)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(info)
+    elapsed = time.perf_counter() - t0
+    elapsed = all_reduce_max(elapsed, info)
+    ms = 1e3 * elapsed / args.steps
+    total_rows = B * info.world_size * args.steps
+    value = total_rows / elapsed
+
+    quality = None
+    if not args.no_eval and info.is_main:
+        quality = fvu_l0(dicts(), held_out.float())
+
+    if info.is_main:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "activations/s",
+            "n_gpus": info.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_ACT_PER_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic (sparse mixture of 4096 unit-norm features, Pythia-70m d_model=512 shape; "
+                    "random-init SAE weights)",
+            "config": {
+                "model": f"pythia-70m-resid-sae-ensemble ({args.kind}, d=512, ratio={args.ratio}, "
+                         f"{args.models} models, l1=logspace(-4,-2,{args.models}))",
+                "global_batch": B * info.world_size,
+                "seq_len": None,
+                "per_gpu_batch": B,
+                "parallelism": f"dp{info.world_size}",
+                "engine": args.engine,
+                "grad_allreduce_dtype": args.grad_dtype,
+            },
+            "model_activations_per_s": round(value * args.models, 1),
+            "baseline_note": "vs_baseline divides by BASELINE.md row 12 (reference math, same shapes, "
+                             "1.86k act/s); no published GPU throughput exists",
+        }
+        if quality is not None:
+            rec["fvu_at_l0"] = [{"l1": float(l), "l0": round(a, 2), "fvu": round(b, 4)}
+                                for l, (a, b) in zip(l1s, quality)]
+        print(json.dumps(rec), flush=True)
+    shutdown(info)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,113 @@
+"""HBM-resident activation ring buffer.
+
+The reference keeps each 2 GiB activation chunk in host memory and, per
+batch, gathers random rows on the CPU and copies them to the GPU
+(``big_sweep.py:170``, ``cluster_runs.py:101-102``).  On MI355X the activations
+live in HBM (288 GB per GPU holds ~280 M rows of d=512 bf16): producers (the
+synthetic generator, the harvester, the chunk loader) append rows, and the
+trainer draws batches with an on-device random gather -- no host round trip
+per step.  Sampling is without replacement within an epoch (a device-side
+permutation), matching ``BatchSampler(RandomSampler(...))`` in the reference.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Callable, Iterable, Optional
+
+import torch
+
+
+def rows_for_budget(d: int, bytes_budget: int, dtype=torch.bfloat16) -> int:
+    return int(bytes_budget // (d * torch.empty((), dtype=dtype).element_size()))
+
+
+def hbm_budget(fraction: float = 0.8, device=None) -> int:
+    """Bytes of free device memory times ``fraction`` (sizes the ring for 288 GB parts)."""
+    free, _ = torch.cuda.mem_get_info(device)
+    return int(free * fraction)
+
+
+class DeviceRing:
+    def __init__(self, capacity: int, d: int, device="cuda", dtype=torch.bfloat16, seed: int = 0):
+        self.capacity = int(capacity)
+        self.d = d
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.buf = torch.empty(self.capacity, d, device=self.device, dtype=dtype)
+        self.size = 0      # valid rows
+        self.head = 0      # next write position
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        self._perm: Optional[torch.Tensor] = None
+        self._cursor = 0
+        self.epoch = 0
+
+    @classmethod
+    def from_hbm(cls, d: int, fraction: float = 0.5, max_rows: Optional[int] = None, device="cuda", **kw):
+        rows = rows_for_budget(d, hbm_budget(fraction, device))
+        if max_rows:
+            rows = min(rows, max_rows)
+        return cls(rows, d, device=device, **kw)
+
+    # ------------------------------------------------------------------ producers
+    def push(self, rows: torch.Tensor):
+        """Append rows (any dtype/device); wraps around, overwriting the oldest rows."""
+        rows = rows.reshape(-1, self.d)
+        n = rows.shape[0]
+        if n > self.capacity:
+            rows = rows[-self.capacity:]
+            n = self.capacity
+        first = min(n, self.capacity - self.head)
+        self.buf[self.head:self.head + first].copy_(rows[:first], non_blocking=True)
+        if n > first:
+            self.buf[: n - first].copy_(rows[first:], non_blocking=True)
+        self.head = (self.head + n) % self.capacity
+        self.size = min(self.capacity, self.size + n)
+        self._perm = None
+
+    def fill(self, producer: Callable[[], torch.Tensor], rows: Optional[int] = None):
+        """Call ``producer()`` until ``rows`` (default: capacity) rows have been pushed."""
+        target = self.capacity if rows is None else min(rows, self.capacity)
+        pushed = 0
+        while pushed < target:
+            chunk = producer()
+            chunk = chunk[: target - pushed]
+            self.push(chunk)
+            pushed += chunk.shape[0]
+        return self
+
+    # ------------------------------------------------------------------ consumer
+    def _new_epoch(self):
+        self._perm = torch.randperm(self.size, device=self.device, generator=self.gen)
+        self._cursor = 0
+        self.epoch += 1
+
+    def sample(self, batch_size: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Random batch (without replacement within an epoch), gathered on device."""
+        if self.size == 0:
+            raise RuntimeError("ring is empty")
+        if self._perm is None or self._cursor + batch_size > self._perm.numel():
+            self._new_epoch()
+        idx = self._perm[self._cursor:self._cursor + batch_size]
+        self._cursor += batch_size
+        if out is None:
+            return self.buf.index_select(0, idx)
+        return torch.index_select(self.buf, 0, idx, out=out)
+
+    def sample_shard(self, batch_size: int, rank: int, world: int, out=None) -> torch.Tensor:
+        """Data-parallel sampling: every rank draws the same global permutation slice and
+        keeps its own contiguous shard (DistributedSampler semantics on device)."""
+        if self._perm is None or self._cursor + batch_size * world > self._perm.numel():
+            self._new_epoch()
+        idx = self._perm[self._cursor + rank * batch_size:self._cursor + (rank + 1) * batch_size]
+        self._cursor += batch_size * world
+        if out is None:
+            return self.buf.index_select(0, idx)
+        return torch.index_select(self.buf, 0, idx, out=out)
+
+    def batches_per_epoch(self, batch_size: int) -> int:
+        return self.size // batch_size
+
+    def view(self) -> torch.Tensor:
+        return self.buf[: self.size]

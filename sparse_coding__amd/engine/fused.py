@@ -1,0 +1,255 @@
+"""``FusedSAEEnsemble``: the MI355X training engine for SAE ensembles.
+
+One training step for ALL models of an ensemble is six kernel launches (the
+reference runs ``vmap(grad(loss))`` + ``vmap(adam.update)``,
+``autoencoders/ensemble.py:175-193``, i.e. dozens of eager ops):
+
+1. ``encode_relu``     c = relu(x W_e^T + b)          (grouped MFMA GEMM, L1/L0 epilogue)
+2. ``decode_residual`` R = c W_hat - x                (MFMA, sum R^2 epilogue)
+3. ``code_grad``       dpre = 1[c>0](R W_hat^T + l d/2) (MFMA, bias-grad column partials)
+4. ``weight_grads``    dW_hat = c^T R, dW_e = dpre^T x (two problems, one launch)
+5. ``adam_rows``       norm-Jacobian + Adam + bf16 shadow for decoder and encoder
+6. ``bias_loss``       reduce partials -> losses, Adam on the bias
+
+State layout (per device): fp32 masters ``[G, n, d]``; Adam moments; bf16
+shadows the GEMMs read (decoder shadow already row-normalised, so no kernel
+ever recomputes norms); per-model hyper-parameters as device vectors
+(``l1_alpha``, ``bias_decay``, ``lr``).  Nothing allocates inside ``step``.
+
+Supported kinds: ``untied`` (FunctionalSAE / FunctionalMaskedSAE / FunctionalFista's
+SAE loss) and ``tied`` (FunctionalTiedSAE with identity centering /
+FunctionalMaskedTiedSAE).  Masked models pass per-model ``dict_size``.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..ops import adam as adam_ops
+from ..ops import gemm as gemm_ops
+
+
+def _stack(models, key, which=0, device=None):
+    return torch.stack([m[which][key].detach().float() for m in models]).to(device).contiguous()
+
+
+class FusedSAEEnsemble:
+    """Fused HIP training engine; API mirrors ``FunctionalEnsemble``."""
+
+    def __init__(self, models, sig, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999),
+                 eps=1e-8, track_feature_counts=True, kind: Optional[str] = None):
+        self.sig = sig
+        self.kind = kind or getattr(sig, "fused_kind", None)
+        if self.kind not in ("untied", "tied"):
+            raise ValueError(f"signature {sig} has no fused implementation")
+        self.device = torch.device(device)
+        self.n_models = G = len(models)
+        self.batch_size = B = int(batch_size)
+        p0, b0 = models[0]
+        self.n, self.d = p0["encoder"].shape
+        n, d = self.n, self.d
+        if B % 128 or n % 128 or d % 256:
+            raise ValueError(f"fused path needs B%128==0, n%128==0, d%256==0 (got B={B}, n={n}, d={d})")
+        if self.kind == "tied":
+            for key in ("center_rot", "center_trans", "center_scale"):
+                if key in b0:
+                    ref = {"center_rot": torch.eye(d), "center_trans": torch.zeros(d),
+                           "center_scale": torch.ones(d)}[key]
+                    for m in models:
+                        if not torch.equal(m[1][key].detach().float().cpu(), ref):
+                            raise ValueError("fused tied path supports identity centering only")
+        dev = self.device
+        self.models_meta = [{k: v for k, v in m[1].items()} for m in models]
+        self.betas, self.eps = betas, eps
+        self.step_count = 0
+
+        # ----- parameters (fp32 masters) and Adam state
+        self.params: Dict[str, torch.Tensor] = {"encoder": _stack(models, "encoder", 0, dev),
+                                                "encoder_bias": _stack(models, "encoder_bias", 0, dev)}
+        if self.kind == "untied":
+            self.params["decoder"] = _stack(models, "decoder", 0, dev)
+        self.m = {k: torch.zeros_like(v) for k, v in self.params.items()}
+        self.v = {k: torch.zeros_like(v) for k, v in self.params.items()}
+        # ----- per-model hyper-parameters as device vectors
+        self.l1 = torch.tensor([float(m[1]["l1_alpha"]) for m in models], device=dev, dtype=torch.float32)
+        self.bias_decay = torch.tensor([float(m[1].get("bias_decay", 0.0)) for m in models], device=dev,
+                                       dtype=torch.float32)
+        lrs = lr if isinstance(lr, (list, tuple)) else [lr] * G
+        self.lr = torch.tensor([float(x) for x in lrs], device=dev, dtype=torch.float32)
+        self.nactive = None
+        if "dict_size" in b0:
+            self.nactive = torch.tensor([int(m[1]["dict_size"]) for m in models], device=dev, dtype=torch.int32)
+
+        # ----- bf16 shadows read by the GEMMs
+        bf = torch.bfloat16
+        self.enc_shadow = torch.empty(G, n, d, device=dev, dtype=bf)
+        self.dec_shadow = torch.empty(G, n, d, device=dev, dtype=bf) if self.kind == "untied" else self.enc_shadow
+        self.refresh_shadows()
+
+        # ----- workspaces
+        tm = B // 128
+        self.c = torch.empty(G, B, n, device=dev, dtype=bf)
+        self.r = torch.empty(G, B, d, device=dev, dtype=bf)
+        self.dpre = torch.empty(G, B, n, device=dev, dtype=bf)
+        # gradient buffers; the last-produced weight gradient shares one flat buffer with the
+        # reduced bias gradient so data-parallel runs all-reduce both with a single collective
+        if self.kind == "untied":
+            self.g_dec = torch.empty(G, n, d, device=dev, dtype=torch.float32)
+            self._g_flat = torch.empty(G * n * d + G * n, device=dev, dtype=torch.float32)
+            self.g_enc = self._g_flat[: G * n * d].view(G, n, d)
+        else:
+            self._g_flat = torch.empty(G * n * d + G * n, device=dev, dtype=torch.float32)
+            self.g_dec = self._g_flat[: G * n * d].view(G, n, d)
+            self.g_enc = None
+        self.g_bias = self._g_flat[G * n * d:].view(G, 1, n)
+        self.grad_scale = 1.0  # data parallel: 1 / world_size (gradients are then summed)
+        self.enc_part = torch.zeros(G, tm * (n // 128), 2, device=dev)
+        self.dec_part = torch.zeros(G, tm * (d // 128), device=dev)
+        self.colpart = torch.zeros(G, tm, n, device=dev)
+        self.track_feature_counts = track_feature_counts
+        self.cnt_part = torch.zeros(G, tm, n, device=dev) if track_feature_counts else None
+        self.feature_counts = torch.zeros(G, n, device=dev) if track_feature_counts else None
+        self.rows_seen = 0
+        self.out = torch.zeros(G, 5, device=dev)
+
+    # ------------------------------------------------------------------ helpers
+    def refresh_shadows(self):
+        """Rebuild the bf16 shadows from the fp32 masters (after any out-of-band edit)."""
+        if self.kind == "untied":
+            adam_ops.shadow_rows(self.params["encoder"], self.enc_shadow, normalize=False)
+            adam_ops.shadow_rows(self.params["decoder"], self.dec_shadow, normalize=True)
+        else:
+            adam_ops.shadow_rows(self.params["encoder"], self.enc_shadow, normalize=True)
+
+    def _x_bf16(self, batch):
+        if batch.dtype != torch.bfloat16:
+            batch = batch.to(torch.bfloat16)
+        if batch.device != self.device:
+            batch = batch.to(self.device, non_blocking=True)
+        return batch.contiguous()
+
+    # ------------------------------------------------------------------ forward/backward
+    def forward(self, x):
+        """Kernels 1-3: codes (+L1/L0), residual (+MSE), code gradient (+bias-grad partials)."""
+        if x.shape[0] != self.batch_size:
+            raise ValueError(f"batch has {x.shape[0]} rows, engine was built for {self.batch_size}")
+        gemm_ops.encode_relu(x, self.enc_shadow, self.params["encoder_bias"], self.c, self.enc_part,
+                             self.cnt_part, self.nactive)
+        gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
+        gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart)
+
+    @property
+    def _alpha(self):
+        return 2.0 * self.grad_scale / (self.batch_size * self.d)
+
+    def wgrad_first(self, x):
+        """Untied: dW_hat = c^T R (decoder).  Tied: the whole dictionary gradient + bias grad."""
+        if self.kind == "untied":
+            gemm_ops.weight_grads([[(self.c, self.r)]], [self.g_dec], self._alpha)
+        else:
+            gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], [self.g_dec], self._alpha)
+            self._reduce_bias_grad()
+
+    def wgrad_second(self, x):
+        """Untied: dW_e = dpre^T x (encoder) + bias grad.  Tied: nothing."""
+        if self.kind == "untied":
+            gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha)
+            self._reduce_bias_grad()
+
+    def _reduce_bias_grad(self):
+        torch.sum(self.colpart, dim=1, keepdim=True, out=self.g_bias)
+        self.g_bias.mul_(self._alpha)
+
+    def forward_backward(self, x):
+        """Kernels 1-4 for the single-device step (both weight gradients in one launch)."""
+        self.forward(x)
+        if self.kind == "untied":
+            gemm_ops.weight_grads([[(self.c, self.r)], [(self.dpre, x)]], [self.g_dec, self.g_enc], self._alpha)
+        else:
+            gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], [self.g_dec], self._alpha)
+
+    def _adam_sets(self):
+        if self.kind == "untied":
+            return [dict(p=self.params["decoder"], g=self.g_dec, m=self.m["decoder"], v=self.v["decoder"],
+                         shadow=self.dec_shadow, norm=True),
+                    dict(p=self.params["encoder"], g=self.g_enc, m=self.m["encoder"], v=self.v["encoder"],
+                         shadow=self.enc_shadow, norm=False)]
+        return [dict(p=self.params["encoder"], g=self.g_dec, m=self.m["encoder"], v=self.v["encoder"],
+                     shadow=self.enc_shadow, norm=True)]
+
+    def adam_first(self):
+        self.step_count += 1
+        adam_ops.adam_rows(self._adam_sets()[:1], self.lr, self.step_count, *self.betas, self.eps)
+
+    def adam_second(self, reduced_bias=True):
+        """Encoder Adam (untied) and bias Adam + loss reduction."""
+        if self.kind == "untied":
+            adam_ops.adam_rows(self._adam_sets()[1:], self.lr, self.step_count, *self.betas, self.eps)
+        self._bias_loss(update=True, reduced=reduced_bias)
+
+    def apply_update(self):
+        """Kernels 5-6: fused Adam on the weights, then bias Adam + loss reduction."""
+        self.step_count += 1
+        adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count, *self.betas, self.eps)
+        self._bias_loss(update=True, reduced=False)
+
+    def _bias_loss(self, update, reduced):
+        G, B, n, d = self.n_models, self.batch_size, self.n, self.d
+        b1, b2 = self.betas
+        if reduced:  # bias gradient already summed (and possibly all-reduced) into g_bias
+            colpart, tm, gscale = self.g_bias, 1, 1.0
+        else:
+            colpart, tm, gscale = self.colpart, B // 128, self._alpha
+        adam_ops.bias_loss(self.params["encoder_bias"], self.m["encoder_bias"], self.v["encoder_bias"],
+                           colpart, tm, self.enc_part, self.enc_part.shape[1], self.dec_part,
+                           self.dec_part.shape[1], self.l1, self.bias_decay, self.lr, self.out, B, d,
+                           self.step_count, gscale=gscale, cnt_part=self.cnt_part,
+                           feat_count=self.feature_counts, b1=b1, b2=b2, eps=self.eps, update=update)
+        if self.track_feature_counts:
+            self.rows_seen += B
+
+    def step_batch(self, batch, expand_dims=True):
+        """One Adam step of every model on ``batch [B, d]``; returns a device tensor [G, 5]:
+        (loss, l_reconstruction, l_l1, l_bias_decay, mean L0).  Never synchronises."""
+        x = self._x_bf16(batch)
+        self.forward_backward(x)
+        self.apply_update()
+        return self.out
+
+    def loss_dicts(self, out=None):
+        out = (self.out if out is None else out).detach().cpu()
+        keys = ["loss", "l_reconstruction", "l_l1", "l_bias_decay", "l0"]
+        return [{k: float(out[i, j]) for j, k in enumerate(keys)} for i in range(self.n_models)]
+
+    # ------------------------------------------------------------------ export
+    def unstack(self, device="cpu"):
+        out = []
+        for i in range(self.n_models):
+            p = {k: v[i].detach().to(device).clone() for k, v in self.params.items()}
+            b = {}
+            for k, v in self.models_meta[i].items():
+                b[k] = v.detach().to(device).clone() if torch.is_tensor(v) else v
+            out.append((p, b))
+        return out
+
+    def to_learned_dicts(self, device="cpu"):
+        return [self.sig.to_learned_dict(p, b) for p, b in self.unstack(device)]
+
+    def state_dict(self):
+        return {"kind": self.kind, "params": self.params, "m": self.m, "v": self.v, "lr": self.lr,
+                "l1": self.l1, "bias_decay": self.bias_decay, "step": self.step_count,
+                "nactive": self.nactive, "feature_counts": self.feature_counts, "rows_seen": self.rows_seen}
+
+    def load_state_dict(self, sd):
+        for k in self.params:
+            self.params[k].copy_(sd["params"][k])
+            self.m[k].copy_(sd["m"][k])
+            self.v[k].copy_(sd["v"][k])
+        self.lr.copy_(sd["lr"]); self.l1.copy_(sd["l1"]); self.bias_decay.copy_(sd["bias_decay"])
+        self.step_count = int(sd["step"])
+        if sd.get("feature_counts") is not None and self.feature_counts is not None:
+            self.feature_counts.copy_(sd["feature_counts"])
+        self.rows_seen = int(sd.get("rows_seen", 0))
+        self.refresh_shadows()

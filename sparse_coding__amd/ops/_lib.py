@@ -1,0 +1,113 @@
+"""ctypes binding to the in-tree gfx950 kernel library (``_sc_kernels.so``).
+
+The library is loaded lazily, after ``torch`` has mapped its HIP runtime.  On a
+machine with a GPU the kernels are mandatory: if the library is missing we try
+one in-tree build and otherwise raise -- there is no silent eager fallback for
+the fused paths.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+_HERE = Path(__file__).resolve().parent
+_LIB_PATH = _HERE / "_sc_kernels.so"
+_lock = threading.Lock()
+_lib = None
+
+c_int, c_long, c_float, c_void_p = C.c_int, C.c_long, C.c_float, C.c_void_p
+c_float_p = C.POINTER(C.c_float)
+
+
+class ScOperand(C.Structure):
+    _fields_ = [("ptr", c_void_p), ("ld", c_long), ("sg", c_long)]
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def _declare(lib):
+    sig = {
+        "sc_gemm": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                    C.POINTER(ScOperand), C.POINTER(ScOperand), C.POINTER(c_void_p), c_float_p,
+                    c_long, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long,
+                    c_void_p, c_void_p, c_void_p, c_float, c_void_p],
+        "sc_adam_rows": [c_int, C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
+                         C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
+                         C.POINTER(c_int), C.POINTER(c_int), c_int, c_int, c_void_p,
+                         c_float, c_float, c_float, c_float, c_float, c_void_p],
+        "sc_shadow_rows": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p],
+        "sc_bias_loss": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                         c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
+                         c_float, c_float, c_int, c_void_p],
+    }
+    optional = {
+        "sc_topk_encode": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                           c_int, c_long, c_void_p],
+        "sc_topk_decode_loss": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                c_int, c_int, c_int, c_int, c_int, c_void_p],
+        "sc_topk_grad_dict": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+        "sc_fista": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+        "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_void_p],
+    }
+    for name, args in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = c_int
+    for name, args in optional.items():
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = c_int
+    return lib
+
+
+def lib():
+    """Return the loaded kernel library, building it in-tree if needed."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not _LIB_PATH.exists():
+            if os.environ.get("SC_NO_AUTOBUILD"):
+                raise KernelError(f"{_LIB_PATH} missing and SC_NO_AUTOBUILD is set")
+            from . import build as _build
+
+            _build.build(verbose=False)
+        _lib = _declare(C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL))
+        return _lib
+
+
+def available() -> bool:
+    """True when the fused HIP path can run (GPU present and library loadable)."""
+    if not torch.cuda.is_available():
+        return False
+    try:
+        lib()
+        return True
+    except Exception:  # pragma: no cover - reported by callers that require it
+        return False
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise KernelError(f"{what} failed with code {rc}")
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,72 @@
+"""Python front-end for the fused Adam / shadow / bias-loss kernels (``csrc/adam.hip``)."""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+
+def _vp(seq):
+    return (C.c_void_p * len(seq))(*[_lib.ptr(t) for t in seq])
+
+
+def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None):
+    """Fused row-wise Adam over one or two parameter sets.
+
+    sets: list of dicts with keys p, g, m, v (fp32 [G, n, d]), shadow (bf16 [G, n, d] or None),
+    norms (fp32 [G, n] or None), norm (bool: parameter is row-normalised inside the loss).
+    lr: fp32 tensor [G] (per-model learning rate); step: 1-based Adam step.
+    """
+    if not 1 <= len(sets) <= 2:
+        raise ValueError("1 or 2 parameter sets")
+    G, n, d = sets[0]["p"].shape
+    for s in sets:
+        for k in ("p", "g", "m", "v"):
+            t = s[k]
+            if t.dtype != torch.float32 or tuple(t.shape) != (G, n, d) or not t.is_contiguous():
+                raise ValueError(f"adam set tensor {k} must be contiguous fp32 {(G, n, d)}")
+        if s.get("shadow") is not None and s["shadow"].dtype != torch.bfloat16:
+            raise ValueError("shadow must be bf16")
+    rows = (C.c_int * len(sets))(*[G * n for _ in sets])
+    norm = (C.c_int * len(sets))(*[int(bool(s["norm"])) for s in sets])
+    bc1 = 1.0 - b1 ** step
+    bc2 = 1.0 - b2 ** step
+    rc = _lib.lib().sc_adam_rows(
+        len(sets), _vp([s["p"] for s in sets]), _vp([s["g"] for s in sets]),
+        _vp([s["m"] for s in sets]), _vp([s["v"] for s in sets]),
+        _vp([s.get("shadow") for s in sets]), _vp([s.get("norms") for s in sets]),
+        rows, norm, d, rows_per_model or n, _lib.ptr(lr), b1, b2, eps, bc1, bc2,
+        _lib.stream_handle(),
+    )
+    _lib.check(rc, "sc_adam_rows")
+
+
+def shadow_rows(p, shadow, norms=None, normalize=True):
+    """bf16 shadow (row-normalised if ``normalize``) of fp32 rows p[..., d]."""
+    d = p.shape[-1]
+    rows = p.numel() // d
+    if not (p.is_contiguous() and shadow.is_contiguous() and shadow.dtype == torch.bfloat16):
+        raise ValueError("shadow_rows needs contiguous fp32 p and bf16 shadow")
+    rc = _lib.lib().sc_shadow_rows(_lib.ptr(p), _lib.ptr(shadow), _lib.ptr(norms), rows, d,
+                                   int(normalize), _lib.stream_handle())
+    _lib.check(rc, "sc_shadow_rows")
+
+
+def bias_loss(b, m, v, colpart, tm, enc_part, enc_tiles, dec_part, dec_tiles, l1, bias_decay, lr,
+              out, B, d, step, gscale, cnt_part=None, feat_count=None, b1=0.9, b2=0.999, eps=1e-8,
+              update=True):
+    """Loss bookkeeping + bias Adam.  ``colpart`` [G, tm, n] holds partial sums of the bias
+    gradient; ``gscale`` converts their sum to dL/db."""
+    G, n = b.shape
+    bc1 = 1.0 - b1 ** max(step, 1)
+    bc2 = 1.0 - b2 ** max(step, 1)
+    rc = _lib.lib().sc_bias_loss(
+        G, _lib.ptr(b), _lib.ptr(m), _lib.ptr(v), _lib.ptr(colpart), tm, _lib.ptr(enc_part),
+        enc_tiles, _lib.ptr(dec_part), dec_tiles, _lib.ptr(cnt_part), _lib.ptr(feat_count),
+        _lib.ptr(l1), _lib.ptr(bias_decay), _lib.ptr(lr), _lib.ptr(out), n, B, d, float(gscale), b1, b2, eps,
+        bc1, bc2, int(update), _lib.stream_handle(),
+    )
+    _lib.check(rc, "sc_bias_loss")

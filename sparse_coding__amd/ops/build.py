@@ -1,0 +1,130 @@
+"""In-tree build of the HIP kernel library for gfx950.
+
+The kernels are plain HIP (no torch headers) exposed through a C ABI, so each
+translation unit compiles in seconds with ``hipcc --offload-arch=gfx950`` and
+the resulting ``_sc_kernels.so`` travels with the repository snapshot.  The
+library is loaded with ctypes *after* ``import torch`` so its NEEDED
+``libamdhip64.so.7`` resolves to the HIP runtime torch already mapped (one
+runtime per process).
+
+Usage::
+
+    python -m sparse_coding__amd.ops.build          # incremental
+    python -m sparse_coding__amd.ops.build --force  # full rebuild
+"""
+
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+BUILD = HERE / "_build"
+LIB = HERE / "_sc_kernels.so"
+RUNTIME_LIB = HERE / "_sc_runtime.so"
+ARCH = os.environ.get("SC_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found; the MI355X kernels need ROCm's hipcc")
+
+
+def _kernel_sources():
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _runtime_sources():
+    return sorted((CSRC / "runtime").glob("*.cpp"))
+
+
+def _headers():
+    return sorted(CSRC.glob("*.h")) + sorted((CSRC / "runtime").glob("*.h"))
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _compile_one(src: Path, force: bool) -> Path:
+    obj = BUILD / (src.stem + ".o")
+    if not force and not _stale(obj, [src, *_headers()]):
+        return obj
+    cmd = [
+        _hipcc(),
+        f"--offload-arch={ARCH}",
+        "-O3",
+        "-std=c++17",
+        "-fPIC",
+        "-munsafe-fp-atomics",
+        f"-I{CSRC}",
+        "-c",
+        str(src),
+        "-o",
+        str(obj),
+    ]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{res.stderr}")
+    return obj
+
+
+def _compile_host(src: Path, force: bool) -> Path:
+    obj = BUILD / (src.stem + ".host.o")
+    if not force and not _stale(obj, [src, *_headers()]):
+        return obj
+    cxx = shutil.which("g++") or "c++"
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-pthread", f"-I{CSRC}", "-c", str(src), "-o", str(obj)]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"g++ failed for {src.name}:\n{res.stderr}")
+    return obj
+
+
+def build(force: bool = False, verbose: bool = True) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    srcs = _kernel_sources()
+    rt_srcs = _runtime_sources()
+    workers = max(1, min(8, os.cpu_count() or 1, len(srcs) + len(rt_srcs)))
+    with cf.ThreadPoolExecutor(workers) as ex:
+        objs = list(ex.map(lambda s: _compile_one(s, force), srcs))
+        rt_objs = list(ex.map(lambda s: _compile_host(s, force), rt_srcs))
+    if force or _stale(LIB, objs):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed:\n{res.stderr}")
+        if verbose:
+            print(f"[sc-build] linked {LIB.name} from {len(objs)} objects")
+    if rt_objs and (force or _stale(RUNTIME_LIB, rt_objs)):
+        cxx = shutil.which("g++") or "c++"
+        cmd = [cxx, "-shared", "-fPIC", "-pthread", *map(str, rt_objs), "-o", str(RUNTIME_LIB)]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"runtime link failed:\n{res.stderr}")
+        if verbose:
+            print(f"[sc-build] linked {RUNTIME_LIB.name} from {len(rt_objs)} objects")
+    return LIB
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    args = ap.parse_args(argv)
+    build(force=args.force)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,289 @@
+// Fused Adam for stacked dictionary parameters (gfx950).
+//
+// Reference semantics: torchopt 0.7.1 `adam` vmapped over the model axis
+// (reference autoencoders/ensemble.py:94-95, :123, :182-191), with the decoder
+// row normalisation done *inside* the loss (autoencoders/sae_ensemble.py:58-59),
+// so the gradient reaching the raw decoder goes through the norm Jacobian:
+//     dW[j] = (dW_hat[j] - W_hat[j] <W_hat[j], dW_hat[j]>) / max(|W[j]|, 1e-8)
+// One wave owns one dictionary row (d elements).  In a single HBM pass it
+// applies the norm Jacobian, the Adam update, recomputes the row norm and
+// writes the bf16 shadow (normalised for NORM rows) that the next step's
+// MFMA GEMMs read.  Bias / loss bookkeeping runs in a second tiny kernel that
+// also reduces the deterministic per-tile partials written by the GEMM
+// epilogues (no float atomics anywhere in the step).
+#include "common.h"
+
+namespace scamd {
+
+struct AdamRows {
+  float* p;         // [rows][d] fp32 master
+  const float* g;   // [rows][d] gradient (w.r.t. the normalised row if norm)
+  float* m;
+  float* v;
+  uint16_t* shadow; // [rows][d] bf16 copy for the GEMMs (normalised if norm)
+  float* norms;     // [rows] optional: new row norms
+  int rows;
+  int norm;         // 1: row-normalised parameter (decoder / tied dict)
+};
+
+struct AdamArgs {
+  AdamRows set[2];
+  int nset;
+  int d;
+  int rows_per_model;
+  const float* lr;  // per model
+  float b1, b2, eps, bc1, bc2;
+};
+
+template <int NV>
+__global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
+  const int lane = threadIdx.x & 63;
+  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  long row = wave;
+  int s = 0;
+  if (row >= a.set[0].rows) {
+    row -= a.set[0].rows;
+    s = 1;
+    if (s >= a.nset || row >= a.set[1].rows) return;
+  }
+  const AdamRows& R = a.set[s];
+  const int d = NV * 256;
+  const long base = row * d;
+  const float lr = a.lr[row / a.rows_per_model];
+  // NV float4 chunks per lane (d == 256 * NV); compile-time so pv/gv stay in VGPRs.
+  const float* P4 = R.p + base;
+  const float* G4 = R.g + base;
+
+  float4 pv[NV], gv[NV];
+  float ss = 0.f, dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int e = (i * 64 + lane) * 4;
+    pv[i] = *reinterpret_cast<const float4*>(P4 + e);
+    gv[i] = *reinterpret_cast<const float4*>(G4 + e);
+    ss += pv[i].x * pv[i].x + pv[i].y * pv[i].y + pv[i].z * pv[i].z + pv[i].w * pv[i].w;
+    dot += pv[i].x * gv[i].x + pv[i].y * gv[i].y + pv[i].z * gv[i].z + pv[i].w * gv[i].w;
+  }
+  float gs = 1.f, ws = 0.f;
+  if (R.norm) {
+    ss = wave_sum(ss);
+    dot = wave_sum(dot);
+    const float nrm = sqrtf(ss);
+    if (nrm > 1e-8f) {
+      const float inv = 1.f / nrm;
+      gs = inv;                 // g' = (g - w_hat <w_hat, g>) / |w|
+      ws = dot * inv * inv * inv;  // w_hat <w_hat,g> / |w| = w <w,g> / |w|^3
+    } else {
+      gs = 1e8f;                // clamp(min=1e-8) has zero derivative below the floor
+      ws = 0.f;
+    }
+  }
+  const float b1 = a.b1, b2 = a.b2, omb1 = 1.f - b1, omb2 = 1.f - b2;
+  const float step = lr / a.bc1, rbc2 = 1.f / a.bc2;
+  float ss2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int e = (i * 64 + lane) * 4;
+    float4 mv = *reinterpret_cast<const float4*>(R.m + base + e);
+    float4 vv = *reinterpret_cast<const float4*>(R.v + base + e);
+    float* pp = reinterpret_cast<float*>(&pv[i]);
+    float* gg = reinterpret_cast<float*>(&gv[i]);
+    float* mm = reinterpret_cast<float*>(&mv);
+    float* vvv = reinterpret_cast<float*>(&vv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gk = gg[k] * gs - pp[k] * ws;
+      mm[k] = b1 * mm[k] + omb1 * gk;
+      vvv[k] = b2 * vvv[k] + omb2 * gk * gk;
+      pp[k] -= step * mm[k] / (sqrtf(vvv[k] * rbc2) + a.eps);
+      ss2 += pp[k] * pp[k];
+    }
+    *reinterpret_cast<float4*>(R.m + base + e) = mv;
+    *reinterpret_cast<float4*>(R.v + base + e) = vv;
+    *reinterpret_cast<float4*>(R.p + base + e) = pv[i];
+  }
+  float sc = 1.f;
+  if (R.norm) {
+    ss2 = wave_sum(ss2);
+    const float nrm = fmaxf(sqrtf(ss2), 1e-8f);
+    sc = 1.f / nrm;
+    if (R.norms && lane == 0) R.norms[row] = nrm;
+  }
+  if (R.shadow) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = (i * 64 + lane) * 4;
+      ushort4 h;
+      h.x = f2bf(pv[i].x * sc);
+      h.y = f2bf(pv[i].y * sc);
+      h.z = f2bf(pv[i].z * sc);
+      h.w = f2bf(pv[i].w * sc);
+      *reinterpret_cast<ushort4*>(R.shadow + base + e) = h;
+    }
+  }
+}
+
+// Writes a bf16 (optionally row-normalised) shadow of fp32 rows; used at init
+// and after any out-of-band parameter change (e.g. FISTA basis update).
+__global__ __launch_bounds__(256) void shadow_rows_kernel(const float* p, uint16_t* shadow, float* norms,
+                                                          long rows, int d, int norm) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* P = p + row * d;
+  float ss = 0.f;
+  for (int e = lane * 4; e < d; e += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(P + e);
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  float sc = 1.f;
+  if (norm) {
+    ss = wave_sum(ss);
+    const float nrm = fmaxf(sqrtf(ss), 1e-8f);
+    sc = 1.f / nrm;
+    if (norms && lane == 0) norms[row] = nrm;
+  }
+  for (int e = lane * 4; e < d; e += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(P + e);
+    ushort4 h;
+    h.x = f2bf(v.x * sc);
+    h.y = f2bf(v.y * sc);
+    h.z = f2bf(v.z * sc);
+    h.w = f2bf(v.w * sc);
+    *reinterpret_cast<ushort4*>(shadow + row * d + e) = h;
+  }
+}
+
+struct BiasArgs {
+  float* b; float* m; float* v;    // [G][n]
+  const float* colpart;            // [G][tm][n] partial sums of dpre_s over row tiles
+  int tm;                          // number of row tiles in colpart
+  const float* enc_part;           // [G][enc_tiles][2] (l1, l0)
+  int enc_tiles;
+  const float* dec_part;           // [G][dec_tiles] (sum R^2)
+  int dec_tiles;
+  const float* cnt_part;           // optional [G][tm][n] feature on-counts
+  float* feat_count;               // optional [G][n] accumulated counts
+  const float* l1;                 // [G]
+  const float* bias_decay;         // [G]
+  const float* lr;                 // [G]
+  float* out;                      // [G][5]: loss, l_rec, l_l1, l_bias_decay, mean L0
+  int n, B, d;
+  float gscale;                    // converts colpart sums to dL/db (2/(B d) for raw dpre_s)
+  float b1, b2, eps, bc1, bc2;
+  int update;                      // 0: only losses (eval)
+};
+
+__global__ __launch_bounds__(256) void bias_loss_kernel(BiasArgs a) {
+  __shared__ float red[8];
+  const int g = blockIdx.x, tid = threadIdx.x;
+  const int n = a.n;
+  float* b = a.b + (long)g * n;
+  float bs = 0.f;
+  for (int j = tid; j < n; j += 256) bs += b[j] * b[j];
+  bs = block_sum_256(bs, red);
+  float l1 = 0.f, l0 = 0.f, se = 0.f;
+  for (int t = tid; t < a.enc_tiles; t += 256) {
+    l1 += a.enc_part[((long)g * a.enc_tiles + t) * 2];
+    l0 += a.enc_part[((long)g * a.enc_tiles + t) * 2 + 1];
+  }
+  for (int t = tid; t < a.dec_tiles; t += 256) se += a.dec_part[(long)g * a.dec_tiles + t];
+  l1 = block_sum_256(l1, red);
+  l0 = block_sum_256(l0, red);
+  se = block_sum_256(se, red);
+  const float bnorm = sqrtf(bs);
+  const float lam = a.l1[g], beta = a.bias_decay[g];
+  if (tid == 0) {
+    const float l_rec = se / ((float)a.B * a.d);
+    const float l_l1 = lam * l1 / a.B;
+    const float l_bd = beta * bnorm;
+    float* o = a.out + g * 5;
+    o[0] = l_rec + l_l1 + l_bd;
+    o[1] = l_rec;
+    o[2] = l_l1;
+    o[3] = l_bd;
+    o[4] = l0 / a.B;
+  }
+  if (a.cnt_part && a.feat_count) {
+    for (int j = tid; j < n; j += 256) {
+      float c = 0.f;
+      for (int t = 0; t < a.tm; ++t) c += a.cnt_part[((long)g * a.tm + t) * n + j];
+      a.feat_count[(long)g * n + j] += c;
+    }
+  }
+  if (!a.update) return;
+  const float lr = a.lr[g];
+  const float step = lr / a.bc1, rbc2 = 1.f / a.bc2;
+  const float bd = (beta != 0.f && bnorm > 0.f) ? beta / bnorm : 0.f;
+  for (int j = tid; j < n; j += 256) {
+    float gsum = 0.f;
+    for (int t = 0; t < a.tm; ++t) gsum += a.colpart[((long)g * a.tm + t) * n + j];
+    const float gj = gsum * a.gscale + bd * b[j];
+    float mj = a.m[(long)g * n + j], vj = a.v[(long)g * n + j];
+    mj = a.b1 * mj + (1.f - a.b1) * gj;
+    vj = a.b2 * vj + (1.f - a.b2) * gj * gj;
+    a.m[(long)g * n + j] = mj;
+    a.v[(long)g * n + j] = vj;
+    b[j] -= step * mj / (sqrtf(vj * rbc2) + a.eps);
+  }
+}
+
+}  // namespace scamd
+
+using namespace scamd;
+
+extern "C" {
+
+int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const* m, float* const* v,
+                 void* const* shadow, float* const* norms, const int* rows, const int* norm, int d,
+                 int rows_per_model, const float* lr, float b1, float b2, float eps, float bc1,
+                 float bc2, hipStream_t stream) {
+  if (d % 256 || d > 4096 || nset < 1 || nset > 2) return 1;
+  AdamArgs a;
+  long total = 0;
+  for (int i = 0; i < nset; ++i) {
+    a.set[i] = {p[i], g[i], m[i], v[i], reinterpret_cast<uint16_t*>(shadow[i]), norms[i], rows[i], norm[i]};
+    total += rows[i];
+  }
+  if (nset == 1) a.set[1] = a.set[0], a.set[1].rows = 0;
+  a.nset = nset; a.d = d; a.rows_per_model = rows_per_model; a.lr = lr;
+  a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2;
+  const long blocks = (total + 3) / 4;
+  switch (d / 256) {
+    case 1: hipLaunchKernelGGL(adam_rows_kernel<1>, dim3(blocks), dim3(256), 0, stream, a); break;
+    case 2: hipLaunchKernelGGL(adam_rows_kernel<2>, dim3(blocks), dim3(256), 0, stream, a); break;
+    case 3: hipLaunchKernelGGL(adam_rows_kernel<3>, dim3(blocks), dim3(256), 0, stream, a); break;
+    case 4: hipLaunchKernelGGL(adam_rows_kernel<4>, dim3(blocks), dim3(256), 0, stream, a); break;
+    case 6: hipLaunchKernelGGL(adam_rows_kernel<6>, dim3(blocks), dim3(256), 0, stream, a); break;
+    case 8: hipLaunchKernelGGL(adam_rows_kernel<8>, dim3(blocks), dim3(256), 0, stream, a); break;
+    case 16: hipLaunchKernelGGL(adam_rows_kernel<16>, dim3(blocks), dim3(256), 0, stream, a); break;
+    default: return 1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_shadow_rows(const float* p, void* shadow, float* norms, long rows, int d, int norm,
+                   hipStream_t stream) {
+  if (d % 4) return 1;
+  hipLaunchKernelGGL(shadow_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, p,
+                     reinterpret_cast<uint16_t*>(shadow), norms, rows, d, norm);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_bias_loss(int G, float* b, float* m, float* v, const float* colpart, int tm,
+                 const float* enc_part, int enc_tiles, const float* dec_part, int dec_tiles,
+                 const float* cnt_part, float* feat_count, const float* l1, const float* bias_decay,
+                 const float* lr, float* out, int n, int B, int d, float gscale, float b1, float b2, float eps,
+                 float bc1, float bc2, int update, hipStream_t stream) {
+  BiasArgs a;
+  a.b = b; a.m = m; a.v = v; a.colpart = colpart; a.tm = tm;
+  a.enc_part = enc_part; a.enc_tiles = enc_tiles; a.dec_part = dec_part; a.dec_tiles = dec_tiles;
+  a.cnt_part = cnt_part; a.feat_count = feat_count;
+  a.l1 = l1; a.bias_decay = bias_decay; a.lr = lr; a.out = out;
+  a.n = n; a.B = B; a.d = d; a.gscale = gscale;
+  a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.update = update;
+  hipLaunchKernelGGL(bias_loss_kernel, dim3(G), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// Shared CDNA4 (gfx950) helpers for the sparse-coding kernels.
+//
+// Everything here is wave64 / MFMA specific: this code is written for MI355X
+// only (hipcc --offload-arch=gfx950) and has no other target.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace scamd {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+#define SC_LDS(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+__device__ __forceinline__ float bf2f(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16 (hipcc lowers the cast to v_cvt_pk_bf16_f32,
+// which keeps NaN a NaN).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for a 256-thread block; `red` must hold >= 4 floats of LDS.
+__device__ __forceinline__ float block_sum_256(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return r;
+}
+
+// Bijective XCD-aware block remap (MI355X has 8 XCDs, each with its own L2).
+// Hardware hands consecutive block ids to different XCDs round-robin; this
+// gives each XCD a contiguous run of logical tiles so neighbouring tiles that
+// share operand panels hit the same L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (orig >> 3);
+}
+
+}  // namespace scamd

@@ -1,0 +1,189 @@
+"""Python front-end of the grouped MFMA GEMM (``csrc/sae_gemm.hip``).
+
+Every function takes already-allocated output tensors so the training step
+never allocates; shapes are checked on the host before launch (a mis-shaped
+launch on MI355X can fault the whole node).
+
+Notation: G = models in the ensemble, B = batch rows, d = activation width,
+n = dictionary size.  bf16 tensors are passed as torch.bfloat16.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+
+EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16 = 0, 1, 2, 3, 4
+TILE_M, TILE_N, TILE_K = 128, 128, 64
+
+
+def _op(t, ld, sg):
+    return _lib.ScOperand(_lib.ptr(t), ld, sg)
+
+
+def _need(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _bf16(t, name):
+    _need(t.dtype == torch.bfloat16, f"{name} must be bfloat16, got {t.dtype}")
+    _need(t.is_cuda, f"{name} must be on the GPU")
+    _need(t.is_contiguous(), f"{name} must be contiguous")
+
+
+def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *,
+            bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
+            colpart=None, l1=None, l1_add_scale=0.0):
+    _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
+    _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
+    nprob = len(outs)
+    A = (_lib.ScOperand * (2 * nprob))(*a_ops)
+    Bo = (_lib.ScOperand * (2 * nprob))(*b_ops)
+    Cp = (C.c_void_p * nprob)(*[_lib.ptr(o) for o in outs])
+    al = (C.c_float * nprob)(*alphas)
+    rc = _lib.lib().sc_gemm(
+        epi, layout, nprob, M, N, K1, K2, G, A, Bo, Cp, al, ldc, sc,
+        _lib.ptr(bias), sbias, _lib.ptr(nactive), _lib.ptr(aux), ldaux, saux,
+        _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1), float(l1_add_scale),
+        _lib.stream_handle(),
+    )
+    _lib.check(rc, f"sc_gemm(epi={epi})")
+
+
+def _x_stride(x, B, d, G):
+    """x may be shared by every model ([B, d]) or per model ([G, B, d])."""
+    if x.dim() == 2:
+        _need(tuple(x.shape) == (B, d), f"x shape {tuple(x.shape)} != {(B, d)}")
+        return 0
+    _need(tuple(x.shape) == (G, B, d), f"x shape {tuple(x.shape)} != {(G, B, d)}")
+    return B * d
+
+
+def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None):
+    """c[g] = relu(x[g] @ w[g]^T + bias[g]) with L1/L0 partials.
+
+    x: [B, d] or [G, B, d] bf16; w: [G, n, d] bf16; bias: [G, n] fp32;
+    c_out: [G, B, n] bf16; part: [G, (B/128)*(n/128), 2] fp32;
+    colpart (optional): [G, B/128, n] fp32 per-feature on-counts.
+    """
+    G, n, d = w.shape
+    B = c_out.shape[1]
+    _bf16(x, "x"); _bf16(w, "w"); _bf16(c_out, "c_out")
+    sx = _x_stride(x, B, d, G)
+    _need(tuple(c_out.shape) == (G, B, n), "c_out shape")
+    _need(tuple(bias.shape) == (G, n) and bias.dtype == torch.float32, "bias shape/dtype")
+    _need(part.numel() >= G * (B // 128) * (n // 128) * 2, "part too small")
+    if colpart is not None:
+        _need(colpart.numel() >= G * (B // 128) * n, "colpart too small")
+    if nactive is not None:
+        _need(nactive.dtype == torch.int32 and nactive.numel() == G, "nactive must be int32[G]")
+    a = [_op(x, d, sx), _op(x, d, sx)]
+    b = [_op(w, d, n * d), _op(w, d, n * d)]
+    _launch(EPI_ENC, 3, B, n, d, 0, G, a, b, [c_out], [1.0], n, B * n,
+            bias=bias, sbias=n, nactive=nactive, part=part, colpart=colpart)
+
+
+def decode_residual(c, w_hat, x, r_out, part):
+    """r[g] = c[g] @ w_hat[g] - x[g]  (bf16 out) with sum(r^2) partials.
+
+    c: [G, B, n] bf16; w_hat: [G, n, d] bf16 (row-normalised dictionary);
+    x: [B, d] or [G, B, d] bf16; r_out: [G, B, d] bf16; part: [G, (B/128)*(d/128)].
+    """
+    G, B, n = c.shape
+    d = w_hat.shape[2]
+    _bf16(c, "c"); _bf16(w_hat, "w_hat"); _bf16(r_out, "r_out")
+    sx = _x_stride(x, B, d, G)
+    _need(tuple(w_hat.shape) == (G, n, d), "w_hat shape")
+    _need(part.numel() >= G * (B // 128) * (d // 128), "part too small")
+    a = [_op(c, n, B * n)] * 2
+    b = [_op(w_hat, d, n * d)] * 2  # stored [K=n][N=d] -> N-major
+    _launch(EPI_DEC, 1, B, d, n, 0, G, a, b, [r_out], [1.0], d, B * d,
+            aux=x, ldaux=d, saux=sx, part=part)
+
+
+def code_grad(r, w_hat, c, l1, dpre_out, colpart):
+    """dpre_s[g] = 1[c>0] * (r[g] @ w_hat[g]^T + l1[g] * d / 2).
+
+    dpre_s is the code gradient in units of the residual: dL/dpre = 2/(B d) * dpre_s.
+    colpart receives per-row-tile column sums (bias gradient partials).
+    """
+    G, B, d = r.shape
+    n = w_hat.shape[1]
+    _bf16(r, "r"); _bf16(w_hat, "w_hat"); _bf16(c, "c"); _bf16(dpre_out, "dpre_out")
+    _need(tuple(c.shape) == (G, B, n) and tuple(dpre_out.shape) == (G, B, n), "c/dpre shape")
+    _need(l1.dtype == torch.float32 and l1.numel() == G, "l1 must be fp32[G]")
+    _need(colpart.numel() >= G * (B // 128) * n, "colpart too small")
+    a = [_op(r, d, B * d)] * 2
+    b = [_op(w_hat, d, n * d)] * 2
+    _launch(EPI_DC, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
+            aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0)
+
+
+def weight_grads(pairs, outs, alpha):
+    """out_i[g] = alpha * sum_segments A_s[g]^T @ B_s[g]   (reduction over batch rows).
+
+    pairs: list (one per problem, 1 or 2 problems) of lists of (A, B) segments
+    (1 or 2 segments, summed along K).  A: [G, Bk, n] bf16 (or [Bk, n] shared),
+    B: [G, Bk, d] bf16 (or [Bk, d] shared).  outs: [G, n, d] fp32.
+    """
+    _need(1 <= len(pairs) == len(outs) <= 2, "1 or 2 problems")
+    G, n, d = outs[0].shape
+    nseg = len(pairs[0])
+    _need(all(len(p) == nseg for p in pairs) and 1 <= nseg <= 2, "segments")
+    ks = []
+    a_ops, b_ops = [], []
+    for p in pairs:
+        seg_a, seg_b = [], []
+        for (A, Bm) in p:
+            _bf16(A, "A"); _bf16(Bm, "B")
+            Bk = A.shape[-2]
+            sa = 0 if A.dim() == 2 else Bk * n
+            sb = 0 if Bm.dim() == 2 else Bk * d
+            _need(A.shape[-1] == n and Bm.shape[-1] == d and Bm.shape[-2] == Bk, "segment shapes")
+            seg_a.append(_op(A, n, sa))
+            seg_b.append(_op(Bm, d, sb))
+        if nseg == 1:
+            seg_a.append(seg_a[0]); seg_b.append(seg_b[0])
+        a_ops += seg_a; b_ops += seg_b
+        ks.append(tuple(x.shape[-2] for x, _ in p))
+    _need(len(set(ks)) == 1, "all problems must share K segments")
+    K1 = ks[0][0]
+    K2 = ks[0][1] if nseg == 2 else 0
+    for o in outs:
+        _need(o.dtype == torch.float32 and tuple(o.shape) == (G, n, d) and o.is_contiguous(), "out")
+    _launch(EPI_F32, 0, n, d, K1, K2, G, a_ops, b_ops, list(outs), [alpha] * len(outs), d, n * d)
+
+
+def matmul_nt(a, b, out, alpha=1.0):
+    """out[g] = alpha * a[g] @ b[g]^T; a: [M, K] or [G, M, K]; b: [G, N, K]; out bf16/fp32 [G, M, N]."""
+    G, N, K = b.shape
+    M = a.shape[-2]
+    _bf16(a, "a"); _bf16(b, "b")
+    sa = 0 if a.dim() == 2 else M * K
+    epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
+    _need(tuple(out.shape) == (G, M, N) and out.is_contiguous(), "out shape")
+    _launch(epi, 3, M, N, K, 0, G, [_op(a, K, sa)] * 2, [_op(b, K, N * K)] * 2, [out], [alpha], N, M * N)
+
+
+def matmul_nn(a, b, out, alpha=1.0):
+    """out[g] = alpha * a[g] @ b[g]; a: [G, M, K] bf16, b: [G, K, N] bf16."""
+    G, M, K = a.shape
+    N = b.shape[2]
+    _bf16(a, "a"); _bf16(b, "b")
+    epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
+    _need(tuple(out.shape) == (G, M, N) and out.is_contiguous(), "out shape")
+    _launch(epi, 1, M, N, K, 0, G, [_op(a, K, M * K)] * 2, [_op(b, N, K * N)] * 2, [out], [alpha], N, M * N)
+
+
+def matmul_tn(a, b, out, alpha=1.0):
+    """out[g] = alpha * a[g]^T @ b[g]; a: [G, K, M], b: [G, K, N] bf16 (reduction over rows)."""
+    G, K, M = a.shape
+    N = b.shape[2]
+    _bf16(a, "a"); _bf16(b, "b")
+    epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
+    _need(tuple(out.shape) == (G, M, N) and out.is_contiguous(), "out shape")
+    _launch(epi, 0, M, N, K, 0, G, [_op(a, M, K * M)] * 2, [_op(b, N, K * N)] * 2, [out], [alpha], N, M * N)

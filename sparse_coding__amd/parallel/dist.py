@@ -1,0 +1,82 @@
+"""Process-group bootstrap: one process per GPU, RCCL ("nccl" backend on ROCm) over xGMI.
+
+Reads the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT).  Without it the job is a single process.  CPU-only runs (tests,
+this container) use gloo, so the distributed logic is exercised without a GPU.
+"""
+
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def enabled(self) -> bool:
+        return self.world_size > 1
+
+
+def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistInfo:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available() and backend != "gloo"
+    if use_cuda:
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        be = backend or ("nccl" if use_cuda else "gloo")
+        kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+        return DistInfo(rank, world, local, device, be)
+    if dist.is_initialized():
+        return DistInfo(dist.get_rank(), dist.get_world_size(), local, device, dist.get_backend())
+    return DistInfo(0, 1, 0, device, "none")
+
+
+def barrier(info: DistInfo):
+    if info.enabled:
+        if info.backend == "nccl":
+            dist.barrier(device_ids=[info.local_rank])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(value: float, info: DistInfo) -> float:
+    if not info.enabled:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def broadcast_(t: torch.Tensor, info: DistInfo, src: int = 0):
+    if info.enabled:
+        dist.broadcast(t, src=src)
+    return t
+
+
+def shutdown(info: DistInfo):
+    if info.enabled and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,181 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from sparse_coding__amd.ops import _lib as L
+
+    L.lib()  # must load: no silent fallback on a GPU box
+    yield
+
+
+def _bf(*shape, scale=1.0, gen=None):
+    return (torch.randn(*shape, device=DEV, generator=gen) * scale).to(torch.bfloat16)
+
+
+def _close(a, b, rtol=2e-2, atol=1e-2):
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item()
+    assert err <= atol + rtol * ref, f"max err {err} vs ref scale {ref}"
+
+
+@pytest.mark.parametrize("G,M,N,K", [(1, 128, 128, 64), (3, 256, 384, 192), (2, 512, 256, 512)])
+def test_matmul_layouts(G, M, N, K):
+    from sparse_coding__amd.ops import gemm
+
+    torch.manual_seed(0)
+    a = _bf(G, M, K)
+    b = _bf(G, N, K)
+    out = torch.empty(G, M, N, device=DEV)
+    gemm.matmul_nt(a, b, out)
+    _close(out, a.float() @ b.float().transpose(1, 2), rtol=1e-3, atol=1e-3)
+
+    bn = _bf(G, K, N)
+    gemm.matmul_nn(a, bn, out)
+    _close(out, a.float() @ bn.float(), rtol=1e-3, atol=1e-3)
+
+    at = _bf(G, K, M)
+    gemm.matmul_tn(at, bn, out, alpha=0.5)
+    _close(out, 0.5 * at.float().transpose(1, 2) @ bn.float(), rtol=1e-3, atol=1e-3)
+
+    out16 = torch.empty(G, M, N, device=DEV, dtype=torch.bfloat16)
+    gemm.matmul_nt(a, b, out16)
+    _close(out16, a.float() @ b.float().transpose(1, 2), rtol=1e-2, atol=1e-2)
+
+
+def test_identity_asymmetric():
+    """A = I with an asymmetric B catches a transposed C write."""
+    from sparse_coding__amd.ops import gemm
+
+    M = K = 128
+    N = 256
+    a = torch.eye(M, K, device=DEV).to(torch.bfloat16)[None]
+    b = torch.arange(N * K, device=DEV, dtype=torch.float32).reshape(1, N, K).remainder(97).to(torch.bfloat16)
+    out = torch.empty(1, M, N, device=DEV)
+    gemm.matmul_nt(a, b, out)
+    torch.testing.assert_close(out, b.float().transpose(1, 2)[:, :M, :], rtol=0, atol=0)
+    bt = b.transpose(1, 2).contiguous()  # [1, K, N]
+    gemm.matmul_nn(a, bt, out)
+    torch.testing.assert_close(out, bt.float()[:, :M, :], rtol=0, atol=0)
+    gemm.matmul_tn(a, bt, out)
+    torch.testing.assert_close(out, bt.float()[:, :M, :], rtol=0, atol=0)
+
+
+def test_sae_epilogues():
+    from sparse_coding__amd.ops import gemm
+
+    torch.manual_seed(1)
+    G, B, d, n = 3, 256, 256, 384
+    x = _bf(B, d)
+    we = _bf(G, n, d, scale=0.05)
+    wd = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1).to(torch.bfloat16)
+    bias = torch.randn(G, n, device=DEV) * 0.1
+    nactive = torch.tensor([n, 256, 128], device=DEV, dtype=torch.int32)
+    c = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
+    part = torch.zeros(G, (B // 128) * (n // 128), 2, device=DEV)
+    cnt = torch.zeros(G, B // 128, n, device=DEV)
+    gemm.encode_relu(x, we, bias, c, part, cnt, nactive)
+    ref = torch.relu(x.float() @ we.float().transpose(1, 2) + bias[:, None, :])
+    for g in range(G):
+        ref[g, :, int(nactive[g]):] = 0
+    _close(c, ref)
+    cf = c.float()
+    torch.testing.assert_close(part[..., 0].sum(1), cf.sum((1, 2)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[..., 1].sum(1), (cf > 0).float().sum((1, 2)), rtol=0, atol=0)
+    torch.testing.assert_close(cnt.sum(1), (cf > 0).float().sum(1), rtol=0, atol=0)
+
+    r = torch.empty(G, B, d, device=DEV, dtype=torch.bfloat16)
+    dpart = torch.zeros(G, (B // 128) * (d // 128), device=DEV)
+    gemm.decode_residual(c, wd, x, r, dpart)
+    rref = cf @ wd.float() - x.float()
+    _close(r, rref)
+    torch.testing.assert_close(dpart.sum(1), (rref ** 2).sum((1, 2)), rtol=2e-2, atol=1e-1)
+
+    l1 = torch.tensor([1e-3, 3e-3, 1e-2], device=DEV)
+    dpre = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
+    colpart = torch.zeros(G, B // 128, n, device=DEV)
+    gemm.code_grad(r, wd, c, l1, dpre, colpart)
+    dref = (r.float() @ wd.float().transpose(1, 2) + (l1 * d / 2)[:, None, None]) * (cf > 0)
+    _close(dpre, dref)
+    torch.testing.assert_close(colpart.sum(1), dpre.float().sum(1), rtol=1e-3, atol=1e-2)
+
+    gd = torch.empty(G, n, d, device=DEV)
+    ge = torch.empty(G, n, d, device=DEV)
+    alpha = 2.0 / (B * d)
+    gemm.weight_grads([[(c, r)], [(dpre, x)]], [gd, ge], alpha)
+    _close(gd, alpha * cf.transpose(1, 2) @ r.float(), rtol=1e-3, atol=1e-6)
+    _close(ge, alpha * dpre.float().transpose(1, 2) @ x.float(), rtol=1e-3, atol=1e-6)
+    gt = torch.empty(G, n, d, device=DEV)
+    gemm.weight_grads([[(c, r), (dpre, x)]], [gt], alpha)
+    _close(gt, gd + ge, rtol=1e-3, atol=1e-6)
+
+
+def test_adam_rows_matches_autograd():
+    from sparse_coding__amd.ops import adam as adam_ops
+
+    torch.manual_seed(2)
+    G, n, d = 2, 128, 512
+    p = torch.randn(G, n, d, device=DEV)
+    p[0, 3] = 0.0  # exercise the 1e-8 clamp branch
+    g_hat = torch.randn(G, n, d, device=DEV) * 1e-3
+    m = torch.randn(G, n, d, device=DEV).abs() * 1e-4
+    v = torch.randn(G, n, d, device=DEV).abs() * 1e-6
+    lr = torch.tensor([1e-3, 2e-3], device=DEV)
+    step = 5
+    # reference: gradient through p / clamp(|p|, 1e-8) via autograd
+    pr = p.clone().requires_grad_()
+    w_hat = pr / torch.clamp(pr.norm(dim=-1, keepdim=True), min=1e-8)
+    (w_hat * g_hat).sum().backward()
+    g = pr.grad
+    b1, b2, eps = 0.9, 0.999, 1e-8
+    m_ref = b1 * m + (1 - b1) * g
+    v_ref = b2 * v + (1 - b2) * g * g
+    p_ref = p - lr[:, None, None] * (m_ref / (1 - b1 ** step)) / (torch.sqrt(v_ref / (1 - b2 ** step)) + eps)
+    shadow = torch.empty(G, n, d, device=DEV, dtype=torch.bfloat16)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    adam_ops.adam_rows([dict(p=p2, g=g_hat, m=m2, v=v2, shadow=shadow, norm=True)], lr, step, b1, b2, eps)
+    torch.testing.assert_close(m2, m_ref, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(v2, v_ref, rtol=1e-4, atol=1e-12)
+    torch.testing.assert_close(p2, p_ref, rtol=1e-4, atol=1e-6)
+    sh_ref = p_ref / torch.clamp(p_ref.norm(dim=-1, keepdim=True), min=1e-8)
+    _close(shadow, sh_ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("kind", ["untied", "tied"])
+def test_fused_step_matches_functional_ensemble(kind):
+    from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.engine.optim import adam
+    from sparse_coding__amd.models.signatures import FunctionalSAE, FunctionalTiedSAE
+
+    torch.manual_seed(3)
+    sig = FunctionalSAE if kind == "untied" else FunctionalTiedSAE
+    d, n, B, G = 256, 512, 256, 3
+    l1s = [1e-4, 1e-3, 1e-2]
+    models = [sig.init(d, n, l1, device=DEV) for l1 in l1s]
+    ref = FunctionalEnsemble([({k: v.clone() for k, v in p.items()}, b) for p, b in models], sig, adam,
+                             {"lr": 1e-3}, device=DEV)
+    fused = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=DEV)
+    feats = torch.nn.functional.normalize(torch.randn(1024, d, device=DEV), dim=-1)
+    for step in range(5):
+        codes = torch.relu(torch.randn(B, 1024, device=DEV) - 2.0)
+        x = (codes @ feats).to(torch.bfloat16)
+        loss_ref, _ = ref.step_batch(x.float())
+        out = fused.step_batch(x)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(out[:, 0], loss_ref["loss"], rtol=3e-2, atol=1e-4)
+        torch.testing.assert_close(out[:, 1], loss_ref["l_reconstruction"], rtol=3e-2, atol=1e-4)
+        torch.testing.assert_close(out[:, 2], loss_ref["l_l1"], rtol=3e-2, atol=1e-5)
+    for k, v in fused.params.items():
+        diff = (v - ref.params[k]).abs().max().item()
+        # 5 Adam steps of lr 1e-3 move params by <= 5e-3; bf16 GEMMs may flip a few signs
+        assert diff < 2.5e-3, (k, diff)
