@@ -48,6 +48,7 @@ def parse(argv=None):
     ap.add_argument("--eval-rows", type=int, default=16384)
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of a HIP graph")
     return ap.parse_args(argv)
 
 
@@ -95,10 +96,17 @@ def main(argv=None):
 
         eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
         trainer = DataParallelFused(eng, info, torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
-        xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
+        if info.world_size == 1 and not args.no_graph:
+            eng.enable_graph()  # whole step = one HIP graph replay
 
-        def step():
-            trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf))
+            def step():
+                ring.sample_shard(B, 0, 1, out=eng.x_static)
+                eng.step_static()
+        else:
+            xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
+
+            def step():
+                trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf))
 
         def dicts():
             return eng.to_learned_dicts(device)

@@ -63,7 +63,10 @@ class FusedSAEEnsemble:
         dev = self.device
         self.models_meta = [{k: v for k, v in m[1].items()} for m in models]
         self.betas, self.eps = betas, eps
-        self.step_count = 0
+        self.step_count = 0  # host mirror of the device counter below
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # completed Adam steps
+        self.use_graph = False
+        self._graph = None
 
         # ----- parameters (fp32 masters) and Adam state
         self.params: Dict[str, torch.Tensor] = {"encoder": _stack(models, "encoder", 0, dev),
@@ -112,7 +115,8 @@ class FusedSAEEnsemble:
         self.cnt_part = torch.zeros(G, tm, n, device=dev) if track_feature_counts else None
         self.feature_counts = torch.zeros(G, n, device=dev) if track_feature_counts else None
         self.rows_seen = 0
-        self.out = torch.zeros(G, 5, device=dev)
+        self.out = torch.zeros(G, 6, device=dev)
+        self.x_static = torch.zeros(B, d, device=dev, dtype=bf)  # graph input buffer
 
     # ------------------------------------------------------------------ helpers
     def refresh_shadows(self):
@@ -180,20 +184,31 @@ class FusedSAEEnsemble:
                      shadow=self.enc_shadow, norm=True)]
 
     def adam_first(self):
-        self.step_count += 1
-        adam_ops.adam_rows(self._adam_sets()[:1], self.lr, self.step_count, *self.betas, self.eps)
+        adam_ops.adam_rows(self._adam_sets()[:1], self.lr, self.step_count + 1, *self.betas, self.eps,
+                           step_dev=self.step_dev)
 
     def adam_second(self, reduced_bias=True):
-        """Encoder Adam (untied) and bias Adam + loss reduction."""
+        """Encoder Adam (untied) and bias Adam + loss reduction (advances the step counter)."""
         if self.kind == "untied":
-            adam_ops.adam_rows(self._adam_sets()[1:], self.lr, self.step_count, *self.betas, self.eps)
+            adam_ops.adam_rows(self._adam_sets()[1:], self.lr, self.step_count + 1, *self.betas, self.eps,
+                               step_dev=self.step_dev)
         self._bias_loss(update=True, reduced=reduced_bias)
+        self._host_step()
 
     def apply_update(self):
         """Kernels 5-6: fused Adam on the weights, then bias Adam + loss reduction."""
-        self.step_count += 1
-        adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count, *self.betas, self.eps)
+        self._apply_update_kernels()
+        self._host_step()
+
+    def _apply_update_kernels(self):
+        adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
+                           step_dev=self.step_dev)
         self._bias_loss(update=True, reduced=False)
+
+    def _host_step(self):
+        self.step_count += 1
+        if self.track_feature_counts:
+            self.rows_seen += self.batch_size
 
     def _bias_loss(self, update, reduced):
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
@@ -205,17 +220,47 @@ class FusedSAEEnsemble:
         adam_ops.bias_loss(self.params["encoder_bias"], self.m["encoder_bias"], self.v["encoder_bias"],
                            colpart, tm, self.enc_part, self.enc_part.shape[1], self.dec_part,
                            self.dec_part.shape[1], self.l1, self.bias_decay, self.lr, self.out, B, d,
-                           self.step_count, gscale=gscale, cnt_part=self.cnt_part,
-                           feat_count=self.feature_counts, b1=b1, b2=b2, eps=self.eps, update=update)
-        if self.track_feature_counts:
-            self.rows_seen += B
+                           self.step_count + 1, gscale=gscale, cnt_part=self.cnt_part,
+                           feat_count=self.feature_counts, b1=b1, b2=b2, eps=self.eps, update=update,
+                           step_dev=self.step_dev)
 
     def step_batch(self, batch, expand_dims=True):
-        """One Adam step of every model on ``batch [B, d]``; returns a device tensor [G, 5]:
-        (loss, l_reconstruction, l_l1, l_bias_decay, mean L0).  Never synchronises."""
+        """One Adam step of every model on ``batch [B, d]``; returns a device tensor [G, 6]:
+        (loss, l_reconstruction, l_l1, l_bias_decay, mean L0, |b|).  Never synchronises."""
+        if self.use_graph:
+            if batch is not self.x_static:
+                self.x_static.copy_(batch, non_blocking=True)
+            return self.step_static()
         x = self._x_bf16(batch)
         self.forward_backward(x)
         self.apply_update()
+        return self.out
+
+    # ------------------------------------------------------------------ HIP graph
+    def enable_graph(self, enabled: bool = True):
+        """Capture the whole step (7 kernels) into one HIP graph; inputs go through
+        ``x_static``.  Removes the per-launch host overhead (the step is launch-bound
+        at small batch)."""
+        self.use_graph = enabled
+        if not enabled:
+            self._graph = None
+        return self
+
+    def _capture(self):
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.forward_backward(self.x_static)
+            self._apply_update_kernels()
+        self._graph = g
+
+    def step_static(self):
+        """Replay the captured step on whatever is in ``x_static`` (fill it first, e.g. with
+        ``torch.index_select(..., out=engine.x_static)``)."""
+        if self._graph is None:
+            self._capture()
+        self._graph.replay()
+        self._host_step()
         return self.out
 
     def loss_dicts(self, out=None):
@@ -249,6 +294,7 @@ class FusedSAEEnsemble:
             self.v[k].copy_(sd["v"][k])
         self.lr.copy_(sd["lr"]); self.l1.copy_(sd["l1"]); self.bias_decay.copy_(sd["bias_decay"])
         self.step_count = int(sd["step"])
+        self.step_dev.fill_(self.step_count)
         if sd.get("feature_counts") is not None and self.feature_counts is not None:
             self.feature_counts.copy_(sd["feature_counts"])
         self.rows_seen = int(sd.get("rows_seen", 0))

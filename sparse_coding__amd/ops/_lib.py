@@ -37,16 +37,16 @@ def _declare(lib):
         "sc_gemm": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                     C.POINTER(ScOperand), C.POINTER(ScOperand), C.POINTER(c_void_p), c_float_p,
                     c_long, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long,
-                    c_void_p, c_void_p, c_void_p, c_float, c_void_p],
+                    c_void_p, c_void_p, c_void_p, c_float, c_int, c_void_p],
         "sc_adam_rows": [c_int, C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
                          C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
                          C.POINTER(c_int), C.POINTER(c_int), c_int, c_int, c_void_p,
-                         c_float, c_float, c_float, c_float, c_float, c_void_p],
+                         c_float, c_float, c_float, c_float, c_float, c_void_p, c_void_p],
         "sc_shadow_rows": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p],
         "sc_bias_loss": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                          c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
-                         c_float, c_float, c_int, c_void_p],
+                         c_float, c_float, c_int, c_void_p, c_void_p],
     }
     optional = {
         "sc_topk_encode": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,

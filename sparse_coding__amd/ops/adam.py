@@ -13,12 +13,14 @@ def _vp(seq):
     return (C.c_void_p * len(seq))(*[_lib.ptr(t) for t in seq])
 
 
-def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None):
+def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, step_dev=None):
     """Fused row-wise Adam over one or two parameter sets.
 
     sets: list of dicts with keys p, g, m, v (fp32 [G, n, d]), shadow (bf16 [G, n, d] or None),
     norms (fp32 [G, n] or None), norm (bool: parameter is row-normalised inside the loss).
-    lr: fp32 tensor [G] (per-model learning rate); step: 1-based Adam step.
+    lr: fp32 tensor [G] (per-model learning rate); step: 1-based Adam step (host value), or
+    ``step_dev``: int32 device counter of completed steps (the kernel uses ``*step_dev + 1``;
+    graph-capturable).
     """
     if not 1 <= len(sets) <= 2:
         raise ValueError("1 or 2 parameter sets")
@@ -39,7 +41,7 @@ def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None):
         _vp([s["m"] for s in sets]), _vp([s["v"] for s in sets]),
         _vp([s.get("shadow") for s in sets]), _vp([s.get("norms") for s in sets]),
         rows, norm, d, rows_per_model or n, _lib.ptr(lr), b1, b2, eps, bc1, bc2,
-        _lib.stream_handle(),
+        _lib.ptr(step_dev), _lib.stream_handle(),
     )
     _lib.check(rc, "sc_adam_rows")
 
@@ -57,7 +59,7 @@ def shadow_rows(p, shadow, norms=None, normalize=True):
 
 def bias_loss(b, m, v, colpart, tm, enc_part, enc_tiles, dec_part, dec_tiles, l1, bias_decay, lr,
               out, B, d, step, gscale, cnt_part=None, feat_count=None, b1=0.9, b2=0.999, eps=1e-8,
-              update=True):
+              update=True, step_dev=None):
     """Loss bookkeeping + bias Adam.  ``colpart`` [G, tm, n] holds partial sums of the bias
     gradient; ``gscale`` converts their sum to dL/db."""
     G, n = b.shape
@@ -67,6 +69,6 @@ def bias_loss(b, m, v, colpart, tm, enc_part, enc_tiles, dec_part, dec_tiles, l1
         G, _lib.ptr(b), _lib.ptr(m), _lib.ptr(v), _lib.ptr(colpart), tm, _lib.ptr(enc_part),
         enc_tiles, _lib.ptr(dec_part), dec_tiles, _lib.ptr(cnt_part), _lib.ptr(feat_count),
         _lib.ptr(l1), _lib.ptr(bias_decay), _lib.ptr(lr), _lib.ptr(out), n, B, d, float(gscale), b1, b2, eps,
-        bc1, bc2, int(update), _lib.stream_handle(),
+        bc1, bc2, int(update), _lib.ptr(step_dev), _lib.stream_handle(),
     )
     _lib.check(rc, "sc_bias_loss")

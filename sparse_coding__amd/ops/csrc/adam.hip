@@ -33,7 +33,15 @@ struct AdamArgs {
   int rows_per_model;
   const float* lr;  // per model
   float b1, b2, eps, bc1, bc2;
+  const int* step;  // optional device step counter (graph-capturable); t = *step + 1
 };
+
+// Adam bias corrections for 1-based step t, computed on the device so a captured
+// HIP graph replays correctly step after step.
+__device__ __forceinline__ void bias_corrections(float b1, float b2, int t, float& bc1, float& bc2) {
+  bc1 = 1.f - __powf(b1, (float)t);
+  bc2 = 1.f - __powf(b2, (float)t);
+}
 
 template <int NV>
 __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
@@ -79,7 +87,9 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
     }
   }
   const float b1 = a.b1, b2 = a.b2, omb1 = 1.f - b1, omb2 = 1.f - b2;
-  const float step = lr / a.bc1, rbc2 = 1.f / a.bc2;
+  float bc1 = a.bc1, bc2 = a.bc2;
+  if (a.step) bias_corrections(b1, b2, *a.step + 1, bc1, bc2);
+  const float step = lr / bc1, rbc2 = 1.f / bc2;
   float ss2 = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -167,18 +177,21 @@ struct BiasArgs {
   const float* l1;                 // [G]
   const float* bias_decay;         // [G]
   const float* lr;                 // [G]
-  float* out;                      // [G][5]: loss, l_rec, l_l1, l_bias_decay, mean L0
+  float* out;                      // [G][6]: loss, l_rec, l_l1, l_bias_decay, mean L0, |b|
   int n, B, d;
   float gscale;                    // converts colpart sums to dL/db (2/(B d) for raw dpre_s)
   float b1, b2, eps, bc1, bc2;
   int update;                      // 0: only losses (eval)
+  int* step;                       // optional device step counter, advanced by loss_reduce
 };
 
-__global__ __launch_bounds__(256) void bias_loss_kernel(BiasArgs a) {
+// Phase 1 (one block per model): reduce the GEMM-epilogue partials to the
+// reference's loss terms and record |b| (pre-update) for the bias-decay term.
+__global__ __launch_bounds__(256) void loss_reduce_kernel(BiasArgs a) {
   __shared__ float red[8];
   const int g = blockIdx.x, tid = threadIdx.x;
   const int n = a.n;
-  float* b = a.b + (long)g * n;
+  const float* b = a.b + (long)g * n;
   float bs = 0.f;
   for (int j = tid; j < n; j += 256) bs += b[j] * b[j];
   bs = block_sum_256(bs, red);
@@ -191,41 +204,51 @@ __global__ __launch_bounds__(256) void bias_loss_kernel(BiasArgs a) {
   l1 = block_sum_256(l1, red);
   l0 = block_sum_256(l0, red);
   se = block_sum_256(se, red);
-  const float bnorm = sqrtf(bs);
-  const float lam = a.l1[g], beta = a.bias_decay[g];
   if (tid == 0) {
+    const float bnorm = sqrtf(bs);
     const float l_rec = se / ((float)a.B * a.d);
-    const float l_l1 = lam * l1 / a.B;
-    const float l_bd = beta * bnorm;
-    float* o = a.out + g * 5;
+    const float l_l1 = a.l1[g] * l1 / a.B;
+    const float l_bd = a.bias_decay[g] * bnorm;
+    float* o = a.out + g * 6;
     o[0] = l_rec + l_l1 + l_bd;
     o[1] = l_rec;
     o[2] = l_l1;
     o[3] = l_bd;
     o[4] = l0 / a.B;
+    o[5] = bnorm;
+    // the step counter advances once per optimizer step; bias_adam (next launch) reads the new value
+    if (g == 0 && a.update && a.step) *a.step += 1;
   }
+}
+
+// Phase 2 (grid: n/256 x G): bias gradient from the per-row-tile column partials,
+// bias-decay term, Adam on the bias; optional feature on-count accumulation.
+__global__ __launch_bounds__(256) void bias_adam_kernel(BiasArgs a) {
+  const int g = blockIdx.y;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int n = a.n;
+  if (j >= n) return;
   if (a.cnt_part && a.feat_count) {
-    for (int j = tid; j < n; j += 256) {
-      float c = 0.f;
-      for (int t = 0; t < a.tm; ++t) c += a.cnt_part[((long)g * a.tm + t) * n + j];
-      a.feat_count[(long)g * n + j] += c;
-    }
+    float c = 0.f;
+    for (int t = 0; t < a.tm; ++t) c += a.cnt_part[((long)g * a.tm + t) * n + j];
+    a.feat_count[(long)g * n + j] += c;
   }
   if (!a.update) return;
-  const float lr = a.lr[g];
-  const float step = lr / a.bc1, rbc2 = 1.f / a.bc2;
+  const float bnorm = a.out[g * 6 + 5];
+  const float beta = a.bias_decay[g];
   const float bd = (beta != 0.f && bnorm > 0.f) ? beta / bnorm : 0.f;
-  for (int j = tid; j < n; j += 256) {
-    float gsum = 0.f;
-    for (int t = 0; t < a.tm; ++t) gsum += a.colpart[((long)g * a.tm + t) * n + j];
-    const float gj = gsum * a.gscale + bd * b[j];
-    float mj = a.m[(long)g * n + j], vj = a.v[(long)g * n + j];
-    mj = a.b1 * mj + (1.f - a.b1) * gj;
-    vj = a.b2 * vj + (1.f - a.b2) * gj * gj;
-    a.m[(long)g * n + j] = mj;
-    a.v[(long)g * n + j] = vj;
-    b[j] -= step * mj / (sqrtf(vj * rbc2) + a.eps);
-  }
+  float gsum = 0.f;
+  for (int t = 0; t < a.tm; ++t) gsum += a.colpart[((long)g * a.tm + t) * n + j];
+  float bc1 = a.bc1, bc2 = a.bc2;
+  if (a.step) bias_corrections(a.b1, a.b2, *a.step, bc1, bc2);
+  const long idx = (long)g * n + j;
+  const float bj = a.b[idx];
+  const float gj = gsum * a.gscale + bd * bj;
+  const float mj = a.b1 * a.m[idx] + (1.f - a.b1) * gj;
+  const float vj = a.b2 * a.v[idx] + (1.f - a.b2) * gj * gj;
+  a.m[idx] = mj;
+  a.v[idx] = vj;
+  a.b[idx] = bj - (a.lr[g] / bc1) * mj / (sqrtf(vj / bc2) + a.eps);
 }
 
 }  // namespace scamd
@@ -237,7 +260,7 @@ extern "C" {
 int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const* m, float* const* v,
                  void* const* shadow, float* const* norms, const int* rows, const int* norm, int d,
                  int rows_per_model, const float* lr, float b1, float b2, float eps, float bc1,
-                 float bc2, hipStream_t stream) {
+                 float bc2, const int* step, hipStream_t stream) {
   if (d % 256 || d > 4096 || nset < 1 || nset > 2) return 1;
   AdamArgs a;
   long total = 0;
@@ -247,7 +270,7 @@ int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const*
   }
   if (nset == 1) a.set[1] = a.set[0], a.set[1].rows = 0;
   a.nset = nset; a.d = d; a.rows_per_model = rows_per_model; a.lr = lr;
-  a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2;
+  a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.step = step;
   const long blocks = (total + 3) / 4;
   switch (d / 256) {
     case 1: hipLaunchKernelGGL(adam_rows_kernel<1>, dim3(blocks), dim3(256), 0, stream, a); break;
@@ -274,15 +297,17 @@ int sc_bias_loss(int G, float* b, float* m, float* v, const float* colpart, int 
                  const float* enc_part, int enc_tiles, const float* dec_part, int dec_tiles,
                  const float* cnt_part, float* feat_count, const float* l1, const float* bias_decay,
                  const float* lr, float* out, int n, int B, int d, float gscale, float b1, float b2, float eps,
-                 float bc1, float bc2, int update, hipStream_t stream) {
+                 float bc1, float bc2, int update, int* step, hipStream_t stream) {
   BiasArgs a;
   a.b = b; a.m = m; a.v = v; a.colpart = colpart; a.tm = tm;
   a.enc_part = enc_part; a.enc_tiles = enc_tiles; a.dec_part = dec_part; a.dec_tiles = dec_tiles;
   a.cnt_part = cnt_part; a.feat_count = feat_count;
   a.l1 = l1; a.bias_decay = bias_decay; a.lr = lr; a.out = out;
   a.n = n; a.B = B; a.d = d; a.gscale = gscale;
-  a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.update = update;
-  hipLaunchKernelGGL(bias_loss_kernel, dim3(G), dim3(256), 0, stream, a);
+  a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.update = update; a.step = step;
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(G), dim3(256), 0, stream, a);
+  if (update || (cnt_part && feat_count))
+    hipLaunchKernelGGL(bias_adam_kernel, dim3((n + 255) / 256, G), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -11,6 +11,7 @@ n = dictionary size.  bf16 tensors are passed as torch.bfloat16.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -18,6 +19,17 @@ from . import _lib
 
 EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16 = 0, 1, 2, 3, 4
 TILE_M, TILE_N, TILE_K = 128, 128, 64
+
+# Pipeline configurations of the kernel (K-tile depth x LDS-DMA ring stages):
+#   0: BK64 x 2 stages (64 KiB LDS)   1: BK32 x 3 stages (48 KiB)   2: BK32 x 4 stages (64 KiB)
+# Per-epilogue defaults come from measurements on MI355X (profiles/); override with
+# SC_GEMM_CFG=<n> for all GEMMs.
+_CFG_DEFAULT = {EPI_ENC: 0, EPI_DEC: 0, EPI_DC: 0, EPI_F32: 0, EPI_BF16: 0}
+_CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
+
+
+def set_config(epi: int, cfg: int):
+    _CFG_DEFAULT[epi] = int(cfg)
 
 
 def _op(t, ld, sg):
@@ -37,7 +49,7 @@ def _bf16(t, name):
 
 def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *,
             bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
-            colpart=None, l1=None, l1_add_scale=0.0):
+            colpart=None, l1=None, l1_add_scale=0.0, cfg=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     nprob = len(outs)
@@ -49,6 +61,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
         epi, layout, nprob, M, N, K1, K2, G, A, Bo, Cp, al, ldc, sc,
         _lib.ptr(bias), sbias, _lib.ptr(nactive), _lib.ptr(aux), ldaux, saux,
         _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1), float(l1_add_scale),
+        int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi])),
         _lib.stream_handle(),
     )
     _lib.check(rc, f"sc_gemm(epi={epi})")

