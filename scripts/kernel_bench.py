@@ -50,10 +50,19 @@ def main():
     res["enc"] = (timeit(lambda: gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c, e.enc_part,
                                                   e.cnt_part, None)), fl)
     res["dec"] = (timeit(lambda: gemm.decode_residual(e.c, e.dec_shadow, x, e.r, e.dec_part)), fl)
-    res["dc"] = (timeit(lambda: gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart)), fl)
+    res["dc"] = (timeit(lambda: gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart, dotpart=e.dotpart)), fl)
     res["wgrad2"] = (timeit(lambda: gemm.weight_grads([[(e.c, e.r)], [(e.dpre, x)]], [e.g_dec, e.g_enc],
                                                       1e-6)), 2 * fl)
-    for cfg in (0, 1, 2):
+    res["enc_nocount"] = (timeit(lambda: gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c,
+                                                          e.enc_part, None, None)), fl)
+    res["enc_plain_bf16"] = (timeit(lambda: gemm.matmul_nt(x, e.enc_shadow, e.c)), fl)
+    res["dc_nodot"] = (timeit(lambda: gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart)), fl)
+    res["wgrad_adam"] = (timeit(lambda: e.wgrad_adam(x)), 2 * fl)
+    e.fuse_adam = False
+    e.overlap_adam = False
+    res["step_no_overlap"] = (timeit(lambda: e.step_batch(x)), 5 * fl)
+    e.overlap_adam = True
+    for cfg in ():
         for epi in range(5):
             gemm.set_config(epi, cfg)
         res[f"enc_cfg{cfg}"] = (timeit(lambda: gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c,

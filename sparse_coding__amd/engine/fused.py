@@ -39,7 +39,8 @@ class FusedSAEEnsemble:
     """Fused HIP training engine; API mirrors ``FunctionalEnsemble``."""
 
     def __init__(self, models, sig, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999),
-                 eps=1e-8, track_feature_counts=True, kind: Optional[str] = None):
+                 eps=1e-8, track_feature_counts=True, kind: Optional[str] = None, fuse_adam: bool = False,
+                 count_every: int = 8):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
         if self.kind not in ("untied", "tied"):
@@ -67,6 +68,7 @@ class FusedSAEEnsemble:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # completed Adam steps
         self.use_graph = False
         self._graph = None
+        self._counted = False
 
         # ----- parameters (fp32 masters) and Adam state
         self.params: Dict[str, torch.Tensor] = {"encoder": _stack(models, "encoder", 0, dev),
@@ -89,6 +91,7 @@ class FusedSAEEnsemble:
         bf = torch.bfloat16
         self.enc_shadow = torch.empty(G, n, d, device=dev, dtype=bf)
         self.dec_shadow = torch.empty(G, n, d, device=dev, dtype=bf) if self.kind == "untied" else self.enc_shadow
+        self.norms = torch.ones(G, n, device=dev)  # row norms of the normalised dictionary
         self.refresh_shadows()
 
         # ----- workspaces
@@ -112,10 +115,24 @@ class FusedSAEEnsemble:
         self.dec_part = torch.zeros(G, tm * (d // 128), device=dev)
         self.colpart = torch.zeros(G, tm, n, device=dev)
         self.track_feature_counts = track_feature_counts
+        # per-feature activation counts are sampled every `count_every` steps (the column
+        # reduction costs ~15% of the encoder GEMM); `rows_seen` counts only sampled rows
+        self.count_every = max(1, int(count_every))
         self.cnt_part = torch.zeros(G, tm, n, device=dev) if track_feature_counts else None
         self.feature_counts = torch.zeros(G, n, device=dev) if track_feature_counts else None
         self.rows_seen = 0
         self.out = torch.zeros(G, 6, device=dev)
+        # Optional: Adam fused into the weight-gradient GEMM (the fp32 gradients never reach
+        # HBM).  Off by default: on MI355X the epilogue's p/m/v traffic does not overlap the
+        # MFMA phase and the separate streaming Adam kernel is faster (profiles/).  Data
+        # parallel runs always use the separate kernel (gradients are all-reduced first).
+        self.fuse_adam = fuse_adam
+        # Side-stream overlap of the decoder Adam with the encoder wgrad: measured slower on
+        # MI355X (the streaming Adam crowds the GEMM's CUs), kept as an option.
+        self.overlap_adam = False
+        self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        self.dotpart = torch.zeros(G, tm, n, device=dev)        # norm-Jacobian row-dot partials
+        self.sqpart = torch.zeros(G, n, d // 128, device=dev)   # updated-row |w|^2 partials
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)  # graph input buffer
 
     # ------------------------------------------------------------------ helpers
@@ -123,9 +140,9 @@ class FusedSAEEnsemble:
         """Rebuild the bf16 shadows from the fp32 masters (after any out-of-band edit)."""
         if self.kind == "untied":
             adam_ops.shadow_rows(self.params["encoder"], self.enc_shadow, normalize=False)
-            adam_ops.shadow_rows(self.params["decoder"], self.dec_shadow, normalize=True)
+            adam_ops.shadow_rows(self.params["decoder"], self.dec_shadow, self.norms, normalize=True)
         else:
-            adam_ops.shadow_rows(self.params["encoder"], self.enc_shadow, normalize=True)
+            adam_ops.shadow_rows(self.params["encoder"], self.enc_shadow, self.norms, normalize=True)
 
     def _x_bf16(self, batch):
         if batch.dtype != torch.bfloat16:
@@ -135,14 +152,39 @@ class FusedSAEEnsemble:
         return batch.contiguous()
 
     # ------------------------------------------------------------------ forward/backward
-    def forward(self, x):
+    def _counting(self):
+        return self.track_feature_counts and (self.step_count % self.count_every == 0)
+
+    def forward(self, x, count=None):
         """Kernels 1-3: codes (+L1/L0), residual (+MSE), code gradient (+bias-grad partials)."""
         if x.shape[0] != self.batch_size:
             raise ValueError(f"batch has {x.shape[0]} rows, engine was built for {self.batch_size}")
+        count = self._counting() if count is None else count
+        self._counted = count
         gemm_ops.encode_relu(x, self.enc_shadow, self.params["encoder_bias"], self.c, self.enc_part,
-                             self.cnt_part, self.nactive)
+                             self.cnt_part if count else None, self.nactive)
         gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
-        gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart)
+        gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
+                           dotpart=self.dotpart if self.fuse_adam else None,
+                           tied_bias=self.params["encoder_bias"] if (self.fuse_adam and self.kind == "tied") else None)
+
+    def wgrad_adam(self, x):
+        """Weight gradients with Adam in the GEMM epilogue, then the decoder-row normalisation."""
+        B = self.batch_size
+        norm_state = dict(norm=True, dotpart=self.dotpart, norms=self.norms, sqpart=self.sqpart)
+        if self.kind == "untied":
+            states = [dict(p=self.params["decoder"], m=self.m["decoder"], v=self.v["decoder"],
+                           shadow=self.dec_shadow, **norm_state),
+                      dict(p=self.params["encoder"], m=self.m["encoder"], v=self.v["encoder"],
+                           shadow=self.enc_shadow, norm=False)]
+            pairs = [[(self.c, self.r)], [(self.dpre, x)]]
+        else:
+            states = [dict(p=self.params["encoder"], m=self.m["encoder"], v=self.v["encoder"],
+                           shadow=self.enc_shadow, **norm_state)]
+            pairs = [[(self.c, self.r), (self.dpre, x)]]
+        gemm_ops.weight_grads_adam(pairs, states, self._alpha, self.lr, self.step_dev, self.betas, self.eps,
+                                   dot_tm=B // 128)
+        adam_ops.normalize_rows(self.dec_shadow, self.sqpart, self.norms)
 
     @property
     def _alpha(self):
@@ -156,19 +198,27 @@ class FusedSAEEnsemble:
             gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], [self.g_dec], self._alpha)
             self._reduce_bias_grad()
 
-    def wgrad_second(self, x):
+    def wgrad_second(self, x, reduce_bias=True):
         """Untied: dW_e = dpre^T x (encoder) + bias grad.  Tied: nothing."""
         if self.kind == "untied":
             gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha)
-            self._reduce_bias_grad()
+            if reduce_bias:
+                self._reduce_bias_grad()
 
     def _reduce_bias_grad(self):
         torch.sum(self.colpart, dim=1, keepdim=True, out=self.g_bias)
         self.g_bias.mul_(self._alpha)
 
     def forward_backward(self, x):
-        """Kernels 1-4 for the single-device step (both weight gradients in one launch)."""
+        """Kernels 1-4 for the single-device step (both weight gradients in one launch).
+        With ``fuse_adam`` the weight gradients are consumed by Adam inside the GEMM."""
         self.forward(x)
+        self.backward_weights(x)
+
+    def backward_weights(self, x):
+        if self.fuse_adam:
+            self.wgrad_adam(x)
+            return
         if self.kind == "untied":
             gemm_ops.weight_grads([[(self.c, self.r)], [(self.dpre, x)]], [self.g_dec, self.g_enc], self._alpha)
         else:
@@ -177,11 +227,11 @@ class FusedSAEEnsemble:
     def _adam_sets(self):
         if self.kind == "untied":
             return [dict(p=self.params["decoder"], g=self.g_dec, m=self.m["decoder"], v=self.v["decoder"],
-                         shadow=self.dec_shadow, norm=True),
+                         shadow=self.dec_shadow, norms=self.norms, norm=True),
                     dict(p=self.params["encoder"], g=self.g_enc, m=self.m["encoder"], v=self.v["encoder"],
                          shadow=self.enc_shadow, norm=False)]
         return [dict(p=self.params["encoder"], g=self.g_dec, m=self.m["encoder"], v=self.v["encoder"],
-                     shadow=self.enc_shadow, norm=True)]
+                     shadow=self.enc_shadow, norms=self.norms, norm=True)]
 
     def adam_first(self):
         adam_ops.adam_rows(self._adam_sets()[:1], self.lr, self.step_count + 1, *self.betas, self.eps,
@@ -201,14 +251,15 @@ class FusedSAEEnsemble:
         self._host_step()
 
     def _apply_update_kernels(self):
-        adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
-                           step_dev=self.step_dev)
+        if not self.fuse_adam:  # with fuse_adam the weights were already updated in wgrad_adam
+            adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
+                               step_dev=self.step_dev)
         self._bias_loss(update=True, reduced=False)
 
     def _host_step(self):
-        self.step_count += 1
-        if self.track_feature_counts:
+        if self._counted:
             self.rows_seen += self.batch_size
+        self.step_count += 1
 
     def _bias_loss(self, update, reduced):
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
@@ -220,8 +271,10 @@ class FusedSAEEnsemble:
         adam_ops.bias_loss(self.params["encoder_bias"], self.m["encoder_bias"], self.v["encoder_bias"],
                            colpart, tm, self.enc_part, self.enc_part.shape[1], self.dec_part,
                            self.dec_part.shape[1], self.l1, self.bias_decay, self.lr, self.out, B, d,
-                           self.step_count + 1, gscale=gscale, cnt_part=self.cnt_part,
-                           feat_count=self.feature_counts, b1=b1, b2=b2, eps=self.eps, update=update,
+                           self.step_count + 1, gscale=gscale,
+                           cnt_part=self.cnt_part if self._counted else None,
+                           feat_count=self.feature_counts if self._counted else None,
+                           b1=b1, b2=b2, eps=self.eps, update=update,
                            step_dev=self.step_dev)
 
     def step_batch(self, batch, expand_dims=True):
@@ -232,8 +285,8 @@ class FusedSAEEnsemble:
                 self.x_static.copy_(batch, non_blocking=True)
             return self.step_static()
         x = self._x_bf16(batch)
-        self.forward_backward(x)
-        self.apply_update()
+        self._step_kernels(x)
+        self._host_step()
         return self.out
 
     # ------------------------------------------------------------------ HIP graph
@@ -246,20 +299,45 @@ class FusedSAEEnsemble:
             self._graph = None
         return self
 
+    def _step_kernels(self, x, count=None):
+        """All kernels of one step.  Optionally (``overlap_adam``) untied models overlap the
+        memory-bound decoder Adam (side stream) with the compute-bound encoder wgrad GEMM."""
+        if self.kind == "untied" and self.overlap_adam and not self.fuse_adam:
+            main = torch.cuda.current_stream(self.device)
+            sets = self._adam_sets()
+            self.forward(x, count)
+            self.wgrad_first(x)
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                adam_ops.adam_rows(sets[:1], self.lr, self.step_count + 1, *self.betas, self.eps,
+                                   step_dev=self.step_dev)
+            self.wgrad_second(x, reduce_bias=False)
+            adam_ops.adam_rows(sets[1:], self.lr, self.step_count + 1, *self.betas, self.eps,
+                               step_dev=self.step_dev)
+            main.wait_stream(self._side)  # join before the step counter advances
+            self._bias_loss(update=True, reduced=False)
+        else:
+            self.forward(x, count)
+            self.backward_weights(x)
+            self._apply_update_kernels()
+
     def _capture(self):
         torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self.forward_backward(self.x_static)
-            self._apply_update_kernels()
-        self._graph = g
+        self._graph = {}
+        for count in (True, False):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._step_kernels(self.x_static, count)
+            self._graph[count] = g
 
     def step_static(self):
         """Replay the captured step on whatever is in ``x_static`` (fill it first, e.g. with
         ``torch.index_select(..., out=engine.x_static)``)."""
         if self._graph is None:
             self._capture()
-        self._graph.replay()
+        count = self._counting()
+        self._counted = count
+        self._graph[count].replay()
         self._host_step()
         return self.out
 

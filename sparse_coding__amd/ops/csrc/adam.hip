@@ -251,6 +251,33 @@ __global__ __launch_bounds__(256) void bias_adam_kernel(BiasArgs a) {
   a.b[idx] = bj - (a.lr[g] / bc1) * mj / (sqrtf(vj / bc2) + a.eps);
 }
 
+// Finishes the decoder shadow after the Adam-fused weight-gradient GEMM: row
+// norm from the per-column-tile partial squares, bf16 shadow scaled in place,
+// norms stored for the next step's norm Jacobian.  One wave per row.
+__global__ __launch_bounds__(256) void normalize_rows_kernel(uint16_t* sh, const float* sqpart, int ntile,
+                                                             float* norms, long rows, int d) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float s2 = lane < ntile ? sqpart[row * ntile + lane] : 0.f;
+  s2 = wave_sum(s2);
+  const float nrm = fmaxf(sqrtf(s2), 1e-8f);
+  const float inv = 1.f / nrm;
+  if (lane == 0 && norms) norms[row] = nrm;
+  uint16_t* S = sh + row * d;
+  for (int e = lane * 8; e < d; e += 512) {
+    u32x4_t v = *reinterpret_cast<const u32x4_t*>(S + e);
+    u32x4_t o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = bf2f((uint16_t)(v[k] & 0xFFFF)) * inv;
+      const float hi = bf2f((uint16_t)(v[k] >> 16)) * inv;
+      o[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    *reinterpret_cast<u32x4_t*>(S + e) = o;
+  }
+}
+
 }  // namespace scamd
 
 using namespace scamd;
@@ -282,6 +309,14 @@ int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const*
     case 16: hipLaunchKernelGGL(adam_rows_kernel<16>, dim3(blocks), dim3(256), 0, stream, a); break;
     default: return 1;
   }
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_normalize_rows(void* sh, const float* sqpart, int ntile, float* norms, long rows, int d,
+                      hipStream_t stream) {
+  if (d % 8 || ntile > 64) return 1;
+  hipLaunchKernelGGL(normalize_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream,
+                     reinterpret_cast<uint16_t*>(sh), sqpart, ntile, norms, rows, d);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -32,7 +32,7 @@ namespace scamd {
 
 constexpr int BM = 128, BN = 128, NT = 256;
 
-enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4 };
+enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5 };
 
 struct Operand {
   const uint16_t* ptr;
@@ -45,6 +45,23 @@ struct Problem {
   Operand b[2];
   void* c;
   float alpha;
+};
+
+// Per-problem state for EPI_ADAM.  mode 1 = row-normalised parameter (decoder /
+// tied dictionary): the gradient reaching the raw rows goes through the norm
+// Jacobian, using the row dots accumulated by the code-gradient epilogue and
+// the current row norms; the updated rows are written unnormalised to the bf16
+// shadow together with per-(row, column-tile) partial squared norms, and a
+// small normalize pass finishes the shadow.
+struct AdamEpi {
+  float* p;
+  float* m;
+  float* v;
+  uint16_t* sh;
+  const float* dotpart;
+  const float* norms;
+  float* sqpart;
+  int mode;
 };
 
 struct GemmParams {
@@ -63,6 +80,15 @@ struct GemmParams {
   float* colpart;      // per-(tile_m, column) partials [G][tiles_m][N] (DC: bias grad, ENC: counts)
   const float* l1;     // DC: l1 coefficient per group
   float l1_add_scale;  // DC: multiplies l1[g] (= d/2 so dpre is in units of R)
+  float* dotpart;      // DC (optional): [G][tiles_m][N] partials of the norm-Jacobian row dots
+  int dc_tied;         // DC: tied dictionary -> dot also gets dpre * (c - b) (uses bias)
+  // --- EPI_ADAM: Adam fused into the weight-gradient epilogue -----------------
+  AdamEpi adam[2];
+  const float* lr;     // [G]
+  const int* step;     // device count of completed steps (t = *step + 1)
+  float b1, b2, eps;
+  int dot_tm;          // row tiles in dotpart
+  float dot_scale;     // converts dotpart sums to <w_hat, dL/dw_hat>
 };
 
 // LDS image of a K-major tile [128 rows][BKT k] bf16.
@@ -84,7 +110,7 @@ __device__ __forceinline__ int mmaj_off(int row, int ch) {
 // s_waitcnt vmcnt(N) only (expcnt/lgkmcnt left at their maxima).
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
-  __builtin_amdgcn_s_waitcnt((N & 15) | (((N >> 4) & 3) << 14) | 0x70 | 0xF00);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // Per-lane byte offsets (relative to the operand's group base) of the 1 KiB
@@ -112,13 +138,38 @@ __device__ __forceinline__ void piece_offsets(uint32_t (&voff)[PPW], long ld, in
   }
 }
 
+// Buffer resource (V#) as four SGPR words for inline asm: base, stride 0,
+// num_records, gfx950 raw-buffer flags.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4_t make_rsrc(const uint16_t* base) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  i32x4_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) & 0xFFFF);
+  r[2] = 0x7FFFFFFF;
+  r[3] = 0x00020000;
+  return r;
+}
+
+// The LDS-DMA is issued from inline asm on purpose: when hipcc sees a
+// buffer_load...lds it conservatively waits vmcnt(0) before the next ds_read of
+// the same LDS array, which would drain the prefetch of tile kt+1 before tile
+// kt's MFMAs and serialise the pipeline.  Hidden in asm, the DMAs are waited for
+// only by the explicit counted vmcnt before each barrier.
 template <int PPW>
-__device__ __forceinline__ void issue_pieces(__amdgpu_buffer_rsrc_t rs, const uint32_t* voff, uint32_t soff,
-                                             char* lds_tile, int wid) {
+__device__ __forceinline__ void issue_pieces(const i32x4_t& rs, const uint32_t* voff, uint32_t soff, char* lds_tile,
+                                             int wid) {
+  const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(lds_tile) + (uint32_t)(wid * PPW * 1024);
 #pragma unroll
-  for (int i = 0; i < PPW; ++i)
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds_tile + (wid * PPW + i) * 1024),
-                                            16, voff[i], soff, 0, 0);
+  for (int i = 0; i < PPW; ++i) {
+    asm volatile(
+        "s_mov_b32 m0, %0\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %3 offen lds"
+        :
+        : "s"(base + i * 1024), "v"(voff[i]), "s"(rs), "s"(soff)
+        : "memory", "m0");
+  }
 }
 
 // Fragment for v_mfma_f32_16x16x32_bf16: lane l holds X[r = rbase + (l&15)][k = 32 ks + 8(l>>4) + j].
@@ -143,9 +194,6 @@ __device__ __forceinline__ bf16x8_t load_frag(const char* lds, int rbase, int ks
   }
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const uint16_t* base) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7FFFFFFF, 0x00020000);
-}
 
 template <bool AK, bool BKM, int EPI, int BKT, int NST>
 __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
@@ -184,10 +232,10 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
   piece_offsets<BKM, BKT, PPW>(vb0, ob0.ld, n0, wid, lane);
   piece_offsets<AK, BKT, PPW>(va1, oa1.ld, m0, wid, lane);
   piece_offsets<BKM, BKT, PPW>(vb1, ob1.ld, n0, wid, lane);
-  const __amdgpu_buffer_rsrc_t ra0 = make_rsrc(oa0.ptr + (long)g * oa0.sg);
-  const __amdgpu_buffer_rsrc_t rb0 = make_rsrc(ob0.ptr + (long)g * ob0.sg);
-  const __amdgpu_buffer_rsrc_t ra1 = make_rsrc(oa1.ptr + (long)g * oa1.sg);
-  const __amdgpu_buffer_rsrc_t rb1 = make_rsrc(ob1.ptr + (long)g * ob1.sg);
+  const i32x4_t ra0 = make_rsrc(oa0.ptr + (long)g * oa0.sg);
+  const i32x4_t rb0 = make_rsrc(ob0.ptr + (long)g * ob0.sg);
+  const i32x4_t ra1 = make_rsrc(oa1.ptr + (long)g * oa1.sg);
+  const i32x4_t rb1 = make_rsrc(ob1.ptr + (long)g * ob1.sg);
   // soffset advance per K-tile: K-major operands step BKT elements, M/N-major BKT rows
   const uint32_t sa0 = AK ? BKT * 2 : (uint32_t)(BKT * oa0.ld * 2), sa1 = AK ? BKT * 2 : (uint32_t)(BKT * oa1.ld * 2);
   const uint32_t sb0 = BKM ? BKT * 2 : (uint32_t)(BKT * ob0.ld * 2), sb1 = BKM ? BKT * 2 : (uint32_t)(BKT * ob1.ld * 2);
@@ -210,6 +258,22 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // acc[i][j][r] = C[row][col0 + r] with row = m0 + wr*64 + i*16 + (lane&15),
+  // col0 = n0 + wc*64 + j*16 + 4*(lane>>4).
+  const int rowb = m0 + wr * 64 + (lane & 15);
+  const int colb = n0 + wc * 64 + 4 * (lane >> 4);
+  // The DEC / DC epilogues read a bf16 tile of x / c at the output positions:
+  // fetch it before the K loop so its HBM latency hides under the MFMAs.
+  uint2 auxv[4][4];
+  if constexpr (EPI == EPI_DEC || EPI == EPI_DC) {
+    const uint16_t* X = p.aux + (long)g * p.saux;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        auxv[i][j] = *reinterpret_cast<const uint2*>(X + (long)(rowb + i * 16) * p.ldaux + colb + j * 16);
+  }
+
 #pragma unroll
   for (int t = 0; t < NST - 1; ++t)
     if (t < nk) SC_ISSUE(t);
@@ -227,8 +291,10 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
     } else {
       wait_vmcnt<0>();
     }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of the stage being recycled are done
-    __builtin_amdgcn_s_barrier();        // raw barrier: no implicit vmcnt(0), DMAs stay in flight
+    // lgkmcnt(0): this wave's reads of the stage being recycled are done; raw barrier
+    // (no implicit vmcnt(0)) so younger DMAs stay in flight; "memory" keeps hipcc from
+    // moving LDS reads across it.
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (kt + NST - 1 < nk) SC_ISSUE(kt + NST - 1);
     const char* la = smem + (kt % NST) * 2 * TB;
     const char* lb = la + TB;
@@ -255,10 +321,6 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
   __syncthreads();  // all reads of the ring done before smem is reused below
 
   // ------------------------------------------------------------------ epilogue
-  // acc[i][j][r] = C[row][col0 + r] with row = m0 + wr*64 + i*16 + (lane&15),
-  // col0 = n0 + wc*64 + j*16 + 4*(lane>>4).
-  const int rowb = m0 + wr * 64 + (lane & 15);
-  const int colb = n0 + wc * 64 + 4 * (lane >> 4);
   float* red = reinterpret_cast<float*>(smem);  // free after the barrier above
 
   if constexpr (EPI == EPI_F32) {
@@ -288,7 +350,7 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
   // Column partial sums (ENC: on-counts, DC: bias gradient): reduce each lane's
   // 4x4 values over rows, then across the 16 lanes sharing a column group, then
   // across the two wave rows through LDS.  Deterministic; one store per column.
-  auto column_partials = [&](f32x4_t (&cs)[4]) {
+  auto column_partials = [&](f32x4_t (&cs)[4], float* dst) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -307,7 +369,8 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
         *reinterpret_cast<f32x4_t*>(red + wr * 128 + wc * 64 + j * 16 + 4 * (lane >> 4)) = cs[j];
     }
     __syncthreads();
-    if (tid < 128) p.colpart[((long)g * tiles_m + tm) * p.N + n0 + tid] = red[tid] + red[128 + tid];
+    if (tid < 128) dst[((long)g * tiles_m + tm) * p.N + n0 + tid] = red[tid] + red[128 + tid];
+    __syncthreads();
   };
 
   if constexpr (EPI == EPI_ENC) {
@@ -342,7 +405,7 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
             make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
       }
     }
-    if (p.colpart) column_partials(cnt);
+    if (p.colpart) column_partials(cnt, p.colpart);
     l1 = block_sum_256(l1, red + 512);
     l0 = block_sum_256(l0, red + 512);
     if (tid == 0) {
@@ -354,7 +417,6 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
   }
   if constexpr (EPI == EPI_DEC) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-    const uint16_t* X = p.aux + (long)g * p.saux;
     float se = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -362,9 +424,9 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
       for (int j = 0; j < 4; ++j) {
         const long row = rowb + i * 16;
         const int col = colb + j * 16;
-        const ushort4 xv = *reinterpret_cast<const ushort4*>(X + row * p.ldaux + col);
-        const float r0 = acc[i][j][0] - bf2f(xv.x), r1 = acc[i][j][1] - bf2f(xv.y);
-        const float r2 = acc[i][j][2] - bf2f(xv.z), r3 = acc[i][j][3] - bf2f(xv.w);
+        const uint2 xv = auxv[i][j];
+        const float r0 = acc[i][j][0] - bf2f(xv.x & 0xFFFF), r1 = acc[i][j][1] - bf2f(xv.x >> 16);
+        const float r2 = acc[i][j][2] - bf2f(xv.y & 0xFFFF), r3 = acc[i][j][3] - bf2f(xv.y >> 16);
         *reinterpret_cast<ushort4*>(C + row * p.ldc + col) = make_ushort4(f2bf(r0), f2bf(r1), f2bf(r2), f2bf(r3));
         se += r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
       }
@@ -374,29 +436,113 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
   }
   if constexpr (EPI == EPI_DC) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-    const uint16_t* Cin = p.aux + (long)g * p.saux;
     const float add = p.l1[g] * p.l1_add_scale;
-    f32x4_t cs[4];
+    const bool want_dot = p.dotpart != nullptr;
+    f32x4_t cs[4], ds[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       cs[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      ds[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int col = colb + j * 16;
+      f32x4_t bj = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if (p.dc_tied) bj = *reinterpret_cast<const f32x4_t*>(p.bias + (long)g * p.sbias + col);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const long row = rowb + i * 16;
-        const int col = colb + j * 16;
-        const ushort4 cv = *reinterpret_cast<const ushort4*>(Cin + row * p.ldaux + col);
-        const uint16_t cvs[4] = {cv.x, cv.y, cv.z, cv.w};
+        const uint2 cv = auxv[i][j];
+        const uint16_t cvs[4] = {(uint16_t)(cv.x & 0xFFFF), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xFFFF),
+                                 (uint16_t)(cv.y >> 16)};
         f32x4_t dv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          dv[r] = cvs[r] != 0 ? acc[i][j][r] + add : 0.f;  // c is a ReLU output: nonzero <=> > 0
+          const float c = bf2f(cvs[r]);
+          dv[r] = c > 0.f ? acc[i][j][r] + add : 0.f;  // c is a ReLU output
           cs[j][r] += dv[r];
+          if (want_dot) {
+            // <w_hat_j, dL/dw_hat_j> (in units of 2/(B d)): decoder path c * (R w_hat^T),
+            // tied encoder path dpre * (x w_hat^T) = dpre * (pre - b) = dpre * (c - b)
+            ds[j][r] += c * acc[i][j][r] + (p.dc_tied ? dv[r] * (c - bj[r]) : 0.f);
+          }
         }
         *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
             make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
       }
     }
-    column_partials(cs);
+    column_partials(cs, p.colpart);
+    if (want_dot) column_partials(ds, p.dotpart);
+    return;
+  }
+  if constexpr (EPI == EPI_ADAM) {
+    // Weight gradient -> Adam in registers; the fp32 gradient never touches HBM.
+    const AdamEpi E = p1 ? p.adam[1] : p.adam[0];
+    const long gb = (long)g * p.sc;
+    const float bc1 = 1.f - __powf(p.b1, (float)(*p.step + 1));
+    const float bc2 = 1.f - __powf(p.b2, (float)(*p.step + 1));
+    const float stp = p.lr[g] / bc1, rbc2 = 1.f / bc2, b1 = p.b1, b2 = p.b2, eps = p.eps;
+    float ca[4], cp[4];
+    if (E.mode) {
+      if (tid < 128) {
+        const int row = m0 + tid;
+        float dsum = 0.f;
+        for (int t = 0; t < p.dot_tm; ++t) dsum += E.dotpart[((long)g * p.dot_tm + t) * p.M + row];
+        red[tid] = dsum * p.dot_scale;
+        red[128 + tid] = E.norms[(long)g * p.M + row];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int lr_ = wr * 64 + i * 16 + (lane & 15);
+        const float dot = red[lr_], nrm = red[128 + lr_];
+        if (nrm > 1e-8f) {
+          const float inv = 1.f / nrm;
+          ca[i] = alpha * inv;      // dW = dW_hat / |w| - w <w_hat, dW_hat> / |w|^2
+          cp[i] = dot * inv * inv;
+        } else {
+          ca[i] = alpha * 1e8f;     // below the clamp floor the norm has zero derivative
+          cp[i] = 0.f;
+        }
+      }
+      __syncthreads();
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { ca[i] = alpha; cp[i] = 0.f; }
+    }
+    float ss[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const long off = gb + (long)(rowb + i * 16) * p.ldc + colb + j * 16;
+        f32x4_t pv = *reinterpret_cast<const f32x4_t*>(E.p + off);
+        f32x4_t mv = *reinterpret_cast<const f32x4_t*>(E.m + off);
+        f32x4_t vv = *reinterpret_cast<const f32x4_t*>(E.v + off);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gr = acc[i][j][r] * ca[i] - pv[r] * cp[i];
+          mv[r] = b1 * mv[r] + (1.f - b1) * gr;
+          vv[r] = b2 * vv[r] + (1.f - b2) * gr * gr;
+          pv[r] -= stp * mv[r] / (sqrtf(vv[r] * rbc2) + eps);
+          ss[i] += pv[r] * pv[r];
+        }
+        *reinterpret_cast<f32x4_t*>(E.p + off) = pv;
+        *reinterpret_cast<f32x4_t*>(E.m + off) = mv;
+        *reinterpret_cast<f32x4_t*>(E.v + off) = vv;
+        *reinterpret_cast<ushort4*>(E.sh + off) = make_ushort4(f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3]));
+      }
+    if (E.mode) {
+      // partial |w_j|^2 over this block's 128 columns -> sqpart[g][row][tn]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ss[i] += __shfl_xor(ss[i], 16, 64);
+        ss[i] += __shfl_xor(ss[i], 32, 64);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[wc * 128 + wr * 64 + i * 16 + lane] = ss[i];
+      }
+      __syncthreads();
+      if (tid < 128) E.sqpart[((long)g * p.M + m0 + tid) * tiles_n + tn] = red[tid] + red[128 + tid];
+    }
     return;
   }
 }
@@ -413,12 +559,25 @@ struct ScOperand {
   long ld, sg;
 };
 
+struct ScAdamEpi {
+  float* p;
+  float* m;
+  float* v;
+  void* sh;
+  const float* dotpart;
+  const float* norms;
+  float* sqpart;
+  int mode;
+};
+
 // layout: bit0 = A is K-major, bit1 = B is K-major.
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             const ScOperand* a /* [nprob][2] */, const ScOperand* b /* [nprob][2] */,
             void* const* c /* [nprob] */, const float* alpha /* [nprob] */, long ldc, long sc,
             const float* bias, long sbias, const int* nactive, const void* aux, long ldaux,
             long saux, float* part, float* colpart, const float* l1, float l1_add_scale,
+            float* dotpart, int dc_tied, const ScAdamEpi* adam /* [nprob] or null */, const float* lr,
+            const int* step, float b1, float b2, float eps, int dot_tm, float dot_scale,
             int cfg, hipStream_t stream) {
   if (M % BM || N % BN || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
   GemmParams p;
@@ -436,29 +595,56 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.bias = bias; p.sbias = sbias; p.nactive = nactive;
   p.aux = reinterpret_cast<const uint16_t*>(aux); p.ldaux = ldaux; p.saux = saux;
   p.part = part; p.colpart = colpart; p.l1 = l1; p.l1_add_scale = l1_add_scale;
+  p.dotpart = dotpart; p.dc_tied = dc_tied;
+  for (int i = 0; i < 2; ++i) {
+    if (adam && i < nprob)
+      p.adam[i] = {adam[i].p, adam[i].m, adam[i].v, reinterpret_cast<uint16_t*>(adam[i].sh), adam[i].dotpart,
+                   adam[i].norms, adam[i].sqpart, adam[i].mode};
+    else
+      p.adam[i] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  }
+  if (epi == EPI_ADAM && (!adam || !lr || !step)) return 4;
+  p.lr = lr; p.step = step; p.b1 = b1; p.b2 = b2; p.eps = eps; p.dot_tm = dot_tm; p.dot_scale = dot_scale;
   const int grid = (M / BM) * (N / BN) * G * nprob;
   const bool ak = layout & 1, bk = layout & 2;
 
+#ifdef SC_GEMM_ALL_CFGS
 #define SC_LAUNCH(AKV, BKV, E)                                                                    \
   switch (cfg) {                                                                                  \
     case 1: hipLaunchKernelGGL((sae_gemm_kernel<AKV, BKV, E, 32, 3>), dim3(grid), dim3(NT), 0, stream, p); break; \
     case 2: hipLaunchKernelGGL((sae_gemm_kernel<AKV, BKV, E, 32, 4>), dim3(grid), dim3(NT), 0, stream, p); break; \
     default: hipLaunchKernelGGL((sae_gemm_kernel<AKV, BKV, E, 64, 2>), dim3(grid), dim3(NT), 0, stream, p); break; \
   }
-#define SC_EPI(AKV, BKV)                                   \
-  switch (epi) {                                           \
-    case EPI_ENC: SC_LAUNCH(AKV, BKV, EPI_ENC); break;     \
-    case EPI_DEC: SC_LAUNCH(AKV, BKV, EPI_DEC); break;     \
-    case EPI_DC: SC_LAUNCH(AKV, BKV, EPI_DC); break;       \
-    case EPI_F32: SC_LAUNCH(AKV, BKV, EPI_F32); break;     \
-    case EPI_BF16: SC_LAUNCH(AKV, BKV, EPI_BF16); break;   \
-    default: return 2;                                     \
+#else
+  // BK64 x 2 stages measured fastest for every step GEMM on MI355X (profiles/kernel_bench_r1_v3.jsonl);
+  // build with -DSC_GEMM_ALL_CFGS to A/B the deeper BK32 rings.
+  (void)cfg;
+#define SC_LAUNCH(AKV, BKV, E) \
+  hipLaunchKernelGGL((sae_gemm_kernel<AKV, BKV, E, 64, 2>), dim3(grid), dim3(NT), 0, stream, p)
+#endif
+  // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
+  // epilogues; the plain F32 / BF16 epilogues exist for every layout.
+  switch (epi) {
+    case EPI_ENC: if (!(ak && bk)) return 5; SC_LAUNCH(true, true, EPI_ENC); break;
+    case EPI_DEC: if (!(ak && !bk)) return 5; SC_LAUNCH(true, false, EPI_DEC); break;
+    case EPI_DC: if (!(ak && bk)) return 5; SC_LAUNCH(true, true, EPI_DC); break;
+    case EPI_ADAM: if (ak || bk) return 5; SC_LAUNCH(false, false, EPI_ADAM); break;
+    case EPI_F32:
+    case EPI_BF16:
+      if (epi == EPI_F32) {
+        if (ak && bk) SC_LAUNCH(true, true, EPI_F32);
+        else if (ak) SC_LAUNCH(true, false, EPI_F32);
+        else if (bk) SC_LAUNCH(false, true, EPI_F32);
+        else SC_LAUNCH(false, false, EPI_F32);
+      } else {
+        if (ak && bk) SC_LAUNCH(true, true, EPI_BF16);
+        else if (ak) SC_LAUNCH(true, false, EPI_BF16);
+        else if (bk) SC_LAUNCH(false, true, EPI_BF16);
+        else SC_LAUNCH(false, false, EPI_BF16);
+      }
+      break;
+    default: return 2;
   }
-  if (ak && bk) { SC_EPI(true, true) }
-  else if (ak && !bk) { SC_EPI(true, false) }
-  else if (!ak && !bk) { SC_EPI(false, false) }
-  else { SC_EPI(false, true) }
-#undef SC_EPI
 #undef SC_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

@@ -17,14 +17,14 @@ import torch
 
 from . import _lib
 
-EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16 = 0, 1, 2, 3, 4
+EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16, EPI_ADAM = 0, 1, 2, 3, 4, 5
 TILE_M, TILE_N, TILE_K = 128, 128, 64
 
 # Pipeline configurations of the kernel (K-tile depth x LDS-DMA ring stages):
 #   0: BK64 x 2 stages (64 KiB LDS)   1: BK32 x 3 stages (48 KiB)   2: BK32 x 4 stages (64 KiB)
 # Per-epilogue defaults come from measurements on MI355X (profiles/); override with
 # SC_GEMM_CFG=<n> for all GEMMs.
-_CFG_DEFAULT = {EPI_ENC: 0, EPI_DEC: 0, EPI_DC: 0, EPI_F32: 0, EPI_BF16: 0}
+_CFG_DEFAULT = {EPI_ENC: 0, EPI_DEC: 0, EPI_DC: 0, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 0}
 _CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
 
 
@@ -49,7 +49,8 @@ def _bf16(t, name):
 
 def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *,
             bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
-            colpart=None, l1=None, l1_add_scale=0.0, cfg=None):
+            colpart=None, l1=None, l1_add_scale=0.0, dotpart=None, dc_tied=False, adam=None,
+            lr=None, step=None, betas=(0.9, 0.999), eps=1e-8, dot_tm=0, dot_scale=0.0, cfg=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     nprob = len(outs)
@@ -61,6 +62,8 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
         epi, layout, nprob, M, N, K1, K2, G, A, Bo, Cp, al, ldc, sc,
         _lib.ptr(bias), sbias, _lib.ptr(nactive), _lib.ptr(aux), ldaux, saux,
         _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1), float(l1_add_scale),
+        _lib.ptr(dotpart), int(bool(dc_tied)), adam, _lib.ptr(lr), _lib.ptr(step),
+        float(betas[0]), float(betas[1]), float(eps), int(dot_tm), float(dot_scale),
         int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi])),
         _lib.stream_handle(),
     )
@@ -118,11 +121,14 @@ def decode_residual(c, w_hat, x, r_out, part):
             aux=x, ldaux=d, saux=sx, part=part)
 
 
-def code_grad(r, w_hat, c, l1, dpre_out, colpart):
+def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None):
     """dpre_s[g] = 1[c>0] * (r[g] @ w_hat[g]^T + l1[g] * d / 2).
 
     dpre_s is the code gradient in units of the residual: dL/dpre = 2/(B d) * dpre_s.
-    colpart receives per-row-tile column sums (bias gradient partials).
+    colpart receives per-row-tile column sums (bias gradient partials).  With ``dotpart``
+    [G, B/128, n] the epilogue also accumulates the norm-Jacobian row dots
+    <w_hat_j, dL/dw_hat_j> (in units of 2/(B d)); ``tied_bias`` ([G, n]) adds the tied
+    dictionary's encoder-path term.
     """
     G, B, d = r.shape
     n = w_hat.shape[1]
@@ -132,8 +138,11 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart):
     _need(colpart.numel() >= G * (B // 128) * n, "colpart too small")
     a = [_op(r, d, B * d)] * 2
     b = [_op(w_hat, d, n * d)] * 2
+    if dotpart is not None:
+        _need(dotpart.numel() >= G * (B // 128) * n, "dotpart too small")
     _launch(EPI_DC, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
-            aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0)
+            aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0,
+            dotpart=dotpart, dc_tied=tied_bias is not None, bias=tied_bias, sbias=n)
 
 
 def weight_grads(pairs, outs, alpha):
@@ -169,6 +178,51 @@ def weight_grads(pairs, outs, alpha):
     for o in outs:
         _need(o.dtype == torch.float32 and tuple(o.shape) == (G, n, d) and o.is_contiguous(), "out")
     _launch(EPI_F32, 0, n, d, K1, K2, G, a_ops, b_ops, list(outs), [alpha] * len(outs), d, n * d)
+
+
+def weight_grads_adam(pairs, states, alpha, lr, step_dev, betas=(0.9, 0.999), eps=1e-8, dot_tm=0):
+    """Weight gradients (as ``weight_grads``) with Adam applied in the epilogue.
+
+    states: one dict per problem with p/m/v (fp32 [G, n, d]), shadow (bf16 [G, n, d], written
+    UNNORMALISED for normalised rows), and for row-normalised parameters (``norm=True``):
+    dotpart [G, dot_tm, n] (from ``code_grad``), norms [G, n] (current row norms) and
+    sqpart [G, n, d/128] (receives partial squared norms; finish with ``adam.normalize_rows``).
+    """
+    _need(1 <= len(pairs) == len(states) <= 2, "1 or 2 problems")
+    G, n, d = states[0]["p"].shape
+    nseg = len(pairs[0])
+    a_ops, b_ops, ks = [], [], []
+    for p in pairs:
+        seg_a, seg_b = [], []
+        for (A, Bm) in p:
+            _bf16(A, "A"); _bf16(Bm, "B")
+            Bk = A.shape[-2]
+            _need(A.shape[-1] == n and Bm.shape[-1] == d and Bm.shape[-2] == Bk, "segment shapes")
+            seg_a.append(_op(A, n, 0 if A.dim() == 2 else Bk * n))
+            seg_b.append(_op(Bm, d, 0 if Bm.dim() == 2 else Bk * d))
+        if nseg == 1:
+            seg_a.append(seg_a[0]); seg_b.append(seg_b[0])
+        a_ops += seg_a; b_ops += seg_b
+        ks.append(tuple(x.shape[-2] for x, _ in p))
+    _need(len(set(ks)) == 1, "all problems must share K segments")
+    eps_arr = (_lib.ScAdamEpi * len(states))()
+    for i, st in enumerate(states):
+        for k in ("p", "m", "v"):
+            t = st[k]
+            _need(t.dtype == torch.float32 and tuple(t.shape) == (G, n, d) and t.is_contiguous(), f"adam {k}")
+        _need(st["shadow"].dtype == torch.bfloat16 and tuple(st["shadow"].shape) == (G, n, d), "shadow")
+        mode = int(bool(st.get("norm")))
+        if mode:
+            _need(st["dotpart"].numel() >= G * dot_tm * n, "dotpart")
+            _need(st["norms"].numel() == G * n and st["sqpart"].numel() >= G * n * (d // 128), "norms/sqpart")
+        eps_arr[i] = _lib.ScAdamEpi(_lib.ptr(st["p"]), _lib.ptr(st["m"]), _lib.ptr(st["v"]), _lib.ptr(st["shadow"]),
+                                    _lib.ptr(st.get("dotpart")), _lib.ptr(st.get("norms")),
+                                    _lib.ptr(st.get("sqpart")), mode)
+    K1 = ks[0][0]
+    K2 = ks[0][1] if nseg == 2 else 0
+    _launch(EPI_ADAM, 0, n, d, K1, K2, G, a_ops, b_ops, [st["p"] for st in states], [alpha] * len(states),
+            d, n * d, adam=eps_arr, lr=lr, step=step_dev, betas=betas, eps=eps, dot_tm=dot_tm,
+            dot_scale=alpha)
 
 
 def matmul_nt(a, b, out, alpha=1.0):

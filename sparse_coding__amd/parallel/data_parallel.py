@@ -39,6 +39,7 @@ class DataParallelFused:
         self.grad_dtype = grad_dtype
         engine.grad_scale = 1.0 / info.world_size
         if info.enabled:
+            engine.fuse_adam = False  # gradients are all-reduced before the (separate) Adam kernels
             self.sync_params()
 
     def sync_params(self):
