@@ -1,0 +1,132 @@
+"""FISTA sparse coding for a whole ensemble: the gfx950 persistent kernel
+(``csrc/fista.hip``) plus the batched-torch oracle it is tested against.
+
+Reference: ``autoencoders/fista.py:99-128`` (solver) and ``:131-138`` (quadratic
+basis update).  Shapes: X [G, B, d] (or [B, d] shared by all models), D [G, n, d]
+row-normalised dictionaries, warm start A0 [G, B, n], lam / eta [G].
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def momentum_schedule(iters: int) -> torch.Tensor:
+    """mom[t] = (t_k - 1) / t_{k+1} with t_1 = 1, t_{k+1} = (1 + sqrt(1 + 4 t_k^2)) / 2."""
+    mom = np.empty(iters, dtype=np.float64)
+    tk_n = 1.0
+    for t in range(iters):
+        tk = tk_n
+        tk_n = (1.0 + math.sqrt(1.0 + 4.0 * tk * tk)) / 2.0
+        mom[t] = (tk - 1.0) / tk_n
+    return torch.from_numpy(mom.astype(np.float32))
+
+
+def step_size(D: torch.Tensor, method: str = "eigh", iters: int = 30) -> torch.Tensor:
+    """eta = 1 / lambda_max(D D^T) per model (reference uses eigvalsh, :104-106).
+
+    ``method="power"`` runs batched power iteration on D^T D ([d, d], cheaper when
+    n > d) with a 1% safety margin so eta never exceeds the true 1/L.
+    """
+    D = D.float()
+    if method == "eigh":
+        gram = D @ D.transpose(-1, -2)
+        return 1.0 / torch.linalg.eigvalsh(gram).amax(dim=-1)
+    G, n, d = D.shape
+    gram = D.transpose(-1, -2) @ D  # same nonzero spectrum, [d, d]
+    v = torch.randn(G, d, 1, device=D.device, generator=torch.Generator(D.device).manual_seed(0))
+    for _ in range(iters):
+        v = gram @ v
+        v = v / v.norm(dim=1, keepdim=True)
+    lam_max = (v.transpose(1, 2) @ gram @ v).squeeze(-1).squeeze(-1)
+    return 1.0 / (1.01 * lam_max)
+
+
+def fista_torch(X, D, lam, A0=None, iters=500, eta=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Batched fp32 oracle: identical arithmetic to the reference loop, all models at once."""
+    D = D.float()
+    G, n, d = D.shape
+    X = X.float()
+    if X.dim() == 2:
+        X = X.expand(G, *X.shape)
+    if eta is None:
+        eta = step_size(D)
+    eta = eta.to(D.device).float().view(G, 1, 1)
+    lam = torch.as_tensor(lam, device=D.device, dtype=torch.float32).view(G, 1, 1)
+    A = torch.zeros(G, X.shape[1], n, device=D.device) if A0 is None else A0.float().clone()
+    Y = A.clone()
+    mom = momentum_schedule(iters).tolist()
+    Dt = D.transpose(1, 2)
+    for t in range(iters):
+        A_prev = A
+        res = X - torch.bmm(Y, D)
+        Y = Y + eta * torch.bmm(res, Dt)
+        A = torch.clamp(Y - eta * lam, min=0.0)
+        Y = A + (A - A_prev) * mom[t]
+    return A, X - torch.bmm(A, D)
+
+
+def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_res: bool = True
+          ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Solve min_A>=0 1/2|X - A D|^2 + lam |A|_1 (ISTA step eta) for every model.
+
+    backend: "hip" (gfx950 kernel, bf16 GEMM operands, fp32 iterates), "torch" (fp32
+    oracle), or "auto" (hip when the GPU kernel supports the shape).
+    """
+    G, n, d = D.shape
+    B = X.shape[-2]
+    use_hip = backend == "hip" or (backend == "auto" and D.is_cuda and _lib.available() and B % 16 == 0
+                                   and n % 128 == 0 and d % 128 == 0)
+    if not use_hip:
+        return fista_torch(X, D, lam, A0, iters, eta)
+    dev = D.device
+    if eta is None:
+        eta = step_size(D)
+    eta = eta.to(dev).float().contiguous()
+    lam = torch.as_tensor(lam, device=dev, dtype=torch.float32).reshape(G).contiguous()
+    Xb = X.to(torch.bfloat16)
+    if Xb.dim() == 2:
+        Xb = Xb.expand(G, *Xb.shape)
+    Xb = Xb.contiguous()
+    Db = D.to(torch.bfloat16).contiguous()
+    Dtb = Db.transpose(1, 2).contiguous()
+    A = torch.empty(G, B, n, device=dev)
+    Res = torch.empty(G, B, d, device=dev) if with_res else None
+    a0 = A0.float().contiguous() if A0 is not None else None
+    mom = momentum_schedule(max(iters, 1)).to(dev)
+    rc = _lib.lib().sc_fista(_lib.ptr(Xb), _lib.ptr(Db), _lib.ptr(Dtb), _lib.ptr(a0), _lib.ptr(eta), _lib.ptr(lam),
+                             _lib.ptr(mom), _lib.ptr(A), _lib.ptr(Res), G, B, n, d, iters, _lib.stream_handle())
+    if rc == 2 and backend == "auto":
+        return fista_torch(X, D, lam, A0, iters, eta)
+    _lib.check(rc, "sc_fista")
+    return A, Res
+
+
+def hessian_ema(H, A, history: int = 300):
+    """H <- H (history-1)/history + mean_b(A^2)/history (reference fista.py:91-92)."""
+    return H * ((history - 1.0) / history) + A.pow(2).mean(dim=-2) / history
+
+
+def quadratic_basis_update(D, Res, A, H, lowest_activation=0.001, step=0.001, nonneg=False,
+                           normalize: str = "column"):
+    """D' = D + (step Res^T A / B / (H + lowest))^T, then renormalise (reference :131-138).
+
+    normalize="column" reproduces the reference (``D.norm(2, 0)``: per activation
+    dimension, SURVEY B#4); "row" normalises each atom (the intended unit-norm dictionary).
+    Batched over models: D [G, n, d], Res [G, B, d], A [G, B, n], H [G, n].
+    """
+    B = A.shape[-2]
+    dB = step * torch.bmm(Res.transpose(1, 2).float(), A.float()) / B  # [G, d, n]
+    dB = dB / (H.unsqueeze(1) + lowest_activation)
+    D = D.float() + dB.transpose(1, 2)
+    if nonneg:
+        D = D.clamp(min=0.0)
+    if normalize == "column":
+        return D / D.norm(dim=1, keepdim=True)
+    return D / D.norm(dim=2, keepdim=True).clamp(min=1e-8)

@@ -1,0 +1,241 @@
+"""CPU tests: checkpoint compatibility, FISTA oracle, top-k, LISTA / misc learners, baselines."""
+
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
+from sparse_coding__amd.engine.optim import adam
+
+REF = "/root/reference/output_basic_test"
+
+
+# ----------------------------------------------------------------------------- checkpoints
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkpoints not mounted")
+@pytest.mark.parametrize("name,cls,rownorm,colnorm", [
+    ("normal", "TiedSAE", 2.02, None),
+    ("Fista_04_10_2023", "Fista", 1.90, None),
+    ("fista10_10_2023_iterative", "Fista", None, 1.0),
+])
+def test_load_shipped_reference_checkpoints(name, cls, rownorm, colnorm):
+    from sparse_coding__amd.utils.checkpoint import load_learned_dicts
+
+    lds = load_learned_dicts(f"{REF}/{name}/learned_dicts_epoch_0.pt")
+    assert len(lds) == 1
+    ld, hp = lds[0]
+    assert type(ld).__name__ == cls and hp == {"dict_size": 512, "l1_alpha": 0.001}
+    assert ld.encoder.shape == (512, 512) and ld.norm_encoder
+    if rownorm:
+        assert abs(float(ld.encoder.norm(dim=-1).mean()) - rownorm) < 0.02
+    if colnorm:  # SURVEY B#4: the iterative FISTA checkpoint is column-normalised
+        torch.testing.assert_close(ld.encoder.norm(dim=0), torch.ones(512), rtol=1e-4, atol=1e-4)
+    x = torch.randn(16, 512)
+    assert ld.predict(x).shape == (16, 512)
+    assert torch.isfinite(ld.encode(x)).all()
+
+
+def test_compat_roundtrip(tmp_path):
+    from sparse_coding__amd.models.learned_dict import TiedSAE, UntiedSAE
+    from sparse_coding__amd.models.topk import TopKLearnedDict
+    from sparse_coding__amd.utils.checkpoint import load_learned_dicts, save_learned_dicts
+
+    lds = [(UntiedSAE(torch.randn(8, 4), torch.randn(8, 4), torch.zeros(8)), {"dict_size": 8, "l1_alpha": 1e-3}),
+           (TiedSAE(torch.randn(8, 4), torch.zeros(8), norm_encoder=True), {"dict_size": 8, "l1_alpha": 2e-3}),
+           (TopKLearnedDict(torch.randn(8, 4), 3), {"sparsity": 3})]
+    p = str(tmp_path / "learned_dicts.pt")
+    save_learned_dicts(lds, p)
+    back = load_learned_dicts(p)
+    assert [type(b).__module__ for b, _ in back] == ["autoencoders.learned_dict"] * 2 + ["autoencoders.topk_encoder"]
+    for (a, ha), (b, hb) in zip(lds, back):
+        assert ha == hb
+        x = torch.randn(5, 4)
+        torch.testing.assert_close(a.encode(x), b.encode(x))
+        assert isinstance(b, type(a))  # aliases subclass the native classes
+
+
+def test_training_state_roundtrip(tmp_path):
+    from sparse_coding__amd.utils.checkpoint import load_training_state, save_training_state
+
+    st = {"params": {"w": torch.randn(3, 4)}, "step": 7, "cursor": [1, 2]}
+    save_training_state(str(tmp_path / "ck.pt"), st, {"cfg": {"lr": 1e-3}})
+    back = load_training_state(str(tmp_path / "ck.pt"))
+    assert back["trainer"]["step"] == 7 and back["extra"]["cfg"]["lr"] == 1e-3
+    torch.testing.assert_close(back["trainer"]["params"]["w"], st["params"]["w"])
+
+
+# ----------------------------------------------------------------------------- FISTA
+def _reference_fista(batch, D, l1, coefs, iters):
+    """Line-by-line semantics of reference autoencoders/fista.py:99-128 (fp64 for a tight check)."""
+    eta = 1.0 / torch.linalg.eigvalsh(D @ D.T).max()
+    tk_n = 1.0
+    ahat = coefs
+    ahat_y = coefs
+    for _ in range(iters):
+        tk = tk_n
+        tk_n = (1 + np.sqrt(1 + 4 * tk ** 2)) / 2
+        ahat_pre = ahat
+        res = batch - ahat_y @ D
+        ahat_y = ahat_y + eta * res @ D.T
+        ahat = (ahat_y - eta * l1).clamp(min=0.0)
+        ahat_y = ahat + (ahat - ahat_pre) * ((tk - 1) / tk_n)
+    return ahat, batch - ahat @ D
+
+
+def test_fista_torch_matches_reference_loop():
+    from sparse_coding__amd.ops.fista import fista_torch
+
+    torch.manual_seed(0)
+    G, B, n, d = 3, 32, 24, 16
+    D = torch.nn.functional.normalize(torch.randn(G, n, d), dim=-1)
+    X = torch.randn(B, d)
+    A0 = torch.relu(torch.randn(G, B, n)) * 0.1
+    lam = torch.tensor([1e-3, 1e-2, 5e-2])
+    A, R = fista_torch(X, D, lam, A0, iters=40)
+    for g in range(G):
+        a_ref, r_ref = _reference_fista(X.double(), D[g].double(), float(lam[g]), A0[g].double(), 40)
+        torch.testing.assert_close(A[g].double(), a_ref, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(R[g].double(), r_ref, rtol=1e-4, atol=1e-5)
+
+
+def test_fista_decreases_objective_and_power_iteration_bound():
+    from sparse_coding__amd.ops.fista import fista_torch, step_size
+
+    torch.manual_seed(1)
+    D = torch.nn.functional.normalize(torch.randn(2, 64, 32), dim=-1)
+    eta_e = step_size(D, "eigh")
+    eta_p = step_size(D, "power", iters=100)
+    assert (eta_p <= eta_e * 1.0001).all() and (eta_p > 0.95 * eta_e).all()
+    X = torch.randn(16, 32)
+    lam = torch.tensor([0.01, 0.05])
+
+    def obj(A, R, l):
+        return 0.5 * R.pow(2).sum() + l * A.abs().sum()
+
+    A5, R5 = fista_torch(X, D, lam, None, iters=5)
+    A50, R50 = fista_torch(X, D, lam, None, iters=50)
+    for g in range(2):
+        assert obj(A50[g], R50[g], lam[g]) <= obj(A5[g], R5[g], lam[g]) + 1e-6
+        assert (A50[g] >= 0).all()
+
+
+def test_fista_dict_update_and_loss2():
+    from sparse_coding__amd.models.fista import FistaDictUpdater, FunctionalFista
+
+    torch.manual_seed(2)
+    models = [FunctionalFista.init(32, 48, l1) for l1 in (1e-3, 1e-2)]
+    ens = FunctionalEnsemble(models, FunctionalFista, adam, {"lr": 1e-3}, device="cpu")
+    x = torch.randn(64, 32)
+    _, (ld, aux) = ens.compute_grads(x)
+    upd = FistaDictUpdater(num_iter=20, backend="torch")
+    new, res, A = upd(ens.params["decoder"], x, aux["c"], ens.buffers["l1_alpha"])
+    assert new.shape == (2, 48, 32)
+    torch.testing.assert_close(new.norm(dim=1), torch.ones(2, 32), rtol=1e-5, atol=1e-5)  # column norm (B#4)
+    upd_row = FistaDictUpdater(num_iter=20, backend="torch", normalize="row")
+    new2, _, _ = upd_row(ens.params["decoder"], x, aux["c"], ens.buffers["l1_alpha"])
+    torch.testing.assert_close(new2.norm(dim=2), torch.ones(2, 48), rtol=1e-5, atol=1e-5)
+    # FISTA-in-the-loss: differentiable through 10 unrolled iterations
+    p, b = models[0]
+    p = {k: v.clone().requires_grad_() for k, v in p.items()}
+    loss, (ldict, _) = FunctionalFista.loss2(p, b, x, num_iter=10)
+    loss.backward()
+    assert p["encoder"].grad is not None and torch.isfinite(p["encoder"].grad).all()
+    assert "l_fista" in ldict
+
+
+# ----------------------------------------------------------------------------- other learners
+def test_topk_encoder_ensemble_no_stacking():
+    from sparse_coding__amd.models.topk import TopKEncoder, TopKLearnedDict
+
+    torch.manual_seed(3)
+    models = [TopKEncoder.init(16, 32, k) for k in (1, 4, 8)]
+    ens = FunctionalEnsemble(models, TopKEncoder, adam, {"lr": 1e-2}, device="cpu", no_stacking=True)
+    x = torch.randn(64, 16)
+    for _ in range(5):
+        loss, aux = ens.step_batch(x)
+    c = aux["c"]
+    assert ((c != 0).sum(-1) <= torch.tensor([1, 4, 8])[:, None]).all()
+    lds = ens.to_learned_dicts()
+    assert all(isinstance(l, TopKLearnedDict) for l in lds) and [l.sparsity for l in lds] == [1, 4, 8]
+
+
+@pytest.mark.parametrize("which", ["lista", "residual", "semilinear", "positive", "direct"])
+def test_misc_learners_train(which):
+    from sparse_coding__amd.models import lista, misc
+
+    torch.manual_seed(4)
+    d, n = 16, 32
+    if which == "lista":
+        sig, models = lista.FunctionalLISTADenoisingSAE, [lista.FunctionalLISTADenoisingSAE.init(d, n, 2, 1e-3)]
+    elif which == "residual":
+        sig, models = lista.FunctionalResidualDenoisingSAE, [lista.FunctionalResidualDenoisingSAE.init(d, n, 2, 1e-3)]
+    elif which == "semilinear":
+        sig, models = misc.SemiLinearSAE, [misc.SemiLinearSAE.init(d, n, 1e-3)]
+    elif which == "positive":
+        sig, models = misc.FunctionalPositiveTiedSAE, [misc.FunctionalPositiveTiedSAE.init(d, n, 1e-3)]
+    else:
+        sig, models = misc.DirectCoefOptimizer, [misc.DirectCoefOptimizer.init(d, n, 1e-3, lr=1e-1)]
+    ens = FunctionalEnsemble(models, sig, adam, {"lr": 3e-3}, device="cpu")
+    x = torch.relu(torch.randn(128, d))
+    first = None
+    for _ in range(40):
+        loss, _ = ens.step_batch(x)
+        first = float(loss["loss"][0]) if first is None else first
+    assert float(loss["loss"][0]) < first
+    ld = ens.to_learned_dicts()[0]
+    assert ld.encode(x).shape == (128, n) and ld.predict(x).shape == x.shape
+
+
+def test_rica_trains():
+    from sparse_coding__amd.models.misc import RICA
+
+    torch.manual_seed(5)
+    m = RICA(8, 16, sparsity_coef=0.1)
+    opt = m.configure_optimizers(lr=1e-2)
+    x = torch.randn(64, 8)
+    l0 = m.train_batch(x, opt)[0]
+    for _ in range(30):
+        l = m.train_batch(x, opt)[0]
+    assert l < l0
+
+
+# ----------------------------------------------------------------------------- baselines
+def test_batched_pca_matches_full_covariance():
+    from sparse_coding__amd.baselines.pca import BatchedPCA, calc_mean
+
+    torch.manual_seed(6)
+    A = torch.randn(1000, 12) @ torch.randn(12, 12) + 3.0
+    pca = BatchedPCA(12, "cpu")
+    for i in range(0, 1000, 128):
+        pca.train_batch(A[i:i + 128])
+    cov = torch.cov(A.T.double(), correction=0)
+    torch.testing.assert_close(pca.cov, cov, rtol=1e-6, atol=1e-8)
+    torch.testing.assert_close(calc_mean(A, 100, "cpu"), A.mean(0), rtol=1e-5, atol=1e-5)
+    enc = pca.to_learned_dict(3)
+    c = enc.encode(A[:10] - A.mean(0))
+    assert ((c != 0).sum(-1) == 3).all()
+    t = pca.to_topk_dict(4)
+    assert t.get_learned_dict().shape == (24, 12)
+    mean, rot, scale = pca.get_centering_transform()
+    assert rot.shape == (12, 12) and (scale > 0).all()
+
+
+def test_ica_and_nmf_fit():
+    from sparse_coding__amd.baselines.ica import ICAEncoder, NMFEncoder
+
+    rng = np.random.default_rng(0)
+    S = torch.tensor(rng.laplace(size=(2000, 4)), dtype=torch.float32)
+    M = torch.tensor(rng.normal(size=(4, 4)), dtype=torch.float32)
+    X = S @ M
+    ica = ICAEncoder(4)
+    ica.train(X)
+    c = ica.encode(X[:5])
+    assert c.shape == (5, 4) and ica.get_learned_dict().shape == (4, 4)
+    assert ica.to_topk_dict(2).get_learned_dict().shape == (8, 4)
+    nmf = NMFEncoder(4, n_components=3, max_iter=300)
+    Xp = X.clone()
+    nmf.train(Xp)
+    assert torch.equal(Xp, X)  # fix B#21: inputs are not mutated
+    assert nmf.encode(X[:5]).shape == (5, 3)
