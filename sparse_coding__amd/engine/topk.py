@@ -1,0 +1,89 @@
+"""``FusedTopKEnsemble``: top-k dictionary learning for many k in one pass (MI355X path).
+
+Per step, for all models at once (reference runs a Python loop over models because
+k differs, ``autoencoders/ensemble.py:100-116``):
+
+1. scores = x D_hat^T                     grouped MFMA GEMM (fp32 out)
+2. (idx, val) = top-k(scores), ReLU       radix-select kernel, per-model k on device
+3. x_hat = sum val D_hat[idx]; R = x_hat - x; code gradients <R, D_hat[idx]>
+                                           one wave per row (sparse gather from L2)
+4. dD_hat = code^T R + dscore^T x          ONE MFMA GEMM with two K segments over the
+                                           scattered (dense bf16) code / dscore
+5. Adam with the row-norm Jacobian (D_hat = dict / |dict|) + bf16 shadow
+"""
+
+from __future__ import annotations
+
+import torch
+
+from ..ops import adam as adam_ops
+from ..ops import gemm as gemm_ops
+from ..ops import topk as topk_ops
+
+
+class FusedTopKEnsemble:
+    def __init__(self, models, sig=None, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999), eps=1e-8):
+        from ..models.topk import TopKEncoder
+
+        self.sig = sig or TopKEncoder
+        self.device = dev = torch.device(device)
+        self.n_models = G = len(models)
+        self.batch_size = B = int(batch_size)
+        self.n, self.d = models[0][0]["dict"].shape
+        n, d = self.n, self.d
+        if B % 128 or n % 128 or d % 256:
+            raise ValueError(f"fused top-k needs B%128==0, n%128==0, d%256==0 (B={B}, n={n}, d={d})")
+        self.params = {"dict": torch.stack([m[0]["dict"].detach().float() for m in models]).to(dev).contiguous()}
+        self.m = {"dict": torch.zeros_like(self.params["dict"])}
+        self.v = {"dict": torch.zeros_like(self.params["dict"])}
+        self.k = torch.tensor([int(m[1]["sparsity"]) for m in models], dtype=torch.int32, device=dev)
+        self.kmax = int(self.k.max())
+        self.meta = [dict(m[1]) for m in models]
+        lrs = lr if isinstance(lr, (list, tuple)) else [lr] * G
+        self.lr = torch.tensor([float(x) for x in lrs], device=dev)
+        self.betas, self.eps = betas, eps
+        self.step_count = 0
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        bf = torch.bfloat16
+        self.shadow = torch.empty(G, n, d, device=dev, dtype=bf)
+        self.norms = torch.ones(G, n, device=dev)
+        adam_ops.shadow_rows(self.params["dict"], self.shadow, self.norms, normalize=True)
+        self.scores = torch.empty(G, B, n, device=dev)
+        self.r = torch.empty(G, B, d, device=dev, dtype=bf)
+        self.row_se = torch.empty(G, B, device=dev)
+        self.codebuf = torch.zeros(G, B, n, device=dev, dtype=bf)
+        self.dscbuf = torch.zeros(G, B, n, device=dev, dtype=bf)
+        self.g = torch.empty(G, n, d, device=dev)
+        self.idx = self.val = None
+
+    def step_batch(self, batch):
+        x = batch.to(self.device, torch.bfloat16).contiguous()
+        G, B, n, d = self.n_models, self.batch_size, self.n, self.d
+        gemm_ops.matmul_nt(x, self.shadow, self.scores)
+        self.idx, self.val = topk_ops.topk_select(self.scores, self.k, self.kmax)
+        topk_ops.decode_grad(self.idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
+                             self.dscbuf)
+        gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g], 2.0 / (B * d))
+        topk_ops.clear(self.idx, self.codebuf, self.dscbuf)
+        adam_ops.adam_rows([dict(p=self.params["dict"], g=self.g, m=self.m["dict"], v=self.v["dict"],
+                                 shadow=self.shadow, norms=self.norms, norm=True)],
+                           self.lr, self.step_count + 1, *self.betas, self.eps, step_dev=self.step_dev)
+        self.step_dev += 1
+        self.step_count += 1
+        return self.row_se.sum(dim=1) / (B * d)  # per-model MSE (the reference's loss), on device
+
+    def encode(self, x):
+        """Dense top-k codes [G, B, n] for ``x`` [B, d] with the current dictionaries."""
+        xb = x.to(self.device, torch.bfloat16).contiguous()
+        scores = torch.empty(self.n_models, x.shape[0], self.n, device=self.device)
+        gemm_ops.matmul_nt(xb, self.shadow, scores)
+        idx, val = topk_ops.topk_select(scores, self.k, self.kmax)
+        return torch.zeros_like(scores).scatter_(-1, idx.long(), val)
+
+    def unstack(self, device="cpu"):
+        return [({"dict": self.params["dict"][i].detach().to(device).clone()},
+                 {k: (v.detach().to(device).clone() if torch.is_tensor(v) else v) for k, v in self.meta[i].items()})
+                for i in range(self.n_models)]
+
+    def to_learned_dicts(self, device="cpu"):
+        return [self.sig.to_learned_dict(p, b) for p, b in self.unstack(device)]

@@ -57,12 +57,11 @@ def _declare(lib):
                          c_float, c_float, c_int, c_void_p, c_void_p],
     }
     optional = {
-        "sc_topk_encode": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                           c_int, c_long, c_void_p],
-        "sc_topk_decode_loss": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                c_int, c_int, c_int, c_int, c_int, c_void_p],
-        "sc_topk_grad_dict": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                              c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+        "sc_topk_select": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                           c_void_p],
+        "sc_topk_decode_grad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+        "sc_topk_clear": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p],
         "sc_fista": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
         "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_void_p],

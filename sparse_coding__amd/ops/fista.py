@@ -97,15 +97,18 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
     Db = D.to(torch.bfloat16).contiguous()
     Dtb = Db.transpose(1, 2).contiguous()
     A = torch.empty(G, B, n, device=dev)
-    Res = torch.empty(G, B, d, device=dev) if with_res else None
     a0 = A0.float().contiguous() if A0 is not None else None
     mom = momentum_schedule(max(iters, 1)).to(dev)
     rc = _lib.lib().sc_fista(_lib.ptr(Xb), _lib.ptr(Db), _lib.ptr(Dtb), _lib.ptr(a0), _lib.ptr(eta), _lib.ptr(lam),
-                             _lib.ptr(mom), _lib.ptr(A), _lib.ptr(Res), G, B, n, d, iters, _lib.stream_handle())
+                             _lib.ptr(mom), _lib.ptr(A), 0, G, B, n, d, iters, _lib.stream_handle())
     if rc == 2 and backend == "auto":
         return fista_torch(X, D, lam, A0, iters, eta)
     _lib.check(rc, "sc_fista")
-    return A, Res
+    if not with_res:
+        return A, None
+    # final residual in fp32 against the exact dictionary (one plain GEMM per model)
+    Xf = X.float() if X.dim() == 3 else X.float().expand(G, *X.shape)
+    return A, Xf - torch.bmm(A, D.float())
 
 
 def hessian_ema(H, A, history: int = 300):

@@ -1,0 +1,45 @@
+"""Host wrappers of the top-k kernels (``csrc/topk.hip``)."""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool = False, relu: bool = True):
+    """Per-row top-k of ``scores`` [G, B, n] fp32 with per-model ``k`` (int32 [G]).
+
+    Returns (idx int32 [G, B, kmax], val fp32 [G, B, kmax]); slots >= k[g] are (0, 0.0).
+    ``absolute`` selects by |score| (PCA-style) and keeps the signed value; ``relu``
+    clamps kept values at 0 (TopKEncoder semantics)."""
+    G, B, n = scores.shape
+    if scores.dtype != torch.float32 or not scores.is_contiguous():
+        raise ValueError("scores must be contiguous fp32")
+    if k.dtype != torch.int32 or k.numel() != G:
+        raise ValueError("k must be int32[G]")
+    idx = torch.empty(G, B, kmax, device=scores.device, dtype=torch.int32)
+    val = torch.empty(G, B, kmax, device=scores.device, dtype=torch.float32)
+    rc = _lib.lib().sc_topk_select(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n, kmax,
+                                   int(absolute), int(relu), _lib.stream_handle())
+    _lib.check(rc, "sc_topk_select")
+    return idx, val
+
+
+def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None):
+    """Sparse decode + residual (bf16 r_out [G, B, d]) + per-row squared error; with the dense
+    buffers, also scatter codes and code gradients <R, D[idx]> (units of R) for the wgrad GEMM."""
+    G, B, kmax = idx.shape
+    n, d = D.shape[1], D.shape[2]
+    sx = 0 if x.dim() == 2 else B * d
+    rc = _lib.lib().sc_topk_decode_grad(_lib.ptr(idx), _lib.ptr(val), _lib.ptr(k), _lib.ptr(D), _lib.ptr(x), sx,
+                                        _lib.ptr(r_out), _lib.ptr(row_se), _lib.ptr(codebuf), _lib.ptr(dscbuf),
+                                        G, B, n, d, kmax, _lib.stream_handle())
+    _lib.check(rc, "sc_topk_decode_grad")
+
+
+def clear(idx, a, b):
+    G, B, kmax = idx.shape
+    n = a.shape[-1]
+    rc = _lib.lib().sc_topk_clear(_lib.ptr(idx), _lib.ptr(a), _lib.ptr(b), G * B, n, kmax, _lib.stream_handle())
+    _lib.check(rc, "sc_topk_clear")

@@ -230,3 +230,73 @@ def test_fused_adam_epilogue_matches_separate_adam():
             assert cos > 0.999, (sig.__name__, k, cos)
         torch.testing.assert_close(a.norms, b.norms, rtol=2e-3, atol=1e-4)
         _close(a.dec_shadow, b.dec_shadow, rtol=2e-2, atol=2e-2)
+
+
+def test_topk_select_exact():
+    from sparse_coding__amd.ops import topk as T
+
+    torch.manual_seed(6)
+    G, B, n = 3, 64, 6144
+    scores = torch.randn(G, B, n, device=DEV)
+    scores[0, 0, :10] = 5.0  # ties at the threshold
+    k = torch.tensor([1, 32, 150], device=DEV, dtype=torch.int32)
+    idx, val = T.topk_select(scores, k, 150, relu=False)
+    for g in range(G):
+        kg = int(k[g])
+        ref = torch.topk(scores[g], kg, dim=-1).values.sort(dim=-1).values
+        got = val[g, :, :kg].sort(dim=-1).values
+        torch.testing.assert_close(got, ref)
+        torch.testing.assert_close(scores[g].gather(-1, idx[g, :, :kg].long()), val[g, :, :kg])
+        assert (val[g, :, kg:] == 0).all()
+        assert idx[g, :, :kg].sort(-1).values.diff(dim=-1).ne(0).all()  # no duplicates
+    ia, va = T.topk_select(scores, k, 150, absolute=True, relu=False)
+    ref = torch.topk(scores[2].abs(), 150, dim=-1).values.sort(-1).values
+    torch.testing.assert_close(va[2].abs().sort(-1).values, ref)
+
+
+def test_fused_topk_matches_autograd():
+    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
+    from sparse_coding__amd.models.topk import TopKEncoder
+
+    torch.manual_seed(7)
+    d, n, B = 256, 1024, 256
+    models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
+    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3)
+    x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
+    mse = eng.step_batch(x)
+    torch.cuda.synchronize()
+    for i, (p, b) in enumerate(models):
+        pr = {"dict": p["dict"].clone().requires_grad_()}
+        loss, _ = TopKEncoder.loss(pr, b, x.float())
+        torch.testing.assert_close(mse[i], loss.detach(), rtol=2e-2, atol=1e-4)
+        loss.backward()
+        g_ref = pr["dict"].grad
+        # one Adam step from zero moments moves every parameter by ~lr * sign(g)
+        moved = eng.params["dict"][i] - p["dict"]
+        agree = (torch.sign(moved) == -torch.sign(g_ref)) | (g_ref.abs() < 1e-7)
+        assert agree.float().mean() > 0.97, agree.float().mean()
+
+
+@pytest.mark.parametrize("G,B,n,d", [(2, 64, 512, 512), (3, 32, 2048, 512), (1, 48, 1024, 1024)])
+def test_fista_kernel_matches_oracle(G, B, n, d):
+    from sparse_coding__amd.ops import fista as F
+
+    torch.manual_seed(8)
+    D = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1)
+    X = torch.randn(B, d, device=DEV)
+    A0 = torch.relu(torch.randn(G, B, n, device=DEV)) * 0.05
+    lam = torch.linspace(1e-3, 3e-2, G, device=DEV)
+    eta = F.step_size(D)
+    # oracle on the same bf16-rounded operands the kernel multiplies
+    Db = D.to(torch.bfloat16).float()
+    Xb = X.to(torch.bfloat16).float()
+    A_ref, _ = F.fista_torch(Xb, Db, lam, A0, iters=30, eta=eta)
+    R_ref = X - torch.bmm(A_ref, D)
+    A, R = F.fista(X, D, lam, A0, iters=30, eta=eta, backend="hip")
+    torch.cuda.synchronize()
+    err_a = (A - A_ref).abs().max().item() / (A_ref.abs().max().item() + 1e-6)
+    err_r = (R - R_ref).abs().max().item() / (R_ref.abs().max().item() + 1e-6)
+    assert err_a < 3e-2 and err_r < 3e-2, (err_a, err_r)
+    def obj(A_, R_):
+        return 0.5 * R_.pow(2).sum((1, 2)) + lam * A_.abs().sum((1, 2))
+    torch.testing.assert_close(obj(A, R), obj(A_ref, R_ref), rtol=1e-2, atol=1e-3)
