@@ -1,0 +1,194 @@
+"""``EnsembleTrainer``: one facade over the three training engines.
+
+* ``FusedSAEEnsemble`` (gfx950 kernels) for untied / tied / masked SAEs and the SAE
+  step of ``FunctionalFista``;
+* ``FusedTopKEnsemble`` (gfx950 kernels) for ``TopKEncoder`` with per-model k;
+* ``FunctionalEnsemble`` (eager torch.func, CPU or GPU) for everything else and as
+  the CPU oracle.
+
+``engine="auto"`` picks the fused path on a GPU when the shapes fit the kernels
+(B % 128, n % 128, d % 256) and otherwise falls back to eager -- explicitly, with
+the reason recorded in ``trainer.engine_reason``.  The FISTA dictionary update of
+the fork (reference ``big_sweep.py:176-198``) is a post-step hook.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..models.fista import FistaDictUpdater, FunctionalFista
+from ..models.signatures import unit_rows
+from ..models.topk import TopKEncoder
+from .ensemble import FunctionalEnsemble
+from .optim import adam
+
+
+def _fused_ok(models, sig, batch_size, device) -> Tuple[bool, str]:
+    if not (torch.cuda.is_available() and torch.device(device).type == "cuda"):
+        return False, "no GPU"
+    from ..ops import _lib
+
+    if not _lib.available():
+        raise RuntimeError("GPU present but the gfx950 kernel library failed to load")
+    p0, b0 = models[0]
+    key = "dict" if sig is TopKEncoder else "encoder"
+    if key not in p0:
+        return False, f"signature {sig.__name__} has no '{key}' parameter"
+    n, d = p0[key].shape
+    if batch_size % 128 or n % 128 or d % 256:
+        return False, f"shape B={batch_size}, n={n}, d={d} not tiled by the fused kernels"
+    if sig is TopKEncoder:
+        return True, "fused top-k"
+    if getattr(sig, "fused_kind", None) is None:
+        return False, f"no fused kernels for {sig.__name__}"
+    if getattr(sig, "fused_kind") == "tied":
+        for k, ref in (("center_rot", None), ("center_trans", 0.0), ("center_scale", 1.0)):
+            if k in b0:
+                t = b0[k].float()
+                ok = torch.equal(t.cpu(), torch.eye(d)) if ref is None else bool((t == ref).all())
+                if not ok:
+                    return False, "non-identity centering (eager path)"
+    return True, f"fused {sig.fused_kind} SAE"
+
+
+class EnsembleTrainer:
+    def __init__(self, models: List[Tuple[dict, dict]], sig, lr: float = 1e-3, batch_size: int = 256,
+                 device="cuda", engine: str = "auto", name: str = "ensemble", args: Optional[dict] = None,
+                 fista_iters: int = 500, fista_backend: str = "auto", persist_hessian: bool = False,
+                 basis_normalize: str = "column", use_graph: bool = False):
+        self.sig = sig
+        self.name = name
+        self.args = dict(args or {})
+        self.batch_size = batch_size
+        self.device = torch.device(device)
+        self.n_models = len(models)
+        self.meta = [dict(b) for _, b in models]
+        ok, why = _fused_ok(models, sig, batch_size, device) if engine in ("auto", "fused") else (False, "eager")
+        if engine == "fused" and not ok:
+            raise ValueError(f"fused engine requested but unavailable: {why}")
+        self.engine_reason = why
+        self.kind = "eager"
+        if ok and sig is TopKEncoder:
+            from .topk import FusedTopKEnsemble
+
+            self.impl = FusedTopKEnsemble(models, sig, lr=lr, batch_size=batch_size, device=device)
+            self.kind = "fused-topk"
+        elif ok:
+            from .fused import FusedSAEEnsemble
+
+            self.impl = FusedSAEEnsemble(models, sig, lr=lr, batch_size=batch_size, device=device)
+            if use_graph:
+                self.impl.enable_graph()
+            self.kind = "fused-sae"
+        else:
+            self.impl = FunctionalEnsemble(models, sig, adam, {"lr": lr}, device=device,
+                                           no_stacking=sig is TopKEncoder)
+        self.fista = None
+        if sig is FunctionalFista:
+            self.fista = FistaDictUpdater(num_iter=fista_iters, persist_hessian=persist_hessian,
+                                          normalize=basis_normalize, backend=fista_backend)
+        self.last_loss = None
+        self.last_losses: Dict[str, torch.Tensor] = {}
+        self.steps = 0
+
+    # ------------------------------------------------------------------ training
+    def step(self, batch: torch.Tensor) -> torch.Tensor:
+        """One optimizer step of every model; returns per-model total loss [G] on device."""
+        if self.kind == "fused-sae":
+            out = self.impl.step_batch(batch)
+            self.last_losses = {"loss": out[:, 0], "l_reconstruction": out[:, 1], "l_l1": out[:, 2],
+                                "l_bias_decay": out[:, 3], "l0": out[:, 4]}
+            codes = None
+        elif self.kind == "fused-topk":
+            mse = self.impl.step_batch(batch)
+            self.last_losses = {"loss": mse}
+            codes = None
+        else:
+            loss, aux = self.impl.step_batch(batch.to(self.device, torch.float32))
+            self.last_losses = dict(loss)
+            codes = aux.get("c") if isinstance(aux, dict) else None
+        if self.fista is not None:
+            self._fista_update(batch, codes)
+        self.steps += 1
+        self.last_loss = self.last_losses["loss"]
+        return self.last_loss
+
+    def _fista_update(self, batch, codes):
+        x = batch.to(self.device, torch.float32)
+        if self.kind == "fused-sae":
+            eng = self.impl
+            new, _, _ = self.fista(eng.params["decoder"], x, eng.c.float(), eng.l1)
+            eng.params["decoder"].copy_(new)
+            eng.refresh_shadows()
+        else:
+            ens = self.impl
+            l1 = ens.buffers["l1_alpha"]
+            new, _, _ = self.fista(ens.params["decoder"], x, codes.float(), l1)
+            ens.params["decoder"].data.copy_(new)
+
+    # ------------------------------------------------------------------ export / state
+    def hyperparams(self, ensemble_hyperparams: Sequence[str] = (), buffer_hyperparams: Sequence[str] = ("l1_alpha",)
+                    ) -> List[dict]:
+        out = []
+        for meta in self.meta:
+            hp = {}
+            for k in ensemble_hyperparams:
+                if k not in self.args:
+                    raise ValueError(f"Hyperparameter {k} not found in args")
+                hp[k] = self.args[k]
+            for k in buffer_hyperparams:
+                if k in meta:
+                    v = meta[k]
+                    hp[k] = v.item() if torch.is_tensor(v) else v
+            out.append(hp)
+        return out
+
+    def to_learned_dicts(self, ensemble_hyperparams=("dict_size",), buffer_hyperparams=("l1_alpha",),
+                         device="cpu") -> List[Tuple[Any, dict]]:
+        lds = self.impl.to_learned_dicts(device)
+        return list(zip(lds, self.hyperparams(ensemble_hyperparams, buffer_hyperparams)))
+
+    def losses_host(self) -> List[Dict[str, float]]:
+        host = {k: v.detach().float().cpu() for k, v in self.last_losses.items() if torch.is_tensor(v)}
+        return [{k: float(v[i]) for k, v in host.items()} for i in range(self.n_models)]
+
+    def state_dict(self) -> Dict[str, Any]:
+        st = {"kind": self.kind, "steps": self.steps, "name": self.name, "args": self.args}
+        if self.kind == "fused-sae":
+            st["impl"] = self.impl.state_dict()
+        elif self.kind == "fused-topk":
+            st["impl"] = {"params": self.impl.params, "m": self.impl.m, "v": self.impl.v,
+                          "step": self.impl.step_count}
+        else:
+            st["impl"] = {"params": self.impl.params, "optim": self.impl.optim_states}
+        if self.fista is not None and self.fista.hessian is not None:
+            st["hessian"] = self.fista.hessian
+        return st
+
+    def load_state_dict(self, st: Dict[str, Any]):
+        if st["kind"] != self.kind:
+            raise ValueError(f"checkpoint engine {st['kind']} != {self.kind}")
+        self.steps = int(st["steps"])
+        imp = st["impl"]
+        if self.kind == "fused-sae":
+            self.impl.load_state_dict(imp)
+        elif self.kind == "fused-topk":
+            for d_ in ("params", "m", "v"):
+                for k, t in imp[d_].items():
+                    getattr(self.impl, d_)[k].copy_(t)
+            self.impl.step_count = int(imp["step"])
+            self.impl.step_dev.fill_(self.impl.step_count)
+            from ..ops import adam as adam_ops
+
+            adam_ops.shadow_rows(self.impl.params["dict"], self.impl.shadow, self.impl.norms, normalize=True)
+        else:
+            from torch.utils import _pytree as pytree
+
+            for a, b in zip(pytree.tree_leaves(self.impl.params), pytree.tree_leaves(imp["params"])):
+                a.data.copy_(b)
+            for a, b in zip(pytree.tree_leaves(self.impl.optim_states), pytree.tree_leaves(imp["optim"])):
+                a.copy_(b)
+        if "hessian" in st and self.fista is not None:
+            self.fista.hessian = st["hessian"].to(self.device)

@@ -1,0 +1,139 @@
+"""The fork's FISTA L1 sweep CLI (reference ``basic_l1_sweep.py:48-152``).
+
+Trains ``l1_value_n`` dictionaries (log-spaced L1) of size ``ratio * d`` over every
+chunk of ``dataset_dir`` for ``n_repetitions`` epochs, saving
+``learned_dicts_epoch_{e}_chunk_{c}.pt`` after every chunk (or
+``learned_dicts_epoch_{e}.pt`` per epoch).  Differences from the reference:
+
+* chunks are read by the native prefetcher into an HBM ring; batches are gathered
+  on device (no host ``BatchSampler``);
+* the FISTA step runs in the persistent gfx950 kernel, the SAE step in the fused
+  kernels (``signature=fista``), or plain tied/untied SAEs (``signature=tied|sae``);
+* no ``time.sleep(600)`` / OS-suspend at the end (B#17);
+* checkpoints are reference-loadable (``autoencoders.*`` class paths).
+
+``python -m sparse_coding__amd.train.basic_l1_sweep --dataset_dir D --output_dir O --ratio 4``
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..data.chunks import ChunkFolder
+from ..data.ring import DeviceRing
+from ..engine.trainer import EnsembleTrainer
+from ..models.fista import FunctionalFista
+from ..models.signatures import FunctionalSAE, FunctionalTiedSAE
+from ..utils import checkpoint as ckpt
+from ..utils.config import SweepArgs
+from .sweep import ensemble_train_loop
+
+_SIGS = {"fista": FunctionalFista, "sae": FunctionalSAE, "tied": FunctionalTiedSAE}
+
+
+class ProgressBar:
+    """Chunk/epoch progress line (reference basic_l1_sweep.py:17-46), tqdm when importable."""
+
+    def __init__(self, total, chunk_idx, n_chunks, epoch_idx, n_repetitions, enabled=True):
+        desc = (f"Epoch {epoch_idx + 1}/{n_repetitions} - " if n_repetitions > 1 else "") + \
+            f"Chunk {chunk_idx + 1}/{n_chunks}"
+        self.bar = None
+        if enabled:
+            try:
+                import tqdm
+
+                self.bar = tqdm.tqdm(total=total, desc=desc, mininterval=1.0)
+            except ImportError:
+                pass
+        self._value = 0
+
+    @property
+    def value(self):
+        return self._value
+
+    @value.setter
+    def value(self, v):
+        if self.bar is not None:
+            self.bar.update(v - self._value)
+        self._value = v
+
+    def __call__(self, i, n):
+        self.value = i
+
+    def close(self):
+        if self.bar is not None:
+            self.bar.close()
+
+
+def basic_l1_sweep(dataset_dir: str, output_dir: str, ratio: float, l1_values=np.logspace(-4, -2, 16),
+                   batch_size: int = 128, device: Optional[str] = None, lr: float = 1e-3, n_repetitions: int = 1,
+                   save_after_every: bool = False, signature: str = "fista", fista_iters: int = 500,
+                   fista_backend: str = "auto", persist_hessian: bool = False, basis_normalize: str = "column",
+                   engine: str = "auto", seed: int = 0, progress: bool = True, max_batches: Optional[int] = None
+                   ) -> List[str]:
+    """Returns the list of checkpoint paths written."""
+    device = torch.device(device or ("cuda:0" if torch.cuda.is_available() else "cpu"))
+    folder = ChunkFolder(dataset_dir)
+    if not folder.indices:
+        raise FileNotFoundError(f"Dataset not found at {dataset_dir}")
+    d = folder.meta(folder.indices[0])[0][1]
+    latent = int(d * ratio)
+    sig = _SIGS[signature]
+    torch.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    print(f"Initializing {len(l1_values)} models with latent dimension {latent}...")
+    models = [sig.init(d, latent, float(l1), device=device) for l1 in l1_values]
+    trainer = EnsembleTrainer(models, sig, lr=lr, batch_size=batch_size, device=device, engine=engine,
+                              name="ensemble", args={"batch_size": batch_size, "device": str(device),
+                                                     "dict_size": latent},
+                              fista_iters=fista_iters, fista_backend=fista_backend,
+                              persist_hessian=persist_hessian, basis_normalize=basis_normalize)
+    rows_max = max(folder.meta(i)[0][0] for i in folder.indices)
+    fused = trainer.kind.startswith("fused")
+    ring = DeviceRing(rows_max, d, device=device, dtype=torch.bfloat16 if fused else torch.float32, seed=seed)
+    os.makedirs(output_dir, exist_ok=True)
+    written = []
+    n_chunks = len(folder)
+    print("Training...")
+    for epoch in range(n_repetitions):
+        order = rng.permutation(folder.indices)
+        handle = folder.prefetch(int(order[0]))
+        for ci, chunk in enumerate(order):
+            host = folder.get(handle)
+            if ci + 1 < len(order):
+                handle = folder.prefetch(int(order[ci + 1]))
+            ring.size = ring.head = 0
+            ring.push(host.to(device, non_blocking=True))
+            n = ring.batches_per_epoch(batch_size)
+            if max_batches is not None:
+                n = min(n, max_batches)
+            bar = ProgressBar(n, ci, n_chunks, epoch, n_repetitions, enabled=progress)
+            ensemble_train_loop(trainer, ring, batch_size, n, progress=bar)
+            bar.close()
+            if save_after_every:
+                path = os.path.join(output_dir, f"learned_dicts_epoch_{epoch}_chunk_{ci}.pt")
+                ckpt.save_learned_dicts(trainer.to_learned_dicts(["dict_size"], ["l1_alpha"]), path)
+                written.append(path)
+        if not save_after_every:
+            path = os.path.join(output_dir, f"learned_dicts_epoch_{epoch}.pt")
+            ckpt.save_learned_dicts(trainer.to_learned_dicts(["dict_size"], ["l1_alpha"]), path)
+            written.append(path)
+    return written
+
+
+def main(argv=None):
+    args = SweepArgs.from_cli(argv)
+    l1_values = np.logspace(args.l1_value_min, args.l1_value_max, args.l1_value_n)
+    basic_l1_sweep(args.dataset_dir, args.output_dir, args.ratio, l1_values, args.batch_size, args.device,
+                   args.adam_lr, args.n_repetitions, args.save_after_every, args.signature, args.fista_iters,
+                   args.fista_backend, args.persist_hessian, args.basis_normalize, args.engine, args.seed)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -125,6 +125,10 @@ def _to_cpu(obj):
         return obj.detach().cpu()
     if isinstance(obj, dict):
         return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, tuple) and hasattr(obj, "_fields"):
+        # optimizer NamedTuples -> plain lists: weights_only loading admits no custom classes,
+        # and restoring walks pytree leaves, whose order is the field order either way
+        return [_to_cpu(v) for v in obj]
     if isinstance(obj, (list, tuple)):
         return type(obj)(_to_cpu(v) for v in obj)
     return obj

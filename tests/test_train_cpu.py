@@ -1,0 +1,301 @@
+"""CPU tests of the training stack: config, logging, chunk I/O (native reader),
+harvester, trainer facade, sweep driver (+resume), experiment catalogue, the fork
+CLI, and data parallelism / sweep sharding over gloo with world_size 2.
+
+Reference test strategy: SURVEY.md section 4 (the reference has only an ad-hoc
+sweep smoke test, ``test/test_sweep.py``; these pin the behaviours it relies on).
+"""
+
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from sparse_coding__amd.data.chunks import ChunkFolder, save_chunk, storage_extent
+from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
+from sparse_coding__amd.engine.optim import adam
+from sparse_coding__amd.engine.trainer import EnsembleTrainer
+from sparse_coding__amd.models.fista import FunctionalFista
+from sparse_coding__amd.models.signatures import FunctionalSAE, FunctionalTiedSAE
+from sparse_coding__amd.utils import checkpoint as ckpt
+from sparse_coding__amd.utils.config import (EnsembleArgs, SweepArgs, SyntheticEnsembleArgs, TrainArgs,
+                                             make_hyperparam_name)
+from sparse_coding__amd.utils.logging import Logger, model_metric_names
+
+
+# ----------------------------------------------------------------------------- config / logging
+def test_config_cli_yaml_roundtrip(tmp_path):
+    cfg = EnsembleArgs.from_cli(["--tied_ae", "false", "--lr", "3e-4", "--dtype", "bfloat16", "--layer", "4"])
+    assert cfg.tied_ae is False and cfg.lr == 3e-4 and cfg.dtype == torch.bfloat16 and cfg.layer == 4
+    cfg2 = EnsembleArgs.from_cli(["--tied_ae", "true"])
+    assert cfg2.tied_ae is True
+    p = tmp_path / "c.yaml"
+    cfg.to_yaml(str(p))
+    back = EnsembleArgs.from_yaml(str(p))
+    assert back.to_dict() == cfg.to_dict()
+    # constructing never parses sys.argv (B#15) and dict(cfg) works (B#14)
+    assert dict(TrainArgs())["lr"] == 1e-3
+    with pytest.raises(ValueError):
+        TrainArgs().update({"no_such_field": 1})
+    assert make_hyperparam_name({"l1_alpha": 1e-3, "dict_size": 512}) == "l1_alpha_1.00E-03_dict_size_512"
+
+
+def test_logger_jsonl(tmp_path):
+    log = Logger.from_config(str(tmp_path), use_wandb=True, config={})  # wandb absent -> JSONL only
+    names = model_metric_names("ens", [{"l1_alpha": 1e-3}], [{"loss": 1.5}])
+    assert names == {"ens_l1_alpha_1.00E-03_loss": 1.5}
+    log.log(names, 10)
+    log.close()
+    rec = json.loads(open(tmp_path / "metrics.jsonl").read().strip())
+    assert rec["step"] == 10 and rec["ens_l1_alpha_1.00E-03_loss"] == 1.5
+
+
+# ----------------------------------------------------------------------------- chunk I/O
+def test_chunk_native_reader(tmp_path):
+    x = torch.randn(1000, 64).half()
+    save_chunk(x, str(tmp_path), 0)
+    save_chunk(x[:10] * 2, str(tmp_path), 1)
+    off, size = storage_extent(str(tmp_path / "0.pt"))
+    assert size == x.numel() * 2 and off > 0
+    f = ChunkFolder(str(tmp_path), threads=3)
+    assert f.indices == [0, 1] and f.n_rows() == 1010
+    h0, h1 = f.prefetch(0), f.prefetch(1)  # two reads in flight
+    assert torch.equal(f.get(h1), x[:10] * 2)
+    assert torch.equal(f.get(h0), x)
+    # reference loader reads our chunk files
+    assert torch.equal(torch.load(tmp_path / "0.pt", weights_only=True), x)
+
+
+def test_chunk_saved_view_falls_back(tmp_path):
+    base = torch.randn(20, 8).half()
+    torch.save(base[5:10], tmp_path / "0.pt")  # a view: storage larger than the tensor
+    f = ChunkFolder(str(tmp_path))
+    assert torch.equal(f.load(0), base[5:10])
+
+
+# ----------------------------------------------------------------------------- harvester
+def test_harvester_residual_and_mlp(tmp_path):
+    from sparse_coding__amd.data.harvest import (ActivationHarvester, build_model, get_activation_size,
+                                                 make_tensor_name, setup_data, synthetic_token_batches)
+
+    model = build_model("pythia-70m", device="cpu", dtype=torch.float32, seed=0)
+    assert get_activation_size("pythia-70m", "mlp") == 2048
+    assert make_tensor_name(2, "residual", "pythia-70m")
+    h = ActivationHarvester(model, [1, 2], "mlp", out_dtype=torch.float32)
+    toks = next(synthetic_token_batches(50304, batch=2, seq_len=16))
+    acts = h.run(toks)
+    h.close()
+    assert acts[1].shape == (32, 2048) and acts[2].shape == (32, 2048)
+    rows = setup_data("pythia-70m", [str(tmp_path / "a"), str(tmp_path / "b")], [0, 1], "residual", n_chunks=2,
+                      device="cpu", batch_size=2, seq_len=16, rows_per_chunk=40, model=model)
+    assert rows == 80
+    for sub in ("a", "b"):
+        f = ChunkFolder(str(tmp_path / sub))
+        assert f.indices == [0, 1] and f.meta(0)[0] == (40, 512) and f.meta(0)[1] == torch.float16
+
+
+# ----------------------------------------------------------------------------- trainer facade
+def test_trainer_eager_matches_functional_ensemble():
+    torch.manual_seed(0)
+    models = [FunctionalSAE.init(32, 64, l1) for l1 in (1e-3, 1e-2)]
+    ref = FunctionalEnsemble([(dict(p), dict(b)) for p, b in models], FunctionalSAE, adam, {"lr": 1e-3})
+    tr = EnsembleTrainer(models, FunctionalSAE, lr=1e-3, batch_size=16, device="cpu")
+    assert tr.kind == "eager" and tr.engine_reason == "no GPU"
+    x = torch.randn(16, 32)
+    for _ in range(3):
+        l_ref, _ = ref.step_batch(x)
+        tr.step(x)
+    torch.testing.assert_close(tr.last_losses["loss"], l_ref["loss"])
+    lds = tr.to_learned_dicts(["dict_size"], ["l1_alpha"]) if "dict_size" in tr.args else tr.to_learned_dicts([], ["l1_alpha"])
+    assert len(lds) == 2 and abs(lds[1][1]["l1_alpha"] - 1e-2) < 1e-9
+    st = tr.state_dict()
+    tr2 = EnsembleTrainer(models, FunctionalSAE, lr=1e-3, batch_size=16, device="cpu")
+    tr2.load_state_dict(st)
+    tr.step(x)
+    tr2.step(x)
+    torch.testing.assert_close(tr.last_losses["loss"], tr2.last_losses["loss"])
+
+
+def test_trainer_fista_hook_changes_decoder():
+    torch.manual_seed(0)
+    models = [FunctionalFista.init(16, 32, 1e-3)]
+    tr = EnsembleTrainer(models, FunctionalFista, batch_size=32, device="cpu", fista_iters=20)
+    before = tr.impl.params["decoder"].detach().clone()
+    tr.step(torch.randn(32, 16))
+    after = tr.impl.params["decoder"].detach()
+    assert not torch.allclose(before, after)
+    torch.testing.assert_close(after[0].norm(dim=0), torch.ones(16), atol=1e-4, rtol=0)  # column norm (B#4)
+
+
+# ----------------------------------------------------------------------------- sweep / CLI
+def _tiny_init(cfg):
+    n = cfg.activation_width * 2
+    ens = []
+    for i, sig in enumerate((FunctionalSAE, FunctionalTiedSAE)):
+        models = [sig.init(cfg.activation_width, n, float(l1)) for l1 in (1e-4, 1e-3)]
+        ens.append((models, sig, {"batch_size": cfg.batch_size, "device": "cpu", "dict_size": n}, f"e{i}"))
+    return ens, ["dict_size"], ["l1_alpha"], {"dict_size": [n], "l1_alpha": [1e-4, 1e-3]}
+
+
+def _sweep_cfg(tmp_path, **kw):
+    cfg = SyntheticEnsembleArgs(use_synthetic_dataset=True, activation_width=32, n_ground_truth_components=64,
+                                chunk_size_gb=64 * 32 * 2 * 8 / 1024 ** 3, n_chunks=2, gen_batch_size=128,
+                                batch_size=32, dataset_folder=str(tmp_path / "data"),
+                                output_folder=str(tmp_path / "out"), device="cpu", log_every=4)
+    return cfg.update(kw)
+
+
+def test_sweep_synthetic_end_to_end(tmp_path):
+    from sparse_coding__amd.train.sweep import sweep
+
+    cfg = _sweep_cfg(tmp_path)
+    lds = sweep(_tiny_init, cfg)
+    assert len(lds) == 4
+    assert sorted(os.listdir(cfg.dataset_folder)) == ["0.pt", "1.pt"]
+    last = os.path.join(cfg.output_folder, "_1", "learned_dicts.pt")
+    loaded = ckpt.load_learned_dicts(last)
+    np.testing.assert_allclose([hp["l1_alpha"] for _, hp in loaded], [1e-4, 1e-3, 1e-4, 1e-3], rtol=1e-6)
+    assert os.path.exists(os.path.join(cfg.output_folder, "_1", "config.yaml"))
+    recs = [json.loads(l) for l in open(os.path.join(cfg.output_folder, "metrics.jsonl"))]
+    assert any(k.endswith("_loss") for r in recs for k in r)
+    # resume: everything done -> no further training, same dictionaries
+    lds2 = sweep(_tiny_init, cfg)
+    assert lds2 == []
+
+
+def test_sweep_resume_mid_run(tmp_path):
+    from sparse_coding__amd.train import sweep as sw
+
+    cfg = _sweep_cfg(tmp_path, n_chunks=3)
+    calls = []
+    orig = sw.ensemble_train_loop
+
+    def stop_after_first(*a, **k):
+        if len(calls) == 2:  # 2 ensembles per chunk: die on chunk 2
+            raise KeyboardInterrupt
+        calls.append(1)
+        return orig(*a, **k)
+
+    sw.ensemble_train_loop = stop_after_first
+    try:
+        with pytest.raises(KeyboardInterrupt):
+            sw.sweep(_tiny_init, cfg)
+    finally:
+        sw.ensemble_train_loop = orig
+    st = ckpt.load_training_state(os.path.join(cfg.output_folder, "train_state_rank0.pt"))
+    assert st["extra"]["next_chunk"] == 1
+    lds = sw.sweep(_tiny_init, cfg)
+    assert len(lds) == 4 and os.path.exists(os.path.join(cfg.output_folder, "_2", "learned_dicts.pt"))
+
+
+def test_experiment_catalogue_shapes():
+    from sparse_coding__amd.train import experiments as E
+
+    cfg = EnsembleArgs(activation_width=512, device="cpu", learned_dict_ratio=2.0)
+    for name in ("tied_vs_not_experiment", "simple_setoff", "long_mlp_sweep", "thresholding_experiment",
+                 "zero_l1_baseline", "run_positive_init", "fista_sweep", "pythia_1_4_b_dict"):
+        ens, eh, bh, ranges = E.INIT_FUNCS[name](cfg)
+        for models, sig, args, ename in ens:
+            assert args["dict_size"] == models[0][0][next(iter(models[0][0]))].shape[0] or sig.__name__
+            assert all(k in args for k in eh)
+    ens, _, _, ranges = E.INIT_FUNCS["simple_setoff"](cfg)
+    l1 = [float(m[1]["l1_alpha"]) for m in ens[0][0]]
+    np.testing.assert_allclose(l1, np.concatenate([[0.0], np.logspace(-4, -2, 8)]), rtol=1e-6)
+    assert E.main([]) == 2
+
+
+def test_basic_l1_sweep_cli(tmp_path):
+    from sparse_coding__amd.train.basic_l1_sweep import main
+
+    for i in range(2):
+        save_chunk(torch.randn(256, 16), str(tmp_path / "data"), i)
+    rc = main(["--dataset_dir", str(tmp_path / "data"), "--output_dir", str(tmp_path / "o"), "--ratio", "2",
+               "--l1_value_n", "2", "--batch_size", "64", "--device", "cpu", "--fista_iters", "10"])
+    assert rc == 0
+    files = sorted(os.listdir(tmp_path / "o"))
+    assert files == ["learned_dicts_epoch_0_chunk_0.pt", "learned_dicts_epoch_0_chunk_1.pt"]
+    lds = ckpt.load_learned_dicts(str(tmp_path / "o" / files[-1]))
+    assert len(lds) == 2 and lds[0][0].get_learned_dict().shape == (32, 16)
+
+
+# ----------------------------------------------------------------------------- gloo world_size 2
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, x, init, out_q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from sparse_coding__amd.parallel.data_parallel import DataParallelEnsemble
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
+
+    info = init_distributed("gloo")
+    torch.manual_seed(100 + rank)  # different init per rank: DP must broadcast rank 0's
+    models = init if rank == 0 else [FunctionalSAE.init(16, 32, 1e-3) for _ in range(2)]
+    ens = FunctionalEnsemble(models, FunctionalSAE, adam, {"lr": 1e-2})
+    dp = DataParallelEnsemble(ens, info, bucket_bytes=1024)
+    shard = x.chunk(world)[rank]
+    for _ in range(3):
+        dp.step_batch(shard)
+    # numpy arrays pickle by value (torch tensors would go through shared memory owned by this process)
+    out_q.put((rank, {k: v.detach().numpy().copy() for k, v in ens.params.items()}))
+    shutdown(info)
+
+
+def test_data_parallel_gloo_matches_single_process():
+    torch.manual_seed(0)
+    init = [FunctionalSAE.init(16, 32, 1e-3) for _ in range(2)]
+    x = torch.randn(64, 16)
+    single = FunctionalEnsemble([(dict(p), dict(b)) for p, b in init], FunctionalSAE, adam, {"lr": 1e-2})
+    for _ in range(3):
+        single.step_batch(x)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, x, init, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in single.params:
+        np.testing.assert_array_equal(res[0][k], res[1][k])
+        np.testing.assert_allclose(res[0][k], single.params[k].detach().numpy(), atol=2e-5, rtol=1e-4)
+
+
+def _shard_worker(rank, world, port, tmp, out_q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
+    from sparse_coding__amd.train.sweep import sweep
+
+    info = init_distributed("gloo")
+    cfg = _sweep_cfg(tmp)
+    lds = sweep(_tiny_init, cfg, info)
+    out_q.put((rank, [type(ld).__name__ for ld, _ in lds]))
+    shutdown(info)
+
+
+def test_sweep_sharded_over_two_ranks(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, tmp_path, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == ["UntiedSAE", "UntiedSAE"] and res[1] == ["TiedSAE", "TiedSAE"]
+    out = tmp_path / "out" / "_1"
+    assert (out / "learned_dicts_rank0.pt").exists() and (out / "learned_dicts_rank1.pt").exists()
