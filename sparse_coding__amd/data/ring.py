@@ -83,28 +83,22 @@ class DeviceRing:
         self._cursor = 0
         self.epoch += 1
 
-    def sample(self, batch_size: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Random batch (without replacement within an epoch), gathered on device."""
-        if self.size == 0:
-            raise RuntimeError("ring is empty")
-        if self._perm is None or self._cursor + batch_size > self._perm.numel():
-            self._new_epoch()
-        idx = self._perm[self._cursor:self._cursor + batch_size]
-        self._cursor += batch_size
-        if out is None:
-            return self.buf.index_select(0, idx)
-        return torch.index_select(self.buf, 0, idx, out=out)
+    def sample(self, batch_size: int, out: Optional[torch.Tensor] = None, return_index: bool = False):
+        """Random batch (without replacement within an epoch), gathered on device.
+        With ``return_index`` also returns the ring row indices ``[batch_size]``."""
+        return self.sample_shard(batch_size, 0, 1, out=out, return_index=return_index)
 
-    def sample_shard(self, batch_size: int, rank: int, world: int, out=None) -> torch.Tensor:
+    def sample_shard(self, batch_size: int, rank: int, world: int, out=None, return_index: bool = False):
         """Data-parallel sampling: every rank draws the same global permutation slice and
         keeps its own contiguous shard (DistributedSampler semantics on device)."""
+        if self.size == 0:
+            raise RuntimeError("ring is empty")
         if self._perm is None or self._cursor + batch_size * world > self._perm.numel():
             self._new_epoch()
         idx = self._perm[self._cursor + rank * batch_size:self._cursor + (rank + 1) * batch_size]
         self._cursor += batch_size * world
-        if out is None:
-            return self.buf.index_select(0, idx)
-        return torch.index_select(self.buf, 0, idx, out=out)
+        rows = self.buf.index_select(0, idx) if out is None else torch.index_select(self.buf, 0, idx, out=out)
+        return (rows, idx) if return_index else rows
 
     def batches_per_epoch(self, batch_size: int) -> int:
         return self.size // batch_size

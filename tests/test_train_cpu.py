@@ -299,3 +299,79 @@ def test_sweep_sharded_over_two_ranks(tmp_path):
     assert res[0] == ["UntiedSAE", "UntiedSAE"] and res[1] == ["TiedSAE", "TiedSAE"]
     out = tmp_path / "out" / "_1"
     assert (out / "learned_dicts_rank0.pt").exists() and (out / "learned_dicts_rank1.pt").exists()
+
+
+# ----------------------------------------------------------------------------- huge-batch DP + resampling
+def test_worst_indices_and_resample():
+    from sparse_coding__amd.train.huge_batch import WorstIndices, resample_dead
+
+    w = WorstIndices(3, "cpu")
+    w.update(torch.tensor([0, 1, 2, 3]), torch.tensor([0.1, 0.9, 0.5, 0.2]))
+    w.update(torch.tensor([7, 8]), torch.tensor([0.7, 0.05]))
+    assert w.get_worst(2).tolist() == [1, 7] and w.get_worst(5).tolist() == [1, 7, 2]
+    enc = torch.ones(5, 4)
+    m = torch.ones(5, 4)
+    vecs = torch.arange(8.0).view(2, 4)
+    n = resample_dead(enc, torch.tensor([1, 3, 4]), vecs, [m])
+    assert n == 2 and torch.equal(m[1], torch.zeros(4)) and torch.equal(m[4], torch.ones(4))
+    torch.testing.assert_close(enc[3], vecs[1] * 0.2 / 2.0)
+
+
+def test_huge_batch_torch_engine_reinit(tmp_path):
+    from sparse_coding__amd.train.huge_batch import HugeBatchArgs, train
+
+    for i in range(2):
+        save_chunk(torch.randn(512, 16), str(tmp_path / "d"), i)
+    cfg = HugeBatchArgs(dataset_folder=str(tmp_path / "d"), output_dir=str(tmp_path / "o"), batch_size=64,
+                        n_features=32, reinit=True, reinit_every=1, device="cpu", l1_alpha=0.5, log_every=2)
+    tr, hist = train(cfg)
+    assert tr.engine == "torch" and all("n_dead_feats" in h for h in hist)
+    # force 5 dead features, then resample them from the worst-reconstructed rows
+    from sparse_coding__amd.data.ring import DeviceRing
+
+    ring = DeviceRing(512, 16, device="cpu", dtype=torch.float32)
+    ring.push(torch.randn(512, 16))
+    tr.reset_counts()
+    with torch.no_grad():
+        tr.module.threshold[:5] = -1e4
+    for _ in range(4):
+        x, idx = ring.sample(64, return_index=True)
+        tr.step(x, idx)
+    before = tr.module.encoder.detach().clone()
+    assert tr.resample(ring) == 5
+    changed = (tr.module.encoder.detach() != before).any(0)
+    assert changed[:5].all() and not changed[5:].any()
+    sd = torch.load(tmp_path / "o" / "sae_1.pt", weights_only=True)
+    assert set(sd) == {"decoder", "encoder", "threshold", "centering"} and sd["encoder"].shape == (16, 32)
+
+
+def _huge_worker(rank, world, port, folder, out, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
+    from sparse_coding__amd.train.huge_batch import HugeBatchArgs, train
+
+    info = init_distributed("gloo")
+    cfg = HugeBatchArgs(dataset_folder=folder, output_dir=out, batch_size=32, n_features=32, reinit=True,
+                        reinit_every=1, device="cpu", l1_alpha=0.5, log_every=0)
+    tr, hist = train(cfg, info)
+    q.put((rank, tr.module.encoder.detach().numpy().copy(), hist[-1]["n_dead_feats"]))
+    shutdown(info)
+
+
+def test_huge_batch_ddp_gloo_two_ranks(tmp_path):
+    for i in range(2):
+        save_chunk(torch.randn(256, 16), str(tmp_path / "d"), i)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_huge_worker, args=(r, 2, port, str(tmp_path / "d"), str(tmp_path / "o"), q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (enc, nd) for r, enc, nd in (q.get(timeout=240) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0][0], res[1][0])  # replicas identical after DDP + resampling
+    assert res[0][1] == res[1][1]

@@ -1,0 +1,124 @@
+"""GPU tests of the training stack on MI355X: the sweep driver and FISTA CLI run the
+fused gfx950 engines end to end, the harvester feeds the HBM ring, chunk I/O lands
+in HBM."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from sparse_coding__amd.data.chunks import ChunkFolder, save_chunk
+from sparse_coding__amd.engine.trainer import EnsembleTrainer
+from sparse_coding__amd.models.signatures import FunctionalSAE, FunctionalTiedSAE
+from sparse_coding__amd.models.topk import TopKEncoder
+from sparse_coding__amd.utils import checkpoint as ckpt
+from sparse_coding__amd.utils.config import SyntheticEnsembleArgs
+
+pytestmark = pytest.mark.gpu
+
+
+def _init(cfg):
+    n = cfg.activation_width * 2
+    ens = []
+    for i, sig in enumerate((FunctionalSAE, FunctionalTiedSAE)):
+        models = [sig.init(cfg.activation_width, n, float(l1)) for l1 in (1e-4, 1e-3, 3e-3)]
+        ens.append((models, sig, {"batch_size": cfg.batch_size, "device": cfg.device, "dict_size": n}, f"e{i}"))
+    return ens, ["dict_size"], ["l1_alpha"], {}
+
+
+def test_sweep_fused_on_gpu(tmp_path):
+    from sparse_coding__amd.train.sweep import sweep
+
+    cfg = SyntheticEnsembleArgs(use_synthetic_dataset=True, activation_width=256, n_ground_truth_components=512,
+                                chunk_size_gb=16384 * 256 * 2 / 1024 ** 3, n_chunks=2, batch_size=256,
+                                dataset_folder=str(tmp_path / "d"), output_folder=str(tmp_path / "o"),
+                                device="cuda:0", log_every=16)
+    lds = sweep(_init, cfg)
+    assert len(lds) == 6
+    loaded = ckpt.load_learned_dicts(os.path.join(cfg.output_folder, "_1", "learned_dicts.pt"))
+    x = torch.load(os.path.join(cfg.dataset_folder, "0.pt"), weights_only=True)[:4096].float()
+    for ld, hp in loaded:
+        ld.to_device("cpu")
+        xh = ld.predict(x)
+        fvu = ((xh - x) ** 2).sum() / ((x - x.mean(0)) ** 2).sum()
+        assert torch.isfinite(fvu)
+        if hp["l1_alpha"] < 2e-4:  # weakly regularised models learn in 128 steps; strong L1 may kill all features
+            assert fvu < 0.9, (type(ld).__name__, hp, float(fvu))
+
+
+def test_trainer_engines_selected():
+    m = [FunctionalSAE.init(256, 512, 1e-3) for _ in range(2)]
+    assert EnsembleTrainer(m, FunctionalSAE, batch_size=256, device="cuda:0").kind == "fused-sae"
+    t = [TopKEncoder.init(256, 512, 8) for _ in range(2)]
+    assert EnsembleTrainer(t, TopKEncoder, batch_size=256, device="cuda:0").kind == "fused-topk"
+    odd = [FunctionalSAE.init(200, 512, 1e-3)]
+    tr = EnsembleTrainer(odd, FunctionalSAE, batch_size=256, device="cuda:0")
+    assert tr.kind == "eager" and "not tiled" in tr.engine_reason
+
+
+def test_fista_cli_on_gpu(tmp_path):
+    from sparse_coding__amd.train.basic_l1_sweep import basic_l1_sweep
+
+    g = torch.Generator().manual_seed(0)
+    for i in range(2):
+        save_chunk(torch.randn(4096, 256, generator=g), str(tmp_path / "d"), i)
+    paths = basic_l1_sweep(str(tmp_path / "d"), str(tmp_path / "o"), 2.0, np.logspace(-4, -3, 2), batch_size=256,
+                           device="cuda:0", save_after_every=True, fista_iters=50, progress=False, max_batches=4)
+    assert len(paths) == 2
+    lds = ckpt.load_learned_dicts(paths[-1])
+    assert all(torch.isfinite(ld.get_learned_dict()).all() for ld, _ in lds)
+
+
+def test_harvest_into_ring_gpu():
+    from sparse_coding__amd.data.harvest import (ActivationHarvester, build_model, harvest_to_ring,
+                                                 synthetic_token_batches)
+    from sparse_coding__amd.data.ring import DeviceRing
+
+    model = build_model("pythia-70m", device="cuda:0", seed=0)
+    h = ActivationHarvester(model, [2], "residual")
+    ring = DeviceRing(8192, 512, device="cuda:0")
+    harvest_to_ring(h, synthetic_token_batches(50304, batch=8, seq_len=256), {2: ring}, 8192, device="cuda:0")
+    h.close()
+    assert ring.size == 8192 and torch.isfinite(ring.view().float()).all()
+    assert ring.view().float().std() > 0
+
+
+def test_chunk_to_hbm(tmp_path):
+    x = torch.randn(20000, 512).half()
+    save_chunk(x, str(tmp_path), 0)
+    f = ChunkFolder(str(tmp_path))
+    y = f.load(0, device="cuda:0")
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), x)
+
+
+def test_huge_batch_fused_reinit(tmp_path):
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.train.huge_batch import HugeBatchArgs, train
+
+    g = torch.Generator().manual_seed(0)
+    for i in range(2):
+        save_chunk(torch.randn(8192, 256, generator=g), str(tmp_path / "d"), i)
+    cfg = HugeBatchArgs(dataset_folder=str(tmp_path / "d"), output_dir=str(tmp_path / "o"), batch_size=256,
+                        n_features=512, reinit=True, reinit_every=1, device="cuda:0", log_every=8)
+    tr, hist = train(cfg)
+    assert tr.engine == "fused" and len(hist) == 2
+    ring = DeviceRing(8192, 256, device="cuda:0")
+    ring.push(torch.randn(8192, 256, generator=g).cuda())
+    tr.reset_counts()
+    with torch.no_grad():
+        tr.impl.params["encoder_bias"][0, :7] = -1e4
+    tr.impl.refresh_shadows()
+    for _ in range(4):
+        x, idx = ring.sample(256, return_index=True)
+        tr.step(x, idx)
+    assert int((tr.feature_counts() == 0).sum()) >= 7
+    before = tr.impl.params["encoder"][0].clone()
+    n_dead = tr.resample(ring)
+    assert n_dead >= 7
+    changed = (tr.impl.params["encoder"][0] != before).any(1)
+    assert changed[:7].all()
+    assert torch.equal(tr.impl.m["encoder"][0, :7], torch.zeros_like(tr.impl.m["encoder"][0, :7]))
+    sd = torch.load(tmp_path / "o" / "sae_1.pt", weights_only=True)
+    assert sd["encoder"].shape == (256, 512) and sd["decoder"].shape == (512, 256)
