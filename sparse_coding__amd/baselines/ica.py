@@ -23,28 +23,40 @@ class ICAEncoder(LearnedDict):
         self.scaler = StandardScaler()
 
     def to_device(self, device):
-        pass
+        for k in ("components", "offset", "scale"):
+            if hasattr(self, k):
+                setattr(self, k, getattr(self, k).to(device))
 
     def encode(self, x):
+        """``((x - mu_s) / sigma_s - mu_ica) @ W^T`` -- sklearn's StandardScaler + FastICA
+        transform as one affine map on the device (fp32)."""
         assert x.shape[1] == self.activation_size
-        xs = self.scaler.transform(x.detach().cpu().numpy().astype(np.float64))
-        return torch.tensor(self.ica.transform(xs), device=x.device, dtype=torch.float32)
+        return ((x.float() - self.offset) / self.scale) @ self.components.T
 
     def train(self, dataset):
+        """Fits on the CPU in float64, then keeps only tensors (components, offsets, scales),
+        so a trained encoder runs on the GPU and loads with ``weights_only=True``."""
         assert dataset.shape[1] == self.activation_size
         xs = self.scaler.fit_transform(dataset.detach().cpu().numpy().astype(np.float64))
         t0 = time.time()
         out = self.ica.fit_transform(xs)
         self.fit_seconds = time.time() - t0
+        mean_ica = self.ica.mean_ if getattr(self.ica, "mean_", None) is not None else 0.0
+        scale = np.where(self.scaler.scale_ == 0, 1.0, self.scaler.scale_)
+        self.components = torch.tensor(self.ica.components_, dtype=torch.float32)
+        # (x - mu_s)/sigma - mu_ica == (x - (mu_s + sigma*mu_ica)) / sigma
+        self.offset = torch.tensor(self.scaler.mean_ + scale * mean_ica, dtype=torch.float32)
+        self.scale = torch.tensor(scale, dtype=torch.float32)
+        self.n_feats = self.components.shape[0]
+        self.ica = self.scaler = None
         return out
 
     def get_learned_dict(self):
-        comps = torch.tensor(self.ica.components_, dtype=torch.float32)
-        return comps / comps.norm(dim=-1, keepdim=True)
+        return self.components / self.components.norm(dim=-1, keepdim=True)
 
     def to_topk_dict(self, sparsity):
-        comps = self.ica.components_
-        return TopKLearnedDict(np.concatenate([comps, -comps], axis=0), sparsity)
+        comps = self.components
+        return TopKLearnedDict(torch.cat([comps, -comps], dim=0), sparsity)
 
 
 class NMFEncoder(LearnedDict):
