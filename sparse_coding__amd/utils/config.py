@@ -240,6 +240,15 @@ class InterpArgs(BaseArgs):
     df_n_feats: int = 200
     top_k: int = 50
     save_loc: str = ""
+    # MI355X / offline additions
+    n_fragments: int = 50000
+    fragment_len: int = 64
+    batch_size: int = 256
+    token_file: str = ""              # LongTensor [N, S] of documents; synthetic Zipf stream if empty
+    explainer: str = "offline"        # offline | endpoint (SC_INTERP_ENDPOINT)
+    explainer_model: str = "gpt-4"
+    simulator_model: str = "gpt-3.5-turbo"
+    seed: int = 0
 
 
 @dataclass

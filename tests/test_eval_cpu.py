@@ -131,3 +131,34 @@ def test_scores_and_plots(tmp_path):
     assert P.main(["fvu", "--dataset", str(tmp_path / "0.pt"), "--files", f"SAE={tmp_path / 'ld.pt'}",
                    "--out", str(tmp_path / "cli"), "--n", "500", "--device", "cpu"]) == 0
     assert (tmp_path / "cli.png").exists()
+
+
+def test_autointerp_offline_pipeline(tmp_path):
+    from sparse_coding__amd.interp.activations import (FeatureActivationDataset, make_feature_activation_dataset,
+                                                       random_fragments)
+    from sparse_coding__amd.interp.autointerp import (TokenListSimulator, TokenStatsExplainer, correlation_score,
+                                                      interpret, parse_folder_name, read_scores)
+
+    lm = _tiny("neox")
+    torch.manual_seed(0)
+    docs = [torch.randint(0, 100, (40,)) for _ in range(64)]
+    frags = random_fragments(iter(docs), 60, fragment_len=16)
+    assert frags.shape == (60, 16)
+    sae = UntiedSAE(torch.randn(12, 32), torch.randn(12, 32), torch.zeros(12))
+    ds = make_feature_activation_dataset(lm, sae, 1, "residual", frags, max_features=8, batch_size=25)
+    assert ds.acts.shape == (60, 16, 8) and ds.maxes.shape == (60, 8)
+    # dataset matches a direct encode
+    _, cache = lm.run_with_cache(frags[:2], names_filter="blocks.1.hook_resid_post")
+    want = sae.encode(cache["blocks.1.hook_resid_post"].reshape(32, 32))[:, :8].reshape(2, 16, 8)
+    torch.testing.assert_close(ds.acts[:2].float(), want, atol=2e-2, rtol=1e-2)
+    ds.save(str(tmp_path / "ds.pt"))
+    ds2 = FeatureActivationDataset.load(str(tmp_path / "ds.pt"))
+    assert torch.equal(ds2.acts, ds.acts)
+    df = ds.to_dataframe()
+    assert float(df["feature_3_activation_5"][7]) == float(ds.acts[7, 5, 3])
+    res = interpret(ds, str(tmp_path / "res" / "sparse_coding"), 4, TokenStatsExplainer(), TokenListSimulator())
+    assert len(res) >= 1 and all(-1.0 <= r["score"] <= 1.0 for r in res.values())
+    scores = read_scores(str(tmp_path / "res"), "top_random")
+    assert "sparse_coding" in scores and len(scores["sparse_coding"][0]) == len(res)
+    assert correlation_score([[0, 1, 2]], [[0, 2, 4]]) == pytest.approx(1.0)
+    assert parse_folder_name("tied_residual_l5_r0_x") == ("tied", "residual", 5, 0.5, "x")
