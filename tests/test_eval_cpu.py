@@ -162,3 +162,39 @@ def test_autointerp_offline_pipeline(tmp_path):
     assert "sparse_coding" in scores and len(scores["sparse_coding"][0]) == len(res)
     assert correlation_score([[0, 1, 2]], [[0, 2, 4]]) == pytest.approx(1.0)
     assert parse_folder_name("tied_residual_l5_r0_x") == ("tied", "residual", 5, 0.5, "x")
+
+
+def test_analysis_helpers():
+    import numpy as np
+
+    from sparse_coding__amd.baselines.pca import BatchedPCA
+    from sparse_coding__amd.eval import analysis as A
+
+    torch.manual_seed(0)
+    lm = _tiny("gpt2")
+    # a dictionary made of the token embeddings is maximally similar to them
+    emb = lm.model.get_input_embeddings().weight.detach()[:20]
+    d = UntiedSAE(emb.clone(), emb.clone(), torch.zeros(20))
+    e, u = A.embed_unembed_similarity(lm, d)
+    assert e == pytest.approx(1.0, abs=1e-5)
+    small = torch.randn(8, 16)
+    large = torch.cat([small[torch.randperm(8)], torch.randn(8, 16)])
+    sims = A.hungarian_max_cosine(small, large)
+    np.testing.assert_allclose(sims, 1.0, atol=1e-5)
+    av, above, full = A.run_mmcs_with_larger([[small, large, torch.randn(32, 16)]])
+    assert av[0, 0] == pytest.approx(1.0, abs=1e-5) and above[0, 0] == 100.0 and av[0, 2] == 0
+    st = A.converged_feature_stats(small, large)
+    assert st["frac_converged"] == 1.0
+    enn = A.effective_number_of_neurons(torch.eye(4))
+    assert torch.allclose(enn, torch.ones(4))
+    x = torch.randn(500, 32)
+    pca = BatchedPCA(32, "cpu")
+    pca.train_batch(x)
+    sets = A.pca_baseline_sets(pca, 32, step=8)
+    sets["Added Noise"] = A.added_noise_set(32, [0.0, 0.5])
+    toks = torch.randint(0, 100, (4, 8))
+    res = A.fvu_vs_perplexity(lm, sets, x, toks, location=(0, "residual"), batch=2)
+    assert len(res["PCA (dynamic)"]) == 2 and res["Added Noise"][0][0] == pytest.approx(0.0, abs=1e-6)
+    sae = UntiedSAE(torch.randn(16, 32), torch.randn(16, 32), torch.zeros(16))
+    corr = A.moment_score_correlations(sae, x, [0, 1, 2, 3], [0.1, 0.5, 0.2, 0.9])
+    assert set(corr) == {"n_active", "mean", "var", "skew", "kurtosis", "l4_norm"}
