@@ -51,6 +51,21 @@ __device__ __forceinline__ float block_sum_256(float v, float* red) {
   return r;
 }
 
+// Block-wide sum over NW waves; `red` must hold >= NW floats of LDS.
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r += red[i];
+  __syncthreads();
+  return r;
+}
+
 // Bijective XCD-aware block remap (MI355X has 8 XCDs, each with its own L2).
 // Hardware hands consecutive block ids to different XCDs round-robin; this
 // gives each XCD a contiguous run of logical tiles so neighbouring tiles that

@@ -14,8 +14,14 @@
 //   EPI_F32 : C = alpha * acc (fp32), used for dW = c^T R and dW_e = dpre^T x
 //   EPI_BF16: C = alpha * acc (bf16), generic inference GEMM
 //
-// Tiling: 128x128 block tile, 256 threads = 4 waves in a 2x2 grid, each wave
-// owns a 64x64 sub-tile = 4x4 v_mfma_f32_16x16x32_bf16 accumulators.  Operands
+// Tiling (template "shape"): a WGM x WGN grid of waves, each owning a
+// (16 WI) x (16 WJ) sub-tile = WI x WJ v_mfma_f32_16x16x32_bf16 accumulators:
+//   S128   : 2x2 waves of 64x64   -> 128x128 block, 256 threads
+//   S256x128: 2x2 waves of 128x64 -> 256x128 block, 256 threads
+//   S256   : 2x4 waves of 128x64  -> 256x256 block, 512 threads, 1 block/CU
+// Bigger tiles raise FLOPs per staged byte (64 -> 85 -> 128 FLOP/B) and per LDS
+// fragment read (per-wave 128x64 reads 12 fragments per 32 MFMAs instead of 8 per
+// 16), which is what limits the short-K (K = d = 512) step GEMMs.  Operands
 // are staged global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds) into an
 // NST-deep ring of BKT-deep K-tiles (configurations: BK64 x 2 stages, BK32 x 3
 // or 4 stages).  Per-lane source offsets are computed once; the K loop only
@@ -30,7 +36,19 @@
 
 namespace scamd {
 
-constexpr int BM = 128, BN = 128, NT = 256;
+template <int WGM_, int WGN_, int WI_, int WJ_>
+struct Shape {
+  static constexpr int WGM = WGM_, WGN = WGN_, WI = WI_, WJ = WJ_;
+  static constexpr int NW = WGM * WGN, NT = NW * 64;
+  static constexpr int BM = WGM * WI * 16, BN = WGN * WJ * 16;
+};
+using S128 = Shape<2, 2, 4, 4>;
+using S256x128 = Shape<2, 2, 8, 4>;
+using S256 = Shape<2, 4, 8, 4>;
+// Partial-sum buffers (scalar parts, column parts, row-dot parts, squared-norm
+// parts) are laid out on a 128x128 sub-tile grid whatever the block shape, so the
+// consumers (loss / bias / Adam kernels) do not depend on the GEMM configuration.
+constexpr int PT = 128;
 
 enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5 };
 
@@ -115,6 +133,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // Per-lane byte offsets (relative to the operand's group base) of the 1 KiB
 // LDS-DMA pieces this wave fills for K-tile 0; later tiles add a scalar soffset.
+// An M/N-major tile wider than 128 is stored as 128-column halves, each its own
+// [BKT][128] swizzled image (BKT/4 pieces per half).
 // The LDS destination of a piece is lane-linear, so the swizzle is applied to
 // the SOURCE: lane L fills physical slot L and fetches the logical chunk the
 // image places there (the XOR swizzles are involutions).
@@ -131,9 +151,11 @@ __device__ __forceinline__ void piece_offsets(uint32_t (&voff)[PPW], long ld, in
       const int ch = (BKT == 64) ? (slot ^ ((row >> 1) & 7)) : (slot ^ (((row >> 2) & 1) << 1));
       voff[i] = (uint32_t)(((long)(r0 + row) * ld + ch * 8) * 2);
     } else {
-      const int row = piece * 4 + (lane >> 4);
+      constexpr int PPH = BKT / 4;  // pieces per 128-column half
+      const int half = piece / PPH;
+      const int row = (piece % PPH) * 4 + (lane >> 4);
       const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-      voff[i] = (uint32_t)(((long)row * ld + r0 + ch * 8) * 2);
+      voff[i] = (uint32_t)(((long)row * ld + r0 + half * 128 + ch * 8) * 2);
     }
   }
 }
@@ -182,6 +204,8 @@ __device__ __forceinline__ bf16x8_t load_frag(const char* lds, int rbase, int ks
   } else {
     // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q,
     // columns 4p..4p+3 of a 4x16 block; lane i receives column i.
+    lds += (rbase >> 7) * (BKT * 256);  // 128-column half image
+    rbase &= 127;
     const int li = lane & 15, q = li >> 2, p = li & 3, g = lane >> 4;
     const int ch = (rbase >> 3) + (p >> 1);
     const int within = (p & 1) * 8;
@@ -195,17 +219,21 @@ __device__ __forceinline__ bf16x8_t load_frag(const char* lds, int rbase, int ks
 }
 
 
-template <bool AK, bool BKM, int EPI, int BKT, int NST>
-__global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
-  constexpr int TB = 128 * BKT * 2;  // bytes per operand tile
-  constexpr int PPW = TB / 1024 / 4; // LDS-DMA pieces per wave per operand tile
-  constexpr int LPT = 2 * PPW;       // DMA instructions per wave per K-tile
-  __shared__ __attribute__((aligned(16))) char smem[NST * 2 * TB];
+template <class S, bool AK, bool BKM, int EPI, int BKT, int NST>
+__global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
+  constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
+  constexpr int TA = BM * BKT * 2, TBB = BN * BKT * 2;  // bytes per operand tile
+  constexpr int PPWA = TA / 1024 / NW, PPWB = TBB / 1024 / NW;  // LDS-DMA pieces per wave
+  constexpr int LPT = PPWA + PPWB;                       // DMA instructions per wave per K-tile
+  constexpr int STG = TA + TBB;
+  static_assert(PPWA * NW * 1024 == TA && PPWB * NW * 1024 == TBB, "tile must split into whole pieces");
+  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
+  const int wr = wid / WGN, wc = wid % WGN;
   const int tiles_m = p.M / BM, tiles_n = p.N / BN;
+  const int ptm = p.M / PT, ptn = p.N / PT;  // partial-buffer grid (128 x 128 sub-tiles)
   const int per_prob = tiles_m * tiles_n * p.G;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int pi = bid / per_prob;
@@ -225,13 +253,18 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
   void* cptr = p1 ? p.prob[1].c : p.prob[0].c;
   const float alpha = p1 ? p.prob[1].alpha : p.prob[0].alpha;
 
-  const int nk1 = p.K1 / BKT, nk = nk1 + p.K2 / BKT;
-  // per-lane DMA source offsets for both K segments (segment 2 only for K-concat GEMMs)
-  uint32_t va0[PPW], vb0[PPW], va1[PPW], vb1[PPW];
-  piece_offsets<AK, BKT, PPW>(va0, oa0.ld, m0, wid, lane);
-  piece_offsets<BKM, BKT, PPW>(vb0, ob0.ld, n0, wid, lane);
-  piece_offsets<AK, BKT, PPW>(va1, oa1.ld, m0, wid, lane);
-  piece_offsets<BKM, BKT, PPW>(vb1, ob1.ld, n0, wid, lane);
+  // Only the weight-gradient style epilogues take a second K segment (K-concat);
+  // the fused forward epilogues never do, and skipping its offsets saves VGPRs.
+  constexpr bool SEG2 = (EPI == EPI_F32 || EPI == EPI_BF16 || EPI == EPI_ADAM);
+  const int nk1 = p.K1 / BKT, nk = nk1 + (SEG2 ? p.K2 / BKT : 0);
+  // per-lane DMA source offsets for both K segments
+  uint32_t va0[PPWA], vb0[PPWB], va1[SEG2 ? PPWA : 1], vb1[SEG2 ? PPWB : 1];
+  piece_offsets<AK, BKT, PPWA>(va0, oa0.ld, m0, wid, lane);
+  piece_offsets<BKM, BKT, PPWB>(vb0, ob0.ld, n0, wid, lane);
+  if constexpr (SEG2) {
+    piece_offsets<AK, BKT, PPWA>(va1, oa1.ld, m0, wid, lane);
+    piece_offsets<BKM, BKT, PPWB>(vb1, ob1.ld, n0, wid, lane);
+  }
   const i32x4_t ra0 = make_rsrc(oa0.ptr + (long)g * oa0.sg);
   const i32x4_t rb0 = make_rsrc(ob0.ptr + (long)g * ob0.sg);
   const i32x4_t ra1 = make_rsrc(oa1.ptr + (long)g * oa1.sg);
@@ -240,37 +273,39 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
   const uint32_t sa0 = AK ? BKT * 2 : (uint32_t)(BKT * oa0.ld * 2), sa1 = AK ? BKT * 2 : (uint32_t)(BKT * oa1.ld * 2);
   const uint32_t sb0 = BKM ? BKT * 2 : (uint32_t)(BKT * ob0.ld * 2), sb1 = BKM ? BKT * 2 : (uint32_t)(BKT * ob1.ld * 2);
 
-#define SC_ISSUE(t)                                                           \
-  do {                                                                        \
-    char* dst_ = smem + ((t) % NST) * 2 * TB;                                 \
-    if ((t) < nk1) {                                                          \
-      issue_pieces<PPW>(ra0, va0, (uint32_t)(t) * sa0, dst_, wid);            \
-      issue_pieces<PPW>(rb0, vb0, (uint32_t)(t) * sb0, dst_ + TB, wid);       \
-    } else {                                                                  \
-      issue_pieces<PPW>(ra1, va1, (uint32_t)((t) - nk1) * sa1, dst_, wid);    \
-      issue_pieces<PPW>(rb1, vb1, (uint32_t)((t) - nk1) * sb1, dst_ + TB, wid); \
-    }                                                                         \
+#define SC_ISSUE(t)                                                              \
+  do {                                                                           \
+    char* dst_ = smem + ((t) % NST) * STG;                                       \
+    if (!SEG2 || (t) < nk1) {                                                    \
+      issue_pieces<PPWA>(ra0, va0, (uint32_t)(t) * sa0, dst_, wid);              \
+      issue_pieces<PPWB>(rb0, vb0, (uint32_t)(t) * sb0, dst_ + TA, wid);         \
+    } else if constexpr (SEG2) {                                                 \
+      issue_pieces<PPWA>(ra1, va1, (uint32_t)((t) - nk1) * sa1, dst_, wid);      \
+      issue_pieces<PPWB>(rb1, vb1, (uint32_t)((t) - nk1) * sb1, dst_ + TA, wid); \
+    }                                                                            \
   } while (0)
 
-  f32x4_t acc[4][4];
+  f32x4_t acc[WI][WJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < WI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // acc[i][j][r] = C[row][col0 + r] with row = m0 + wr*64 + i*16 + (lane&15),
-  // col0 = n0 + wc*64 + j*16 + 4*(lane>>4).
-  const int rowb = m0 + wr * 64 + (lane & 15);
-  const int colb = n0 + wc * 64 + 4 * (lane >> 4);
+  // acc[i][j][r] = C[row][col0 + r] with row = m0 + wr*16WI + i*16 + (lane&15),
+  // col0 = n0 + wc*16WJ + j*16 + 4*(lane>>4).
+  const int rowb = m0 + wr * (WI * 16) + (lane & 15);
+  const int colb = n0 + wc * (WJ * 16) + 4 * (lane >> 4);
   // The DEC / DC epilogues read a bf16 tile of x / c at the output positions:
-  // fetch it before the K loop so its HBM latency hides under the MFMAs.
-  uint2 auxv[4][4];
-  if constexpr (EPI == EPI_DEC || EPI == EPI_DC) {
+  // fetch it before the K loop so its HBM latency hides under the MFMAs (small
+  // per-wave tiles only; at 128x64 per wave the registers are needed by the loop).
+  constexpr bool AUX_EARLY = (EPI == EPI_DEC || EPI == EPI_DC) && WI * WJ <= 16;
+  uint2 auxv[WI][WJ];
+  if constexpr (AUX_EARLY) {
     const uint16_t* X = p.aux + (long)g * p.saux;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < WJ; ++j)
         auxv[i][j] = *reinterpret_cast<const uint2*>(X + (long)(rowb + i * 16) * p.ldaux + colb + j * 16);
   }
 
@@ -296,23 +331,23 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
     // moving LDS reads across it.
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (kt + NST - 1 < nk) SC_ISSUE(kt + NST - 1);
-    const char* la = smem + (kt % NST) * 2 * TB;
-    const char* lb = la + TB;
+    const char* la = smem + (kt % NST) * STG;
+    const char* lb = la + TA;
 #pragma unroll
     for (int ks = 0; ks < BKT / 32; ++ks) {
-      bf16x8_t fa[4], fb[4];
+      bf16x8_t fa[WI], fb[WJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = load_frag<AK, BKT>(la, wr * 64 + i * 16, ks, lane);
+      for (int j = 0; j < WJ; ++j) fb[j] = load_frag<BKM, BKT>(lb, wc * (WJ * 16) + j * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = load_frag<BKM, BKT>(lb, wc * 64 + j * 16, ks, lane);
+      for (int i = 0; i < WI; ++i) fa[i] = load_frag<AK, BKT>(la, wr * (WI * 16) + i * 16, ks, lane);
       // Operands swapped (B-side rows as the MFMA's A): each lane then holds
       // 4 consecutive OUTPUT COLUMNS of one output row, so the epilogue
       // issues 8/16-byte vector stores instead of 2-byte scatters.
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < WI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < WJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
@@ -326,9 +361,9 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
   if constexpr (EPI == EPI_F32) {
     float* C = reinterpret_cast<float*>(cptr) + (long)g * p.sc;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < WJ; ++j) {
         const f32x4_t v = acc[i][j] * alpha;
         *reinterpret_cast<f32x4_t*>(C + (long)(rowb + i * 16) * p.ldc + colb + j * 16) = v;
       }
@@ -337,9 +372,9 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
   if constexpr (EPI == EPI_BF16) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < WJ; ++j) {
         ushort4 h;
         h.x = f2bf(alpha * acc[i][j][0]); h.y = f2bf(alpha * acc[i][j][1]);
         h.z = f2bf(alpha * acc[i][j][2]); h.w = f2bf(alpha * acc[i][j][3]);
@@ -347,109 +382,118 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
       }
     return;
   }
-  // Column partial sums (ENC: on-counts, DC: bias gradient): reduce each lane's
-  // 4x4 values over rows, then across the 16 lanes sharing a column group, then
-  // across the two wave rows through LDS.  Deterministic; one store per column.
-  auto column_partials = [&](f32x4_t (&cs)[4], float* dst) {
+  // Column partial sums (ENC: on-counts, DC: bias gradient) per 128-row slot, in
+  // two steps so no per-column array stays live across the epilogue: (1) right
+  // after fragment column j is produced, reduce its 4 columns over the lane's
+  // rows and the 16 lanes sharing them (xor shuffles) and park the result in LDS
+  // (region `slot` of `red`); (2) after a barrier, sum the wave rows of each
+  // 128-row slot and store one value per (slot, column).  Deterministic.
+  constexpr int WPS = PT / (WI * 16);  // wave rows per 128-row slot
+  auto colred_lane = [&](f32x4_t v, int j, int region) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = cs[j][r];
-        v += __shfl_xor(v, 1, 64);
-        v += __shfl_xor(v, 2, 64);
-        v += __shfl_xor(v, 4, 64);
-        v += __shfl_xor(v, 8, 64);
-        cs[j][r] = v;
-      }
-    __syncthreads();
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *reinterpret_cast<f32x4_t*>(red + wr * 128 + wc * 64 + j * 16 + 4 * (lane >> 4)) = cs[j];
+    for (int r = 0; r < 4; ++r) {
+      v[r] += __shfl_xor(v[r], 1, 64);
+      v[r] += __shfl_xor(v[r], 2, 64);
+      v[r] += __shfl_xor(v[r], 4, 64);
+      v[r] += __shfl_xor(v[r], 8, 64);
     }
-    __syncthreads();
-    if (tid < 128) dst[((long)g * tiles_m + tm) * p.N + n0 + tid] = red[tid] + red[128 + tid];
-    __syncthreads();
+    if ((lane & 15) == 0)
+      *reinterpret_cast<f32x4_t*>(red + region * (S::WGM * BN) + wr * BN + wc * (WJ * 16) + j * 16 +
+                                  4 * (lane >> 4)) = v;
+  };
+  auto colred_store = [&](float* dst, int region) {
+    const float* rr = red + region * (S::WGM * BN);
+    for (int idx = tid; idx < (BM / PT) * BN; idx += NT) {
+      const int s = idx / BN, col = idx - s * BN;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPS; ++w) v += rr[(s * WPS + w) * BN + col];
+      dst[((long)g * ptm + m0 / PT + s) * p.N + n0 + col] = v;
+    }
+  };
+  // Scalar partials live on the 128x128 grid: the block total goes to its first
+  // sub-tile, the block's other sub-tiles get zero (consumers sum them all).
+  auto scalar_partial = [&](float* base, int nstat, int stat, float v) {
+    if (tid < (BM / PT) * (BN / PT)) {
+      const int sm = tid / (BN / PT), sn = tid - sm * (BN / PT);
+      base[((long)g * ptm * ptn + (m0 / PT + sm) * ptn + n0 / PT + sn) * nstat + stat] = tid == 0 ? v : 0.f;
+    }
   };
 
   if constexpr (EPI == EPI_ENC) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     const float* bias = p.bias + (long)g * p.sbias;
-    const int nact = p.nactive ? p.nactive[g] : p.N;
-    const bool masked = nact < p.N;  // block-uniform: only masked ensembles pay for the test
+    const int nact = p.nactive ? p.nactive[g] : p.N;  // masked SAEs: live columns [0, nact)
+    const bool counting = p.colpart != nullptr;
     float l1 = 0.f, l0 = 0.f;
-    f32x4_t cnt[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < WJ; ++j) {
       const int col = colb + j * 16;
       const f32x4_t bj = *reinterpret_cast<const f32x4_t*>(bias + col);
-      cnt[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      f32x4_t cnt = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < WI; ++i) {
         f32x4_t v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[i][j][r] + bj[r], 0.f);
-        if (masked) {
+        // branch-free (a block-uniform `if (masked)` made hipcc version the whole
+        // epilogue and spill at 128x64 per wave)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (col + r < nact) ? v[r] : 0.f;
-        }
+        for (int r = 0; r < 4; ++r) v[r] = (col + r < nact) ? v[r] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           l1 += v[r];
           const float on = v[r] > 0.f ? 1.f : 0.f;
           l0 += on;
-          cnt[j][r] += on;
+          cnt[r] += on;
         }
         *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + col) =
             make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
       }
+      colred_lane(cnt, j, 0);  // unconditional: a branch here re-versions the loop
     }
-    if (p.colpart) column_partials(cnt, p.colpart);
-    l1 = block_sum_256(l1, red + 512);
-    l0 = block_sum_256(l0, red + 512);
-    if (tid == 0) {
-      float* part = p.part + ((long)g * tiles_m * tiles_n + tm * tiles_n + tn) * 2;
-      part[0] = l1;
-      part[1] = l0;
-    }
+    l1 = block_sum<NW>(l1, red + 4096);  // its barriers also publish the colred_lane writes
+    l0 = block_sum<NW>(l0, red + 4096);
+    if (counting) colred_store(p.colpart, 0);
+    scalar_partial(p.part, 2, 0, l1);
+    scalar_partial(p.part, 2, 1, l0);
     return;
   }
   if constexpr (EPI == EPI_DEC) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     float se = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < WJ; ++j) {
         const long row = rowb + i * 16;
         const int col = colb + j * 16;
-        const uint2 xv = auxv[i][j];
+        const uint2 xv = AUX_EARLY ? auxv[i][j]
+                                   : *reinterpret_cast<const uint2*>(p.aux + (long)g * p.saux + row * p.ldaux + col);
         const float r0 = acc[i][j][0] - bf2f(xv.x & 0xFFFF), r1 = acc[i][j][1] - bf2f(xv.x >> 16);
         const float r2 = acc[i][j][2] - bf2f(xv.y & 0xFFFF), r3 = acc[i][j][3] - bf2f(xv.y >> 16);
         *reinterpret_cast<ushort4*>(C + row * p.ldc + col) = make_ushort4(f2bf(r0), f2bf(r1), f2bf(r2), f2bf(r3));
         se += r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
       }
-    se = block_sum_256(se, red);
-    if (tid == 0) p.part[(long)g * tiles_m * tiles_n + tm * tiles_n + tn] = se;
+    se = block_sum<NW>(se, red);
+    scalar_partial(p.part, 1, 0, se);
     return;
   }
   if constexpr (EPI == EPI_DC) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     const float add = p.l1[g] * p.l1_add_scale;
     const bool want_dot = p.dotpart != nullptr;
-    f32x4_t cs[4], ds[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      cs[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      ds[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WJ; ++j) {
+      f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f}, ds = f32x4_t{0.f, 0.f, 0.f, 0.f};
       const int col = colb + j * 16;
       f32x4_t bj = f32x4_t{0.f, 0.f, 0.f, 0.f};
       if (p.dc_tied) bj = *reinterpret_cast<const f32x4_t*>(p.bias + (long)g * p.sbias + col);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < WI; ++i) {
         const long row = rowb + i * 16;
-        const uint2 cv = auxv[i][j];
+        const uint2 cv = AUX_EARLY ? auxv[i][j]
+                                   : *reinterpret_cast<const uint2*>(p.aux + (long)g * p.saux + row * p.ldaux + col);
         const uint16_t cvs[4] = {(uint16_t)(cv.x & 0xFFFF), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xFFFF),
                                  (uint16_t)(cv.y >> 16)};
         f32x4_t dv;
@@ -457,19 +501,22 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
         for (int r = 0; r < 4; ++r) {
           const float c = bf2f(cvs[r]);
           dv[r] = c > 0.f ? acc[i][j][r] + add : 0.f;  // c is a ReLU output
-          cs[j][r] += dv[r];
+          cs[r] += dv[r];
           if (want_dot) {
             // <w_hat_j, dL/dw_hat_j> (in units of 2/(B d)): decoder path c * (R w_hat^T),
             // tied encoder path dpre * (x w_hat^T) = dpre * (pre - b) = dpre * (c - b)
-            ds[j][r] += c * acc[i][j][r] + (p.dc_tied ? dv[r] * (c - bj[r]) : 0.f);
+            ds[r] += c * acc[i][j][r] + (p.dc_tied ? dv[r] * (c - bj[r]) : 0.f);
           }
         }
         *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
             make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
       }
+      colred_lane(cs, j, 0);
+      if (want_dot) colred_lane(ds, j, 1);
     }
-    column_partials(cs, p.colpart);
-    if (want_dot) column_partials(ds, p.dotpart);
+    __syncthreads();
+    colred_store(p.colpart, 0);
+    if (want_dot) colred_store(p.dotpart, 1);
     return;
   }
   if constexpr (EPI == EPI_ADAM) {
@@ -479,20 +526,20 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
     const float bc1 = 1.f - __powf(p.b1, (float)(*p.step + 1));
     const float bc2 = 1.f - __powf(p.b2, (float)(*p.step + 1));
     const float stp = p.lr[g] / bc1, rbc2 = 1.f / bc2, b1 = p.b1, b2 = p.b2, eps = p.eps;
-    float ca[4], cp[4];
+    float ca[WI], cp[WI];
     if (E.mode) {
-      if (tid < 128) {
-        const int row = m0 + tid;
+      for (int r = tid; r < BM; r += NT) {
+        const int row = m0 + r;
         float dsum = 0.f;
         for (int t = 0; t < p.dot_tm; ++t) dsum += E.dotpart[((long)g * p.dot_tm + t) * p.M + row];
-        red[tid] = dsum * p.dot_scale;
-        red[128 + tid] = E.norms[(long)g * p.M + row];
+        red[r] = dsum * p.dot_scale;
+        red[BM + r] = E.norms[(long)g * p.M + row];
       }
       __syncthreads();
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int lr_ = wr * 64 + i * 16 + (lane & 15);
-        const float dot = red[lr_], nrm = red[128 + lr_];
+      for (int i = 0; i < WI; ++i) {
+        const int lr_ = wr * (WI * 16) + i * 16 + (lane & 15);
+        const float dot = red[lr_], nrm = red[BM + lr_];
         if (nrm > 1e-8f) {
           const float inv = 1.f / nrm;
           ca[i] = alpha * inv;      // dW = dW_hat / |w| - w <w_hat, dW_hat> / |w|^2
@@ -505,13 +552,15 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
       __syncthreads();
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { ca[i] = alpha; cp[i] = 0.f; }
+      for (int i = 0; i < WI; ++i) { ca[i] = alpha; cp[i] = 0.f; }
     }
-    float ss[4] = {0.f, 0.f, 0.f, 0.f};
+    float ss[WI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < WI; ++i) ss[i] = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+    for (int i = 0; i < WI; ++i)
+#pragma unroll
+      for (int j = 0; j < WJ; ++j) {
         const long off = gb + (long)(rowb + i * 16) * p.ldc + colb + j * 16;
         f32x4_t pv = *reinterpret_cast<const f32x4_t*>(E.p + off);
         f32x4_t mv = *reinterpret_cast<const f32x4_t*>(E.m + off);
@@ -530,18 +579,25 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
         *reinterpret_cast<ushort4*>(E.sh + off) = make_ushort4(f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3]));
       }
     if (E.mode) {
-      // partial |w_j|^2 over this block's 128 columns -> sqpart[g][row][tn]
+      // partial |w_j|^2 over each 128-column slot -> sqpart[g][row][slot]
+      constexpr int WPC = PT / (WJ * 16);  // wave columns per 128-column slot
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < WI; ++i) {
         ss[i] += __shfl_xor(ss[i], 16, 64);
         ss[i] += __shfl_xor(ss[i], 32, 64);
       }
       if (lane < 16) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) red[wc * 128 + wr * 64 + i * 16 + lane] = ss[i];
+        for (int i = 0; i < WI; ++i) red[wc * BM + wr * (WI * 16) + i * 16 + lane] = ss[i];
       }
       __syncthreads();
-      if (tid < 128) E.sqpart[((long)g * p.M + m0 + tid) * tiles_n + tn] = red[tid] + red[128 + tid];
+      for (int idx = tid; idx < (BN / PT) * BM; idx += NT) {
+        const int s = idx / BM, row = idx - s * BM;
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < WPC; ++w) v += red[(s * WPC + w) * BM + row];
+        E.sqpart[((long)g * p.M + m0 + row) * ptn + n0 / PT + s] = v;
+      }
     }
     return;
   }
@@ -550,6 +606,45 @@ __global__ __launch_bounds__(NT) void sae_gemm_kernel(GemmParams p) {
 }  // namespace scamd
 
 using namespace scamd;
+
+namespace {
+
+template <class S>
+bool fits(int M, int N) { return M % S::BM == 0 && N % S::BN == 0; }
+
+template <class S>
+long n_blocks(int M, int N, int G, int nprob) { return (long)(M / S::BM) * (N / S::BN) * G * nprob; }
+
+template <class S, int BKT, int NST>
+int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
+  const dim3 grid((unsigned)n_blocks<S>(p.M, p.N, p.G, nprob)), block(S::NT);
+#define SC_L(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_kernel<S, AKV, BKV, E, BKT, NST>), grid, block, 0, stream, p)
+  // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
+  // epilogues; the plain F32 / BF16 epilogues exist for every layout.
+  switch (epi) {
+    case EPI_ENC: if (!(ak && bk)) return 5; SC_L(true, true, EPI_ENC); break;
+    case EPI_DEC: if (!(ak && !bk)) return 5; SC_L(true, false, EPI_DEC); break;
+    case EPI_DC: if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC); break;
+    case EPI_ADAM: if (ak || bk) return 5; SC_L(false, false, EPI_ADAM); break;
+    case EPI_F32:
+      if (ak && bk) SC_L(true, true, EPI_F32);
+      else if (ak) SC_L(true, false, EPI_F32);
+      else if (bk) SC_L(false, true, EPI_F32);
+      else SC_L(false, false, EPI_F32);
+      break;
+    case EPI_BF16:
+      if (ak && bk) SC_L(true, true, EPI_BF16);
+      else if (ak) SC_L(true, false, EPI_BF16);
+      else if (bk) SC_L(false, true, EPI_BF16);
+      else SC_L(false, false, EPI_BF16);
+      break;
+    default: return 2;
+  }
+#undef SC_L
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+}  // namespace
 
 // ------------------------------------------------------------------ C ABI
 extern "C" {
@@ -570,7 +665,17 @@ struct ScAdamEpi {
   int mode;
 };
 
+
+// Block shape chosen by sc_gemm when cfg == 0: the largest tile that divides the
+// problem and still gives at least one block per CU (256 CUs on MI355X).
+int sc_gemm_shape(int M, int N, int G, int nprob) {
+  if (fits<S256>(M, N) && n_blocks<S256>(M, N, G, nprob) >= 256) return 3;
+  if (fits<S256x128>(M, N) && n_blocks<S256x128>(M, N, G, nprob) >= 256) return 2;
+  return 1;
+}
+
 // layout: bit0 = A is K-major, bit1 = B is K-major.
+// cfg: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256.
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             const ScOperand* a /* [nprob][2] */, const ScOperand* b /* [nprob][2] */,
             void* const* c /* [nprob] */, const float* alpha /* [nprob] */, long ldc, long sc,
@@ -579,7 +684,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             float* dotpart, int dc_tied, const ScAdamEpi* adam /* [nprob] or null */, const float* lr,
             const int* step, float b1, float b2, float eps, int dot_tm, float dot_scale,
             int cfg, hipStream_t stream) {
-  if (M % BM || N % BN || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
+  if (M % PT || N % PT || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
   GemmParams p;
   for (int i = 0; i < nprob; ++i) {
     for (int s = 0; s < 2; ++s) {
@@ -605,48 +710,14 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   }
   if (epi == EPI_ADAM && (!adam || !lr || !step)) return 4;
   p.lr = lr; p.step = step; p.b1 = b1; p.b2 = b2; p.eps = eps; p.dot_tm = dot_tm; p.dot_scale = dot_scale;
-  const int grid = (M / BM) * (N / BN) * G * nprob;
   const bool ak = layout & 1, bk = layout & 2;
-
-#ifdef SC_GEMM_ALL_CFGS
-#define SC_LAUNCH(AKV, BKV, E)                                                                    \
-  switch (cfg) {                                                                                  \
-    case 1: hipLaunchKernelGGL((sae_gemm_kernel<AKV, BKV, E, 32, 3>), dim3(grid), dim3(NT), 0, stream, p); break; \
-    case 2: hipLaunchKernelGGL((sae_gemm_kernel<AKV, BKV, E, 32, 4>), dim3(grid), dim3(NT), 0, stream, p); break; \
-    default: hipLaunchKernelGGL((sae_gemm_kernel<AKV, BKV, E, 64, 2>), dim3(grid), dim3(NT), 0, stream, p); break; \
+  int shape = cfg & 3;
+  if (shape == 0) shape = sc_gemm_shape(M, N, G, nprob);
+  switch (shape) {
+    case 3: if (!fits<S256>(M, N)) return 6; return launch<S256, 64, 2>(epi, ak, bk, p, nprob, stream);
+    case 2: if (!fits<S256x128>(M, N)) return 6; return launch<S256x128, 64, 2>(epi, ak, bk, p, nprob, stream);
+    default: return launch<S128, 64, 2>(epi, ak, bk, p, nprob, stream);
   }
-#else
-  // BK64 x 2 stages measured fastest for every step GEMM on MI355X (profiles/kernel_bench_r1_v3.jsonl);
-  // build with -DSC_GEMM_ALL_CFGS to A/B the deeper BK32 rings.
-  (void)cfg;
-#define SC_LAUNCH(AKV, BKV, E) \
-  hipLaunchKernelGGL((sae_gemm_kernel<AKV, BKV, E, 64, 2>), dim3(grid), dim3(NT), 0, stream, p)
-#endif
-  // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
-  // epilogues; the plain F32 / BF16 epilogues exist for every layout.
-  switch (epi) {
-    case EPI_ENC: if (!(ak && bk)) return 5; SC_LAUNCH(true, true, EPI_ENC); break;
-    case EPI_DEC: if (!(ak && !bk)) return 5; SC_LAUNCH(true, false, EPI_DEC); break;
-    case EPI_DC: if (!(ak && bk)) return 5; SC_LAUNCH(true, true, EPI_DC); break;
-    case EPI_ADAM: if (ak || bk) return 5; SC_LAUNCH(false, false, EPI_ADAM); break;
-    case EPI_F32:
-    case EPI_BF16:
-      if (epi == EPI_F32) {
-        if (ak && bk) SC_LAUNCH(true, true, EPI_F32);
-        else if (ak) SC_LAUNCH(true, false, EPI_F32);
-        else if (bk) SC_LAUNCH(false, true, EPI_F32);
-        else SC_LAUNCH(false, false, EPI_F32);
-      } else {
-        if (ak && bk) SC_LAUNCH(true, true, EPI_BF16);
-        else if (ak) SC_LAUNCH(true, false, EPI_BF16);
-        else if (bk) SC_LAUNCH(false, true, EPI_BF16);
-        else SC_LAUNCH(false, false, EPI_BF16);
-      }
-      break;
-    default: return 2;
-  }
-#undef SC_LAUNCH
-  return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 }  // extern "C"

@@ -20,16 +20,44 @@ from . import _lib
 EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16, EPI_ADAM = 0, 1, 2, 3, 4, 5
 TILE_M, TILE_N, TILE_K = 128, 128, 64
 
-# Pipeline configurations of the kernel (K-tile depth x LDS-DMA ring stages):
-#   0: BK64 x 2 stages (64 KiB LDS)   1: BK32 x 3 stages (48 KiB)   2: BK32 x 4 stages (64 KiB)
+# Block shapes of the kernel (BK64 x 2-stage LDS-DMA ring for all of them):
+#   0: automatic -- the largest shape that divides (M, N) and still launches >= 256 blocks
+#   1: 128x128, 4 waves of 64x64        2: 256x128, 4 waves of 128x64
+#   3: 256x256, 8 waves of 128x64 (one block per CU)
 # Per-epilogue defaults come from measurements on MI355X (profiles/); override with
 # SC_GEMM_CFG=<n> for all GEMMs.
-_CFG_DEFAULT = {EPI_ENC: 0, EPI_DEC: 0, EPI_DC: 0, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 0}
+# Measured at B=2048, d=512, n=2048, G=8 (profiles/kernel_bench_r1_v6.jsonl): the fused
+# epilogues are fastest on 128x128 blocks (two blocks per CU overlap one block's epilogue
+# with the other's MFMA loop: enc 61 vs 84 us on 256x256), the plain fp32 weight-gradient
+# GEMM (K = B = 2048) on 256x256 blocks (65 vs 74 us) -- "auto" picks that.
+_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 1}
 _CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
+SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 
 
 def set_config(epi: int, cfg: int):
     _CFG_DEFAULT[epi] = int(cfg)
+
+
+class force_shape:
+    """Context manager: run every GEMM with block shape ``cfg`` (tests / A-B timing)."""
+
+    def __init__(self, cfg: int):
+        self.cfg = int(cfg)
+
+    def __enter__(self):
+        global _CFG_OVERRIDE
+        self._old, _CFG_OVERRIDE = _CFG_OVERRIDE, self.cfg
+        return self
+
+    def __exit__(self, *exc):
+        global _CFG_OVERRIDE
+        _CFG_OVERRIDE = self._old
+
+
+def shape_fits(cfg: int, M: int, N: int) -> bool:
+    bm, bn = SHAPES.get(int(cfg), (128, 128))
+    return M % bm == 0 and N % bn == 0
 
 
 def _op(t, ld, sg):
@@ -53,6 +81,8 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
             lr=None, step=None, betas=(0.9, 0.999), eps=1e-8, dot_tm=0, dot_scale=0.0, cfg=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
+    cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
+    _need(cfg == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg)} does not tile M={M}, N={N}")
     nprob = len(outs)
     A = (_lib.ScOperand * (2 * nprob))(*a_ops)
     Bo = (_lib.ScOperand * (2 * nprob))(*b_ops)
@@ -64,7 +94,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
         _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1), float(l1_add_scale),
         _lib.ptr(dotpart), int(bool(dc_tied)), adam, _lib.ptr(lr), _lib.ptr(step),
         float(betas[0]), float(betas[1]), float(eps), int(dot_tm), float(dot_scale),
-        int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi])),
+        cfg,
         _lib.stream_handle(),
     )
     _lib.check(rc, f"sc_gemm(epi={epi})")

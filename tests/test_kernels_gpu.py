@@ -28,8 +28,21 @@ def _close(a, b, rtol=2e-2, atol=1e-2):
     assert err <= atol + rtol * ref, f"max err {err} vs ref scale {ref}"
 
 
-@pytest.mark.parametrize("G,M,N,K", [(1, 128, 128, 64), (3, 256, 384, 192), (2, 512, 256, 512)])
-def test_matmul_layouts(G, M, N, K):
+SHAPE_CFGS = [1, 2, 3]  # 128x128, 256x128, 256x256 blocks
+
+
+@pytest.mark.parametrize("cfg", SHAPE_CFGS)
+@pytest.mark.parametrize("G,M,N,K", [(1, 128, 128, 64), (3, 256, 384, 192), (2, 512, 256, 512), (2, 256, 512, 128)])
+def test_matmul_layouts(G, M, N, K, cfg):
+    from sparse_coding__amd.ops import gemm
+
+    if not gemm.shape_fits(cfg, M, N):
+        pytest.skip("block shape does not tile this problem")
+    with gemm.force_shape(cfg):
+        _matmul_layouts(G, M, N, K)
+
+
+def _matmul_layouts(G, M, N, K):
     from sparse_coding__amd.ops import gemm
 
     torch.manual_seed(0)
@@ -70,11 +83,18 @@ def test_identity_asymmetric():
     torch.testing.assert_close(out, bt.float()[:, :M, :], rtol=0, atol=0)
 
 
-def test_sae_epilogues():
+@pytest.mark.parametrize("cfg", SHAPE_CFGS)
+def test_sae_epilogues(cfg):
+    from sparse_coding__amd.ops import gemm
+
+    with gemm.force_shape(cfg):
+        _sae_epilogues(3, 512, 256, 512 if cfg > 1 else 384)
+
+
+def _sae_epilogues(G, B, d, n):
     from sparse_coding__amd.ops import gemm
 
     torch.manual_seed(1)
-    G, B, d, n = 3, 256, 256, 384
     x = _bf(B, d)
     we = _bf(G, n, d, scale=0.05)
     wd = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1).to(torch.bfloat16)
@@ -151,9 +171,17 @@ def test_adam_rows_matches_autograd():
     _close(shadow, sh_ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("cfg", SHAPE_CFGS)
 @pytest.mark.parametrize("fuse_adam", [True, False])
 @pytest.mark.parametrize("kind", ["untied", "tied"])
-def test_fused_step_matches_functional_ensemble(kind, fuse_adam):
+def test_fused_step_matches_functional_ensemble(kind, fuse_adam, cfg):
+    from sparse_coding__amd.ops import gemm
+
+    with gemm.force_shape(cfg):
+        _fused_step_matches(kind, fuse_adam)
+
+
+def _fused_step_matches(kind, fuse_adam):
     from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
     from sparse_coding__amd.engine.fused import FusedSAEEnsemble
     from sparse_coding__amd.engine.optim import adam
