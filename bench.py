@@ -47,6 +47,13 @@ def parse(argv=None):
     ap.add_argument("--ring-rows", type=int, default=1 << 21)
     ap.add_argument("--eval-rows", type=int, default=16384)
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--dp-chunks", type=int, default=2,
+                    help="N>1: split the ensemble into this many model chunks whose gradient all-reduce "
+                         "overlaps the next chunk's compute (1 = one reduction per step)")
+    ap.add_argument("--dist-backend", choices=["auto", "nccl", "gloo"], default="auto",
+                    help="auto = RCCL ('nccl') on GPUs; gloo only for rehearsals")
+    ap.add_argument("--shared-gpu", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (with --dist-backend gloo on a 1-GPU box)")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of a HIP graph")
     return ap.parse_args(argv)
@@ -75,7 +82,8 @@ def main(argv=None):
     args = parse(argv)
     from sparse_coding__amd.parallel.dist import all_reduce_max, barrier, init_distributed, shutdown
 
-    info = init_distributed()
+    info = init_distributed(None if args.dist_backend == "auto" else args.dist_backend,
+                            device="cuda:0" if args.shared_gpu else None)
     if not torch.cuda.is_available():
         print("bench.py needs an MI355X (torch.cuda.is_available() is False)", file=sys.stderr)
         return 2
@@ -90,12 +98,27 @@ def main(argv=None):
     ring, held_out = build_ring(args, device)
     B = args.batch
 
-    if args.engine == "fused":
+    grad_dtype = torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32
+    if args.engine == "fused" and info.world_size > 1:
+        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+        from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
+
+        engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device)
+                   for m in split_models(models, args.dp_chunks)]
+        trainer = ChunkedDataParallel([FusedChunk(e) for e in engines], info, grad_dtype)
+        xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
+
+        def step():
+            trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf))
+
+        def dicts():
+            return [ld for e in engines for ld in e.to_learned_dicts(device)]
+    elif args.engine == "fused":
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.parallel.data_parallel import DataParallelFused
 
         eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
-        trainer = DataParallelFused(eng, info, torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32)
+        trainer = DataParallelFused(eng, info, grad_dtype)
         if info.world_size == 1 and not args.no_graph:
             eng.enable_graph()  # whole step = one HIP graph replay
 
@@ -166,6 +189,7 @@ def main(argv=None):
                 "per_gpu_batch": B,
                 "parallelism": f"dp{info.world_size}",
                 "engine": args.engine,
+                "dp_chunks": args.dp_chunks if info.world_size > 1 else None,
                 "grad_allreduce_dtype": args.grad_dtype,
             },
             "model_activations_per_s": round(value * args.models, 1),

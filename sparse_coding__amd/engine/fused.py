@@ -102,11 +102,15 @@ class FusedSAEEnsemble:
         # gradient buffers; the last-produced weight gradient shares one flat buffer with the
         # reduced bias gradient so data-parallel runs all-reduce both with a single collective
         if self.kind == "untied":
-            self.g_dec = torch.empty(G, n, d, device=dev, dtype=torch.float32)
-            self._g_flat = torch.empty(G * n * d + G * n, device=dev, dtype=torch.float32)
+            # one allocation [g_dec | g_enc | g_bias]: data-parallel runs can reduce all of a
+            # chunk's gradients with one collective (grad_all) or in two ([g_dec], [g_enc|g_bias])
+            self.grad_all = torch.empty(2 * G * n * d + G * n, device=dev, dtype=torch.float32)
+            self.g_dec = self.grad_all[: G * n * d].view(G, n, d)
+            self._g_flat = self.grad_all[G * n * d:]
             self.g_enc = self._g_flat[: G * n * d].view(G, n, d)
         else:
             self._g_flat = torch.empty(G * n * d + G * n, device=dev, dtype=torch.float32)
+            self.grad_all = self._g_flat
             self.g_dec = self._g_flat[: G * n * d].view(G, n, d)
             self.g_enc = None
         self.g_bias = self._g_flat[G * n * d:].view(G, 1, n)

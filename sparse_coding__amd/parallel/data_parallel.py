@@ -128,3 +128,140 @@ class DataParallelEnsemble:
             self._reduce(grads)
         self.ensemble.apply_grads(grads)
         return loss, aux
+
+
+# ----------------------------------------------------------------------------- model-chunk pipelining
+class FusedChunk:
+    """Adapter: one ``FusedSAEEnsemble`` (a chunk of the ensemble's models) as a pipeline stage."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        engine.fuse_adam = False  # gradients are reduced before Adam
+
+    def set_grad_scale(self, s: float):
+        self.engine.grad_scale = s
+
+    def params(self):
+        return list(self.engine.params.values())
+
+    def after_param_sync(self):
+        self.engine.refresh_shadows()
+
+    def compute_grads(self, x):
+        e = self.engine
+        e.forward(x)
+        e.wgrad_first(x)
+        e.wgrad_second(x, reduce_bias=True)  # pre-scaled by 1/world: SUM all-reduce = mean
+        return e.grad_all
+
+    def apply_update(self, grad_flat):
+        e = self.engine
+        e.adam_first()
+        e.adam_second(reduced_bias=True)
+        return e.out
+
+
+class EagerChunk:
+    """Adapter: one eager ``FunctionalEnsemble`` chunk (CPU / gloo tests, unfused signatures)."""
+
+    def __init__(self, ensemble):
+        self.ens = ensemble
+        self.scale = 1.0
+        self._grads = None
+        self._spec = None
+        self.last = None
+
+    def set_grad_scale(self, s: float):
+        self.scale = s
+
+    def params(self):
+        return [t.data for t in pytree.tree_leaves(self.ens.params)]
+
+    def after_param_sync(self):
+        pass
+
+    def compute_grads(self, x):
+        grads, (loss, aux) = self.ens.compute_grads(x)
+        self.last = loss
+        leaves, self._spec = pytree.tree_flatten(grads)
+        self._shapes = [t.shape for t in leaves]
+        return torch.cat([t.reshape(-1) for t in leaves]) * self.scale
+
+    def apply_update(self, grad_flat):
+        leaves, off = [], 0
+        for shp in self._shapes:
+            k = int(torch.Size(shp).numel())
+            leaves.append(grad_flat[off:off + k].view(shp))
+            off += k
+        self.ens.apply_grads(pytree.tree_unflatten(leaves, self._spec))
+        return self.last
+
+
+class ChunkedDataParallel:
+    """Data parallelism with the ensemble split into model chunks whose gradient
+    all-reduce overlaps the NEXT chunk's compute.
+
+    The models of an ensemble are independent, so chunk k's update needs only chunk
+    k's reduced gradients.  Per step (compute stream | RCCL stream)::
+
+        fwd+bwd chunk 0            -> AR(grads 0)
+        fwd+bwd chunk 1            |  AR 0 in flight      -> AR(grads 1)
+        wait AR 0; Adam chunk 0    |  AR 1 in flight
+        fwd+bwd chunk 2            |                      -> AR(grads 2)
+        wait AR 1; Adam chunk 1    ...
+
+    Only the last chunk's all-reduce is exposed (a 1/K share of the traffic), instead of
+    the whole ensemble's gradients as in a reduce-after-backward step.  Every rank issues
+    the same collectives in the same order; gradients are pre-scaled by 1/world so a SUM
+    all-reduce yields the global mean.  Numerically identical to training each chunk on
+    the global batch (the reference's DDP semantics, huge_batch_size.py:259-345).
+    """
+
+    def __init__(self, chunks, info: DistInfo, grad_dtype: torch.dtype = torch.float32):
+        self.chunks = list(chunks)
+        self.info = info
+        self.grad_dtype = grad_dtype
+        for c in self.chunks:
+            c.set_grad_scale(1.0 / info.world_size)
+        if info.enabled:
+            for c in self.chunks:
+                for t in c.params():
+                    dist.broadcast(t, src=0)
+                c.after_param_sync()
+
+    def _reduce_async(self, flat):
+        if not self.info.enabled:
+            return None, flat
+        if self.grad_dtype == torch.float32 or flat.dtype == self.grad_dtype:
+            return dist.all_reduce(flat, async_op=True), flat
+        buf = flat.to(self.grad_dtype)
+        return (dist.all_reduce(buf, async_op=True), (buf, flat))
+
+    @staticmethod
+    def _finish(work, payload):
+        if work is not None:
+            work.wait()
+        if isinstance(payload, tuple):
+            payload[1].copy_(payload[0])
+            return payload[1]
+        return payload
+
+    def step_batch(self, x):
+        outs = [None] * len(self.chunks)
+        pending = []
+        for k, c in enumerate(self.chunks):
+            flat = c.compute_grads(x)
+            pending.append((k, self._reduce_async(flat)))
+            if len(pending) > 1:  # previous chunk's reduction had this chunk's compute to hide behind
+                j, (w, payload) = pending.pop(0)
+                outs[j] = self.chunks[j].apply_update(self._finish(w, payload))
+        for j, (w, payload) in pending:
+            outs[j] = self.chunks[j].apply_update(self._finish(w, payload))
+        return outs
+
+
+def split_models(models, n_chunks: int):
+    """Contiguous, near-equal chunks of an ensemble's model list."""
+    n_chunks = max(1, min(n_chunks, len(models)))
+    per = -(-len(models) // n_chunks)
+    return [models[i:i + per] for i in range(0, len(models), per)]

@@ -32,12 +32,17 @@ class DistInfo:
         return self.world_size > 1
 
 
-def init_distributed(backend: str | None = None, timeout_s: int = 600) -> DistInfo:
+def init_distributed(backend: str | None = None, timeout_s: int = 600, device=None) -> DistInfo:
+    """``device`` overrides the per-rank device (e.g. several gloo ranks sharing one GPU in a test)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available() and backend != "gloo"
-    if use_cuda:
+    if device is not None:
+        device = torch.device(device)
+        if device.type == "cuda":
+            torch.cuda.set_device(device)
+    elif use_cuda:
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:

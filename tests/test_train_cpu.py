@@ -375,3 +375,42 @@ def test_huge_batch_ddp_gloo_two_ranks(tmp_path):
         assert p.exitcode == 0
     np.testing.assert_array_equal(res[0][0], res[1][0])  # replicas identical after DDP + resampling
     assert res[0][1] == res[1][1]
+
+
+def _chunked_worker(rank, world, port, x, init, out_q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, EagerChunk, split_models
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
+
+    info = init_distributed("gloo")
+    torch.manual_seed(200 + rank)  # different params per rank (DP must broadcast rank 0's), same hyper-params
+    models = init if rank == 0 else [FunctionalSAE.init(16, 32, float(b["l1_alpha"])) for _, b in init]
+    chunks = [EagerChunk(FunctionalEnsemble(m, FunctionalSAE, adam, {"lr": 1e-2})) for m in split_models(models, 3)]
+    dp = ChunkedDataParallel(chunks, info)
+    for _ in range(3):
+        dp.step_batch(x.chunk(world)[rank])
+    enc = torch.cat([c.ens.params["encoder"].detach() for c in chunks]).numpy().copy()
+    out_q.put((rank, enc))
+    shutdown(info)
+
+
+def test_chunked_data_parallel_gloo_matches_single_process():
+    torch.manual_seed(0)
+    init = [FunctionalSAE.init(16, 32, l1) for l1 in (1e-4, 3e-4, 1e-3, 1e-3)]  # no dead features: Adam would amplify rounding
+    x = torch.randn(64, 16)
+    single = FunctionalEnsemble([(dict(p), dict(b)) for p, b in init], FunctionalSAE, adam, {"lr": 1e-2})
+    for _ in range(3):
+        single.step_batch(x)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chunked_worker, args=(r, 2, port, x, init, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0], res[1])
+    np.testing.assert_allclose(res[0], single.params["encoder"].detach().numpy(), atol=2e-5, rtol=1e-4)

@@ -122,3 +122,67 @@ def test_huge_batch_fused_reinit(tmp_path):
     assert torch.equal(tr.impl.m["encoder"][0, :7], torch.zeros_like(tr.impl.m["encoder"][0, :7]))
     sd = torch.load(tmp_path / "o" / "sae_1.pt", weights_only=True)
     assert sd["encoder"].shape == (256, 512) and sd["decoder"].shape == (512, 256)
+
+
+def _dp_gpu_worker(rank, world, port, x, init, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
+
+    info = init_distributed("gloo", device="cuda:0")  # two ranks share the box's one GPU; gloo moves CUDA tensors
+    torch.manual_seed(300 + rank)
+    models = [({k: v.cuda() for k, v in p.items()}, {k: v.cuda() for k, v in b.items()}) for p, b in init]
+    if rank:
+        models = [(dict((k, torch.randn_like(v)) for k, v in p.items()), b) for p, b in models]
+    engines = [FusedSAEEnsemble(m, FunctionalSAE, lr=1e-3, batch_size=x.shape[0] // world, device="cuda:0")
+               for m in split_models(models, 2)]
+    dp = ChunkedDataParallel([FusedChunk(e) for e in engines], info)
+    xs = x.cuda().chunk(world)[rank].contiguous()
+    for _ in range(3):
+        dp.step_batch(xs)
+    torch.cuda.synchronize()
+    q.put((rank, torch.cat([e.params["decoder"] for e in engines]).cpu().numpy()))
+    shutdown(info)
+
+
+def test_chunked_dp_fused_two_ranks_one_gpu():
+    """Two gloo ranks sharing cuda:0 run the chunk-pipelined fused DP step; replicas stay
+    identical and match single-process training on the global batch."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+
+    torch.manual_seed(0)
+    d, n, B = 256, 512, 512
+    init = [FunctionalSAE.init(d, n, l1) for l1 in (1e-4, 3e-4, 1e-3, 2e-3)]
+    feats = torch.nn.functional.normalize(torch.randn(1024, d), dim=-1)
+    x = (torch.relu(torch.randn(B, 1024) - 2.0) @ feats).to(torch.bfloat16)
+    ref = FusedSAEEnsemble([({k: v.cuda() for k, v in p.items()}, {k: v.cuda() for k, v in b.items()})
+                            for p, b in init], FunctionalSAE, lr=1e-3, batch_size=B, device="cuda:0")
+    for _ in range(3):
+        ref.step_batch(x.cuda())
+    torch.cuda.synchronize()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_gpu_worker, args=(r, 2, port, x, init, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0], res[1])
+    want = ref.params["decoder"].cpu().numpy()
+    # bf16 GEMM partial sums differ between the half batches and the full batch: compare updates
+    init_dec = np.stack([p["decoder"].numpy() for p, _ in init])
+    du, dr = (res[0] - init_dec).ravel(), (want - init_dec).ravel()
+    cos = float(du @ dr / (np.linalg.norm(du) * np.linalg.norm(dr)))
+    assert cos > 0.99, cos
