@@ -198,3 +198,43 @@ def test_analysis_helpers():
     sae = UntiedSAE(torch.randn(16, 32), torch.randn(16, 32), torch.zeros(16))
     corr = A.moment_score_correlations(sae, x, [0, 1, 2, 3], [0.1, 0.5, 0.2, 0.9])
     assert set(corr) == {"n_active", "mean", "var", "skew", "kurtosis", "l4_norm"}
+
+
+def test_case_study_tools():
+    from sparse_coding__amd.interp import case_studies as CS
+
+    lm = _tiny("neox")
+    torch.manual_seed(0)
+    sae = UntiedSAE(torch.randn(12, 32), torch.randn(12, 32), torch.zeros(12))
+    toks = torch.randint(0, 100, (3, 8))
+    acts = CS.feature_activations(lm, sae, 1, "residual", toks, feature=2)
+    assert acts.shape == (3, 8)
+    flat = acts.flatten()
+    top = CS.get_feature_datapoints(flat, 4, "max")
+    assert float(flat[top[0]]) == float(flat.max())
+    assert len(CS.get_feature_datapoints(flat, 4, "uniform")) >= 1
+    assert CS.unravel(top[:1], 8)[0] == (int(top[0]) // 8, int(top[0]) % 8)
+    eff = CS.ablate_tokens(lm, sae, 1, "residual", toks[0], 2, position=5, replacement=7)
+    assert eff.shape == (6,)
+    # steering: adding a tied feature's (unit) atom raises that feature's pre-activation by the scale
+    from sparse_coding__amd.models.learned_dict import TiedSAE
+
+    tied = TiedSAE(torch.randn(12, 32), torch.zeros(12) + 0.5, norm_encoder=True)
+    name = "blocks.0.hook_resid_post"
+    before = CS.feature_activations(lm, tied, 0, "residual", toks, feature=3)
+    with lm.hooks([(name, CS.add_feature_direction(tied, 3, 5.0))]):
+        _, cache = lm.run_with_cache(toks, names_filter=[name], return_type=None)
+    after = tied.encode(cache[name].reshape(-1, 32))[:, 3].reshape(3, 8)
+    assert (after >= before - 1e-4).all() and after.sum() > before.sum()
+    d = CS.logit_diff_under(lm, toks, name, CS.ablate_feature_direction(sae, 3))
+    assert d.shape == (3, 8, 100)
+    up, down = CS.logit_lens(lm, sae, 3, k=5)
+    assert len(up) == 5 and up[0][1] >= down[0][1]
+    gen = CS.generate_text(lm, toks[:, :4], n_new=3)
+    assert gen.shape == (3, 7)
+    a, hi, lo = CS.best_context_token(lm, sae, 0, "residual", toks[0, :3], 3, vocab_size=100, batch_size=40)
+    assert a.shape == (100,) and float(a[hi[0]]) == float(a.max())
+    assert "#" in CS.render_activations(["a", "b"], [0.0, 1.0])
+    assert CS.gini(torch.tensor([0.0, 0.0, 1.0])) > CS.gini(torch.ones(3))
+    ld, hp = CS.select_dict([(sae, {"l1_alpha": 1e-3, "dict_size": 12})], l1_alpha=1e-3)
+    assert hp["dict_size"] == 12

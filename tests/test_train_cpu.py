@@ -414,3 +414,38 @@ def test_chunked_data_parallel_gloo_matches_single_process():
         assert p.exitcode == 0
     np.testing.assert_array_equal(res[0], res[1])
     np.testing.assert_allclose(res[0], single.params["encoder"].detach().numpy(), atol=2e-5, rtol=1e-4)
+
+
+def _job(x, device=None, progress=None):
+    progress.value += 1
+    return x * 2, device
+
+
+def test_launcher_and_dispatch(tmp_path):
+    from sparse_coding__amd.train.launch import dispatch, launch
+
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys\nopen(sys.argv[1] + '/r' + os.environ['RANK'], 'w').write("
+                      "os.environ['WORLD_SIZE'] + ' ' + os.environ['MASTER_ADDR'])\n")
+    codes = launch(str(script), 3, [str(tmp_path)], module=False, timeout=60)
+    assert codes == [0, 0, 0]
+    assert sorted(p.name for p in tmp_path.glob("r[0-9]")) == ["r0", "r1", "r2"]
+    assert (tmp_path / "r1").read_text() == "3 127.0.0.1"
+    res = dispatch([(_job, (i,), {}) for i in range(5)], ["cpu:a", "cpu:b"])
+    assert [r for r, _ in res] and [r[0] for r, _ in res] == [0, 2, 4, 6, 8]
+    assert {r[1] for r, _ in res} <= {"cpu:a", "cpu:b"}
+
+
+def test_remote_command_builders(monkeypatch):
+    from sparse_coding__amd.utils import remote as R
+
+    monkeypatch.setenv("SC_REMOTE_HOST", "user@box")
+    cmd = R.rsync_push(".", remote_dir="proj", port=2222)
+    assert cmd[:2] == ["rsync", "-rv"] and cmd[-1] == "user@box:proj" and "ssh -p 2222" in cmd
+    assert R.scp_push(["a", "b"], remote_dir="d")[-1] == "user@box:d"
+    assert R.run(["echo", "x"], dry_run=True) == 0
+    d = R.dotdict(a=1)
+    d.b = 2
+    assert d.a == 1 and d["b"] == 2 and d.c is None
+    with pytest.raises(RuntimeError):
+        R.upload_to_s3(__file__, bucket="b")
