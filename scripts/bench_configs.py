@@ -1,0 +1,132 @@
+"""Throughput of the other BASELINE.json configs (bench.py covers config 2 / 3).
+
+  python scripts/bench_configs.py cpu      # config 1: tied SAE d=128 ratio 2 l1=1e-3, CPU eager
+  python scripts/bench_configs.py topk     # config 4: GPT-2-small residual (d=768), ratio 8, top-k
+  python scripts/bench_configs.py fista    # config 5: FISTA 300-step dictionary learning, d=1024
+  python scripts/bench_configs.py mlp      # config 3 shapes on one GPU: Pythia-70m MLP (d=2048)
+
+Every line is one JSON record: activations/s over the timed steps (full steps: gather,
+forward, backward, optimiser, and for FISTA the solve + basis update), synthetic data,
+random-init weights.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np
+import torch
+
+
+def _timed(step, steps, warmup, sync):
+    for _ in range(warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    return time.perf_counter() - t0
+
+
+def _ring(d, device, rows=1 << 19, feats=None, k=32):
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.data.synthetic import RandomDatasetGenerator
+
+    gen = RandomDatasetGenerator(d, feats or 8 * d, 65536, k, 0.999, False, device, seed=7)
+    ring = DeviceRing(rows, d, device=device, dtype=torch.bfloat16 if device != "cpu" else torch.float32, seed=1)
+    ring.fill(lambda: gen.send(None))
+    return ring
+
+
+def cfg_cpu(a):
+    from sparse_coding__amd.engine.trainer import EnsembleTrainer
+    from sparse_coding__amd.models.signatures import FunctionalTiedSAE
+
+    torch.manual_seed(0)
+    B = 256
+    models = [FunctionalTiedSAE.init(128, 256, 1e-3)]
+    tr = EnsembleTrainer(models, FunctionalTiedSAE, batch_size=B, device="cpu")
+    ring = _ring(128, "cpu", rows=1 << 16)
+    el = _timed(lambda: tr.step(ring.sample(B)), a.steps, a.warmup, lambda: None)
+    return {"config": "1: tied SAE d=128 ratio 2 l1=1e-3, CPU closed-form engine (reference row 10: 82.9k act/s)",
+            "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
+            "batch": B, "threads": torch.get_num_threads()}
+
+
+def cfg_topk(a):
+    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
+    from sparse_coding__amd.models.topk import TopKEncoder
+
+    dev = "cuda:0"
+    torch.manual_seed(0)
+    d, ratio, B = 768, 8, a.batch
+    n = d * ratio
+    ks = [8, 16, 24, 32, 48, 64, 96, 128][: a.models]
+    models = [TopKEncoder.init(d, n, k, device=dev) for k in ks]
+    eng = FusedTopKEnsemble(models, lr=1e-3, batch_size=B, device=dev)
+    ring = _ring(d, dev)
+    xbuf = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
+    el = _timed(lambda: eng.step_batch(ring.sample(B, out=xbuf)), a.steps, a.warmup, torch.cuda.synchronize)
+    return {"config": f"4: GPT-2-small residual d={d}, ratio {ratio} (n={n}), fused top-k, k={ks}",
+            "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
+            "batch": B, "models": len(ks), "dtype": "bf16", "data": "synthetic"}
+
+
+def cfg_fista(a):
+    from sparse_coding__amd.engine.trainer import EnsembleTrainer
+    from sparse_coding__amd.models.fista import FunctionalFista
+
+    dev = "cuda:0"
+    torch.manual_seed(0)
+    d, ratio, B = 1024, a.ratio, a.batch
+    n = int(d * ratio)
+    l1s = np.logspace(-4, -2, a.models)
+    models = [FunctionalFista.init(d, n, float(l1), device=dev) for l1 in l1s]
+    tr = EnsembleTrainer(models, FunctionalFista, batch_size=B, device=dev, fista_iters=a.iters,
+                         fista_backend="hip")
+    ring = _ring(d, dev)
+    xbuf = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
+    el = _timed(lambda: tr.step(ring.sample(B, out=xbuf)), a.steps, a.warmup, torch.cuda.synchronize)
+    # FISTA solve alone
+    from sparse_coding__amd.ops import fista as F
+
+    D = torch.nn.functional.normalize(torch.randn(a.models, n, d, device=dev), dim=-1)
+    x = ring.sample(B).float()
+    eta = F.step_size(D)
+    lam = torch.tensor(l1s, device=dev, dtype=torch.float32)
+    el_solve = _timed(lambda: F.fista(x, D, lam, None, a.iters, eta, backend="hip", with_res=False), 5, 1,
+                      torch.cuda.synchronize) / 5
+    return {"config": f"5: FISTA {a.iters}-step dictionary learning, Pythia-410m-shaped d={d}, n={n}, "
+                      f"{a.models} models (reference row 13: 452 ms per model-solve, d=n=512, 500 it, B=256, CPU)",
+            "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
+            "solve_ms_all_models": round(1e3 * el_solve, 3),
+            "solve_ms_per_model": round(1e3 * el_solve / a.models, 3), "batch": B, "engine": tr.kind}
+
+
+def cfg_mlp(a):
+    import bench
+
+    return json.loads(json.dumps({"note": "run bench.py --d 2048 --ratio 4 for MLP shapes"}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("which", choices=["cpu", "topk", "fista", "mlp"])
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--models", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=300)
+    ap.add_argument("--ratio", type=float, default=1.0)
+    a = ap.parse_args()
+    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp}[a.which](a)
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

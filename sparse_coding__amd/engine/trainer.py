@@ -21,6 +21,7 @@ import torch
 from ..models.fista import FistaDictUpdater, FunctionalFista
 from ..models.signatures import unit_rows
 from ..models.topk import TopKEncoder
+from . import analytic
 from .ensemble import FunctionalEnsemble
 from .optim import adam
 
@@ -82,6 +83,10 @@ class EnsembleTrainer:
             if use_graph:
                 self.impl.enable_graph()
             self.kind = "fused-sae"
+        elif engine in ("auto", "analytic") and analytic.supports(sig):
+            # closed-form gradients with batched GEMMs (no vmap/autograd): the CPU fast path
+            self.impl = analytic.AnalyticSAEEnsemble(models, sig, lr=lr, device=device)
+            self.kind = "analytic"
         else:
             self.impl = FunctionalEnsemble(models, sig, adam, {"lr": lr}, device=device,
                                            no_stacking=sig is TopKEncoder)
@@ -161,6 +166,8 @@ class EnsembleTrainer:
         elif self.kind == "fused-topk":
             st["impl"] = {"params": self.impl.params, "m": self.impl.m, "v": self.impl.v,
                           "step": self.impl.step_count}
+        elif self.kind == "analytic":
+            st["impl"] = self.impl.state_dict()
         else:
             st["impl"] = {"params": self.impl.params, "optim": self.impl.optim_states}
         if self.fista is not None and self.fista.hessian is not None:
@@ -172,7 +179,7 @@ class EnsembleTrainer:
             raise ValueError(f"checkpoint engine {st['kind']} != {self.kind}")
         self.steps = int(st["steps"])
         imp = st["impl"]
-        if self.kind == "fused-sae":
+        if self.kind in ("fused-sae", "analytic"):
             self.impl.load_state_dict(imp)
         elif self.kind == "fused-topk":
             for d_ in ("params", "m", "v"):

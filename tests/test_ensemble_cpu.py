@@ -108,3 +108,42 @@ def test_sgd_optimizer_runs():
     models = [S.FunctionalSAE.init(8, 16, 1e-3)]
     ens = FunctionalEnsemble(models, S.FunctionalSAE, sgd, {"lr": 1e-2, "momentum": 0.9}, device="cpu")
     ens.step_batch(torch.randn(16, 8))
+
+
+def _analytic_vs_autograd(sig, models, steps=3, lr=1e-3):
+    import torch
+
+    from sparse_coding__amd.engine.analytic import AnalyticSAEEnsemble
+    from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
+    from sparse_coding__amd.engine.optim import adam
+
+    clone = lambda ms: [({k: v.clone() for k, v in p.items()}, {k: v.clone() for k, v in b.items()}) for p, b in ms]
+    ref = FunctionalEnsemble(clone(models), sig, adam, {"lr": lr})
+    ana = AnalyticSAEEnsemble(clone(models), sig, lr=lr)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(steps):
+        x = torch.randn(64, models[0][0]["encoder"].shape[1], generator=g)
+        lr_, _ = ref.step_batch(x)
+        la, _ = ana.step_batch(x)
+        for k in la:
+            torch.testing.assert_close(la[k], lr_[k], rtol=1e-5, atol=1e-6)
+    for k in ana.params:
+        torch.testing.assert_close(ana.params[k], ref.params[k].detach(), rtol=1e-4, atol=1e-5)
+
+
+def test_analytic_engine_matches_autograd_all_sae_kinds():
+    import torch
+
+    from sparse_coding__amd.models.signatures import (FunctionalMaskedSAE, FunctionalMaskedTiedSAE, FunctionalSAE,
+                                                      FunctionalTiedSAE)
+
+    torch.manual_seed(0)
+    _analytic_vs_autograd(FunctionalSAE, [FunctionalSAE.init(16, 32, l1, bias_decay=bd)
+                                          for l1, bd in ((1e-3, 0.0), (3e-3, 0.1))])
+    rot = torch.linalg.qr(torch.randn(16, 16))[0]
+    _analytic_vs_autograd(FunctionalTiedSAE, [FunctionalTiedSAE.init(16, 32, 1e-3, bias_decay=0.05, rotation=rot,
+                                                                     translation=torch.randn(16),
+                                                                     scaling=torch.rand(16) + 0.5)
+                                              for _ in range(2)])
+    _analytic_vs_autograd(FunctionalMaskedTiedSAE, [FunctionalMaskedTiedSAE.init(16, s, 32, 1e-3) for s in (16, 32)])
+    _analytic_vs_autograd(FunctionalMaskedSAE, [FunctionalMaskedSAE.init(16, s, 32, 1e-3) for s in (8, 32)])

@@ -104,7 +104,7 @@ def test_trainer_eager_matches_functional_ensemble():
     models = [FunctionalSAE.init(32, 64, l1) for l1 in (1e-3, 1e-2)]
     ref = FunctionalEnsemble([(dict(p), dict(b)) for p, b in models], FunctionalSAE, adam, {"lr": 1e-3})
     tr = EnsembleTrainer(models, FunctionalSAE, lr=1e-3, batch_size=16, device="cpu")
-    assert tr.kind == "eager" and tr.engine_reason == "no GPU"
+    assert tr.kind == "analytic" and tr.engine_reason == "no GPU"
     x = torch.randn(16, 32)
     for _ in range(3):
         l_ref, _ = ref.step_batch(x)

@@ -54,7 +54,7 @@ def test_trainer_engines_selected():
     assert EnsembleTrainer(t, TopKEncoder, batch_size=256, device="cuda:0").kind == "fused-topk"
     odd = [FunctionalSAE.init(200, 512, 1e-3)]
     tr = EnsembleTrainer(odd, FunctionalSAE, batch_size=256, device="cuda:0")
-    assert tr.kind == "eager" and "not tiled" in tr.engine_reason
+    assert tr.kind == "analytic" and "not tiled" in tr.engine_reason
 
 
 def test_fista_cli_on_gpu(tmp_path):
