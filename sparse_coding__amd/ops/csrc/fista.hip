@@ -63,7 +63,11 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int rb = a.B / FR;
-  const int g = blockIdx.x / rb, r0 = (blockIdx.x % rb) * FR;
+  // XCD-aware order: each XCD works on a contiguous run of row blocks, i.e. on one or two
+  // models, so its L2 holds those dictionaries (D and D^T, 4 n d bytes) instead of a slice
+  // of every model's.
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int g = bid / rb, r0 = (bid % rb) * FR;
   const uint16_t* X = a.X + ((long)g * a.B + r0) * d;
   const uint16_t* D = a.D + (long)g * n * d;
   const uint16_t* Dt = a.Dt + (long)g * d * n;

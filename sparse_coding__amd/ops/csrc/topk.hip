@@ -5,9 +5,10 @@
 // vmap over models because k changes the output shape (no_stacking=True,
 // big_sweep_experiments.py:246-253); here k lives in device memory and every
 // model runs in the same launches:
-//   topk_select_kernel   : exact per-row radix select (4 x 8-bit passes over the
-//                          orderable bit pattern, LDS histograms), scores kept in
-//                          registers; emits (idx, value) pairs.
+//   topk_select_kernel   : exact per-row radix select (11/11/10-bit passes over the
+//                          orderable bit pattern, per-wave LDS histograms, parallel
+//                          digit search), scores kept in registers; emits (idx, value)
+//                          pairs in column order.
 //   topk_decode_grad     : one wave per row: sparse decode x_hat = sum_j v_j D[idx_j]
 //                          (bf16 dictionary gathered from L2), residual, per-row
 //                          squared error, then the k code gradients <R, D[idx_j]>
@@ -22,77 +23,152 @@ __device__ __forceinline__ uint32_t order_key(float f) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // larger float -> larger key
 }
 
+// Exact per-row top-k by radix select on the orderable bit pattern: three digit
+// passes (11, 11, 10 bits).  Each pass builds the histogram of the still-eligible
+// keys in four per-wave copies (a quarter of the LDS-atomic contention of one
+// shared histogram: the leading digit of similar-magnitude scores hits few bins),
+// then all 256 threads locate the digit holding the k-th largest key with a
+// block-wide suffix scan (no serial bin walk).  Selected entries are written in a
+// fixed thread-major order from one packed block scan, ties at the threshold are
+// taken in that order, so the output is deterministic.
+constexpr int TK_NT = 256;
+constexpr int TK_BINS = 2048;
+
 template <int PER>  // keys per thread (n <= 256 * PER)
-__global__ __launch_bounds__(256) void topk_select_kernel(const float* __restrict__ scores, const int* __restrict__ kv,
-                                                          int* __restrict__ idx, float* __restrict__ val, int B, int n,
-                                                          int kmax, int absolute, int relu) {
-  __shared__ uint32_t hist[256];
-  __shared__ int sel[4];  // digit, count above, out cursor, tie cursor
+__global__ __launch_bounds__(TK_NT) void topk_select_kernel(const float* __restrict__ scores, const int* __restrict__ kv,
+                                                            int* __restrict__ idx, float* __restrict__ val, int B, int n,
+                                                            int kmax, int absolute, int relu) {
+  __shared__ uint32_t hist[4][TK_BINS];
+  __shared__ uint32_t wsum[8];
+  __shared__ int sel[2];  // selected digit, keys strictly above it
   const long row = blockIdx.x;
   const int g = row / B;
   const int k = min(kv[g], n);
   const float* S = scores + row * n;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t key[PER];
   float sv[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    const int c = tid + i * 256;
+    const int c = tid + i * TK_NT;
     const float s = c < n ? S[c] : 0.f;
     sv[i] = s;
     key[i] = c < n ? order_key(absolute ? fabsf(s) : s) : 0u;  // padding sorts below every real key
   }
   uint32_t prefix = 0, mask = 0;
   int remaining = k;
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    hist[tid] = 0;
+  const int shifts[3] = {21, 10, 0};
+  const int widths[3] = {11, 11, 10};
+#pragma unroll
+  for (int pass = 0; pass < 3; ++pass) {
+    if (k == 0) break;
+    const int shift = shifts[pass];
+    const uint32_t dmask = (1u << widths[pass]) - 1u;
+    for (int b = tid; b < 4 * TK_BINS; b += TK_NT) (&hist[0][0])[b] = 0;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      if (tid + i * 256 < n && (key[i] & mask) == prefix) atomicAdd(&hist[(key[i] >> shift) & 255u], 1u);
+      if (tid + i * TK_NT < n && (key[i] & mask) == prefix) atomicAdd(&hist[w][(key[i] >> shift) & dmask], 1u);
     }
     __syncthreads();
-    if (tid == 0) {
-      int above = 0, b = 255;
-      for (; b > 0; --b) {
-        if (above + (int)hist[b] >= remaining) break;
-        above += hist[b];
+    // thread t owns bins [8t, 8t + 8) (descending search: high bins first)
+    uint32_t cnt[8], tot = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int b = tid * 8 + j;
+      cnt[j] = hist[0][b] + hist[1][b] + hist[2][b] + hist[3][b];
+      tot += cnt[j];
+    }
+    // suffix sum over threads: above(t) = sum of totals of threads > t
+    uint32_t incl = tot;  // inclusive suffix scan within the wave (lanes above)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_down(incl, o, 64);
+      if (lane + o < 64) incl += v;
+    }
+    if (lane == 0) wsum[w] = incl;  // wave total
+    __syncthreads();
+    uint32_t above = incl - tot;  // lanes above within the wave
+    for (int ww = w + 1; ww < 4; ++ww) above += wsum[ww];
+    // the k-th largest key lies in this thread's range iff above < remaining <= above + tot
+    if (above < (uint32_t)remaining && (uint32_t)remaining <= above + tot) {
+      uint32_t a = above;
+      int j = 7;
+      for (; j > 0; --j) {
+        if (a + cnt[j] >= (uint32_t)remaining) break;
+        a += cnt[j];
       }
-      sel[0] = b;
-      sel[1] = above;
+      sel[0] = tid * 8 + j;
+      sel[1] = (int)a;
     }
     __syncthreads();
     prefix |= (uint32_t)sel[0] << shift;
-    mask |= 255u << shift;
+    mask |= dmask << shift;
     remaining -= sel[1];
     __syncthreads();
   }
-  // prefix is now the k-th largest key; take everything above it and `remaining` ties
-  if (tid == 0) { sel[2] = 0; sel[3] = 0; }
-  __syncthreads();
+  // prefix is the k-th largest key: take every key above it and the first `remaining`
+  // ties.  Output order is thread-major (thread t's keys in i order, then thread t+1):
+  // deterministic, one block-wide scan of packed (above, tie) counts.
   int* I = idx + row * kmax;
   float* V = val + row * kmax;
+  if (k > 0) {
+    uint32_t na = 0, nt = 0;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = tid + i * 256;
-    if (c >= n || k == 0) continue;
-    bool take = key[i] > prefix;
-    if (!take && key[i] == prefix) take = atomicAdd(&sel[3], 1) < remaining;
-    if (take) {
-      const int pos = atomicAdd(&sel[2], 1);
-      I[pos] = c;
-      V[pos] = relu ? fmaxf(sv[i], 0.f) : sv[i];
+    for (int i = 0; i < PER; ++i) {
+      const bool valid = tid + i * TK_NT < n;
+      na += (valid && key[i] > prefix) ? 1u : 0u;
+      nt += (valid && key[i] == prefix) ? 1u : 0u;
+    }
+    const uint32_t packed = (na << 16) | nt;  // n <= 65535
+    uint32_t incl = packed;  // inclusive prefix within the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t excl = incl - packed;
+    for (int ww = 0; ww < w; ++ww) excl += wsum[ww];
+    int pos_a = (int)(excl >> 16);          // keys above the threshold before this thread
+    int tie_rank = (int)(excl & 0xFFFFu);   // ties before this thread
+    // taken ties occupy the slots after every key above; keys above come first in slot order
+    uint32_t tot = 0;
+    for (int ww = 0; ww < 4; ++ww) tot += wsum[ww];
+    const int total_above = (int)(tot >> 16);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * TK_NT;
+      if (c >= n) continue;
+      int pos = -1;
+      if (key[i] > prefix) {
+        pos = pos_a++;
+      } else if (key[i] == prefix) {
+        if (tie_rank < remaining) pos = total_above + tie_rank;
+        ++tie_rank;
+      }
+      if (pos >= 0) {
+        I[pos] = c;
+        V[pos] = relu ? fmaxf(sv[i], 0.f) : sv[i];
+      }
     }
   }
   // pad the unused slots of models with k < kmax
-  for (int j = k + tid; j < kmax; j += 256) {
+  for (int j = k + tid; j < kmax; j += TK_NT) {
     I[j] = 0;
     V[j] = 0.f;
   }
 }
 
 // One wave per (model, row).  D: [G][n][d] bf16 normalised dictionary (gathered rows).
-template <int NV>  // d == 256 * NV ... handled generically with NV = ceil(d / 256)
+// Decode gathers the k dictionary rows four at a time (indices and values are
+// wave-uniform scalar loads issued ahead of the row loads).  The k code gradients
+// <R, D[idx_j]> are reduced sixteen at a time with a butterfly reduce-scatter:
+// every lane accumulates 16 partial dots, four exchange steps (8, 4, 2, 1) leave lane
+// L with dot j = L & 15 summed over its 16-lane group, two more finish the wave --
+// 17 shuffles per 16 dots instead of 6 per dot.
+template <int NV>  // d <= 256 * NV
 __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
     const int* __restrict__ idx, const float* __restrict__ val, const int* __restrict__ kv,
     const uint16_t* __restrict__ D, const uint16_t* __restrict__ X, long sx, uint16_t* __restrict__ R,
@@ -109,19 +185,29 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
   float acc[NV * 4];
 #pragma unroll
   for (int e = 0; e < NV * 4; ++e) acc[e] = 0.f;
-  for (int j = 0; j < k; ++j) {
-    const float w = V[j];
-    if (w == 0.f) continue;  // wave-uniform
-    const uint16_t* Dr = Dg + (long)I[j] * d;
+  for (int j0 = 0; j0 < k; j0 += 4) {
+    int ij[4];
+    float wj[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = j0 + u < k;
+      ij[u] = ok ? I[j0 + u] : 0;
+      wj[u] = ok ? V[j0 + u] : 0.f;  // zero weight: contributes nothing
+    }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = (v * 64 + lane) * 4;
       if (e < d) {
-        const ushort4 h = *reinterpret_cast<const ushort4*>(Dr + e);
-        acc[v * 4 + 0] += w * bf2f(h.x);
-        acc[v * 4 + 1] += w * bf2f(h.y);
-        acc[v * 4 + 2] += w * bf2f(h.z);
-        acc[v * 4 + 3] += w * bf2f(h.w);
+        ushort4 h[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) h[u] = *reinterpret_cast<const ushort4*>(Dg + (long)ij[u] * d + e);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc[v * 4 + 0] += wj[u] * bf2f(h[u].x);
+          acc[v * 4 + 1] += wj[u] * bf2f(h[u].y);
+          acc[v * 4 + 2] += wj[u] * bf2f(h[u].z);
+          acc[v * 4 + 3] += wj[u] * bf2f(h[u].w);
+        }
       }
     }
   }
@@ -150,23 +236,47 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
   // code gradients (units of R): dscore_j = 1[v_j > 0] <R, D[idx_j]>; scatter code and dscore
   uint16_t* Cb = codebuf + row * (long)n;
   uint16_t* Sb = dscbuf + row * (long)n;
-  for (int j = 0; j < k; ++j) {
-    const float w = V[j];
-    const uint16_t* Dr = Dg + (long)I[j] * d;
-    float dot = 0.f;
+  for (int j0 = 0; j0 < k; j0 += 16) {
+    float p[16];
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int e = (v * 64 + lane) * 4;
-      if (e < d) {
-        const ushort4 h = *reinterpret_cast<const ushort4*>(Dr + e);
-        dot += acc[v * 4 + 0] * bf2f(h.x) + acc[v * 4 + 1] * bf2f(h.y) + acc[v * 4 + 2] * bf2f(h.z) +
-               acc[v * 4 + 3] * bf2f(h.w);
+    for (int u = 0; u < 16; ++u) {
+      const int j = j0 + u;
+      const int ij = j < k ? I[j] : 0;
+      const uint16_t* Dr = Dg + (long)ij * d;
+      float dot = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int e = (v * 64 + lane) * 4;
+        if (e < d) {
+          const ushort4 h = *reinterpret_cast<const ushort4*>(Dr + e);
+          dot += acc[v * 4 + 0] * bf2f(h.x) + acc[v * 4 + 1] * bf2f(h.y) + acc[v * 4 + 2] * bf2f(h.z) +
+                 acc[v * 4 + 3] * bf2f(h.w);
+        }
+      }
+      p[u] = dot;
+    }
+    // butterfly reduce-scatter over lane bits 3..0: lane L keeps index L & 15
+#pragma unroll
+    for (int sft = 8; sft >= 1; sft >>= 1) {
+      const bool upper = (lane & sft) != 0;
+#pragma unroll
+      for (int t = 0; t < sft; ++t) {
+        const float send = upper ? p[t] : p[t + sft];
+        const float keep = upper ? p[t + sft] : p[t];
+        p[t] = keep + __shfl_xor(send, sft, 64);
       }
     }
-    dot = wave_sum(dot);
-    if (lane == 0 && w > 0.f) {
-      Cb[I[j]] = f2bf(w);
-      Sb[I[j]] = f2bf(dot);
+    float dot = p[0];
+    dot += __shfl_xor(dot, 16, 64);
+    dot += __shfl_xor(dot, 32, 64);
+    const int j = j0 + (lane & 15);
+    if (lane < 16 && j < k) {
+      const float w = V[j];
+      if (w > 0.f) {
+        const int c = I[j];
+        Cb[c] = f2bf(w);
+        Sb[c] = f2bf(dot);
+      }
     }
   }
 }

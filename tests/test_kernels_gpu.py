@@ -276,7 +276,10 @@ def test_topk_select_exact():
         torch.testing.assert_close(got, ref)
         torch.testing.assert_close(scores[g].gather(-1, idx[g, :, :kg].long()), val[g, :, :kg])
         assert (val[g, :, kg:] == 0).all()
-        assert idx[g, :, :kg].sort(-1).values.diff(dim=-1).ne(0).all()  # no duplicates
+        assert idx[g, :, :kg].sort(-1).values.diff(dim=-1).gt(0).all()  # no duplicates
+    assert int(idx[0, 0, 0]) == 0  # k=1 among 10 tied maxima: thread-major order takes index 0
+    idx2, val2 = T.topk_select(scores, k, 150, relu=False)
+    assert torch.equal(idx2, idx) and torch.equal(val2, val)
     ia, va = T.topk_select(scores, k, 150, absolute=True, relu=False)
     ref = torch.topk(scores[2].abs(), 150, dim=-1).values.sort(-1).values
     torch.testing.assert_close(va[2].abs().sort(-1).values, ref)
