@@ -23,6 +23,8 @@ FunctionalMaskedTiedSAE).  Masked models pass per-model ``dict_size``.
 
 from __future__ import annotations
 
+import os
+
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -306,7 +308,8 @@ class FusedSAEEnsemble:
     def _step_kernels(self, x, count=None):
         """All kernels of one step.  Optionally (``overlap_adam``) untied models overlap the
         memory-bound decoder Adam (side stream) with the compute-bound encoder wgrad GEMM."""
-        if self.kind == "untied" and self.overlap_adam and not self.fuse_adam:
+        if (self.kind == "untied" and self.overlap_adam and not self.fuse_adam
+                and os.environ.get("SC_SERIALIZE_STREAMS", "0") in ("", "0")):
             main = torch.cuda.current_stream(self.device)
             sets = self._adam_sets()
             self.forward(x, count)

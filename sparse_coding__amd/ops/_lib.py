@@ -107,9 +107,24 @@ def available() -> bool:
         return False
 
 
+_DEBUG_SYNC = os.environ.get("SC_DEBUG_SYNC", "0") not in ("", "0")
+
+
+def set_debug_sync(on: bool):
+    """Synchronise after every kernel launch and surface asynchronous faults at the
+    launch that caused them (``utils.debug.debug_mode``; env ``SC_DEBUG_SYNC=1``)."""
+    global _DEBUG_SYNC
+    _DEBUG_SYNC = bool(on)
+
+
 def check(rc: int, what: str):
     if rc != 0:
         raise KernelError(f"{what} failed with code {rc}")
+    if _DEBUG_SYNC and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+        try:
+            torch.cuda.current_stream().synchronize()
+        except RuntimeError as e:  # a fault inside the kernel just launched
+            raise KernelError(f"{what} faulted: {e}") from e
 
 
 def ptr(t) -> int:

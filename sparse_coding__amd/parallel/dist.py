@@ -49,6 +49,9 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600, device=No
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # fail fast: a dead or hung rank aborts the collective (and the job) after
+        # `timeout_s` instead of hanging every other rank
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         be = backend or ("nccl" if use_cuda else "gloo")
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":

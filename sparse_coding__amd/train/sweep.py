@@ -76,6 +76,62 @@ def unstacked_to_learned_dicts(trainer: EnsembleTrainer, args: dict, ensemble_hp
     return trainer.to_learned_dicts(ensemble_hparams, buffer_hparams)
 
 
+def filter_learned_dicts(learned_dicts, hyperparam_filters: dict):
+    """Dicts whose hyper-parameters match (floats to rel 1e-3) -- reference big_sweep.py:61-74."""
+    from math import isclose
+
+    return [(ld, hp) for ld, hp in learned_dicts
+            if all(isclose(hp[k], v, rel_tol=1e-3) if isinstance(v, float) else hp[k] == v
+                   for k, v in hyperparam_filters.items())]
+
+
+@torch.no_grad()
+def log_standard_metrics(learned_dicts, sample: torch.Tensor, chunk_num: int, hyperparam_ranges: dict,
+                         logger: Optional[Logger], image_dir: Optional[str] = None):
+    """Per-dict ever-active counts on a sample (numbers to the logger) and, with
+    ``image_dir``, MMCS-with-larger-dict grids and code-sparsity histograms as PNGs
+    (reference big_sweep.py:87-158, wandb images there)."""
+    from itertools import product
+
+    from ..eval import metrics as M
+
+    log = {}
+    for ld, hp in learned_dicts:
+        ld.to_device(sample.device)
+        name = make_hyperparam_name(hp)
+        n_act = int(M.batched_calc_feature_n_ever_active(ld, sample, threshold=1))
+        log[name + "_n_active"] = n_act
+        log[name + "_prop_active"] = n_act / ld.get_learned_dict().shape[0]
+    if logger is not None:
+        logger.log(log, chunk_num)
+    if not image_dir:
+        return log
+    from ..eval import plotting as P
+
+    os.makedirs(image_dir, exist_ok=True)
+    l1_values = list(hyperparam_ranges.get("l1_alpha", []))
+    sizes = list(hyperparam_ranges.get("dict_size", []))
+    grid_hps = [k for k in hyperparam_ranges if k not in ("l1_alpha", "dict_size")]
+    if len(sizes) > 1 and l1_values:
+        for setting in product(*[hyperparam_ranges[h] for h in grid_hps]):
+            base = dict(zip(grid_hps, setting))
+            scores = np.zeros((len(l1_values), len(sizes) - 1))
+            for i, l1 in enumerate(l1_values):
+                small = filter_learned_dicts(learned_dicts, {**base, "l1_alpha": float(l1), "dict_size": sizes[0]})
+                for j, size in enumerate(sizes[1:]):
+                    large = filter_learned_dicts(learned_dicts, {**base, "l1_alpha": float(l1), "dict_size": size})
+                    if small and large:
+                        scores[i, j] = float(M.mcs_duplicates(small[0][0], large[0][0]).mean())
+            img = P.plot_grid(scores, [f"{v:.1e}" for v in l1_values], sizes[1:], "l1_alpha", "dict_size",
+                              cmap="viridis")
+            img.save(os.path.join(image_dir, f"mmcs_grid_{chunk_num}_{make_hyperparam_name(base) or 'all'}.png"))
+    for ld, hp in learned_dicts:
+        img = P.plot_hist(M.mean_nonzero_activations(ld, sample).cpu(), "Mean nonzero activations", "Frequency",
+                          bins=20)
+        img.save(os.path.join(image_dir, f"sparsity_hist_{chunk_num}_{make_hyperparam_name(hp)}.png"))
+    return log
+
+
 def _load_chunk_into_ring(folder: ChunkFolder, handle, ring: DeviceRing, means: Optional[torch.Tensor]):
     host = folder.get(handle)
     ring.size = 0
@@ -170,6 +226,10 @@ def sweep(ensemble_init_func, cfg, info: Optional[DistInfo] = None) -> List[Tupl
             if t is not None:
                 learned_dicts.extend(t.to_learned_dicts(cfg.ensemble_hyperparams, cfg.buffer_hyperparams))
         logger.log({"chunk": i, "chunk_idx": chunk_idx, "chunk_seconds": time.time() - t0}, global_step)
+        if learned_dicts and i % 10 == 0:  # reference cadence (big_sweep.py:416)
+            sample = ring.view()[torch.randperm(ring.size, device=ring.device)[:2000]].float()
+            log_standard_metrics(learned_dicts, sample, i, hparam_ranges, logger,
+                                 os.path.join(cfg.output_folder, "images") if cfg.wandb_images else None)
         suffix = "" if info.world_size == 1 else f"_rank{info.rank}"
         if i == len(chunk_order) - 1 or (i + 1) in CHECKPOINT_COUNTS:
             it_folder = os.path.join(cfg.output_folder, f"_{i}")

@@ -449,3 +449,18 @@ def test_remote_command_builders(monkeypatch):
     assert d.a == 1 and d["b"] == 2 and d.c is None
     with pytest.raises(RuntimeError):
         R.upload_to_s3(__file__, bucket="b")
+
+
+def test_log_standard_metrics_images(tmp_path):
+    from sparse_coding__amd.models.learned_dict import TiedSAE
+    from sparse_coding__amd.train.sweep import filter_learned_dicts, log_standard_metrics
+
+    torch.manual_seed(0)
+    lds = [(TiedSAE(torch.randn(n, 8), torch.zeros(n) - 0.1, norm_encoder=True), {"l1_alpha": l1, "dict_size": n})
+           for n in (16, 32) for l1 in (1e-3, 1e-2)]
+    assert len(filter_learned_dicts(lds, {"dict_size": 16})) == 2
+    log = log_standard_metrics(lds, torch.randn(500, 8), 0, {"l1_alpha": [1e-3, 1e-2], "dict_size": [16, 32]},
+                               None, str(tmp_path / "img"))
+    assert 0 < log["l1_alpha_1.00E-03_dict_size_16_prop_active"] <= 1
+    files = sorted(p.name for p in (tmp_path / "img").iterdir())
+    assert any(f.startswith("mmcs_grid_0") for f in files) and sum(f.startswith("sparsity_hist") for f in files) == 4
