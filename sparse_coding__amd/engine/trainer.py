@@ -58,7 +58,7 @@ class EnsembleTrainer:
     def __init__(self, models: List[Tuple[dict, dict]], sig, lr: float = 1e-3, batch_size: int = 256,
                  device="cuda", engine: str = "auto", name: str = "ensemble", args: Optional[dict] = None,
                  fista_iters: int = 500, fista_backend: str = "auto", persist_hessian: bool = False,
-                 basis_normalize: str = "column", use_graph: bool = False):
+                 basis_normalize: str = "column", use_graph: bool = False, fista_eta: str = "tracked"):
         self.sig = sig
         self.name = name
         self.args = dict(args or {})
@@ -93,7 +93,7 @@ class EnsembleTrainer:
         self.fista = None
         if sig is FunctionalFista:
             self.fista = FistaDictUpdater(num_iter=fista_iters, persist_hessian=persist_hessian,
-                                          normalize=basis_normalize, backend=fista_backend)
+                                          normalize=basis_normalize, backend=fista_backend, eta_method=fista_eta)
         self.last_loss = None
         self.last_losses: Dict[str, torch.Tensor] = {}
         self.steps = 0

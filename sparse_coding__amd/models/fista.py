@@ -138,15 +138,22 @@ class FistaDictUpdater:
     persist_hessian: bool = True   # False reproduces B#3
     normalize: str = "column"      # "column" reproduces B#4, "row" = unit-norm atoms
     backend: str = "auto"          # "hip" | "torch" | "auto"
-    eta_method: str = "eigh"
+    eta_method: str = "tracked"   # "eigh" = exact per call (reference); "tracked" = warm power
+                                  # iteration + exact refresh every 50 calls, 0.1% safe margin
     step: float = 0.001
     lowest_activation: float = 0.001
     hessian: Optional[torch.Tensor] = None
+    _eta: Optional[object] = None  # EtaTracker state when eta_method == "tracked"
 
     def __call__(self, decoder: torch.Tensor, batch: torch.Tensor, codes: torch.Tensor, l1: torch.Tensor):
         """decoder [G, n, d] raw; batch [B, d]; codes [G, B, n]; returns (new decoder, residual, A)."""
         D = unit_rows(decoder.float())
-        eta = fista_ops.step_size(D, self.eta_method)
+        if self.eta_method == "tracked":
+            if self._eta is None:
+                self._eta = fista_ops.EtaTracker()
+            eta = self._eta(D)
+        else:
+            eta = fista_ops.step_size(D, self.eta_method)
         A, res = fista_ops.fista(batch, D, l1, codes, self.num_iter, eta, backend=self.backend)
         G, n = D.shape[0], D.shape[1]
         H0 = self.hessian if (self.persist_hessian and self.hessian is not None) else torch.zeros(G, n, device=D.device)

@@ -74,8 +74,8 @@ def basic_l1_sweep(dataset_dir: str, output_dir: str, ratio: float, l1_values=np
                    batch_size: int = 128, device: Optional[str] = None, lr: float = 1e-3, n_repetitions: int = 1,
                    save_after_every: bool = False, signature: str = "fista", fista_iters: int = 500,
                    fista_backend: str = "auto", persist_hessian: bool = False, basis_normalize: str = "column",
-                   engine: str = "auto", seed: int = 0, progress: bool = True, max_batches: Optional[int] = None
-                   ) -> List[str]:
+                   engine: str = "auto", seed: int = 0, progress: bool = True, max_batches: Optional[int] = None,
+                   fista_eta: str = "tracked") -> List[str]:
     """Returns the list of checkpoint paths written."""
     device = torch.device(device or ("cuda:0" if torch.cuda.is_available() else "cpu"))
     folder = ChunkFolder(dataset_dir)
@@ -92,7 +92,7 @@ def basic_l1_sweep(dataset_dir: str, output_dir: str, ratio: float, l1_values=np
                               name="ensemble", args={"batch_size": batch_size, "device": str(device),
                                                      "dict_size": latent},
                               fista_iters=fista_iters, fista_backend=fista_backend,
-                              persist_hessian=persist_hessian, basis_normalize=basis_normalize)
+                              persist_hessian=persist_hessian, basis_normalize=basis_normalize, fista_eta=fista_eta)
     rows_max = max(folder.meta(i)[0][0] for i in folder.indices)
     fused = trainer.kind.startswith("fused")
     ring = DeviceRing(rows_max, d, device=device, dtype=torch.bfloat16 if fused else torch.float32, seed=seed)
@@ -131,7 +131,8 @@ def main(argv=None):
     l1_values = np.logspace(args.l1_value_min, args.l1_value_max, args.l1_value_n)
     basic_l1_sweep(args.dataset_dir, args.output_dir, args.ratio, l1_values, args.batch_size, args.device,
                    args.adam_lr, args.n_repetitions, args.save_after_every, args.signature, args.fista_iters,
-                   args.fista_backend, args.persist_hessian, args.basis_normalize, args.engine, args.seed)
+                   args.fista_backend, args.persist_hessian, args.basis_normalize, args.engine, args.seed,
+                   fista_eta=args.fista_eta)
     return 0
 
 

@@ -175,6 +175,7 @@ def sweep(ensemble_init_func, cfg, info: Optional[DistInfo] = None) -> List[Tupl
                                         fista_backend=getattr(cfg, "fista_backend", "auto"),
                                         persist_hessian=getattr(cfg, "persist_hessian", False),
                                         basis_normalize=getattr(cfg, "basis_normalize", "column"),
+                                        fista_eta=getattr(cfg, "fista_eta", "tracked"),
                                         use_graph=cfg.use_graph))
 
     n_chunks = len(folder)

@@ -281,6 +281,7 @@ class SweepArgs(EnsembleArgs):
     adam_lr: float = 1e-3
     fista_iters: int = 500
     fista_backend: str = "auto"
+    fista_eta: str = "tracked"        # "eigh" reproduces the reference's exact eigvalsh per call
     persist_hessian: bool = False     # reference quirk B#3 (throwaway EMA) by default
     basis_normalize: str = "column"   # reference quirk B#4 by default
     signature: str = "fista"          # fista | sae | tied

@@ -331,3 +331,39 @@ def test_fista_kernel_matches_oracle(G, B, n, d):
     def obj(A_, R_):
         return 0.5 * R_.pow(2).sum((1, 2)) + lam * A_.abs().sum((1, 2))
     torch.testing.assert_close(obj(A, R), obj(A_ref, R_ref), rtol=1e-2, atol=1e-3)
+
+
+def test_fused_and_topk_steps_deterministic_under_debug_mode():
+    """Every training-path kernel is deterministic (no float atomics): two runs from the
+    same state agree bitwise; debug mode also syncs after each launch."""
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+    from sparse_coding__amd.models.topk import TopKEncoder
+    from sparse_coding__amd.utils import debug
+
+    xs = [torch.randn(256, 256, device=DEV).to(torch.bfloat16) for _ in range(3)]
+
+    def make_sae():
+        torch.manual_seed(9)
+        return FusedSAEEnsemble([FunctionalSAE.init(256, 512, l1, device=DEV) for l1 in (1e-4, 1e-3)],
+                                FunctionalSAE, batch_size=256, device=DEV)
+
+    def run_sae(e):
+        for x in xs:
+            e.step_batch(x)
+        return {**e.params, "out": e.out}
+
+    def make_topk():
+        torch.manual_seed(9)
+        return FusedTopKEnsemble([TopKEncoder.init(256, 512, k, device=DEV) for k in (4, 16)], batch_size=256,
+                                 device=DEV)
+
+    def run_topk(e):
+        for x in xs:
+            e.step_batch(x)
+        return dict(e.params)
+
+    with debug.debug_mode():
+        debug.assert_deterministic(make_sae, run_sae)
+        debug.assert_deterministic(make_topk, run_topk)

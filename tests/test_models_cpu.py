@@ -239,3 +239,18 @@ def test_ica_and_nmf_fit():
     nmf.train(Xp)
     assert torch.equal(Xp, X)  # fix B#21: inputs are not mutated
     assert nmf.encode(X[:5]).shape == (5, 3)
+
+
+def test_eta_tracker_conservative_and_accurate():
+    import torch
+
+    from sparse_coding__amd.ops import fista as F
+
+    torch.manual_seed(0)
+    D = torch.nn.functional.normalize(torch.randn(3, 64, 32), dim=-1)
+    tr = F.EtaTracker(refresh_every=4)
+    for step in range(9):
+        D = torch.nn.functional.normalize(D + 1e-3 * torch.randn_like(D), dim=-1)
+        est, exact = tr(D), F.step_size(D)
+        assert (est <= exact * (1 + 1e-6)).all()            # never a larger step than 1/L
+        assert ((exact - est) / exact).abs().max() < 2e-3   # within the margin
