@@ -35,7 +35,7 @@ constexpr int TK_NT = 256;
 constexpr int TK_BINS = 2048;
 
 template <int PER>  // keys per thread (n <= 256 * PER)
-__global__ __launch_bounds__(TK_NT) void topk_select_kernel(const float* __restrict__ scores, const int* __restrict__ kv,
+__global__ __launch_bounds__(TK_NT, 4) void topk_select_kernel(const float* __restrict__ scores, const int* __restrict__ kv,
                                                             int* __restrict__ idx, float* __restrict__ val, int B, int n,
                                                             int kmax, int absolute, int relu) {
   __shared__ uint32_t hist[4][TK_BINS];
@@ -304,7 +304,7 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
 #define SC_T(P) \
   if (per <= P) { hipLaunchKernelGGL((topk_select_kernel<P>), grid, dim3(256), 0, stream, scores, k, idx, val, B, n, kmax, absolute, relu); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
-  SC_T(4) SC_T(8) SC_T(16) SC_T(32) SC_T(64)
+  SC_T(4) SC_T(8) SC_T(16) SC_T(24) SC_T(32) SC_T(48) SC_T(64)
 #undef SC_T
   return 1;
 }
