@@ -63,7 +63,7 @@ def main():
     res["step_no_overlap"] = (timeit(lambda: e.step_batch(x)), 5 * fl)
     e.overlap_adam = False
     for cfg in (1, 2, 3):
-        for epi in range(6):
+        for epi in range(7):
             gemm.set_config(epi, cfg)
         res[f"enc_cfg{cfg}"] = (timeit(lambda: gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c,
                                                                 e.enc_part, e.cnt_part, None)), fl)
@@ -72,7 +72,7 @@ def main():
         res[f"wgrad2_cfg{cfg}"] = (timeit(lambda: gemm.weight_grads([[(e.c, e.r)], [(e.dpre, x)]],
                                                                     [e.g_dec, e.g_enc], 1e-6)), 2 * fl)
         res[f"step_cfg{cfg}"] = (timeit(lambda: e.step_batch(x)), 5 * fl)
-    for epi in range(6):
+    for epi in range(7):
         gemm.set_config(epi, 0)
     res["adam"] = (timeit(lambda: adam_ops.adam_rows(e._adam_sets(), e.lr, 3)), 0)
     res["bias_loss"] = (timeit(lambda: e._bias_loss(True, False)), 0)

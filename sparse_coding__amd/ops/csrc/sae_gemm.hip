@@ -6,6 +6,8 @@
 // (reference autoencoders/ensemble.py:119-123) with explicit kernels:
 //
 //   EPI_ENC : c = relu(x W_e^T + b)  (+ masked tail), bf16 store, L1/L0 partials
+//   EPI_ENC_CNT: EPI_ENC + per-feature fire counts (a separate instantiation: the
+//             count reduction costs ~10% of the kernel and runs only on sampled steps)
 //             (autoencoders/sae_ensemble.py:54-56, :354 masked_fill_)
 //   EPI_DEC : R = c W_hat - x, bf16 store, sum(R^2) partials
 //             (autoencoders/sae_ensemble.py:58-62)
@@ -50,7 +52,7 @@ using S256 = Shape<2, 4, 8, 4>;
 // consumers (loss / bias / Adam kernels) do not depend on the GEMM configuration.
 constexpr int PT = 128;
 
-enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5 };
+enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5, EPI_ENC_CNT = 6 };
 
 struct Operand {
   const uint16_t* ptr;
@@ -256,6 +258,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   // Only the weight-gradient style epilogues take a second K segment (K-concat);
   // the fused forward epilogues never do, and skipping its offsets saves VGPRs.
   constexpr bool SEG2 = (EPI == EPI_F32 || EPI == EPI_BF16 || EPI == EPI_ADAM);
+  constexpr bool ENC = (EPI == EPI_ENC || EPI == EPI_ENC_CNT);
   const int nk1 = p.K1 / BKT, nk = nk1 + (SEG2 ? p.K2 / BKT : 0);
   // per-lane DMA source offsets for both K segments
   uint32_t va0[PPWA], vb0[PPWB], va1[SEG2 ? PPWA : 1], vb1[SEG2 ? PPWB : 1];
@@ -420,11 +423,11 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
     }
   };
 
-  if constexpr (EPI == EPI_ENC) {
+  if constexpr (ENC) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     const float* bias = p.bias + (long)g * p.sbias;
     const int nact = p.nactive ? p.nactive[g] : p.N;  // masked SAEs: live columns [0, nact)
-    const bool counting = p.colpart != nullptr;
+    constexpr bool counting = EPI == EPI_ENC_CNT;
     float l1 = 0.f, l0 = 0.f;
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
@@ -450,11 +453,11 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
         *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + col) =
             make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
       }
-      colred_lane(cnt, j, 0);  // unconditional: a branch here re-versions the loop
+      if constexpr (counting) colred_lane(cnt, j, 0);
     }
     l1 = block_sum<NW>(l1, red + 4096);  // its barriers also publish the colred_lane writes
     l0 = block_sum<NW>(l0, red + 4096);
-    if (counting) colred_store(p.colpart, 0);
+    if constexpr (counting) colred_store(p.colpart, 0);
     scalar_partial(p.part, 2, 0, l1);
     scalar_partial(p.part, 2, 1, l0);
     return;
@@ -623,6 +626,7 @@ int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_
   // epilogues; the plain F32 / BF16 epilogues exist for every layout.
   switch (epi) {
     case EPI_ENC: if (!(ak && bk)) return 5; SC_L(true, true, EPI_ENC); break;
+    case EPI_ENC_CNT: if (!(ak && bk)) return 5; SC_L(true, true, EPI_ENC_CNT); break;
     case EPI_DEC: if (!(ak && !bk)) return 5; SC_L(true, false, EPI_DEC); break;
     case EPI_DC: if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC); break;
     case EPI_ADAM: if (ak || bk) return 5; SC_L(false, false, EPI_ADAM); break;

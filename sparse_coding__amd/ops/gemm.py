@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 
-EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16, EPI_ADAM = 0, 1, 2, 3, 4, 5
+EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16, EPI_ADAM, EPI_ENC_CNT = 0, 1, 2, 3, 4, 5, 6
 TILE_M, TILE_N, TILE_K = 128, 128, 64
 
 # Block shapes of the kernel (BK64 x 2-stage LDS-DMA ring for all of them):
@@ -30,7 +30,7 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 # epilogues are fastest on 128x128 blocks (two blocks per CU overlap one block's epilogue
 # with the other's MFMA loop: enc 61 vs 84 us on 256x256), the plain fp32 weight-gradient
 # GEMM (K = B = 2048) on 256x256 blocks (65 vs 74 us) -- "auto" picks that.
-_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 1}
+_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 1, EPI_ENC_CNT: 1}
 _CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 
@@ -129,7 +129,7 @@ def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None):
         _need(nactive.dtype == torch.int32 and nactive.numel() == G, "nactive must be int32[G]")
     a = [_op(x, d, sx), _op(x, d, sx)]
     b = [_op(w, d, n * d), _op(w, d, n * d)]
-    _launch(EPI_ENC, 3, B, n, d, 0, G, a, b, [c_out], [1.0], n, B * n,
+    _launch(EPI_ENC_CNT if colpart is not None else EPI_ENC, 3, B, n, d, 0, G, a, b, [c_out], [1.0], n, B * n,
             bias=bias, sbias=n, nactive=nactive, part=part, colpart=colpart)
 
 
