@@ -55,14 +55,23 @@ class FusedSAEEnsemble:
         n, d = self.n, self.d
         if B % 128 or n % 128 or d % 256:
             raise ValueError(f"fused path needs B%128==0, n%128==0, d%256==0 (got B={B}, n={n}, d={d})")
-        if self.kind == "tied":
-            for key in ("center_rot", "center_trans", "center_scale"):
-                if key in b0:
-                    ref = {"center_rot": torch.eye(d), "center_trans": torch.zeros(d),
-                           "center_scale": torch.ones(d)}[key]
-                    for m in models:
-                        if not torch.equal(m[1][key].detach().float().cpu(), ref):
-                            raise ValueError("fused tied path supports identity centering only")
+        # Tied SAEs may carry a fixed affine centering x_c = ((x - t) R^T) * s per model
+        # (reference sae_ensemble.py:126-131).  Non-identity centering runs as one extra
+        # grouped GEMM (x R^T) plus an elementwise pass into a per-model x_c buffer; every
+        # later kernel then reads x_c (per-model operand stride).
+        self.centering = None
+        if self.kind == "tied" and "center_rot" in b0:
+            eye = torch.eye(d)
+            ident = all(torch.equal(m[1]["center_rot"].detach().float().cpu(), eye)
+                        and not bool(m[1]["center_trans"].detach().any())
+                        and bool((m[1]["center_scale"].detach() == 1).all()) for m in models)
+            if not ident:
+                rot = torch.stack([m[1]["center_rot"].detach().float() for m in models]).to(device)
+                trans = torch.stack([m[1]["center_trans"].detach().float() for m in models]).to(device)
+                scale = torch.stack([m[1]["center_scale"].detach().float() for m in models]).to(device)
+                self.centering = {"rot": rot.to(torch.bfloat16).contiguous(),
+                                  "tR": torch.bmm(trans.unsqueeze(1), rot.transpose(1, 2)),  # [G, 1, d]
+                                  "scale": scale.unsqueeze(1).contiguous()}
         dev = self.device
         self.models_meta = [{k: v for k, v in m[1].items()} for m in models]
         self.betas, self.eps = betas, eps
@@ -140,6 +149,9 @@ class FusedSAEEnsemble:
         self.dotpart = torch.zeros(G, tm, n, device=dev)        # norm-Jacobian row-dot partials
         self.sqpart = torch.zeros(G, n, d // 128, device=dev)   # updated-row |w|^2 partials
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)  # graph input buffer
+        if self.centering is not None:
+            self._xr = torch.empty(G, B, d, device=dev)              # x R^T (fp32)
+            self.x_c = torch.empty(G, B, d, device=dev, dtype=bf)    # centred input per model
 
     # ------------------------------------------------------------------ helpers
     def refresh_shadows(self):
@@ -149,6 +161,18 @@ class FusedSAEEnsemble:
             adam_ops.shadow_rows(self.params["decoder"], self.dec_shadow, self.norms, normalize=True)
         else:
             adam_ops.shadow_rows(self.params["encoder"], self.enc_shadow, self.norms, normalize=True)
+
+    def prepare(self, x):
+        """The kernels' input: ``x`` itself, or its per-model centred copy for tied SAEs
+        with non-identity centering."""
+        if self.centering is None:
+            return x
+        c = self.centering
+        gemm_ops.matmul_nt(x, c["rot"], self._xr)
+        torch.sub(self._xr, c["tR"], out=self._xr)
+        self._xr.mul_(c["scale"])
+        self.x_c.copy_(self._xr)
+        return self.x_c
 
     def _x_bf16(self, batch):
         if batch.dtype != torch.bfloat16:
@@ -308,6 +332,7 @@ class FusedSAEEnsemble:
     def _step_kernels(self, x, count=None):
         """All kernels of one step.  Optionally (``overlap_adam``) untied models overlap the
         memory-bound decoder Adam (side stream) with the compute-bound encoder wgrad GEMM."""
+        x = self.prepare(x)
         if (self.kind == "untied" and self.overlap_adam and not self.fuse_adam
                 and os.environ.get("SC_SERIALIZE_STREAMS", "0") in ("", "0")):
             main = torch.cuda.current_stream(self.device)
@@ -347,6 +372,33 @@ class FusedSAEEnsemble:
         self._graph[count].replay()
         self._host_step()
         return self.out
+
+    @torch.no_grad()
+    def evaluate(self, rows: torch.Tensor):
+        """FVU and mean L0 of every model on ``rows`` [N, d] (N a multiple of the batch size),
+        from the encoder / decoder kernels' own epilogue partials -- no extra passes over the
+        codes (reference standard_metrics.py:303-312 computed per model in fp32 torch).
+        Returns (fvu [G], l0 [G]) on the device."""
+        B, G = self.batch_size, self.n_models
+        N = rows.shape[0] - rows.shape[0] % B
+        if N == 0:
+            raise ValueError(f"need at least {B} rows")
+        se = torch.zeros(G, device=self.device, dtype=torch.float64)
+        l0 = torch.zeros(G, device=self.device, dtype=torch.float64)
+        s1 = torch.zeros(G, self.d, device=self.device, dtype=torch.float64)
+        s2 = torch.zeros(G, device=self.device, dtype=torch.float64)
+        for i in range(0, N, B):
+            x = self.prepare(self._x_bf16(rows[i:i + B]))
+            gemm_ops.encode_relu(x, self.enc_shadow, self.params["encoder_bias"], self.c, self.enc_part, None,
+                                 self.nactive)
+            gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
+            se += self.dec_part.sum(1).double()
+            l0 += self.enc_part[..., 1].sum(1).double()
+            xf = x.double() if x.dim() == 3 else x.double().expand(G, B, self.d)
+            s1 += xf.sum(1)
+            s2 += xf.pow(2).sum((1, 2))
+        var = s2 - s1.pow(2).sum(-1) / N  # total sum of squares about the mean
+        return (se / var).float(), (l0 / N).float()
 
     def loss_dicts(self, out=None):
         out = (self.out if out is None else out).detach().cpu()

@@ -44,13 +44,6 @@ def _fused_ok(models, sig, batch_size, device) -> Tuple[bool, str]:
         return True, "fused top-k"
     if getattr(sig, "fused_kind", None) is None:
         return False, f"no fused kernels for {sig.__name__}"
-    if getattr(sig, "fused_kind") == "tied":
-        for k, ref in (("center_rot", None), ("center_trans", 0.0), ("center_scale", 1.0)):
-            if k in b0:
-                t = b0[k].float()
-                ok = torch.equal(t.cpu(), torch.eye(d)) if ref is None else bool((t == ref).all())
-                if not ok:
-                    return False, "non-identity centering (eager path)"
     return True, f"fused {sig.fused_kind} SAE"
 
 

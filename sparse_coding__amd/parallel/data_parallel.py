@@ -66,6 +66,7 @@ class DataParallelFused:
         x = e._x_bf16(batch)
         if not self.info.enabled:
             return e.step_batch(x)
+        x = e.prepare(x)
         e.forward(x)
         e.wgrad_first(x)
         first = e.g_dec if e.kind == "untied" else e._g_flat
@@ -149,6 +150,7 @@ class FusedChunk:
 
     def compute_grads(self, x):
         e = self.engine
+        x = e.prepare(e._x_bf16(x))
         e.forward(x)
         e.wgrad_first(x)
         e.wgrad_second(x, reduce_bias=True)  # pre-scaled by 1/world: SUM all-reduce = mean

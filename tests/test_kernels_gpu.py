@@ -367,3 +367,49 @@ def test_fused_and_topk_steps_deterministic_under_debug_mode():
     with debug.debug_mode():
         debug.assert_deterministic(make_sae, run_sae)
         debug.assert_deterministic(make_topk, run_topk)
+
+
+def test_fused_tied_with_affine_centering_matches_closed_form():
+    """Non-identity centering buffers run in the fused engine (x R^T GEMM + elementwise)."""
+    from sparse_coding__amd.engine.analytic import AnalyticSAEEnsemble
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalTiedSAE
+
+    torch.manual_seed(11)
+    d, n, B = 256, 512, 256
+    models = []
+    for l1 in (1e-4, 1e-3):
+        rot = torch.linalg.qr(torch.randn(d, d))[0]
+        models.append(FunctionalTiedSAE.init(d, n, l1, rotation=rot, translation=0.1 * torch.randn(d),
+                                             scaling=torch.rand(d) + 0.5))
+    dev_models = [({k: v.to(DEV) for k, v in p.items()}, {k: v.to(DEV) for k, v in b.items()}) for p, b in models]
+    fused = FusedSAEEnsemble(dev_models, FunctionalTiedSAE, batch_size=B, device=DEV)
+    ref = AnalyticSAEEnsemble(dev_models, FunctionalTiedSAE, device=DEV)
+    for _ in range(4):
+        x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
+        out = fused.step_batch(x)
+        losses, _ = ref.step_batch(x.float())
+        torch.testing.assert_close(out[:, 1], losses["l_reconstruction"], rtol=3e-2, atol=1e-4)
+    init = torch.stack([m[0]["encoder"] for m in dev_models])
+    du, dr = (fused.params["encoder"] - init).flatten(), (ref.params["encoder"] - init).flatten()
+    assert torch.nn.functional.cosine_similarity(du, dr, dim=0).item() > 0.97
+
+
+def test_fused_evaluate_matches_metrics():
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.eval.metrics import batched_fvu_l0
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+
+    torch.manual_seed(12)
+    d, n, B = 256, 512, 256
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-2)]
+    e = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV)
+    feats = torch.nn.functional.normalize(torch.randn(1024, d, device=DEV), dim=-1)
+    for _ in range(20):
+        e.step_batch((torch.relu(torch.randn(B, 1024, device=DEV) - 2) @ feats).to(torch.bfloat16))
+    rows = (torch.relu(torch.randn(4 * B, 1024, device=DEV) - 2) @ feats).to(torch.bfloat16)
+    fvu, l0 = e.evaluate(rows)
+    for g, ld in enumerate(e.to_learned_dicts(DEV)):
+        f_ref, l_ref = batched_fvu_l0(ld, rows.float())
+        assert abs(float(fvu[g]) - f_ref) < 0.02 + 0.02 * f_ref, (g, float(fvu[g]), f_ref)
+        assert abs(float(l0[g]) - l_ref) < 0.05 * max(l_ref, 1.0), (g, float(l0[g]), l_ref)
