@@ -187,8 +187,8 @@ class FusedSAEEnsemble:
 
     def forward(self, x, count=None):
         """Kernels 1-3: codes (+L1/L0), residual (+MSE), code gradient (+bias-grad partials)."""
-        if x.shape[0] != self.batch_size:
-            raise ValueError(f"batch has {x.shape[0]} rows, engine was built for {self.batch_size}")
+        if x.shape[-2] != self.batch_size:
+            raise ValueError(f"batch has {x.shape[-2]} rows, engine was built for {self.batch_size}")
         count = self._counting() if count is None else count
         self._counted = count
         gemm_ops.encode_relu(x, self.enc_shadow, self.params["encoder_bias"], self.c, self.enc_part,
@@ -378,6 +378,7 @@ class FusedSAEEnsemble:
         """FVU and mean L0 of every model on ``rows`` [N, d] (N a multiple of the batch size),
         from the encoder / decoder kernels' own epilogue partials -- no extra passes over the
         codes (reference standard_metrics.py:303-312 computed per model in fp32 torch).
+        For centred tied models the FVU is measured in the centred space the model sees.
         Returns (fvu [G], l0 [G]) on the device."""
         B, G = self.batch_size, self.n_models
         N = rows.shape[0] - rows.shape[0] % B
