@@ -46,7 +46,21 @@ def parse(argv=None):
     ap.add_argument("--engine", choices=["fused", "eager"], default="fused")
     ap.add_argument("--ring-rows", type=int, default=1 << 21)
     ap.add_argument("--eval-rows", type=int, default=16384)
+    ap.add_argument("--act-norm", type=float, default=9.0,
+                    help="mean L2 norm the synthetic rows are scaled to.  Calibrated on the reference's "
+                         "shipped Pythia-70m layer-2 TiedSAE (l1=1e-3: L0~77, unit-norm atoms, bias ~-0.85 "
+                         "=> |x|^2 ~ 77 codes of O(1)), so the reference's L1 range logspace(-4,-2) spans "
+                         "dense to very sparse codes as it does on the real activations")
+    ap.add_argument("--quality-steps", type=int, default=3000,
+                    help="after the timed region, keep training (untimed) until this many steps in total "
+                         "before the FVU@L0 evaluation (the timed K steps alone are far from converged)")
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--parallelism", choices=["auto", "es", "dp"], default="auto",
+                    help="N>1: 'es' = ensemble-axis sharding (each GPU owns models/N models and trains "
+                         "them on the all-gathered global batch: identical updates to data parallel on the "
+                         "global batch, but only the 2 MB batch crosses xGMI instead of 67 MB of gradients); "
+                         "'dp' = data parallel with chunk-pipelined RCCL gradient all-reduce; "
+                         "auto = es when models %% N == 0")
     ap.add_argument("--dp-chunks", type=int, default=2,
                     help="N>1: split the ensemble into this many model chunks whose gradient all-reduce "
                          "overlaps the next chunk's compute (1 = one reduction per step)")
@@ -54,6 +68,9 @@ def parse(argv=None):
                     help="auto = RCCL ('nccl') on GPUs; gloo only for rehearsals")
     ap.add_argument("--shared-gpu", action="store_true",
                     help="rehearsal: every rank on cuda:0 (with --dist-backend gloo on a 1-GPU box)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="create the process group even at N=1 and run the N>1 code path (rehearses the "
+                         "sharded step with real RCCL collectives on a one-GPU box)")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of a HIP graph")
     return ap.parse_args(argv)
@@ -66,9 +83,11 @@ def build_ring(args, device):
     gen = RandomDatasetGenerator(activation_dim=args.d, n_ground_truth_components=8 * args.d,
                                  batch_size=65536, feature_num_nonzero=32, feature_prob_decay=0.999,
                                  correlated=False, device=device, seed=1234)
+    probe = gen.send(None)
+    scale = args.act_norm / float(probe.norm(dim=-1).mean()) if args.act_norm > 0 else 1.0
     ring = DeviceRing(args.ring_rows, args.d, device=device, seed=4321)
-    ring.fill(lambda: gen.send(None))
-    held_out = gen.send(None)[: args.eval_rows]
+    ring.fill(lambda: gen.send(None) * scale)
+    held_out = gen.send(None)[: args.eval_rows] * scale
     return ring, held_out
 
 
@@ -83,7 +102,7 @@ def main(argv=None):
     from sparse_coding__amd.parallel.dist import all_reduce_max, barrier, init_distributed, shutdown
 
     info = init_distributed(None if args.dist_backend == "auto" else args.dist_backend,
-                            device="cuda:0" if args.shared_gpu else None)
+                            device="cuda:0" if args.shared_gpu else None, force=args.force_dist)
     if not torch.cuda.is_available():
         print("bench.py needs an MI355X (torch.cuda.is_available() is False)", file=sys.stderr)
         return 2
@@ -99,7 +118,32 @@ def main(argv=None):
     B = args.batch
 
     grad_dtype = torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32
-    if args.engine == "fused" and info.world_size > 1:
+    par = args.parallelism
+    if par == "auto":
+        par = "es" if (info.world_size > 1 and args.models % info.world_size == 0) else "dp"
+    if args.force_dist and args.parallelism == "auto":
+        par = "es"
+    if info.world_size == 1 and not args.force_dist:
+        par = "dp"
+    if args.engine == "fused" and par == "es":
+        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+        from sparse_coding__amd.parallel.ensemble_shard import EnsembleSharded
+
+        es = EnsembleSharded(models, lambda m, bs: FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=bs, device=device),
+                             info, batch_per_rank=B, d=args.d)
+        if not args.no_graph:
+            es.enable_graph()
+        metas = [b for _, b in models]
+
+        def sample(out):
+            return ring.sample_shard(B, info.rank, info.world_size, out=out)
+
+        def step():
+            es.step_sampled(sample)
+
+        def dicts():
+            return es.to_learned_dicts(metas, sig, device)
+    elif args.engine == "fused" and (info.world_size > 1 or args.force_dist):
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
 
@@ -163,8 +207,17 @@ def main(argv=None):
     value = total_rows / elapsed
 
     quality = None
-    if not args.no_eval and info.is_main:
-        quality = fvu_l0(dicts(), held_out.float())
+    trained = args.warmup + args.steps
+    if not args.no_eval:
+        while trained < args.quality_steps:  # untimed: train on toward convergence before evaluating
+            step()
+            trained += 1
+        torch.cuda.synchronize()
+        lds = dicts()  # collective in the sharded mode: every rank takes part
+        if info.is_main:
+            quality = fvu_l0(lds, held_out.float())
+    if par == "es":
+        es.flush()
 
     if info.is_main:
         rec = {
@@ -179,17 +232,17 @@ def main(argv=None):
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_ACT_PER_S, 2),
             "dtype": "bf16",
-            "data": "synthetic (sparse mixture of 4096 unit-norm features, Pythia-70m d_model=512 shape; "
-                    "random-init SAE weights)",
+            "data": "synthetic (sparse mixture of 4096 unit-norm features, Pythia-70m d_model=512 shape, "
+                    f"rows scaled to mean norm {args.act_norm}; random-init SAE weights)",
             "config": {
                 "model": f"pythia-70m-resid-sae-ensemble ({args.kind}, d=512, ratio={args.ratio}, "
                          f"{args.models} models, l1=logspace(-4,-2,{args.models}))",
                 "global_batch": B * info.world_size,
                 "seq_len": None,
                 "per_gpu_batch": B,
-                "parallelism": f"dp{info.world_size}",
+                "parallelism": f"{par}{info.world_size}",
                 "engine": args.engine,
-                "dp_chunks": args.dp_chunks if info.world_size > 1 else None,
+                "dp_chunks": args.dp_chunks if par == "dp" and info.world_size > 1 else None,
                 "grad_allreduce_dtype": args.grad_dtype,
             },
             "model_activations_per_s": round(value * args.models, 1),
@@ -199,6 +252,8 @@ def main(argv=None):
         if quality is not None:
             rec["fvu_at_l0"] = [{"l1": float(l), "l0": round(a, 2), "fvu": round(b, 4)}
                                 for l, (a, b) in zip(l1s, quality)]
+            rec["fvu_eval"] = {"train_steps": trained, "held_out_rows": int(held_out.shape[0]),
+                               "act_norm": args.act_norm}
         print(json.dumps(rec), flush=True)
     shutdown(info)
     return 0

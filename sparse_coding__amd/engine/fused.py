@@ -42,7 +42,7 @@ class FusedSAEEnsemble:
 
     def __init__(self, models, sig, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999),
                  eps=1e-8, track_feature_counts=True, kind: Optional[str] = None, fuse_adam: bool = False,
-                 count_every: int = 8):
+                 count_every: int = 8, wgrad_split="auto"):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
         if self.kind not in ("untied", "tied"):
@@ -125,6 +125,16 @@ class FusedSAEEnsemble:
             self.g_dec = self._g_flat[: G * n * d].view(G, n, d)
             self.g_enc = None
         self.g_bias = self._g_flat[G * n * d:].view(G, 1, n)
+        # Split-K of the single-device weight-gradient GEMM: with few models on a large
+        # batch (ensemble sharding gives each GPU G/N models on N*B rows) the 256x256 grid
+        # has fewer blocks than CUs, so the K = B reduction is split over blocks and the
+        # Adam kernel sums the partial slabs.  (Data-parallel paths use the flat buffers.)
+        nprob = 2 if self.kind == "untied" else 1
+        kdim = B if self.kind == "untied" else 2 * B
+        self.wsplit = (gemm_ops.wgrad_split(G, n, d, kdim, nprob) if wgrad_split == "auto" else int(wgrad_split))
+        self.g_parts = (torch.empty(nprob, self.wsplit, G, n, d, device=dev, dtype=torch.float32)
+                        if self.wsplit > 1 else None)
+        self._g_from_parts = False
         self.grad_scale = 1.0  # data parallel: 1 / world_size (gradients are then summed)
         self.enc_part = torch.zeros(G, tm * (n // 128), 2, device=dev)
         self.dec_part = torch.zeros(G, tm * (d // 128), device=dev)
@@ -149,6 +159,7 @@ class FusedSAEEnsemble:
         self.dotpart = torch.zeros(G, tm, n, device=dev)        # norm-Jacobian row-dot partials
         self.sqpart = torch.zeros(G, n, d // 128, device=dev)   # updated-row |w|^2 partials
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)  # graph input buffer
+        self._static_inputs = [self.x_static]
         if self.centering is not None:
             self._xr = torch.empty(G, B, d, device=dev)              # x R^T (fp32)
             self.x_c = torch.empty(G, B, d, device=dev, dtype=bf)    # centred input per model
@@ -222,6 +233,7 @@ class FusedSAEEnsemble:
 
     def wgrad_first(self, x):
         """Untied: dW_hat = c^T R (decoder).  Tied: the whole dictionary gradient + bias grad."""
+        self._g_from_parts = False
         if self.kind == "untied":
             gemm_ops.weight_grads([[(self.c, self.r)]], [self.g_dec], self._alpha)
         else:
@@ -249,19 +261,31 @@ class FusedSAEEnsemble:
         if self.fuse_adam:
             self.wgrad_adam(x)
             return
+        split = self.g_parts is not None
+        self._g_from_parts = split
         if self.kind == "untied":
-            gemm_ops.weight_grads([[(self.c, self.r)], [(self.dpre, x)]], [self.g_dec, self.g_enc], self._alpha)
+            outs = [self.g_parts[0], self.g_parts[1]] if split else [self.g_dec, self.g_enc]
+            gemm_ops.weight_grads([[(self.c, self.r)], [(self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit)
         else:
-            gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], [self.g_dec], self._alpha)
+            outs = [self.g_parts[0]] if split else [self.g_dec]
+            gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit)
 
     def _adam_sets(self):
+        parts = self._g_from_parts
+        g_dec = self.g_parts[0, 0] if parts else self.g_dec
         if self.kind == "untied":
-            return [dict(p=self.params["decoder"], g=self.g_dec, m=self.m["decoder"], v=self.v["decoder"],
+            g_enc = self.g_parts[1, 0] if parts else self.g_enc
+            return [dict(p=self.params["decoder"], g=g_dec, m=self.m["decoder"], v=self.v["decoder"],
                          shadow=self.dec_shadow, norms=self.norms, norm=True),
-                    dict(p=self.params["encoder"], g=self.g_enc, m=self.m["encoder"], v=self.v["encoder"],
+                    dict(p=self.params["encoder"], g=g_enc, m=self.m["encoder"], v=self.v["encoder"],
                          shadow=self.enc_shadow, norm=False)]
-        return [dict(p=self.params["encoder"], g=self.g_dec, m=self.m["encoder"], v=self.v["encoder"],
+        return [dict(p=self.params["encoder"], g=g_dec, m=self.m["encoder"], v=self.v["encoder"],
                      shadow=self.enc_shadow, norms=self.norms, norm=True)]
+
+    def _adam_split_kw(self):
+        if self._g_from_parts:
+            return dict(nsplit=self.wsplit, gstride=self.n_models * self.n * self.d)
+        return {}
 
     def adam_first(self):
         adam_ops.adam_rows(self._adam_sets()[:1], self.lr, self.step_count + 1, *self.betas, self.eps,
@@ -283,7 +307,7 @@ class FusedSAEEnsemble:
     def _apply_update_kernels(self):
         if not self.fuse_adam:  # with fuse_adam the weights were already updated in wgrad_adam
             adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
-                               step_dev=self.step_dev)
+                               step_dev=self.step_dev, **self._adam_split_kw())
         self._bias_loss(update=True, reduced=False)
 
     def _host_step(self):
@@ -311,8 +335,10 @@ class FusedSAEEnsemble:
         """One Adam step of every model on ``batch [B, d]``; returns a device tensor [G, 6]:
         (loss, l_reconstruction, l_l1, l_bias_decay, mean L0, |b|).  Never synchronises."""
         if self.use_graph:
-            if batch is not self.x_static:
-                self.x_static.copy_(batch, non_blocking=True)
+            for i, t in enumerate(self._static_inputs):
+                if batch is t:
+                    return self.step_static(i)
+            self.x_static.copy_(batch, non_blocking=True)
             return self.step_static()
         x = self._x_bf16(batch)
         self._step_kernels(x)
@@ -353,23 +379,34 @@ class FusedSAEEnsemble:
             self.backward_weights(x)
             self._apply_update_kernels()
 
+    def add_static_input(self, t: torch.Tensor) -> int:
+        """Register another persistent input buffer [B, d] bf16: ``step_batch(t)`` then replays
+        a graph captured on ``t`` itself (no copy into ``x_static``; e.g. the two halves of a
+        double-buffered batch prefetch).  Returns its index for ``step_static``."""
+        if t.dtype != torch.bfloat16 or tuple(t.shape) != (self.batch_size, self.d) or not t.is_contiguous():
+            raise ValueError("static inputs must be contiguous bf16 [batch_size, d]")
+        self._static_inputs.append(t)
+        self._graph = None  # recapture on next use
+        return len(self._static_inputs) - 1
+
     def _capture(self):
         torch.cuda.synchronize(self.device)
         self._graph = {}
-        for count in (True, False):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._step_kernels(self.x_static, count)
-            self._graph[count] = g
+        for i, xin in enumerate(self._static_inputs):
+            for count in (True, False):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._step_kernels(xin, count)
+                self._graph[(count, i)] = g
 
-    def step_static(self):
+    def step_static(self, which: int = 0):
         """Replay the captured step on whatever is in ``x_static`` (fill it first, e.g. with
-        ``torch.index_select(..., out=engine.x_static)``)."""
+        ``torch.index_select(..., out=engine.x_static)``), or on static input ``which``."""
         if self._graph is None:
             self._capture()
         count = self._counting()
         self._counted = count
-        self._graph[count].replay()
+        self._graph[(count, which)].replay()
         self._host_step()
         return self.out
 

@@ -13,26 +13,41 @@ def _vp(seq):
     return (C.c_void_p * len(seq))(*[_lib.ptr(t) for t in seq])
 
 
-def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, step_dev=None):
+def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, step_dev=None, nsplit=1,
+              gstride=0, row0=0):
     """Fused row-wise Adam over one or two parameter sets.
 
     sets: list of dicts with keys p, g, m, v (fp32 [G, n, d]), shadow (bf16 [G, n, d] or None),
     norms (fp32 [G, n] or None), norm (bool: parameter is row-normalised inside the loss).
     lr: fp32 tensor [G] (per-model learning rate); step: 1-based Adam step (host value), or
     ``step_dev``: int32 device counter of completed steps (the kernel uses ``*step_dev + 1``;
-    graph-capturable).
+    graph-capturable).  ``nsplit`` > 1: each ``g`` is the first of ``nsplit`` split-K partial
+    slabs ``gstride`` elements apart, summed in the kernel.  ``row0``: global index of the
+    sets' first row (row-sharded updates; the per-model lr is ``lr[(row0 + row) // n]``).
+    Tensors may be [G, n, d] or [rows, d] (then pass ``rows_per_model``).
     """
     if not 1 <= len(sets) <= 2:
         raise ValueError("1 or 2 parameter sets")
-    G, n, d = sets[0]["p"].shape
+    shp = tuple(sets[0]["p"].shape)
+    d = shp[-1]
+    nrows = sets[0]["p"].numel() // d
+    n = shp[1] if len(shp) == 3 else None
     for s in sets:
         for k in ("p", "g", "m", "v"):
             t = s[k]
-            if t.dtype != torch.float32 or tuple(t.shape) != (G, n, d) or not t.is_contiguous():
-                raise ValueError(f"adam set tensor {k} must be contiguous fp32 {(G, n, d)}")
-        if s.get("shadow") is not None and s["shadow"].dtype != torch.bfloat16:
-            raise ValueError("shadow must be bf16")
-    rows = (C.c_int * len(sets))(*[G * n for _ in sets])
+            if t.dtype != torch.float32 or tuple(t.shape) != shp or not t.is_contiguous():
+                raise ValueError(f"adam set tensor {k} must be contiguous fp32 {shp}")
+        if s.get("shadow") is not None and (s["shadow"].dtype != torch.bfloat16 or s["shadow"].numel() != nrows * d):
+            raise ValueError("shadow must be bf16 of the parameter's size")
+        if s.get("norms") is not None and s["norms"].numel() != nrows:
+            raise ValueError("norms must have one entry per row")
+        if nsplit > 1 and s["g"].untyped_storage().nbytes() < (s["g"].storage_offset() + (nsplit - 1) * gstride
+                                                               + nrows * d) * 4:
+            raise ValueError("gradient storage too small for nsplit slabs")
+    rpm = rows_per_model or n
+    if not rpm:
+        raise ValueError("rows_per_model is required for 2-D parameter sets")
+    rows = (C.c_int * len(sets))(*[nrows for _ in sets])
     norm = (C.c_int * len(sets))(*[int(bool(s["norm"])) for s in sets])
     bc1 = 1.0 - b1 ** step
     bc2 = 1.0 - b2 ** step
@@ -40,8 +55,8 @@ def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, s
         len(sets), _vp([s["p"] for s in sets]), _vp([s["g"] for s in sets]),
         _vp([s["m"] for s in sets]), _vp([s["v"] for s in sets]),
         _vp([s.get("shadow") for s in sets]), _vp([s.get("norms") for s in sets]),
-        rows, norm, d, rows_per_model or n, _lib.ptr(lr), b1, b2, eps, bc1, bc2,
-        _lib.ptr(step_dev), _lib.stream_handle(),
+        rows, norm, d, rpm, _lib.ptr(lr), b1, b2, eps, bc1, bc2,
+        _lib.ptr(step_dev), int(nsplit), int(gstride), int(row0), _lib.stream_handle(),
     )
     _lib.check(rc, "sc_adam_rows")
 

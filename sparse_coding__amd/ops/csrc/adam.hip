@@ -31,6 +31,9 @@ struct AdamArgs {
   int nset;
   int d;
   int rows_per_model;
+  long row0;        // global row index of row 0 (row-sharded updates): lr index = (row0 + row) / rows_per_model
+  int nsplit;       // the gradient arrives as `nsplit` split-K partial slabs ...
+  long gstride;     // ... `gstride` elements apart (summed here; 1 = a plain gradient)
   const float* lr;  // per model
   float b1, b2, eps, bc1, bc2;
   const int* step;  // optional device step counter (graph-capturable); t = *step + 1
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   const AdamRows& R = a.set[s];
   const int d = NV * 256;
   const long base = row * d;
-  const float lr = a.lr[row / a.rows_per_model];
+  const float lr = a.lr[(row + a.row0) / a.rows_per_model];
   // NV float4 chunks per lane (d == 256 * NV); compile-time so pv/gv stay in VGPRs.
   const float* P4 = R.p + base;
   const float* G4 = R.g + base;
@@ -69,6 +72,10 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
     const int e = (i * 64 + lane) * 4;
     pv[i] = *reinterpret_cast<const float4*>(P4 + e);
     gv[i] = *reinterpret_cast<const float4*>(G4 + e);
+    for (int sp = 1; sp < a.nsplit; ++sp) {  // split-K partials of the weight-gradient GEMM
+      const float4 q = *reinterpret_cast<const float4*>(G4 + sp * a.gstride + e);
+      gv[i].x += q.x; gv[i].y += q.y; gv[i].z += q.z; gv[i].w += q.w;
+    }
     ss += pv[i].x * pv[i].x + pv[i].y * pv[i].y + pv[i].z * pv[i].z + pv[i].w * pv[i].w;
     dot += pv[i].x * gv[i].x + pv[i].y * gv[i].y + pv[i].z * gv[i].z + pv[i].w * gv[i].w;
   }
@@ -287,8 +294,8 @@ extern "C" {
 int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const* m, float* const* v,
                  void* const* shadow, float* const* norms, const int* rows, const int* norm, int d,
                  int rows_per_model, const float* lr, float b1, float b2, float eps, float bc1,
-                 float bc2, const int* step, hipStream_t stream) {
-  if (d % 256 || d > 4096 || nset < 1 || nset > 2) return 1;
+                 float bc2, const int* step, int nsplit, long gstride, long row0, hipStream_t stream) {
+  if (d % 256 || d > 4096 || nset < 1 || nset > 2 || nsplit < 1) return 1;
   AdamArgs a;
   long total = 0;
   for (int i = 0; i < nset; ++i) {
@@ -298,6 +305,7 @@ int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const*
   if (nset == 1) a.set[1] = a.set[0], a.set[1].rows = 0;
   a.nset = nset; a.d = d; a.rows_per_model = rows_per_model; a.lr = lr;
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.step = step;
+  a.nsplit = nsplit; a.gstride = gstride; a.row0 = row0;
   const long blocks = (total + 3) / 4;
   switch (d / 256) {
     case 1: hipLaunchKernelGGL(adam_rows_kernel<1>, dim3(blocks), dim3(256), 0, stream, a); break;

@@ -109,6 +109,11 @@ struct GemmParams {
   float b1, b2, eps;
   int dot_tm;          // row tiles in dotpart
   float dot_scale;     // converts dotpart sums to <w_hat, dL/dw_hat>
+  // --- split-K (plain F32 / BF16 epilogues only): K-tile range split over `ksplit`
+  // blocks per output tile; split s writes its partial product at c + s * split_stride
+  // (the consumer -- the Adam kernel for weight gradients -- sums the slabs).
+  int ksplit;
+  long split_stride;
 };
 
 // LDS image of a K-major tile [128 rows][BKT k] bf16.
@@ -236,10 +241,13 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   const int wr = wid / WGN, wc = wid % WGN;
   const int tiles_m = p.M / BM, tiles_n = p.N / BN;
   const int ptm = p.M / PT, ptn = p.N / PT;  // partial-buffer grid (128 x 128 sub-tiles)
-  const int per_prob = tiles_m * tiles_n * p.G;
+  const int per_split = tiles_m * tiles_n * p.G;
+  const int per_prob = per_split * p.ksplit;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int pi = bid / per_prob;
   int rem = bid - pi * per_prob;
+  const int ksi = rem / per_split;
+  rem -= ksi * per_split;
   const int g = rem / (tiles_m * tiles_n);
   rem -= g * tiles_m * tiles_n;
   const int tm = rem / tiles_n, tn = rem - tm * tiles_n;
@@ -253,13 +261,18 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   const Operand ob0 = p1 ? p.prob[1].b[0] : p.prob[0].b[0];
   const Operand ob1 = p1 ? p.prob[1].b[1] : p.prob[0].b[1];
   void* cptr = p1 ? p.prob[1].c : p.prob[0].c;
+  if constexpr (EPI == EPI_F32) cptr = reinterpret_cast<float*>(cptr) + ksi * p.split_stride;
+  if constexpr (EPI == EPI_BF16) cptr = reinterpret_cast<uint16_t*>(cptr) + ksi * p.split_stride;
   const float alpha = p1 ? p.prob[1].alpha : p.prob[0].alpha;
 
   // Only the weight-gradient style epilogues take a second K segment (K-concat);
   // the fused forward epilogues never do, and skipping its offsets saves VGPRs.
   constexpr bool SEG2 = (EPI == EPI_F32 || EPI == EPI_BF16 || EPI == EPI_ADAM);
   constexpr bool ENC = (EPI == EPI_ENC || EPI == EPI_ENC_CNT);
-  const int nk1 = p.K1 / BKT, nk = nk1 + (SEG2 ? p.K2 / BKT : 0);
+  const int nk1 = p.K1 / BKT, nk_all = nk1 + (SEG2 ? p.K2 / BKT : 0);
+  // this block's K-tile range [kbeg, nk) (the whole range unless split-K)
+  const int kbeg = (int)(((long)ksi * nk_all) / p.ksplit);
+  const int nk = (int)(((long)(ksi + 1) * nk_all) / p.ksplit);
   // per-lane DMA source offsets for both K segments
   uint32_t va0[PPWA], vb0[PPWB], va1[SEG2 ? PPWA : 1], vb1[SEG2 ? PPWB : 1];
   piece_offsets<AK, BKT, PPWA>(va0, oa0.ld, m0, wid, lane);
@@ -314,9 +327,9 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
 
 #pragma unroll
   for (int t = 0; t < NST - 1; ++t)
-    if (t < nk) SC_ISSUE(t);
+    if (kbeg + t < nk) SC_ISSUE(kbeg + t);
 
-  for (int kt = 0; kt < nk; ++kt) {
+  for (int kt = kbeg; kt < nk; ++kt) {
     // Tile kt must have landed; tiles kt+1 .. kt+NST-2 may stay in flight.
     const int younger = min(NST - 2, nk - 1 - kt);
     if constexpr (NST >= 4) {
@@ -620,7 +633,7 @@ long n_blocks(int M, int N, int G, int nprob) { return (long)(M / S::BM) * (N / 
 
 template <class S, int BKT, int NST>
 int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
-  const dim3 grid((unsigned)n_blocks<S>(p.M, p.N, p.G, nprob)), block(S::NT);
+  const dim3 grid((unsigned)(n_blocks<S>(p.M, p.N, p.G, nprob) * p.ksplit)), block(S::NT);
 #define SC_L(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_kernel<S, AKV, BKV, E, BKT, NST>), grid, block, 0, stream, p)
   // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
   // epilogues; the plain F32 / BF16 epilogues exist for every layout.
@@ -687,8 +700,9 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             long saux, float* part, float* colpart, const float* l1, float l1_add_scale,
             float* dotpart, int dc_tied, const ScAdamEpi* adam /* [nprob] or null */, const float* lr,
             const int* step, float b1, float b2, float eps, int dot_tm, float dot_scale,
-            int cfg, hipStream_t stream) {
+            int cfg, int ksplit, long split_stride, hipStream_t stream) {
   if (M % PT || N % PT || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
+  if (ksplit < 1 || ksplit > (K1 + K2) / 64 || (ksplit > 1 && epi != EPI_F32 && epi != EPI_BF16)) return 7;
   GemmParams p;
   for (int i = 0; i < nprob; ++i) {
     for (int s = 0; s < 2; ++s) {
@@ -714,6 +728,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   }
   if (epi == EPI_ADAM && (!adam || !lr || !step)) return 4;
   p.lr = lr; p.step = step; p.b1 = b1; p.b2 = b2; p.eps = eps; p.dot_tm = dot_tm; p.dot_scale = dot_scale;
+  p.ksplit = ksplit; p.split_stride = split_stride;
   const bool ak = layout & 1, bk = layout & 2;
   int shape = cfg & 3;
   if (shape == 0) shape = sc_gemm_shape(M, N, G, nprob);

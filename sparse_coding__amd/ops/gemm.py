@@ -78,7 +78,8 @@ def _bf16(t, name):
 def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *,
             bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
             colpart=None, l1=None, l1_add_scale=0.0, dotpart=None, dc_tied=False, adam=None,
-            lr=None, step=None, betas=(0.9, 0.999), eps=1e-8, dot_tm=0, dot_scale=0.0, cfg=None):
+            lr=None, step=None, betas=(0.9, 0.999), eps=1e-8, dot_tm=0, dot_scale=0.0, cfg=None,
+            ksplit=1, split_stride=0):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
@@ -94,7 +95,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
         _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1), float(l1_add_scale),
         _lib.ptr(dotpart), int(bool(dc_tied)), adam, _lib.ptr(lr), _lib.ptr(step),
         float(betas[0]), float(betas[1]), float(eps), int(dot_tm), float(dot_scale),
-        cfg,
+        cfg, int(ksplit), int(split_stride),
         _lib.stream_handle(),
     )
     _lib.check(rc, f"sc_gemm(epi={epi})")
@@ -175,15 +176,28 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None):
             dotpart=dotpart, dc_tied=tied_bias is not None, bias=tied_bias, sbias=n)
 
 
-def weight_grads(pairs, outs, alpha):
+def wgrad_split(G, n, d, K, nprob):
+    """Split-K factor for the weight-gradient GEMM: 1 while the 256x256 grid already fills
+    the 256 CUs; otherwise the smallest power of two that reaches 256 blocks and keeps
+    >= 1024 rows of K per split (few models on a large gathered batch, e.g. one model per
+    GPU with ensemble sharding at N = 8)."""
+    tiles = nprob * G * max(1, n // 256) * max(1, d // 256)
+    s = 1
+    while tiles * s < 256 and K // (2 * s) >= 1024 and K % (2 * s * 64) == 0:
+        s *= 2
+    return s
+
+
+def weight_grads(pairs, outs, alpha, ksplit=1):
     """out_i[g] = alpha * sum_segments A_s[g]^T @ B_s[g]   (reduction over batch rows).
 
     pairs: list (one per problem, 1 or 2 problems) of lists of (A, B) segments
     (1 or 2 segments, summed along K).  A: [G, Bk, n] bf16 (or [Bk, n] shared),
-    B: [G, Bk, d] bf16 (or [Bk, d] shared).  outs: [G, n, d] fp32.
+    B: [G, Bk, d] bf16 (or [Bk, d] shared).  outs: [G, n, d] fp32, or with ``ksplit`` > 1
+    [ksplit, G, n, d] partial slabs (their sum is the product; the Adam kernel sums them).
     """
     _need(1 <= len(pairs) == len(outs) <= 2, "1 or 2 problems")
-    G, n, d = outs[0].shape
+    G, n, d = outs[0].shape[-3:]
     nseg = len(pairs[0])
     _need(all(len(p) == nseg for p in pairs) and 1 <= nseg <= 2, "segments")
     ks = []
@@ -205,9 +219,14 @@ def weight_grads(pairs, outs, alpha):
     _need(len(set(ks)) == 1, "all problems must share K segments")
     K1 = ks[0][0]
     K2 = ks[0][1] if nseg == 2 else 0
+    want = (G, n, d) if ksplit == 1 else (ksplit, G, n, d)
     for o in outs:
-        _need(o.dtype == torch.float32 and tuple(o.shape) == (G, n, d) and o.is_contiguous(), "out")
-    _launch(EPI_F32, 0, n, d, K1, K2, G, a_ops, b_ops, list(outs), [alpha] * len(outs), d, n * d)
+        _need(o.dtype == torch.float32 and tuple(o.shape) == want and o.is_contiguous(), f"out must be {want}")
+    cfg = None
+    if ksplit > 1:
+        cfg = 3 if shape_fits(3, n, d) else 1
+    _launch(EPI_F32, 0, n, d, K1, K2, G, a_ops, b_ops, list(outs), [alpha] * len(outs), d, n * d,
+            cfg=cfg, ksplit=ksplit, split_stride=G * n * d)
 
 
 def weight_grads_adam(pairs, states, alpha, lr, step_dev, betas=(0.9, 0.999), eps=1e-8, dot_tm=0):

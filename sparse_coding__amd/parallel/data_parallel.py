@@ -232,7 +232,7 @@ class ChunkedDataParallel:
                 c.after_param_sync()
 
     def _reduce_async(self, flat):
-        if not self.info.enabled:
+        if not dist.is_initialized():
             return None, flat
         if self.grad_dtype == torch.float32 or flat.dtype == self.grad_dtype:
             return dist.all_reduce(flat, async_op=True), flat

@@ -32,8 +32,10 @@ class DistInfo:
         return self.world_size > 1
 
 
-def init_distributed(backend: str | None = None, timeout_s: int = 600, device=None) -> DistInfo:
-    """``device`` overrides the per-rank device (e.g. several gloo ranks sharing one GPU in a test)."""
+def init_distributed(backend: str | None = None, timeout_s: int = 600, device=None, force: bool = False) -> DistInfo:
+    """``device`` overrides the per-rank device (e.g. several gloo ranks sharing one GPU in a test).
+    ``force`` creates the process group even for a single process (rehearses the collective
+    code paths with real RCCL on a one-GPU box)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -47,7 +49,8 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600, device=No
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
+        os.environ.setdefault("MASTER_PORT", "29511")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # fail fast: a dead or hung rank aborts the collective (and the job) after
         # `timeout_s` instead of hanging every other rank
@@ -86,5 +89,5 @@ def broadcast_(t: torch.Tensor, info: DistInfo, src: int = 0):
 
 
 def shutdown(info: DistInfo):
-    if info.enabled and dist.is_initialized():
+    if dist.is_initialized():
         dist.destroy_process_group()
