@@ -1,0 +1,36 @@
+"""Runs each kernel of the fused SAE step (config 2 shapes) a few times, plus the top-k
+select of config 4, for rocprofv3 counter collection (scripts/gpu_pmc2.sh)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+from sparse_coding__amd.models.signatures import FunctionalSAE
+from sparse_coding__amd.ops import adam as adam_ops
+from sparse_coding__amd.ops import gemm
+from sparse_coding__amd.ops import topk as topk_ops
+
+B, d, n, G = 2048, 512, 2048, 8
+dev = "cuda"
+models = [FunctionalSAE.init(d, n, 1e-3 * (i + 1), device=dev) for i in range(G)]
+e = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=dev)
+x = (torch.randn(B, d, device=dev) * 0.4).to(torch.bfloat16)
+for _ in range(3):
+    e.step_batch(x)
+torch.cuda.synchronize()
+for _ in range(5):
+    gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c, e.enc_part, None, None)
+    gemm.decode_residual(e.c, e.dec_shadow, x, e.r, e.dec_part)
+    gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart)
+    gemm.weight_grads([[(e.c, e.r)], [(e.dpre, x)]], [e.g_dec, e.g_enc], 1e-6)
+    adam_ops.adam_rows(e._adam_sets(), e.lr, 5, step_dev=None)
+torch.cuda.synchronize()
+# config 4 top-k select: 8 models, B=2048, n=6144
+scores = torch.randn(8, 2048, 6144, device=dev)
+k = torch.tensor([8, 16, 24, 32, 48, 64, 96, 128], dtype=torch.int32, device=dev)
+for _ in range(3):
+    topk_ops.topk_select(scores, k, 128)
+torch.cuda.synchronize()
+print("done")

@@ -395,7 +395,9 @@ class FusedSAEEnsemble:
         for i, xin in enumerate(self._static_inputs):
             for count in (True, False):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                # thread_local: RCCL's watchdog thread may query events of in-flight
+                # collectives while this thread captures (ensemble-sharded runs)
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     self._step_kernels(xin, count)
                 self._graph[(count, i)] = g
 

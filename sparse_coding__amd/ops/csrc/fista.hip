@@ -165,6 +165,84 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Gram form (n <= 2d pays; used for n <= d): the gradient step
+//     Y += eta (X - Y D) D^T = Y + eta (C - Y Gm),   C = X D^T [B, n],  Gm = D D^T [n, n]
+// needs ONE [16, n] x [n, n] product per iteration instead of the two products
+// [16, n] x [n, d] and [16, d] x [d, n] above: 2 B n^2 instead of 4 B n d FLOPs and
+// one n^2 (instead of 2 n d) bf16 operand stream from L2 per iteration.  C is computed
+// once per solve (a plain GEMM); it and the fp32 iterates stay in VGPRs.  Gm is
+// symmetric, so a wave reads the rows of its own output columns along k (contiguous
+// 16-byte loads).
+template <int NW>
+__global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restrict__ C, const uint16_t* __restrict__ Gm,
+                                                        const float* __restrict__ A0, const float* __restrict__ eta_,
+                                                        const float* __restrict__ lam_, const float* __restrict__ mom,
+                                                        float* __restrict__ Aout, int B, int T) {
+  constexpr int n = NW * 128;
+  constexpr int nrb = n * 2;
+  __shared__ __attribute__((aligned(16))) char Ybf[FR * nrb];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rb = B / FR;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int g = bid / rb, r0 = (bid % rb) * FR;
+  const uint16_t* Gg = Gm + (long)g * n * n;
+  const float eta = eta_[g], thr = eta_[g] * lam_[g];
+  const int row = lane & 15, q = lane >> 4;
+  const int nbase = w * NW * 16;
+  f32x4_t Y[NW], Ap[NW], Cr[NW];
+#pragma unroll
+  for (int t = 0; t < NW; ++t) {
+    const int col = nbase + t * 16 + 4 * q;
+    const long off = ((long)g * B + r0 + row) * n + col;
+    Cr[t] = *reinterpret_cast<const f32x4_t*>(C + off);
+    f32x4_t v = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (A0) v = *reinterpret_cast<const f32x4_t*>(A0 + off);
+    Y[t] = v;
+    Ap[t] = v;
+    lds_put4(Ybf, row, col, nrb, v[0], v[1], v[2], v[3]);
+  }
+  __syncthreads();
+  for (int it = 0; it < T; ++it) {
+    // Z[16, n_w] = Ybf[16, n] x Gm[n, n_w]
+    f32x4_t Z[NW];
+#pragma unroll
+    for (int t = 0; t < NW; ++t) Z[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < n; k0 += 32) {
+      const bf16x8_t fy = lds_frag(Ybf, row, k0 + 8 * q, nrb);
+#pragma unroll
+      for (int t = 0; t < NW; ++t) {
+        const bf16x8_t fg = *reinterpret_cast<const bf16x8_t*>(Gg + (long)(nbase + t * 16 + row) * n + k0 + 8 * q);
+        Z[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fg, fy, Z[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave has read all of Ybf before it is overwritten
+    const float mo = mom[it];
+    const bool final_iter = it + 1 == T;
+#pragma unroll
+    for (int t = 0; t < NW; ++t) {
+      f32x4_t an;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float y = Y[t][r] + eta * (Cr[t][r] - Z[t][r]);
+        an[r] = fmaxf(y - thr, 0.f);
+        Y[t][r] = an[r] + (an[r] - Ap[t][r]) * mo;
+      }
+      Ap[t] = an;
+      if (!final_iter) {
+        const int col = nbase + t * 16 + 4 * q;
+        lds_put4(Ybf, row, col, nrb, Y[t][0], Y[t][1], Y[t][2], Y[t][3]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < NW; ++t) {
+    const int col = nbase + t * 16 + 4 * q;
+    *reinterpret_cast<f32x4_t*>(Aout + ((long)g * B + r0 + row) * n + col) = Ap[t];
+  }
+}
+
 }  // namespace scamd
 
 using namespace scamd;
@@ -193,6 +271,22 @@ int sc_fista(const void* X, const void* D, const void* Dt, const float* A0, cons
   SC_F(8, 8) SC_F(8, 16)
 #undef SC_F
   return 2;  // shape not instantiated: caller falls back to the torch path
+}
+
+// Gram-form solver: C = X D^T [G][B][n] fp32, Gm = D D^T [G][n][n] bf16.
+int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* eta, const float* lam,
+                  const float* mom, float* A, int G, int B, int n, int T, hipStream_t stream) {
+  if (B % FR || n % 128 || T < 0) return 1;
+  dim3 grid(G * (B / FR));
+  const uint16_t* gm = reinterpret_cast<const uint16_t*>(Gm);
+#define SC_G(NWV)                                                                                      \
+  if (n == NWV * 128) {                                                                                \
+    hipLaunchKernelGGL((fista_gram_kernel<NWV>), grid, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
+    return hipGetLastError() == hipSuccess ? 0 : 3;                                                    \
+  }
+  SC_G(2) SC_G(4) SC_G(6) SC_G(8)
+#undef SC_G
+  return 2;
 }
 
 }  // extern "C"

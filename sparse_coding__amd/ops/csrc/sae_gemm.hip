@@ -631,9 +631,15 @@ bool fits(int M, int N) { return M % S::BM == 0 && N % S::BN == 0; }
 template <class S>
 long n_blocks(int M, int N, int G, int nprob) { return (long)(M / S::BM) * (N / S::BN) * G * nprob; }
 
-template <class S, int BKT, int NST>
+// FULL = every (layout, epilogue) pair; the alternative K pipelines (deeper LDS rings,
+// selected with cfg bits 2-3) instantiate only the step's epilogues and the weight-gradient
+// layout, to keep the build small.
+template <class S, int BKT, int NST, bool FULL = true>
 int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
   const dim3 grid((unsigned)(n_blocks<S>(p.M, p.N, p.G, nprob) * p.ksplit)), block(S::NT);
+  if constexpr (!FULL) {
+    if (epi == EPI_ADAM || epi == EPI_BF16 || (epi == EPI_F32 && (ak || bk))) return 8;
+  }
 #define SC_L(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_kernel<S, AKV, BKV, E, BKT, NST>), grid, block, 0, stream, p)
   // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
   // epilogues; the plain F32 / BF16 epilogues exist for every layout.
@@ -642,18 +648,26 @@ int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_
     case EPI_ENC_CNT: if (!(ak && bk)) return 5; SC_L(true, true, EPI_ENC_CNT); break;
     case EPI_DEC: if (!(ak && !bk)) return 5; SC_L(true, false, EPI_DEC); break;
     case EPI_DC: if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC); break;
-    case EPI_ADAM: if (ak || bk) return 5; SC_L(false, false, EPI_ADAM); break;
+    case EPI_ADAM:
+      if constexpr (FULL) { if (ak || bk) return 5; SC_L(false, false, EPI_ADAM); }
+      break;
     case EPI_F32:
-      if (ak && bk) SC_L(true, true, EPI_F32);
-      else if (ak) SC_L(true, false, EPI_F32);
-      else if (bk) SC_L(false, true, EPI_F32);
-      else SC_L(false, false, EPI_F32);
+      if constexpr (FULL) {
+        if (ak && bk) SC_L(true, true, EPI_F32);
+        else if (ak) SC_L(true, false, EPI_F32);
+        else if (bk) SC_L(false, true, EPI_F32);
+        else SC_L(false, false, EPI_F32);
+      } else {
+        SC_L(false, false, EPI_F32);
+      }
       break;
     case EPI_BF16:
-      if (ak && bk) SC_L(true, true, EPI_BF16);
-      else if (ak) SC_L(true, false, EPI_BF16);
-      else if (bk) SC_L(false, true, EPI_BF16);
-      else SC_L(false, false, EPI_BF16);
+      if constexpr (FULL) {
+        if (ak && bk) SC_L(true, true, EPI_BF16);
+        else if (ak) SC_L(true, false, EPI_BF16);
+        else if (bk) SC_L(false, true, EPI_BF16);
+        else SC_L(false, false, EPI_BF16);
+      }
       break;
     default: return 2;
   }
@@ -692,7 +706,8 @@ int sc_gemm_shape(int M, int N, int G, int nprob) {
 }
 
 // layout: bit0 = A is K-major, bit1 = B is K-major.
-// cfg: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256.
+// cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256;
+// bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4, 2: BK64 x 3, 3: BK32 x 3).
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             const ScOperand* a /* [nprob][2] */, const ScOperand* b /* [nprob][2] */,
             void* const* c /* [nprob] */, const float* alpha /* [nprob] */, long ldc, long sc,
@@ -731,11 +746,24 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.ksplit = ksplit; p.split_stride = split_stride;
   const bool ak = layout & 1, bk = layout & 2;
   int shape = cfg & 3;
+  const int pipe = (cfg >> 2) & 3;  // 0: BK64 x 2 stages, 1: BK32 x 4, 2: BK64 x 3, 3: BK32 x 3
   if (shape == 0) shape = sc_gemm_shape(M, N, G, nprob);
   switch (shape) {
-    case 3: if (!fits<S256>(M, N)) return 6; return launch<S256, 64, 2>(epi, ak, bk, p, nprob, stream);
-    case 2: if (!fits<S256x128>(M, N)) return 6; return launch<S256x128, 64, 2>(epi, ak, bk, p, nprob, stream);
-    default: return launch<S128, 64, 2>(epi, ak, bk, p, nprob, stream);
+    case 3:
+      if (!fits<S256>(M, N)) return 6;
+      if (pipe == 1) return launch<S256, 32, 4, false>(epi, ak, bk, p, nprob, stream);
+      if (pipe == 3) return launch<S256, 32, 3, false>(epi, ak, bk, p, nprob, stream);
+      if (pipe == 2) return 8;  // 192 KB of LDS
+      return launch<S256, 64, 2>(epi, ak, bk, p, nprob, stream);
+    case 2:
+      if (!fits<S256x128>(M, N)) return 6;
+      if (pipe) return 8;
+      return launch<S256x128, 64, 2>(epi, ak, bk, p, nprob, stream);
+    default:
+      if (pipe == 1) return launch<S128, 32, 4, false>(epi, ak, bk, p, nprob, stream);
+      if (pipe == 2) return launch<S128, 64, 3, false>(epi, ak, bk, p, nprob, stream);
+      if (pipe == 3) return launch<S128, 32, 3, false>(epi, ak, bk, p, nprob, stream);
+      return launch<S128, 64, 2>(epi, ak, bk, p, nprob, stream);
   }
 }
 

@@ -33,6 +33,10 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 _CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 1, EPI_ENC_CNT: 1}
 _CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
+# cfg bits 2-3 select the K pipeline: 0 BK64 x 2-stage LDS ring (default), 1 BK32 x 4,
+# 2 BK64 x 3, 3 BK32 x 3 (the alternatives exist for the step's epilogues and the
+# weight-gradient layout only; 256x256 has no BK64 x 3: 192 KB of LDS).
+PIPES = {0: (64, 2), 1: (32, 4), 2: (64, 3), 3: (32, 3)}
 
 
 def set_config(epi: int, cfg: int):
@@ -56,7 +60,7 @@ class force_shape:
 
 
 def shape_fits(cfg: int, M: int, N: int) -> bool:
-    bm, bn = SHAPES.get(int(cfg), (128, 128))
+    bm, bn = SHAPES.get(int(cfg) & 3, (128, 128))
     return M % bm == 0 and N % bn == 0
 
 
@@ -83,7 +87,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
-    _need(cfg == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg)} does not tile M={M}, N={N}")
+    _need((cfg & 3) == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg & 3)} does not tile M={M}, N={N}")
     nprob = len(outs)
     A = (_lib.ScOperand * (2 * nprob))(*a_ops)
     Bo = (_lib.ScOperand * (2 * nprob))(*b_ops)

@@ -80,6 +80,7 @@ class EnsembleSharded:
         self.engine.enable_graph()
         for t in self.gbuf:
             self.engine.add_static_input(t)
+        self.engine._capture()  # now, before any collective is in flight
         return self
 
     # ------------------------------------------------------------------ batch assembly

@@ -83,12 +83,15 @@ def test_identity_asymmetric():
     torch.testing.assert_close(out, bt.float()[:, :M, :], rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("cfg", SHAPE_CFGS)
+PIPE_CFGS = [1 | 1 << 2, 1 | 2 << 2, 1 | 3 << 2, 3 | 1 << 2, 3 | 3 << 2]  # deeper K pipelines
+
+
+@pytest.mark.parametrize("cfg", SHAPE_CFGS + PIPE_CFGS)
 def test_sae_epilogues(cfg):
     from sparse_coding__amd.ops import gemm
 
     with gemm.force_shape(cfg):
-        _sae_epilogues(3, 512, 256, 512 if cfg > 1 else 384)
+        _sae_epilogues(3, 512, 256, 512 if cfg != 1 else 384)
 
 
 def _sae_epilogues(G, B, d, n):
@@ -308,9 +311,13 @@ def test_fused_topk_matches_autograd():
         assert agree.float().mean() > 0.97, agree.float().mean()
 
 
-@pytest.mark.parametrize("G,B,n,d", [(2, 64, 512, 512), (3, 32, 2048, 512), (1, 48, 1024, 1024)])
-def test_fista_kernel_matches_oracle(G, B, n, d):
+@pytest.mark.parametrize("form", ["direct", "gram"])
+@pytest.mark.parametrize("G,B,n,d", [(2, 64, 512, 512), (3, 32, 2048, 512), (1, 48, 1024, 1024), (2, 256, 512, 1024)])
+def test_fista_kernel_matches_oracle(G, B, n, d, form):
     from sparse_coding__amd.ops import fista as F
+
+    if form == "gram" and n not in F.GRAM_N:
+        pytest.skip("gram form instantiated for n <= 1024")
 
     torch.manual_seed(8)
     D = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1)
@@ -323,7 +330,7 @@ def test_fista_kernel_matches_oracle(G, B, n, d):
     Xb = X.to(torch.bfloat16).float()
     A_ref, _ = F.fista_torch(Xb, Db, lam, A0, iters=30, eta=eta)
     R_ref = X - torch.bmm(A_ref, D)
-    A, R = F.fista(X, D, lam, A0, iters=30, eta=eta, backend="hip")
+    A, R = F.fista(X, D, lam, A0, iters=30, eta=eta, backend="hip", form=form)
     torch.cuda.synchronize()
     err_a = (A - A_ref).abs().max().item() / (A_ref.abs().max().item() + 1e-6)
     err_r = (R - R_ref).abs().max().item() / (R_ref.abs().max().item() + 1e-6)
