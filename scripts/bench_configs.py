@@ -33,13 +33,19 @@ def _timed(step, steps, warmup, sync):
     return time.perf_counter() - t0
 
 
-def _ring(d, device, rows=1 << 19, feats=None, k=32):
-    from sparse_coding__amd.data.ring import DeviceRing
+def _ring(d, device, rows=1 << 19, feats=None, k=32, gb=0.0):
+    """HBM ring of synthetic rows; ``gb`` > 0 sizes it in GB of device memory instead (the
+    288 GB MI355X holds ~130 M rows of d = 1024 bf16 in a 270 GB ring)."""
+    from sparse_coding__amd.data.ring import DeviceRing, rows_for_budget
     from sparse_coding__amd.data.synthetic import RandomDatasetGenerator
 
     gen = RandomDatasetGenerator(d, feats or 8 * d, 65536, k, 0.999, False, device, seed=7)
-    ring = DeviceRing(rows, d, device=device, dtype=torch.bfloat16 if device != "cpu" else torch.float32, seed=1)
-    ring.fill(lambda: gen.send(None))
+    dt = torch.bfloat16 if device != "cpu" else torch.float32
+    if gb > 0:
+        rows = rows_for_budget(d, int(gb * 1e9), dt)
+    ring = DeviceRing(rows, d, device=device, dtype=dt, seed=1)
+    scale = 9.0 / float(gen.send(None).norm(dim=-1).mean())  # bench.py --act-norm calibration
+    ring.fill(lambda: gen.send(None) * scale)
     return ring
 
 
@@ -89,7 +95,9 @@ def cfg_fista(a):
     models = [FunctionalFista.init(d, n, float(l1), device=dev) for l1 in l1s]
     tr = EnsembleTrainer(models, FunctionalFista, batch_size=B, device=dev, fista_iters=a.iters,
                          fista_backend="hip")
-    ring = _ring(d, dev)
+    t0 = time.perf_counter()
+    ring = _ring(d, dev, gb=a.ring_gb)
+    fill_s = time.perf_counter() - t0
     xbuf = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
     el = _timed(lambda: tr.step(ring.sample(B, out=xbuf)), a.steps, a.warmup, torch.cuda.synchronize)
     # FISTA solve alone
@@ -99,13 +107,21 @@ def cfg_fista(a):
     x = ring.sample(B).float()
     eta = F.step_size(D)
     lam = torch.tensor(l1s, device=dev, dtype=torch.float32)
-    el_solve = _timed(lambda: F.fista(x, D, lam, None, a.iters, eta, backend="hip", with_res=False), 5, 1,
-                      torch.cuda.synchronize) / 5
+    solves = {}
+    for form in ("direct", "gram"):
+        if form == "gram" and n not in F.GRAM_N:
+            continue
+        solves[form] = _timed(lambda: F.fista(x, D, lam, None, a.iters, eta, backend="hip", with_res=False,
+                                              form=form), 3, 1, torch.cuda.synchronize) / 3
+    el_solve = min(solves.values())
     return {"config": f"5: FISTA {a.iters}-step dictionary learning, Pythia-410m-shaped d={d}, n={n}, "
                       f"{a.models} models (reference row 13: 452 ms per model-solve, d=n=512, 500 it, B=256, CPU)",
             "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
             "solve_ms_all_models": round(1e3 * el_solve, 3),
-            "solve_ms_per_model": round(1e3 * el_solve / a.models, 3), "batch": B, "engine": tr.kind}
+            "solve_ms_per_model": round(1e3 * el_solve / a.models, 3),
+            "solve_ms_by_form": {k: round(1e3 * v, 3) for k, v in solves.items()},
+            "batch": B, "engine": tr.kind, "ring_rows": ring.capacity,
+            "ring_gb": round(ring.capacity * d * 2 / 1e9, 1), "ring_fill_s": round(fill_s, 1)}
 
 
 def cfg_mlp(a):
@@ -123,6 +139,7 @@ def main():
     ap.add_argument("--models", type=int, default=8)
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--ratio", type=float, default=1.0)
+    ap.add_argument("--ring-gb", type=float, default=0.0, help="fista: ring size in GB of HBM (0: 512k rows)")
     a = ap.parse_args()
     rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp}[a.which](a)
     print(json.dumps(rec), flush=True)

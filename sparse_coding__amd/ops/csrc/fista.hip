@@ -208,6 +208,9 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
     f32x4_t Z[NW];
 #pragma unroll
     for (int t = 0; t < NW; ++t) Z[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // n is a compile-time constant here: cap the unroll, a full one hoists every Gm load
+    // (NW x n / 32 fragments) and spills
+#pragma unroll 2
     for (int k0 = 0; k0 < n; k0 += 32) {
       const bf16x8_t fy = lds_frag(Ybf, row, k0 + 8 * q, nrb);
 #pragma unroll
@@ -268,7 +271,7 @@ int sc_fista(const void* X, const void* D, const void* Dt, const float* A0, cons
   SC_F(2, 2) SC_F(2, 4) SC_F(2, 8) SC_F(2, 16)
   SC_F(4, 4) SC_F(4, 8) SC_F(4, 16)
   SC_F(6, 6) SC_F(6, 12)
-  SC_F(8, 8) SC_F(8, 16)
+  SC_F(8, 4) SC_F(8, 8) SC_F(8, 16)
 #undef SC_F
   return 2;  // shape not instantiated: caller falls back to the torch path
 }

@@ -15,6 +15,7 @@
 //                          scattered into dense bf16 buffers for the MFMA wgrad GEMM.
 //   topk_clear           : zeroes exactly the scattered positions afterwards.
 #include "common.h"
+#include <stdlib.h>
 
 namespace scamd {
 
@@ -161,6 +162,145 @@ __global__ __launch_bounds__(TK_NT, 4) void topk_select_kernel(const float* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-per-row exact top-k (n <= 64 * PL): the row's keys live in one wave's VGPRs,
+// so there is no LDS histogram, no atomics and no block barrier (the radix kernel
+// above pays 3 x (histogram clear, bank-conflicted LDS atomics, scan) behind 256-thread
+// barriers).  Every count is a ballot + scalar popcount: one v_cmp per key and no
+// cross-lane reduction latency.  The k-th largest key T is found by bisection on its
+// bits (MSB first: t | bit is kept iff count(key >= t | bit) >= k).  The first S1 = 12
+// bits scan all keys; then the keys sharing t's top 12 bits (the "bucket", a handful
+// for score rows) are compacted one per lane and each remaining bit costs one ballot.
+// Output: every key > T and the first (k - count(> T)) keys == T, in column order.
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+template <int PL>
+__global__ __launch_bounds__(256) void topk_wave_kernel(const float* __restrict__ scores, const int* __restrict__ kv,
+                                                      int* __restrict__ idx, float* __restrict__ val, long rows, int B,
+                                                      int n, int kmax, int absolute, int relu) {
+  constexpr int S1 = 12;            // full-scan bisection steps before compaction
+  constexpr int LOW = 32 - S1;      // bits resolved on the compacted bucket
+  __shared__ uint32_t cbuf[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long row = (long)blockIdx.x * 4 + w;
+  if (row >= rows) return;          // per-wave work only: no block barrier below
+  const int g = (int)(row / B);
+  const int k = min(kv[g], n);
+  const float* S = scores + row * n;
+  int* I = idx + row * kmax;
+  float* V = val + row * kmax;
+  uint32_t key[PL];
+#pragma unroll
+  for (int i = 0; i < PL / 4; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < n) v = *reinterpret_cast<const float4*>(S + c);
+    const float f[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) key[4 * i + j] = c < n ? order_key(absolute ? fabsf(f[j]) : f[j]) : 0u;
+  }
+  if (k > 0) {
+    uint32_t t = 0;
+#pragma unroll 1
+    for (int b = 31; b >= LOW; --b) {
+      const uint32_t cand = t | (1u << b);
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) cnt += __popcll(__ballot(key[i] >= cand));
+      if (cnt >= k) t = cand;
+    }
+    const uint32_t hi = t >> LOW;
+    int n_above = 0, nb = 0;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const uint32_t h = key[i] >> LOW;
+      n_above += __popcll(__ballot(h > hi));
+      nb += __popcll(__ballot(h == hi));
+    }
+    int gt;
+    if (nb <= 64) {
+      int off = 0;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) {
+        const bool in = (key[i] >> LOW) == hi;
+        const uint64_t m = __ballot(in);
+        if (in) cbuf[w][off + lanes_below(m)] = key[i];
+        off += __popcll(m);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const bool valid = lane < nb;
+      const uint32_t ck = valid ? cbuf[w][lane] : 0u;
+#pragma unroll 1
+      for (int b = LOW - 1; b >= 0; --b) {
+        const uint32_t cand = t | (1u << b);
+        if (n_above + __popcll(__ballot(valid && ck >= cand)) >= k) t = cand;
+      }
+      gt = n_above + __popcll(__ballot(valid && ck > t));
+    } else {  // a crowded bucket (many equal / near-equal scores): finish by full scans
+#pragma unroll 1
+      for (int b = LOW - 1; b >= 0; --b) {
+        const uint32_t cand = t | (1u << b);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < PL; ++i) cnt += __popcll(__ballot(key[i] >= cand));
+        if (cnt >= k) t = cand;
+      }
+      gt = 0;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) gt += __popcll(__ballot(key[i] > t));
+    }
+    const int need_ties = k - gt;
+    // output in column order: chunk i covers columns [256 i, 256 i + 256), lane l owns
+    // columns 256 i + 4 l + j (j < 4), so column order = (lane, j) within a chunk
+    int base = 0, ties_seen = 0;
+#pragma unroll
+    for (int i = 0; i < PL / 4; ++i) {
+      uint64_t me[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) me[j] = __ballot(key[4 * i + j] == t);
+      int tie_rank = ties_seen;  // ties in earlier columns of the row
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tie_rank += lanes_below(me[j]);
+      bool take[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t kk = key[4 * i + j];
+        take[j] = kk > t || (kk == t && tie_rank < need_ties);
+        tie_rank += kk == t ? 1 : 0;
+      }
+      uint64_t mt[4];
+      int pos = base, tot = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mt[j] = __ballot(take[j]);
+        pos += lanes_below(mt[j]);
+        tot += __popcll(mt[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (take[j]) {
+          const int c = (i * 64 + lane) * 4 + j;
+          const float sv = S[c];
+          I[pos] = c;
+          V[pos] = relu ? fmaxf(sv, 0.f) : sv;
+          ++pos;
+        }
+      }
+      base += tot;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ties_seen += __popcll(me[j]);
+    }
+  }
+  for (int j = k + lane; j < kmax; j += 64) {
+    I[j] = 0;
+    V[j] = 0.f;
+  }
+}
+
 // One wave per (model, row).  D: [G][n][d] bf16 normalised dictionary (gathered rows).
 // Decode gathers the k dictionary rows four at a time (indices and values are
 // wave-uniform scalar loads issued ahead of the row loads).  The k code gradients
@@ -299,6 +439,16 @@ extern "C" {
 
 int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int G, int B, int n, int kmax,
                    int absolute, int relu, hipStream_t stream) {
+  if (n % 4 == 0 && n <= 64 * 128 && !getenv("SC_TOPK_RADIX")) {
+    const long rows = (long)G * B;
+    dim3 wgrid((unsigned)((rows + 3) / 4));
+#define SC_W(P) \
+    if (n <= 64 * P) { hipLaunchKernelGGL((topk_wave_kernel<P>), wgrid, dim3(256), 0, stream, scores, k, idx, val, rows, B, n, \
+                                          kmax, absolute, relu); \
+      return hipGetLastError() == hipSuccess ? 0 : 3; }
+    SC_W(16) SC_W(32) SC_W(64) SC_W(96) SC_W(128)
+#undef SC_W
+  }
   const int per = (n + 255) / 256;
   dim3 grid((unsigned)G * B);
 #define SC_T(P) \

@@ -263,13 +263,19 @@ def test_fused_adam_epilogue_matches_separate_adam():
         _close(a.dec_shadow, b.dec_shadow, rtol=2e-2, atol=2e-2)
 
 
-def test_topk_select_exact():
+@pytest.mark.parametrize("radix", [False, True])
+@pytest.mark.parametrize("n", [6144, 1000])
+def test_topk_select_exact(radix, n, monkeypatch):
     from sparse_coding__amd.ops import topk as T
 
+    if radix:
+        monkeypatch.setenv("SC_TOPK_RADIX", "1")  # the block-radix kernel instead of wave bisection
     torch.manual_seed(6)
-    G, B, n = 3, 64, 6144
+    G, B = 3, 64
     scores = torch.randn(G, B, n, device=DEV)
     scores[0, 0, :10] = 5.0  # ties at the threshold
+    scores[2, 1, 100:400] = 0.75  # a crowded bucket: 300 equal keys straddle the threshold
+    scores[2, 1, 400:] = -1.0
     k = torch.tensor([1, 32, 150], device=DEV, dtype=torch.int32)
     idx, val = T.topk_select(scores, k, 150, relu=False)
     for g in range(G):
