@@ -228,27 +228,44 @@ __global__ __launch_bounds__(256) void loss_reduce_kernel(BiasArgs a) {
   }
 }
 
-// Phase 2 (grid: n/256 x G): bias gradient from the per-row-tile column partials,
+// Phase 2 (grid: n/32 x G, 256 threads = 8 row-groups x 32 columns): bias gradient from
+// the per-row-tile column partials (each row-group sums every 8th tile, then an LDS
+// reduce -- at a large gathered batch there are B/128 = 128 tiles per column), the
 // bias-decay term, Adam on the bias; optional feature on-count accumulation.
 __global__ __launch_bounds__(256) void bias_adam_kernel(BiasArgs a) {
+  __shared__ float gred[8][33], cred[8][33];
   const int g = blockIdx.y;
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int j = blockIdx.x * 32 + col;
   const int n = a.n;
-  if (j >= n) return;
-  if (a.cnt_part && a.feat_count) {
-    float c = 0.f;
-    for (int t = 0; t < a.tm; ++t) c += a.cnt_part[((long)g * a.tm + t) * n + j];
-    a.feat_count[(long)g * n + j] += c;
+  const bool ok = j < n;
+  const bool counting = a.cnt_part && a.feat_count;
+  float gs = 0.f, cs = 0.f;
+  if (ok) {
+    for (int t = grp; t < a.tm; t += 8) {
+      const long o = ((long)g * a.tm + t) * n + j;
+      if (a.update) gs += a.colpart[o];
+      if (counting) cs += a.cnt_part[o];
+    }
   }
+  gred[grp][col] = gs;
+  cred[grp][col] = cs;
+  __syncthreads();
+  if (grp != 0 || !ok) return;
+  float gsum = 0.f, csum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    gsum += gred[r][col];
+    csum += cred[r][col];
+  }
+  const long idx = (long)g * n + j;
+  if (counting) a.feat_count[idx] += csum;
   if (!a.update) return;
   const float bnorm = a.out[g * 6 + 5];
   const float beta = a.bias_decay[g];
   const float bd = (beta != 0.f && bnorm > 0.f) ? beta / bnorm : 0.f;
-  float gsum = 0.f;
-  for (int t = 0; t < a.tm; ++t) gsum += a.colpart[((long)g * a.tm + t) * n + j];
   float bc1 = a.bc1, bc2 = a.bc2;
   if (a.step) bias_corrections(a.b1, a.b2, *a.step, bc1, bc2);
-  const long idx = (long)g * n + j;
   const float bj = a.b[idx];
   const float gj = gsum * a.gscale + bd * bj;
   const float mj = a.b1 * a.m[idx] + (1.f - a.b1) * gj;
@@ -350,7 +367,7 @@ int sc_bias_loss(int G, float* b, float* m, float* v, const float* colpart, int 
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.update = update; a.step = step;
   hipLaunchKernelGGL(loss_reduce_kernel, dim3(G), dim3(256), 0, stream, a);
   if (update || (cnt_part && feat_count))
-    hipLaunchKernelGGL(bias_adam_kernel, dim3((n + 255) / 256, G), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(bias_adam_kernel, dim3((n + 31) / 32, G), dim3(256), 0, stream, a);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -52,9 +52,9 @@ __global__ __launch_bounds__(TK_NT, 4) void topk_select_kernel(const float* __re
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = tid + i * TK_NT;
-    const float s = c < n ? S[c] : 0.f;
+    const float s = S[min(c, n - 1)];  // unconditional load + branch-free mask (see topk_wave_kernel)
     sv[i] = s;
-    key[i] = c < n ? order_key(absolute ? fabsf(s) : s) : 0u;  // padding sorts below every real key
+    key[i] = order_key(absolute ? fabsf(s) : s) & (0u - (uint32_t)(c < n));  // padding sorts below every key
   }
   uint32_t prefix = 0, mask = 0;
   int remaining = k;
@@ -172,6 +172,19 @@ __global__ __launch_bounds__(TK_NT, 4) void topk_select_kernel(const float* __re
 // bits scan all keys; then the keys sharing t's top 12 bits (the "bucket", a handful
 // for score rows) are compacted one per lane and each remaining bit costs one ballot.
 // Output: every key > T and the first (k - count(> T)) keys == T, in column order.
+// Wave-wide integer sum on the DPP path (row scans + row broadcasts, then lane 63):
+// six VALU adds and a readlane instead of ds_bpermute round trips or a per-key ballot +
+// scalar popcount chain (the CU's one scalar unit serialises those across its waves).
+__device__ __forceinline__ int wave_total(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
 __device__ __forceinline__ int lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
@@ -188,18 +201,21 @@ __global__ __launch_bounds__(256) void topk_wave_kernel(const float* __restrict_
   if (row >= rows) return;          // per-wave work only: no block barrier below
   const int g = (int)(row / B);
   const int k = min(kv[g], n);
-  const float* S = scores + row * n;
+  const float* S = reinterpret_cast<const float*>(__builtin_assume_aligned(scores + row * n, 16));
   int* I = idx + row * kmax;
   float* V = val + row * kmax;
   uint32_t key[PL];
 #pragma unroll
   for (int i = 0; i < PL / 4; ++i) {
     const int c = (i * 64 + lane) * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c < n) v = *reinterpret_cast<const float4*>(S + c);
+    // unconditional (clamped, 16-byte aligned: n % 4 == 0) loads and a branch-free mask: a
+    // guarded load or key makes hipcc branch and wait vmcnt(0) per load, serialising them
+    const float4 v = *reinterpret_cast<const float4*>(
+        __builtin_assume_aligned(S + (min(c, n - 4) & ~3), 16));
+    const uint32_t live = 0u - (uint32_t)(c < n);
     const float f[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) key[4 * i + j] = c < n ? order_key(absolute ? fabsf(f[j]) : f[j]) : 0u;
+    for (int j = 0; j < 4; ++j) key[4 * i + j] = order_key(absolute ? fabsf(f[j]) : f[j]) & live;
   }
   if (k > 0) {
     uint32_t t = 0;
@@ -208,27 +224,34 @@ __global__ __launch_bounds__(256) void topk_wave_kernel(const float* __restrict_
       const uint32_t cand = t | (1u << b);
       int cnt = 0;
 #pragma unroll
-      for (int i = 0; i < PL; ++i) cnt += __popcll(__ballot(key[i] >= cand));
-      if (cnt >= k) t = cand;
+      for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
+      if (wave_total(cnt) >= k) t = cand;
     }
     const uint32_t hi = t >> LOW;
-    int n_above = 0, nb = 0;
+    int above = 0, inb = 0;
 #pragma unroll
     for (int i = 0; i < PL; ++i) {
       const uint32_t h = key[i] >> LOW;
-      n_above += __popcll(__ballot(h > hi));
-      nb += __popcll(__ballot(h == hi));
+      above += h > hi ? 1 : 0;
+      inb += h == hi ? 1 : 0;
     }
+    const int n_above = wave_total(above), nb = wave_total(inb);
     int gt;
     if (nb <= 64) {
-      int off = 0;
+      // lane offsets: exclusive scan of the per-lane bucket counts (DPP row scan + row
+      // totals through lanes 15/31/47), then each lane writes its own bucket keys
+      int incl = inb;
+      incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xf, 0xf, false);
+      incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xf, 0xf, false);
+      incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xf, 0xf, false);
+      incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xf, 0xf, false);
+      const int r0 = __builtin_amdgcn_readlane(incl, 15), r1 = __builtin_amdgcn_readlane(incl, 31);
+      const int r2 = __builtin_amdgcn_readlane(incl, 47);
+      const int rowoff = lane < 16 ? 0 : lane < 32 ? r0 : lane < 48 ? r0 + r1 : r0 + r1 + r2;
+      int off = rowoff + incl - inb;
 #pragma unroll
-      for (int i = 0; i < PL; ++i) {
-        const bool in = (key[i] >> LOW) == hi;
-        const uint64_t m = __ballot(in);
-        if (in) cbuf[w][off + lanes_below(m)] = key[i];
-        off += __popcll(m);
-      }
+      for (int i = 0; i < PL; ++i)
+        if ((key[i] >> LOW) == hi) cbuf[w][off++] = key[i];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -246,12 +269,13 @@ __global__ __launch_bounds__(256) void topk_wave_kernel(const float* __restrict_
         const uint32_t cand = t | (1u << b);
         int cnt = 0;
 #pragma unroll
-        for (int i = 0; i < PL; ++i) cnt += __popcll(__ballot(key[i] >= cand));
-        if (cnt >= k) t = cand;
+        for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
+        if (wave_total(cnt) >= k) t = cand;
       }
-      gt = 0;
+      int c2 = 0;
 #pragma unroll
-      for (int i = 0; i < PL; ++i) gt += __popcll(__ballot(key[i] > t));
+      for (int i = 0; i < PL; ++i) c2 += key[i] > t ? 1 : 0;
+      gt = wave_total(c2);
     }
     const int need_ties = k - gt;
     // output in column order: chunk i covers columns [256 i, 256 i + 256), lane l owns
@@ -334,20 +358,23 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
       ij[u] = ok ? I[j0 + u] : 0;
       wj[u] = ok ? V[j0 + u] : 0.f;  // zero weight: contributes nothing
     }
+    // loads are unconditional (clamped column): a guarded load makes hipcc branch and
+    // wait vmcnt(0) per load; lanes past d accumulate values that are zeroed below
+    ushort4 h[NV][4];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const int e = (v * 64 + lane) * 4;
-      if (e < d) {
-        ushort4 h[4];
+      const int e = min((v * 64 + lane) * 4, d - 4);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) h[u] = *reinterpret_cast<const ushort4*>(Dg + (long)ij[u] * d + e);
+      for (int u = 0; u < 4; ++u) h[v][u] = *reinterpret_cast<const ushort4*>(Dg + (long)ij[u] * d + e);
+    }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          acc[v * 4 + 0] += wj[u] * bf2f(h[u].x);
-          acc[v * 4 + 1] += wj[u] * bf2f(h[u].y);
-          acc[v * 4 + 2] += wj[u] * bf2f(h[u].z);
-          acc[v * 4 + 3] += wj[u] * bf2f(h[u].w);
-        }
+    for (int v = 0; v < NV; ++v) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc[v * 4 + 0] += wj[u] * bf2f(h[v][u].x);
+        acc[v * 4 + 1] += wj[u] * bf2f(h[v][u].y);
+        acc[v * 4 + 2] += wj[u] * bf2f(h[v][u].z);
+        acc[v * 4 + 3] += wj[u] * bf2f(h[v][u].w);
       }
     }
   }
@@ -358,7 +385,9 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int e = (v * 64 + lane) * 4;
-    if (e < d) {
+    if (e >= d) {  // outside the row: zero so the code-gradient dots below ignore it
+      acc[v * 4 + 0] = acc[v * 4 + 1] = acc[v * 4 + 2] = acc[v * 4 + 3] = 0.f;
+    } else {
       const ushort4 h = *reinterpret_cast<const ushort4*>(Xr + e);
       acc[v * 4 + 0] -= bf2f(h.x);
       acc[v * 4 + 1] -= bf2f(h.y);
@@ -386,12 +415,10 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
       float dot = 0.f;
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
-        const int e = (v * 64 + lane) * 4;
-        if (e < d) {
-          const ushort4 h = *reinterpret_cast<const ushort4*>(Dr + e);
-          dot += acc[v * 4 + 0] * bf2f(h.x) + acc[v * 4 + 1] * bf2f(h.y) + acc[v * 4 + 2] * bf2f(h.z) +
-                 acc[v * 4 + 3] * bf2f(h.w);
-        }
+        const int e = min((v * 64 + lane) * 4, d - 4);  // unconditional; acc is 0 past d
+        const ushort4 h = *reinterpret_cast<const ushort4*>(Dr + e);
+        dot += acc[v * 4 + 0] * bf2f(h.x) + acc[v * 4 + 1] * bf2f(h.y) + acc[v * 4 + 2] * bf2f(h.z) +
+               acc[v * 4 + 3] * bf2f(h.w);
       }
       p[u] = dot;
     }
@@ -439,14 +466,15 @@ extern "C" {
 
 int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int G, int B, int n, int kmax,
                    int absolute, int relu, hipStream_t stream) {
-  if (n % 4 == 0 && n <= 64 * 128 && !getenv("SC_TOPK_RADIX")) {
+  // wave bisection wins up to 64 keys per lane (measured: n = 2048 67 vs 147 us, n = 6144 310 vs 223 us)
+  if (n % 4 == 0 && n <= 64 * 64 && !getenv("SC_TOPK_RADIX")) {
     const long rows = (long)G * B;
     dim3 wgrid((unsigned)((rows + 3) / 4));
 #define SC_W(P) \
     if (n <= 64 * P) { hipLaunchKernelGGL((topk_wave_kernel<P>), wgrid, dim3(256), 0, stream, scores, k, idx, val, rows, B, n, \
                                           kmax, absolute, relu); \
       return hipGetLastError() == hipSuccess ? 0 : 3; }
-    SC_W(16) SC_W(32) SC_W(64) SC_W(96) SC_W(128)
+    SC_W(16) SC_W(32) SC_W(64)
 #undef SC_W
   }
   const int per = (n + 255) / 256;
