@@ -33,7 +33,7 @@ def main():
         "dc": (lambda: gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart), fl),
         "wgrad2": (lambda: gemm.weight_grads([[(e.c, e.r)], [(e.dpre, x)]], [e.g_dec, e.g_enc], 1e-6), 2 * fl),
     }
-    for cfg in (1, 5, 9, 13, 2, 3, 7, 15):
+    for cfg in (1, 5, 9, 13, 2, 3, 7, 11, 15):
         for name, (fn, f) in kernels.items():
             if not gemm.shape_fits(cfg, B if name != "wgrad2" else n, n if name in ("enc", "enc_cnt", "dc") else d):
                 continue

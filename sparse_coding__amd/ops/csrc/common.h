@@ -27,10 +27,29 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, b);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// DPP lane shuffle of a float (row_shr / row_bcast controls; lanes whose source is outside
+// the row read 0, so adding the result is a scan step).
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROW_MASK, 0xf, false));
+}
+
+// Inclusive scan within each 16-lane row: lane 15 of a row ends with the row's sum.
+__device__ __forceinline__ float row16_scan(float v) {
+  v += dpp_f<0x111>(v);  // row_shr:1
+  v += dpp_f<0x112>(v);  // row_shr:2
+  v += dpp_f<0x114>(v);  // row_shr:4
+  v += dpp_f<0x118>(v);  // row_shr:8
   return v;
+}
+
+// Wave-wide sum on the DPP path (row scans, row broadcasts, lane 63 read back): six VALU
+// adds and a readlane instead of six ds_bpermute round trips.  Uniform result.
+__device__ __forceinline__ float wave_sum(float v) {
+  v = row16_scan(v);
+  v += dpp_f<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+  v += dpp_f<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
 __device__ __forceinline__ float wave_max(float v) {

@@ -406,14 +406,11 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   // 128-row slot and store one value per (slot, column).  Deterministic.
   constexpr int WPS = PT / (WI * 16);  // wave rows per 128-row slot
   auto colred_lane = [&](f32x4_t v, int j, int region) {
+    // sum over the 16 lanes of a DPP row (the fragment's 16 output rows): lane 15 ends
+    // with the total -- four DPP adds per value instead of four ds_bpermute shuffles
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      v[r] += __shfl_xor(v[r], 1, 64);
-      v[r] += __shfl_xor(v[r], 2, 64);
-      v[r] += __shfl_xor(v[r], 4, 64);
-      v[r] += __shfl_xor(v[r], 8, 64);
-    }
-    if ((lane & 15) == 0)
+    for (int r = 0; r < 4; ++r) v[r] = row16_scan(v[r]);
+    if ((lane & 15) == 15)
       *reinterpret_cast<f32x4_t*>(red + region * (S::WGM * BN) + wr * BN + wc * (WJ * 16) + j * 16 +
                                   4 * (lane >> 4)) = v;
   };
@@ -707,7 +704,7 @@ int sc_gemm_shape(int M, int N, int G, int nprob) {
 
 // layout: bit0 = A is K-major, bit1 = B is K-major.
 // cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256;
-// bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4, 2: BK64 x 3, 3: BK32 x 3).
+// bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4, 2: BK32 x 2, 3: BK32 x 3).
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             const ScOperand* a /* [nprob][2] */, const ScOperand* b /* [nprob][2] */,
             void* const* c /* [nprob] */, const float* alpha /* [nprob] */, long ldc, long sc,
@@ -746,14 +743,14 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.ksplit = ksplit; p.split_stride = split_stride;
   const bool ak = layout & 1, bk = layout & 2;
   int shape = cfg & 3;
-  const int pipe = (cfg >> 2) & 3;  // 0: BK64 x 2 stages, 1: BK32 x 4, 2: BK64 x 3, 3: BK32 x 3
+  const int pipe = (cfg >> 2) & 3;  // 0: BK64 x 2 stages, 1: BK32 x 4, 2: BK32 x 2, 3: BK32 x 3
   if (shape == 0) shape = sc_gemm_shape(M, N, G, nprob);
   switch (shape) {
     case 3:
       if (!fits<S256>(M, N)) return 6;
       if (pipe == 1) return launch<S256, 32, 4, false>(epi, ak, bk, p, nprob, stream);
       if (pipe == 3) return launch<S256, 32, 3, false>(epi, ak, bk, p, nprob, stream);
-      if (pipe == 2) return 8;  // 192 KB of LDS
+      if (pipe == 2) return launch<S256, 32, 2, false>(epi, ak, bk, p, nprob, stream);
       return launch<S256, 64, 2>(epi, ak, bk, p, nprob, stream);
     case 2:
       if (!fits<S256x128>(M, N)) return 6;
@@ -761,7 +758,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
       return launch<S256x128, 64, 2>(epi, ak, bk, p, nprob, stream);
     default:
       if (pipe == 1) return launch<S128, 32, 4, false>(epi, ak, bk, p, nprob, stream);
-      if (pipe == 2) return launch<S128, 64, 3, false>(epi, ak, bk, p, nprob, stream);
+      if (pipe == 2) return launch<S128, 32, 2, false>(epi, ak, bk, p, nprob, stream);  // 32 KB: 4-5 blocks/CU
       if (pipe == 3) return launch<S128, 32, 3, false>(epi, ak, bk, p, nprob, stream);
       return launch<S128, 64, 2>(epi, ak, bk, p, nprob, stream);
   }

@@ -34,9 +34,9 @@ _CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_
 _CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 # cfg bits 2-3 select the K pipeline: 0 BK64 x 2-stage LDS ring (default), 1 BK32 x 4,
-# 2 BK64 x 3, 3 BK32 x 3 (the alternatives exist for the step's epilogues and the
-# weight-gradient layout only; 256x256 has no BK64 x 3: 192 KB of LDS).
-PIPES = {0: (64, 2), 1: (32, 4), 2: (64, 3), 3: (32, 3)}
+# 2 BK32 x 2 (smallest LDS footprint: most co-resident blocks), 3 BK32 x 3 (the
+# alternatives exist for the step's epilogues and the weight-gradient layout only).
+PIPES = {0: (64, 2), 1: (32, 4), 2: (32, 2), 3: (32, 3)}
 
 
 def set_config(epi: int, cfg: int):

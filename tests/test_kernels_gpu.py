@@ -83,7 +83,7 @@ def test_identity_asymmetric():
     torch.testing.assert_close(out, bt.float()[:, :M, :], rtol=0, atol=0)
 
 
-PIPE_CFGS = [1 | 1 << 2, 1 | 2 << 2, 1 | 3 << 2, 3 | 1 << 2, 3 | 3 << 2]  # deeper K pipelines
+PIPE_CFGS = [1 | 1 << 2, 1 | 2 << 2, 1 | 3 << 2, 3 | 1 << 2, 3 | 2 << 2, 3 | 3 << 2]  # deeper K pipelines
 
 
 @pytest.mark.parametrize("cfg", SHAPE_CFGS + PIPE_CFGS)
