@@ -125,9 +125,38 @@ def cfg_fista(a):
 
 
 def cfg_mlp(a):
-    import bench
+    """Config 3 shapes on one GPU: Pythia-70m MLP-out width d_mlp = 2048, ratio 4 (n = 8192),
+    8-model L1 sweep, fused engine in one HIP graph; plus the per-GPU step of the
+    ensemble-sharded layout at N = 2, 4, 8 (G/N models on N*B gathered rows) that the
+    8-GPU run uses."""
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
 
-    return json.loads(json.dumps({"note": "run bench.py --d 2048 --ratio 4 for MLP shapes"}))
+    dev = "cuda:0"
+    torch.manual_seed(0)
+    d, ratio, B = 2048, 4, a.batch
+    n = d * ratio
+    l1s = np.logspace(-4, -2, a.models)
+    models = [FunctionalSAE.init(d, n, float(l), device=dev) for l in l1s]
+    ring = _ring(d, dev, rows=1 << 18)
+    out = {"config": f"3: Pythia-70m MLP-out shapes d={d}, ratio {ratio} (n={n}), {a.models} models, fused, "
+                     "per-GPU work of the 8-GPU ensemble-sharded run", "unit": "activations/s", "batch": B,
+           "dtype": "bf16", "data": "synthetic", "per_n": []}
+    for N in (1, 2, 4, 8):
+        if a.models % N:
+            continue
+        gb = N * B
+        eng = FusedSAEEnsemble(models[: a.models // N], FunctionalSAE, lr=1e-3, batch_size=gb, device=dev)
+        eng.enable_graph()
+        el = _timed(lambda: (ring.sample(gb, out=eng.x_static), eng.step_static()), a.steps, a.warmup,
+                    torch.cuda.synchronize)
+        ms = 1e3 * el / a.steps
+        out["per_n"].append({"N": N, "models_per_gpu": a.models // N, "rows_per_step": gb, "ms_per_step": round(ms, 3),
+                             "job_activations_per_s": round(gb / ms * 1e3, 1), "wgrad_split": eng.wsplit})
+        del eng
+        torch.cuda.empty_cache()
+    out["value"] = out["per_n"][0]["job_activations_per_s"]
+    return out
 
 
 def main():

@@ -57,6 +57,10 @@ def main():
                                                           e.enc_part, None, None)), fl)
     res["enc_plain_bf16"] = (timeit(lambda: gemm.matmul_nt(x, e.enc_shadow, e.c)), fl)
     res["dc_nodot"] = (timeit(lambda: gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart)), fl)
+    res["dc_mask"] = (timeit(lambda: gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart,
+                                                    mask=e.cmask)), fl)
+    res["enc_mask"] = (timeit(lambda: gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c,
+                                                       e.enc_part, None, None, mask_out=e.cmask)), fl)
     res["wgrad_adam"] = (timeit(lambda: e.wgrad_adam(x)), 2 * fl)
     e.fuse_adam = False
     e.overlap_adam = False

@@ -110,6 +110,9 @@ class FusedSAEEnsemble:
         self.c = torch.empty(G, B, n, device=dev, dtype=bf)
         self.r = torch.empty(G, B, d, device=dev, dtype=bf)
         self.dpre = torch.empty(G, B, n, device=dev, dtype=bf)
+        # activity bitmask of c written by the encoder epilogue, read by the code-gradient
+        # epilogue instead of c itself (1/16 of the bytes)
+        self.cmask = torch.empty(gemm_ops.code_mask_shape(G, B, n), device=dev, dtype=torch.int64)
         # gradient buffers; the last-produced weight gradient shares one flat buffer with the
         # reduced bias gradient so data-parallel runs all-reduce both with a single collective
         if self.kind == "untied":
@@ -203,11 +206,12 @@ class FusedSAEEnsemble:
         count = self._counting() if count is None else count
         self._counted = count
         gemm_ops.encode_relu(x, self.enc_shadow, self.params["encoder_bias"], self.c, self.enc_part,
-                             self.cnt_part if count else None, self.nactive)
+                             self.cnt_part if count else None, self.nactive, mask_out=self.cmask)
         gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
         gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                            dotpart=self.dotpart if self.fuse_adam else None,
-                           tied_bias=self.params["encoder_bias"] if (self.fuse_adam and self.kind == "tied") else None)
+                           tied_bias=self.params["encoder_bias"] if (self.fuse_adam and self.kind == "tied") else None,
+                           mask=self.cmask)
 
     def wgrad_adam(self, x):
         """Weight gradients with Adam in the GEMM epilogue, then the decoder-row normalisation."""

@@ -52,7 +52,15 @@ using S256 = Shape<2, 4, 8, 4>;
 // consumers (loss / bias / Adam kernels) do not depend on the GEMM configuration.
 constexpr int PT = 128;
 
-enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5, EPI_ENC_CNT = 6 };
+enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5, EPI_ENC_CNT = 6,
+       EPI_DC_MASK = 7 };
+
+// Activity bitmask of the codes, in MFMA-fragment order: for the 16x16 output fragment at
+// (row/16, col/16) the encoder epilogue stores its four wave ballots (bit l of word r: lane
+// l's value r, i.e. output row 16 i + (l & 15), column 16 j + 4 (l >> 4) + r, is > 0).  The
+// code-gradient epilogue only needs 1[c > 0]: reading these 32 bytes per fragment instead
+// of the bf16 codes (512 bytes) removes B n G x 2 bytes of HBM reads per step.
+// Layout [G][B/16][n/16][4] uint64; every GEMM block shape uses the same fragment map.
 
 struct Operand {
   const uint16_t* ptr;
@@ -109,6 +117,7 @@ struct GemmParams {
   float b1, b2, eps;
   int dot_tm;          // row tiles in dotpart
   float dot_scale;     // converts dotpart sums to <w_hat, dL/dw_hat>
+  uint64_t* cmask;     // ENC: optional activity-bitmask output; DC_MASK: its input
   // --- split-K (plain F32 / BF16 epilogues only): K-tile range split over `ksplit`
   // blocks per output tile; split s writes its partial product at c + s * split_stride
   // (the consumer -- the Adam kernel for weight gradients -- sums the slabs).
@@ -462,6 +471,16 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
         }
         *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + col) =
             make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
+        if (p.cmask) {  // block-uniform
+          const uint64_t b0 = __ballot(v[0] > 0.f), b1 = __ballot(v[1] > 0.f);
+          const uint64_t b2 = __ballot(v[2] > 0.f), b3 = __ballot(v[3] > 0.f);
+          const long frag = ((long)g * (p.M >> 4) + ((rowb + i * 16) >> 4)) * (p.N >> 4) + ((colb + j * 16) >> 4);
+          if (lane == 0) {
+            u32x4_t* dst = reinterpret_cast<u32x4_t*>(p.cmask + frag * 4);
+            dst[0] = u32x4_t{(uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32)};
+            dst[1] = u32x4_t{(uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32)};
+          }
+        }
       }
       if constexpr (counting) colred_lane(cnt, j, 0);
     }
@@ -530,6 +549,35 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
     __syncthreads();
     colred_store(p.colpart, 0);
     if (want_dot) colred_store(p.dotpart, 1);
+    return;
+  }
+  if constexpr (EPI == EPI_DC_MASK) {
+    // EPI_DC with the code activity read from the encoder's bitmask (no norm-Jacobian dots)
+    uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
+    const float add = p.l1[g] * p.l1_add_scale;
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) {
+      f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int col = colb + j * 16;
+#pragma unroll
+      for (int i = 0; i < WI; ++i) {
+        const long row = rowb + i * 16;
+        const long frag = ((long)g * (p.M >> 4) + ((rowb + i * 16) >> 4)) * (p.N >> 4) + (col >> 4);
+        const uint64_t* mk = p.cmask + frag * 4;  // wave-uniform address
+        f32x4_t dv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool on = (mk[r] >> lane) & 1ull;
+          dv[r] = on ? acc[i][j][r] + add : 0.f;
+          cs[r] += dv[r];
+        }
+        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
+            make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
+      }
+      colred_lane(cs, j, 0);
+    }
+    __syncthreads();
+    colred_store(p.colpart, 0);
     return;
   }
   if constexpr (EPI == EPI_ADAM) {
@@ -645,6 +693,7 @@ int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_
     case EPI_ENC_CNT: if (!(ak && bk)) return 5; SC_L(true, true, EPI_ENC_CNT); break;
     case EPI_DEC: if (!(ak && !bk)) return 5; SC_L(true, false, EPI_DEC); break;
     case EPI_DC: if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC); break;
+    case EPI_DC_MASK: if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC_MASK); break;
     case EPI_ADAM:
       if constexpr (FULL) { if (ak || bk) return 5; SC_L(false, false, EPI_ADAM); }
       break;
@@ -712,8 +761,9 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             long saux, float* part, float* colpart, const float* l1, float l1_add_scale,
             float* dotpart, int dc_tied, const ScAdamEpi* adam /* [nprob] or null */, const float* lr,
             const int* step, float b1, float b2, float eps, int dot_tm, float dot_scale,
-            int cfg, int ksplit, long split_stride, hipStream_t stream) {
+            int cfg, int ksplit, long split_stride, void* cmask, hipStream_t stream) {
   if (M % PT || N % PT || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
+  if (epi == EPI_DC_MASK && !cmask) return 4;
   if (ksplit < 1 || ksplit > (K1 + K2) / 64 || (ksplit > 1 && epi != EPI_F32 && epi != EPI_BF16)) return 7;
   GemmParams p;
   for (int i = 0; i < nprob; ++i) {
@@ -731,6 +781,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.aux = reinterpret_cast<const uint16_t*>(aux); p.ldaux = ldaux; p.saux = saux;
   p.part = part; p.colpart = colpart; p.l1 = l1; p.l1_add_scale = l1_add_scale;
   p.dotpart = dotpart; p.dc_tied = dc_tied;
+  p.cmask = reinterpret_cast<uint64_t*>(cmask);
   for (int i = 0; i < 2; ++i) {
     if (adam && i < nprob)
       p.adam[i] = {adam[i].p, adam[i].m, adam[i].v, reinterpret_cast<uint16_t*>(adam[i].sh), adam[i].dotpart,

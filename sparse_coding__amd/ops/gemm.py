@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 
-EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16, EPI_ADAM, EPI_ENC_CNT = 0, 1, 2, 3, 4, 5, 6
+EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16, EPI_ADAM, EPI_ENC_CNT, EPI_DC_MASK = 0, 1, 2, 3, 4, 5, 6, 7
 TILE_M, TILE_N, TILE_K = 128, 128, 64
 
 # Block shapes of the kernel (BK64 x 2-stage LDS-DMA ring for all of them):
@@ -30,7 +30,8 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 # epilogues are fastest on 128x128 blocks (two blocks per CU overlap one block's epilogue
 # with the other's MFMA loop: enc 61 vs 84 us on 256x256), the plain fp32 weight-gradient
 # GEMM (K = B = 2048) on 256x256 blocks (65 vs 74 us) -- "auto" picks that.
-_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 1, EPI_ENC_CNT: 1}
+_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 1, EPI_ENC_CNT: 1,
+                EPI_DC_MASK: 1}
 _CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 # cfg bits 2-3 select the K pipeline: 0 BK64 x 2-stage LDS ring (default), 1 BK32 x 4,
@@ -83,7 +84,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
             bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
             colpart=None, l1=None, l1_add_scale=0.0, dotpart=None, dc_tied=False, adam=None,
             lr=None, step=None, betas=(0.9, 0.999), eps=1e-8, dot_tm=0, dot_scale=0.0, cfg=None,
-            ksplit=1, split_stride=0):
+            ksplit=1, split_stride=0, cmask=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
@@ -99,7 +100,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
         _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1), float(l1_add_scale),
         _lib.ptr(dotpart), int(bool(dc_tied)), adam, _lib.ptr(lr), _lib.ptr(step),
         float(betas[0]), float(betas[1]), float(eps), int(dot_tm), float(dot_scale),
-        cfg, int(ksplit), int(split_stride),
+        cfg, int(ksplit), int(split_stride), _lib.ptr(cmask),
         _lib.stream_handle(),
     )
     _lib.check(rc, f"sc_gemm(epi={epi})")
@@ -114,12 +115,19 @@ def _x_stride(x, B, d, G):
     return B * d
 
 
-def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None):
+def code_mask_shape(G, B, n):
+    """Shape of the encoder's activity bitmask (fragment-ordered ballots, see sae_gemm.hip)."""
+    return (G, B // 16, n // 16, 4)
+
+
+def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=None):
     """c[g] = relu(x[g] @ w[g]^T + bias[g]) with L1/L0 partials.
 
     x: [B, d] or [G, B, d] bf16; w: [G, n, d] bf16; bias: [G, n] fp32;
     c_out: [G, B, n] bf16; part: [G, (B/128)*(n/128), 2] fp32;
-    colpart (optional): [G, B/128, n] fp32 per-feature on-counts.
+    colpart (optional): [G, B/128, n] fp32 per-feature on-counts;
+    mask_out (optional): int64 ``code_mask_shape(G, B, n)``: the activity bitmask ``code_grad``
+    can read instead of the codes.
     """
     G, n, d = w.shape
     B = c_out.shape[1]
@@ -132,10 +140,13 @@ def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None):
         _need(colpart.numel() >= G * (B // 128) * n, "colpart too small")
     if nactive is not None:
         _need(nactive.dtype == torch.int32 and nactive.numel() == G, "nactive must be int32[G]")
+    if mask_out is not None:
+        _need(mask_out.dtype == torch.int64 and tuple(mask_out.shape) == code_mask_shape(G, B, n)
+              and mask_out.is_contiguous(), "mask_out must be contiguous int64 code_mask_shape(G, B, n)")
     a = [_op(x, d, sx), _op(x, d, sx)]
     b = [_op(w, d, n * d), _op(w, d, n * d)]
     _launch(EPI_ENC_CNT if colpart is not None else EPI_ENC, 3, B, n, d, 0, G, a, b, [c_out], [1.0], n, B * n,
-            bias=bias, sbias=n, nactive=nactive, part=part, colpart=colpart)
+            bias=bias, sbias=n, nactive=nactive, part=part, colpart=colpart, cmask=mask_out)
 
 
 def decode_residual(c, w_hat, x, r_out, part):
@@ -156,14 +167,15 @@ def decode_residual(c, w_hat, x, r_out, part):
             aux=x, ldaux=d, saux=sx, part=part)
 
 
-def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None):
+def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, mask=None):
     """dpre_s[g] = 1[c>0] * (r[g] @ w_hat[g]^T + l1[g] * d / 2).
 
     dpre_s is the code gradient in units of the residual: dL/dpre = 2/(B d) * dpre_s.
     colpart receives per-row-tile column sums (bias gradient partials).  With ``dotpart``
     [G, B/128, n] the epilogue also accumulates the norm-Jacobian row dots
     <w_hat_j, dL/dw_hat_j> (in units of 2/(B d)); ``tied_bias`` ([G, n]) adds the tied
-    dictionary's encoder-path term.
+    dictionary's encoder-path term.  ``mask`` (the encoder's ``mask_out``) replaces the
+    read of ``c`` by the 16x smaller activity bitmask when no dots are requested.
     """
     G, B, d = r.shape
     n = w_hat.shape[1]
@@ -175,6 +187,11 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None):
     b = [_op(w_hat, d, n * d)] * 2
     if dotpart is not None:
         _need(dotpart.numel() >= G * (B // 128) * n, "dotpart too small")
+    if mask is not None and dotpart is None:
+        _need(mask.dtype == torch.int64 and tuple(mask.shape) == code_mask_shape(G, B, n), "mask shape")
+        _launch(EPI_DC_MASK, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
+                colpart=colpart, l1=l1, l1_add_scale=d / 2.0, cmask=mask)
+        return
     _launch(EPI_DC, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
             aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0,
             dotpart=dotpart, dc_tied=tied_bias is not None, bias=tied_bias, sbias=n)

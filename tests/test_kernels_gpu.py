@@ -106,7 +106,8 @@ def _sae_epilogues(G, B, d, n):
     c = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
     part = torch.zeros(G, (B // 128) * (n // 128), 2, device=DEV)
     cnt = torch.zeros(G, B // 128, n, device=DEV)
-    gemm.encode_relu(x, we, bias, c, part, cnt, nactive)
+    cmask = torch.zeros(gemm.code_mask_shape(G, B, n), device=DEV, dtype=torch.int64)
+    gemm.encode_relu(x, we, bias, c, part, cnt, nactive, mask_out=cmask)
     ref = torch.relu(x.float() @ we.float().transpose(1, 2) + bias[:, None, :])
     for g in range(G):
         ref[g, :, int(nactive[g]):] = 0
@@ -131,6 +132,12 @@ def _sae_epilogues(G, B, d, n):
     _close(dpre, dref)
     # bias-gradient partials are accumulated from the unrounded fp32 values
     _close(colpart.sum(1), dref.sum(1), rtol=1e-2, atol=1e-2)
+    # the bitmask path (activity read from the encoder's ballots) is bit-identical
+    dpre_m = torch.empty_like(dpre)
+    colpart_m = torch.zeros_like(colpart)
+    gemm.code_grad(r, wd, c, l1, dpre_m, colpart_m, mask=cmask)
+    assert torch.equal(dpre_m, dpre)
+    assert torch.equal(colpart_m, colpart)
 
     gd = torch.empty(G, n, d, device=DEV)
     ge = torch.empty(G, n, d, device=DEV)
