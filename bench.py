@@ -118,6 +118,10 @@ def main(argv=None):
     B = args.batch
 
     grad_dtype = torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32
+
+    def finish():
+        return None
+
     par = args.parallelism
     if par == "auto":
         par = "es" if (info.world_size > 1 and args.models % info.world_size == 0) else "dp"
@@ -149,11 +153,14 @@ def main(argv=None):
 
         engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device)
                    for m in split_models(models, args.dp_chunks)]
-        trainer = ChunkedDataParallel([FusedChunk(e) for e in engines], info, grad_dtype)
+        # cross-step: the last chunk's all-reduce overlaps the next step's first (encoder) GEMMs
+        trainer = ChunkedDataParallel([FusedChunk(e) for e in engines], info, grad_dtype, cross_step=True)
         xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
 
         def step():
             trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf))
+
+        finish = trainer.flush
 
         def dicts():
             return [ld for e in engines for ld in e.to_learned_dicts(device)]
@@ -198,6 +205,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    finish()  # work the last timed step still has in flight (cross-step pipelining)
     torch.cuda.synchronize()
     barrier(info)
     elapsed = time.perf_counter() - t0
@@ -212,6 +220,7 @@ def main(argv=None):
         while trained < args.quality_steps:  # untimed: train on toward convergence before evaluating
             step()
             trained += 1
+        finish()
         torch.cuda.synchronize()
         lds = dicts()  # collective in the sharded mode: every rank takes part
         if info.is_main:

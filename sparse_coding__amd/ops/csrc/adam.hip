@@ -65,17 +65,29 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   const float* P4 = R.p + base;
   const float* G4 = R.g + base;
 
-  float4 pv[NV], gv[NV];
-  float ss = 0.f, dot = 0.f;
+  // every load of the row is issued up front (p, g, m, v: 4 NV float4 per lane in flight)
+  // so one memory round trip covers the row; the moments do not wait for the norm reductions
+  float4 pv[NV], gv[NV], mv_[NV], vv_[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int e = (i * 64 + lane) * 4;
     pv[i] = *reinterpret_cast<const float4*>(P4 + e);
     gv[i] = *reinterpret_cast<const float4*>(G4 + e);
-    for (int sp = 1; sp < a.nsplit; ++sp) {  // split-K partials of the weight-gradient GEMM
-      const float4 q = *reinterpret_cast<const float4*>(G4 + sp * a.gstride + e);
-      gv[i].x += q.x; gv[i].y += q.y; gv[i].z += q.z; gv[i].w += q.w;
+    mv_[i] = *reinterpret_cast<const float4*>(R.m + base + e);
+    vv_[i] = *reinterpret_cast<const float4*>(R.v + base + e);
+  }
+  if (a.nsplit > 1) {  // split-K partials of the weight-gradient GEMM (few-model shards)
+    for (int sp = 1; sp < a.nsplit; ++sp) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const float4 q = *reinterpret_cast<const float4*>(G4 + sp * a.gstride + (i * 64 + lane) * 4);
+        gv[i].x += q.x; gv[i].y += q.y; gv[i].z += q.z; gv[i].w += q.w;
+      }
     }
+  }
+  float ss = 0.f, dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
     ss += pv[i].x * pv[i].x + pv[i].y * pv[i].y + pv[i].z * pv[i].z + pv[i].w * pv[i].w;
     dot += pv[i].x * gv[i].x + pv[i].y * gv[i].y + pv[i].z * gv[i].z + pv[i].w * gv[i].w;
   }
@@ -101,8 +113,8 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int e = (i * 64 + lane) * 4;
-    float4 mv = *reinterpret_cast<const float4*>(R.m + base + e);
-    float4 vv = *reinterpret_cast<const float4*>(R.v + base + e);
+    float4 mv = mv_[i];
+    float4 vv = vv_[i];
     float* pp = reinterpret_cast<float*>(&pv[i]);
     float* gg = reinterpret_cast<float*>(&gv[i]);
     float* mm = reinterpret_cast<float*>(&mv);

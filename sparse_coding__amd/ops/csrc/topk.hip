@@ -349,28 +349,29 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
   float acc[NV * 4];
 #pragma unroll
   for (int e = 0; e < NV * 4; ++e) acc[e] = 0.f;
-  for (int j0 = 0; j0 < k; j0 += 4) {
-    int ij[4];
-    float wj[4];
+  constexpr int RU = NV <= 2 ? 8 : 4;  // gathered rows per iteration (loads in flight: NV * RU; more costs occupancy)
+  for (int j0 = 0; j0 < k; j0 += RU) {
+    int ij[RU];
+    float wj[RU];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < RU; ++u) {
       const bool ok = j0 + u < k;
       ij[u] = ok ? I[j0 + u] : 0;
       wj[u] = ok ? V[j0 + u] : 0.f;  // zero weight: contributes nothing
     }
     // loads are unconditional (clamped column): a guarded load makes hipcc branch and
     // wait vmcnt(0) per load; lanes past d accumulate values that are zeroed below
-    ushort4 h[NV][4];
+    ushort4 h[NV][RU];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int e = min((v * 64 + lane) * 4, d - 4);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) h[v][u] = *reinterpret_cast<const ushort4*>(Dg + (long)ij[u] * d + e);
+      for (int u = 0; u < RU; ++u) h[v][u] = *reinterpret_cast<const ushort4*>(Dg + (long)ij[u] * d + e);
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RU; ++u) {
         acc[v * 4 + 0] += wj[u] * bf2f(h[v][u].x);
         acc[v * 4 + 1] += wj[u] * bf2f(h[v][u].y);
         acc[v * 4 + 2] += wj[u] * bf2f(h[v][u].z);

@@ -219,10 +219,17 @@ class ChunkedDataParallel:
     the global batch (the reference's DDP semantics, huge_batch_size.py:259-345).
     """
 
-    def __init__(self, chunks, info: DistInfo, grad_dtype: torch.dtype = torch.float32):
+    def __init__(self, chunks, info: DistInfo, grad_dtype: torch.dtype = torch.float32,
+                 cross_step: bool = False):
         self.chunks = list(chunks)
         self.info = info
         self.grad_dtype = grad_dtype
+        # cross_step: the LAST chunk's all-reduce is left in flight at the end of a step and
+        # completed (wait + Adam) only after the next step's first chunk has computed, so
+        # it overlaps the next step's encoder GEMM instead of being exposed.  Call
+        # ``flush()`` before reading parameters.
+        self.cross_step = cross_step and len(self.chunks) > 1
+        self._carry = None
         for c in self.chunks:
             c.set_grad_scale(1.0 / info.world_size)
         if info.enabled:
@@ -251,15 +258,33 @@ class ChunkedDataParallel:
     def step_batch(self, x):
         outs = [None] * len(self.chunks)
         pending = []
+        last = len(self.chunks) - 1
         for k, c in enumerate(self.chunks):
+            if k == last and self._carry is not None:
+                raise RuntimeError("unreachable: carried update must complete before its chunk computes")
             flat = c.compute_grads(x)
+            if k == 0 and self._carry is not None:
+                # the previous step's last chunk: its reduction overlapped this chunk's compute
+                j, (w, payload) = self._carry
+                self._carry = None
+                outs[j] = self.chunks[j].apply_update(self._finish(w, payload))
             pending.append((k, self._reduce_async(flat)))
             if len(pending) > 1:  # previous chunk's reduction had this chunk's compute to hide behind
                 j, (w, payload) = pending.pop(0)
                 outs[j] = self.chunks[j].apply_update(self._finish(w, payload))
+        if self.cross_step:
+            self._carry = pending.pop()  # completes during the next step's first chunk
         for j, (w, payload) in pending:
             outs[j] = self.chunks[j].apply_update(self._finish(w, payload))
         return outs
+
+    def flush(self):
+        """Complete a carried (cross-step) update; parameters are then current."""
+        if self._carry is not None:
+            j, (w, payload) = self._carry
+            self._carry = None
+            return self.chunks[j].apply_update(self._finish(w, payload))
+        return None
 
 
 def split_models(models, n_chunks: int):

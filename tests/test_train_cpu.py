@@ -377,7 +377,7 @@ def test_huge_batch_ddp_gloo_two_ranks(tmp_path):
     assert res[0][1] == res[1][1]
 
 
-def _chunked_worker(rank, world, port, x, init, out_q):
+def _chunked_worker(rank, world, port, x, init, out_q, cross=False):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, EagerChunk, split_models
@@ -387,15 +387,17 @@ def _chunked_worker(rank, world, port, x, init, out_q):
     torch.manual_seed(200 + rank)  # different params per rank (DP must broadcast rank 0's), same hyper-params
     models = init if rank == 0 else [FunctionalSAE.init(16, 32, float(b["l1_alpha"])) for _, b in init]
     chunks = [EagerChunk(FunctionalEnsemble(m, FunctionalSAE, adam, {"lr": 1e-2})) for m in split_models(models, 3)]
-    dp = ChunkedDataParallel(chunks, info)
+    dp = ChunkedDataParallel(chunks, info, cross_step=cross)
     for _ in range(3):
         dp.step_batch(x.chunk(world)[rank])
+    dp.flush()
     enc = torch.cat([c.ens.params["encoder"].detach() for c in chunks]).numpy().copy()
     out_q.put((rank, enc))
     shutdown(info)
 
 
-def test_chunked_data_parallel_gloo_matches_single_process():
+@pytest.mark.parametrize("cross", [False, True])
+def test_chunked_data_parallel_gloo_matches_single_process(cross):
     torch.manual_seed(0)
     init = [FunctionalSAE.init(16, 32, l1) for l1 in (1e-4, 3e-4, 1e-3, 1e-3)]  # no dead features: Adam would amplify rounding
     x = torch.randn(64, 16)
@@ -405,7 +407,7 @@ def test_chunked_data_parallel_gloo_matches_single_process():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_chunked_worker, args=(r, 2, port, x, init, q)) for r in range(2)]
+    procs = [ctx.Process(target=_chunked_worker, args=(r, 2, port, x, init, q, cross)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=180) for _ in procs)
