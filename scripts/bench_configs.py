@@ -159,9 +159,60 @@ def cfg_mlp(a):
     return out
 
 
+def cfg_harvest(a):
+    """Activation harvest into the HBM ring (reference activation_dataset.py:326-391; notebook
+    rate BASELINE row 7: 29.1 k act/s harvest + encode): random-init Pythia-70m / Pythia-410m
+    in bf16, forward stopped after the hooked layer, [(b s), d] rows pushed into a DeviceRing;
+    then the same with an 8-model SAE encode of every harvested batch."""
+    from sparse_coding__amd.data.harvest import ActivationHarvester, build_model, get_activation_size
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+    from sparse_coding__amd.ops import gemm
+
+    dev = "cuda:0"
+    out = {"config": "harvest: random-init LM forward -> hook -> HBM ring (+ 8-model encode)", "unit": "activations/s",
+           "runs": []}
+    for name, layer in (("pythia-70m", 2), ("pythia-410m", 12)):
+        model = build_model(name, device=dev, dtype=torch.bfloat16)
+        d = get_activation_size(name, "residual")
+        h = ActivationHarvester(model, [layer], "residual")
+        bs, seq = 64, 256
+        toks = [torch.randint(0, 50000, (bs, seq), device=dev) for _ in range(4)]
+        ring = DeviceRing(1 << 22, d, device=dev)
+        it = [0]
+
+        def harvest():
+            acts = h.run(toks[it[0] % 4])[layer]
+            it[0] += 1
+            ring.push(acts)
+            return acts
+
+        el = _timed(harvest, a.steps, a.warmup, torch.cuda.synchronize)
+        rows = bs * seq * a.steps
+        rec = {"model": name, "layer": layer, "d": d, "batch_tokens": bs * seq, "harvest_act_per_s": round(rows / el, 1)}
+        if d % 256 == 0:
+            models = [FunctionalSAE.init(d, 4 * d, 1e-3, device=dev) for _ in range(8)]
+            eng = FusedSAEEnsemble(models, FunctionalSAE, batch_size=bs * seq, device=dev)
+
+            def harvest_encode():
+                acts = harvest()
+                gemm.encode_relu(acts, eng.enc_shadow, eng.params["encoder_bias"], eng.c, eng.enc_part, None, None)
+
+            el2 = _timed(harvest_encode, a.steps, a.warmup, torch.cuda.synchronize)
+            rec["harvest_plus_8model_encode_act_per_s"] = round(rows / el2, 1)
+            del eng
+        out["runs"].append(rec)
+        h.close()
+        del model, ring
+        torch.cuda.empty_cache()
+    out["value"] = out["runs"][0]["harvest_act_per_s"]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["cpu", "topk", "fista", "mlp"])
+    ap.add_argument("which", choices=["cpu", "topk", "fista", "mlp", "harvest"])
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=2048)
@@ -170,7 +221,7 @@ def main():
     ap.add_argument("--ratio", type=float, default=1.0)
     ap.add_argument("--ring-gb", type=float, default=0.0, help="fista: ring size in GB of HBM (0: 512k rows)")
     a = ap.parse_args()
-    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp}[a.which](a)
+    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp, "harvest": cfg_harvest}[a.which](a)
     print(json.dumps(rec), flush=True)
 
 
