@@ -15,6 +15,7 @@
 // threshold stay fp32, only the GEMM operands are rounded to bf16.  The
 // dictionary (bf16, L2-resident: 2 n d bytes) is streamed from L2 each phase.
 #include "common.h"
+#include <stdlib.h>
 
 namespace scamd {
 
@@ -174,76 +175,104 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
 // once per solve (a plain GEMM); it and the fp32 iterates stay in VGPRs.  Gm is
 // symmetric, so a wave reads the rows of its own output columns along k (contiguous
 // 16-byte loads).
-template <int NW>
+// RT row tiles of 16 per workgroup: every Gm fragment a wave streams from L2 feeds RT
+// MFMAs, so RT = 2 halves the L2 traffic per FLOP of the 16-row version (the solver is
+// L2-bound: one n x n bf16 stream per iteration per workgroup; measured 1.5-1.8x).  The
+// fp32 iterates Y and A_prev stay in VGPRs; C = X D^T is re-read (L2) per iteration.  Each
+// wave's columns are produced in HALVES passes (GEMM over all of k for half of its
+// columns, then their FISTA update) so only half the accumulators are live, and the bf16
+// copy of Y is double-buffered in LDS (read the current iterate, write the next): one
+// barrier per iteration.
+template <int NW, int RT, int HALVES>
 __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restrict__ C, const uint16_t* __restrict__ Gm,
                                                         const float* __restrict__ A0, const float* __restrict__ eta_,
                                                         const float* __restrict__ lam_, const float* __restrict__ mom,
                                                         float* __restrict__ Aout, int B, int T) {
-  constexpr int n = NW * 128;
+  constexpr int n = NW * 128;  // 8 waves x NW 16-column tiles
   constexpr int nrb = n * 2;
-  __shared__ __attribute__((aligned(16))) char Ybf[FR * nrb];
+  constexpr int R = FR * RT;   // rows per workgroup
+  constexpr int NH = NW / HALVES;
+  static_assert(NW % HALVES == 0, "halves must split the tiles");
+  __shared__ __attribute__((aligned(16))) char Ybuf[2 * R * nrb];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rb = B / FR;
+  const int rb = B / R;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int g = bid / rb, r0 = (bid % rb) * FR;
+  const int g = bid / rb, r0 = (bid % rb) * R;
   const uint16_t* Gg = Gm + (long)g * n * n;
   const float eta = eta_[g], thr = eta_[g] * lam_[g];
   const int row = lane & 15, q = lane >> 4;
   const int nbase = w * NW * 16;
-  f32x4_t Y[NW], Ap[NW], Cr[NW];
+  const float* Cg = C + ((long)g * B + r0) * n;
+  f32x4_t Y[RT][NW], Ap[RT][NW];
 #pragma unroll
-  for (int t = 0; t < NW; ++t) {
-    const int col = nbase + t * 16 + 4 * q;
-    const long off = ((long)g * B + r0 + row) * n + col;
-    Cr[t] = *reinterpret_cast<const f32x4_t*>(C + off);
-    f32x4_t v = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    if (A0) v = *reinterpret_cast<const f32x4_t*>(A0 + off);
-    Y[t] = v;
-    Ap[t] = v;
-    lds_put4(Ybf, row, col, nrb, v[0], v[1], v[2], v[3]);
-  }
+  for (int u = 0; u < RT; ++u)
+#pragma unroll
+    for (int t = 0; t < NW; ++t) {
+      const int col = nbase + t * 16 + 4 * q;
+      f32x4_t v = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if (A0) v = *reinterpret_cast<const f32x4_t*>(A0 + ((long)g * B + r0 + u * FR + row) * n + col);
+      Y[u][t] = v;
+      Ap[u][t] = v;
+      lds_put4(Ybuf, u * FR + row, col, nrb, v[0], v[1], v[2], v[3]);
+    }
   __syncthreads();
   for (int it = 0; it < T; ++it) {
-    // Z[16, n_w] = Ybf[16, n] x Gm[n, n_w]
-    f32x4_t Z[NW];
-#pragma unroll
-    for (int t = 0; t < NW; ++t) Z[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // n is a compile-time constant here: cap the unroll, a full one hoists every Gm load
-    // (NW x n / 32 fragments) and spills
-#pragma unroll 2
-    for (int k0 = 0; k0 < n; k0 += 32) {
-      const bf16x8_t fy = lds_frag(Ybf, row, k0 + 8 * q, nrb);
-#pragma unroll
-      for (int t = 0; t < NW; ++t) {
-        const bf16x8_t fg = *reinterpret_cast<const bf16x8_t*>(Gg + (long)(nbase + t * 16 + row) * n + k0 + 8 * q);
-        Z[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fg, fy, Z[t], 0, 0, 0);
-      }
-    }
-    __syncthreads();  // every wave has read all of Ybf before it is overwritten
+    const char* Ycur = Ybuf + (it & 1) * (R * nrb);
+    char* Ynxt = Ybuf + ((it + 1) & 1) * (R * nrb);
     const float mo = mom[it];
     const bool final_iter = it + 1 == T;
 #pragma unroll
-    for (int t = 0; t < NW; ++t) {
-      f32x4_t an;
+    for (int h = 0; h < HALVES; ++h) {
+      // Z[R, this half of n_w] = Ycur[R, n] x Gm[n, half]
+      f32x4_t Z[RT][NH];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float y = Y[t][r] + eta * (Cr[t][r] - Z[t][r]);
-        an[r] = fmaxf(y - thr, 0.f);
-        Y[t][r] = an[r] + (an[r] - Ap[t][r]) * mo;
+      for (int u = 0; u < RT; ++u)
+#pragma unroll
+        for (int t = 0; t < NH; ++t) Z[u][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      // n is a compile-time constant here: cap the unroll, a full one hoists every Gm
+      // load (NH x n / 32 fragments) and spills; the largest state keeps one step
+      constexpr int UNR = RT * NW >= 16 ? 1 : 2;
+#pragma unroll UNR
+      for (int k0 = 0; k0 < n; k0 += 32) {
+        bf16x8_t fy[RT];
+#pragma unroll
+        for (int u = 0; u < RT; ++u) fy[u] = lds_frag(Ycur, u * FR + row, k0 + 8 * q, nrb);
+#pragma unroll
+        for (int t = 0; t < NH; ++t) {
+          const int c16 = nbase + (h * NH + t) * 16;
+          const bf16x8_t fg = *reinterpret_cast<const bf16x8_t*>(Gg + (long)(c16 + row) * n + k0 + 8 * q);
+#pragma unroll
+          for (int u = 0; u < RT; ++u) Z[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fg, fy[u], Z[u][t], 0, 0, 0);
+        }
       }
-      Ap[t] = an;
-      if (!final_iter) {
-        const int col = nbase + t * 16 + 4 * q;
-        lds_put4(Ybf, row, col, nrb, Y[t][0], Y[t][1], Y[t][2], Y[t][3]);
-      }
+      // FISTA update of this half: Y += eta (C - Z); A = relu(Y - eta lambda); Y = A + mom (A - A_prev)
+#pragma unroll
+      for (int u = 0; u < RT; ++u)
+#pragma unroll
+        for (int t = 0; t < NH; ++t) {
+          const int tt = h * NH + t;
+          const int col = nbase + tt * 16 + 4 * q;
+          const f32x4_t cv = *reinterpret_cast<const f32x4_t*>(Cg + (long)(u * FR + row) * n + col);
+          f32x4_t an;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float y = Y[u][tt][r] + eta * (cv[r] - Z[u][t][r]);
+            an[r] = fmaxf(y - thr, 0.f);
+            Y[u][tt][r] = an[r] + (an[r] - Ap[u][tt][r]) * mo;
+          }
+          Ap[u][tt] = an;
+          if (!final_iter) lds_put4(Ynxt, u * FR + row, col, nrb, Y[u][tt][0], Y[u][tt][1], Y[u][tt][2], Y[u][tt][3]);
+        }
     }
-    __syncthreads();
+    __syncthreads();  // the next iterate is complete in Ynxt; nobody reads Ycur any more
   }
 #pragma unroll
-  for (int t = 0; t < NW; ++t) {
-    const int col = nbase + t * 16 + 4 * q;
-    *reinterpret_cast<f32x4_t*>(Aout + ((long)g * B + r0 + row) * n + col) = Ap[t];
-  }
+  for (int u = 0; u < RT; ++u)
+#pragma unroll
+    for (int t = 0; t < NW; ++t) {
+      const int col = nbase + t * 16 + 4 * q;
+      *reinterpret_cast<f32x4_t*>(Aout + ((long)g * B + r0 + u * FR + row) * n + col) = Ap[u][t];
+    }
 }
 
 }  // namespace scamd
@@ -280,14 +309,18 @@ int sc_fista(const void* X, const void* D, const void* Dt, const float* A0, cons
 int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* eta, const float* lam,
                   const float* mom, float* A, int G, int B, int n, int T, hipStream_t stream) {
   if (B % FR || n % 128 || T < 0) return 1;
-  dim3 grid(G * (B / FR));
   const uint16_t* gm = reinterpret_cast<const uint16_t*>(Gm);
-#define SC_G(NWV)                                                                                      \
-  if (n == NWV * 128) {                                                                                \
-    hipLaunchKernelGGL((fista_gram_kernel<NWV>), grid, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
-    return hipGetLastError() == hipSuccess ? 0 : 3;                                                    \
+  // 32-row workgroups when they still give >= 2 per CU (256 CUs); else 16 rows
+  const bool two = (B % (2 * FR) == 0) && (long)G * (B / (2 * FR)) >= 512 && !getenv("SC_FISTA_RT1");
+  const dim3 g2(G * (B / (2 * FR))), g1(G * (B / FR));
+  // (NW, halves): 32 rows x n fp32 iterates need the column passes split in two past n = 512
+#define SC_G(NWV, H2)                                                                                      \
+  if (n == NWV * 128) {                                                                                    \
+    if (two) hipLaunchKernelGGL((fista_gram_kernel<NWV, 2, H2>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
+    else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, 1>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
+    return hipGetLastError() == hipSuccess ? 0 : 3;                                                        \
   }
-  SC_G(2) SC_G(4) SC_G(6) SC_G(8)
+  SC_G(2, 1) SC_G(4, 1) SC_G(6, 2) SC_G(8, 4)
 #undef SC_G
   return 2;
 }

@@ -505,3 +505,24 @@ def test_graph_static_inputs_match_eager():
     torch.cuda.synchronize()
     for k in eager.params:
         torch.testing.assert_close(graph.params[k], eager.params[k], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("n", [512, 1024])
+def test_fista_gram_row_tiles_match(n, monkeypatch):
+    """The 32-row Gram solver (two row tiles, column passes, double-buffered LDS) is
+    bit-identical to the 16-row one, which test_fista_kernel_matches_oracle pins."""
+    from sparse_coding__amd.ops import fista as F
+
+    torch.manual_seed(9)
+    G, B = 4, 4096  # G * B / 32 >= 512 workgroups selects the 32-row kernel
+    D = torch.nn.functional.normalize(torch.randn(G, n, n, device=DEV), dim=-1)
+    X = torch.randn(B, n, device=DEV) * 0.3
+    A0 = torch.relu(torch.randn(G, B, n, device=DEV)) * 0.02
+    lam = torch.linspace(1e-3, 1e-2, G, device=DEV)
+    eta = F.step_size(D)
+    A2, _ = F.fista(X, D, lam, A0, iters=12, eta=eta, backend="hip", with_res=False, form="gram")
+    monkeypatch.setenv("SC_FISTA_RT1", "1")
+    A1, _ = F.fista(X, D, lam, A0, iters=12, eta=eta, backend="hip", with_res=False, form="gram")
+    torch.cuda.synchronize()
+    assert torch.equal(A1, A2)
+    assert A1.abs().sum() > 0
