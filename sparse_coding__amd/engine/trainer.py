@@ -51,7 +51,8 @@ class EnsembleTrainer:
     def __init__(self, models: List[Tuple[dict, dict]], sig, lr: float = 1e-3, batch_size: int = 256,
                  device="cuda", engine: str = "auto", name: str = "ensemble", args: Optional[dict] = None,
                  fista_iters: int = 500, fista_backend: str = "auto", persist_hessian: bool = False,
-                 basis_normalize: str = "column", use_graph: bool = False, fista_eta: str = "tracked"):
+                 basis_normalize: str = "column", use_graph: bool = False, fista_eta: str = "tracked",
+                 dist=None, parallel: str = "none"):
         self.sig = sig
         self.name = name
         self.args = dict(args or {})
@@ -59,12 +60,24 @@ class EnsembleTrainer:
         self.device = torch.device(device)
         self.n_models = len(models)
         self.meta = [dict(b) for _, b in models]
+        self.es = None
+        self.local = slice(0, len(models))
+        if parallel == "es":
+            # ensemble-axis sharding (parallel/ensemble_shard.py): this rank trains its block
+            # of the models on the all-gathered global batch; `step` takes this rank's rows
+            self._init_sharded(models, sig, lr, batch_size, device, engine, dist, use_graph)
+            models = list(models[self.local])
+        elif parallel != "none":
+            raise ValueError(f"parallel must be 'none' or 'es', got {parallel!r}")
         ok, why = _fused_ok(models, sig, batch_size, device) if engine in ("auto", "fused") else (False, "eager")
         if engine == "fused" and not ok:
             raise ValueError(f"fused engine requested but unavailable: {why}")
         self.engine_reason = why
         self.kind = "eager"
-        if ok and sig is TopKEncoder:
+        if self.es is not None:
+            self.impl = self.es.engine
+            self.kind = self._es_kind
+        elif ok and sig is TopKEncoder:
             from .topk import FusedTopKEnsemble
 
             self.impl = FusedTopKEnsemble(models, sig, lr=lr, batch_size=batch_size, device=device)
@@ -91,9 +104,54 @@ class EnsembleTrainer:
         self.last_losses: Dict[str, torch.Tensor] = {}
         self.steps = 0
 
+    def _init_sharded(self, models, sig, lr, batch_size, device, engine, dist, use_graph):
+        from ..parallel.dist import DistInfo
+        from ..parallel.ensemble_shard import EnsembleSharded, shard_range
+
+        info = dist if dist is not None else DistInfo(device=torch.device(device))
+        lo, hi = shard_range(len(models), info)
+        self.local = slice(lo, hi)
+        d = models[0][0]["encoder"].shape[1]
+        gb = batch_size * info.world_size
+        fused, _ = _fused_ok(list(models[lo:hi]), sig, gb, device) if engine in ("auto", "fused") else (False, "")
+        if fused and sig is not TopKEncoder:
+            from .fused import FusedSAEEnsemble
+
+            def factory(ms, bs):
+                return FusedSAEEnsemble(ms, sig, lr=lr, batch_size=bs, device=device)
+            self._es_kind = "fused-sae"
+            dtype = torch.bfloat16
+        elif analytic.supports(sig):
+            def factory(ms, bs):
+                return analytic.AnalyticSAEEnsemble(ms, sig, lr=lr, device=device)
+            self._es_kind = "analytic"
+            dtype = torch.float32
+        else:
+            raise ValueError(f"ensemble sharding supports the SAE signatures, not {sig.__name__}")
+        self.es = EnsembleSharded(models, factory, info, batch_per_rank=batch_size, d=d, dtype=dtype)
+        if use_graph and self._es_kind == "fused-sae":
+            self.es.enable_graph()
+
     # ------------------------------------------------------------------ training
     def step(self, batch: torch.Tensor) -> torch.Tensor:
-        """One optimizer step of every model; returns per-model total loss [G] on device."""
+        """One optimizer step of every model; returns per-model total loss [G] on device
+        (with ensemble sharding: of this rank's models, on the gathered global batch)."""
+        if self.es is not None:
+            x = batch.to(self.device, self.es.gbuf[0].dtype)
+            out = self.es.step_batch(x)
+            if self.kind == "fused-sae":
+                self.last_losses = {"loss": out[:, 0], "l_reconstruction": out[:, 1], "l_l1": out[:, 2],
+                                    "l_bias_decay": out[:, 3], "l0": out[:, 4]}
+                codes = None
+            else:
+                loss, aux = out
+                self.last_losses = dict(loss)
+                codes = aux.get("c") if isinstance(aux, dict) else None
+            if self.fista is not None:
+                self._fista_update(self.es.gbuf[1 - self.es._cur], codes)  # the gathered batch just used
+            self.steps += 1
+            self.last_loss = self.last_losses["loss"]
+            return self.last_loss
         if self.kind == "fused-sae":
             out = self.impl.step_batch(batch)
             self.last_losses = {"loss": out[:, 0], "l_reconstruction": out[:, 1], "l_l1": out[:, 2],
@@ -127,10 +185,11 @@ class EnsembleTrainer:
             ens.params["decoder"].data.copy_(new)
 
     # ------------------------------------------------------------------ export / state
-    def hyperparams(self, ensemble_hyperparams: Sequence[str] = (), buffer_hyperparams: Sequence[str] = ("l1_alpha",)
-                    ) -> List[dict]:
+    def hyperparams(self, ensemble_hyperparams: Sequence[str] = (), buffer_hyperparams: Sequence[str] = ("l1_alpha",),
+                    local: bool = False) -> List[dict]:
+        """Per-model hyper-parameters (``local``: only this rank's models under ensemble sharding)."""
         out = []
-        for meta in self.meta:
+        for meta in (self.meta[self.local] if local else self.meta):
             hp = {}
             for k in ensemble_hyperparams:
                 if k not in self.args:
@@ -145,6 +204,10 @@ class EnsembleTrainer:
 
     def to_learned_dicts(self, ensemble_hyperparams=("dict_size",), buffer_hyperparams=("l1_alpha",),
                          device="cpu") -> List[Tuple[Any, dict]]:
+        """Every model's LearnedDict (a collective under ensemble sharding: all ranks call it)."""
+        if self.es is not None:
+            lds = self.es.to_learned_dicts(self.meta, self.sig, device)
+            return list(zip(lds, self.hyperparams(ensemble_hyperparams, buffer_hyperparams)))
         lds = self.impl.to_learned_dicts(device)
         return list(zip(lds, self.hyperparams(ensemble_hyperparams, buffer_hyperparams)))
 

@@ -75,8 +75,18 @@ def basic_l1_sweep(dataset_dir: str, output_dir: str, ratio: float, l1_values=np
                    save_after_every: bool = False, signature: str = "fista", fista_iters: int = 500,
                    fista_backend: str = "auto", persist_hessian: bool = False, basis_normalize: str = "column",
                    engine: str = "auto", seed: int = 0, progress: bool = True, max_batches: Optional[int] = None,
-                   fista_eta: str = "tracked") -> List[str]:
-    """Returns the list of checkpoint paths written."""
+                   fista_eta: str = "tracked", parallel: str = "none") -> List[str]:
+    """Returns the list of checkpoint paths written.  ``parallel="es"`` (launch with torchrun):
+    each rank trains l1_values/world of the models on the all-gathered global batch of
+    world x batch_size rows (parallel/ensemble_shard.py); rank 0 writes the checkpoints."""
+    info = None
+    rank, world = 0, 1
+    if parallel == "es":
+        from ..parallel.dist import init_distributed
+
+        info = init_distributed()
+        rank, world = info.rank, info.world_size
+        device = info.device
     device = torch.device(device or ("cuda:0" if torch.cuda.is_available() else "cpu"))
     folder = ChunkFolder(dataset_dir)
     if not folder.indices:
@@ -92,7 +102,8 @@ def basic_l1_sweep(dataset_dir: str, output_dir: str, ratio: float, l1_values=np
                               name="ensemble", args={"batch_size": batch_size, "device": str(device),
                                                      "dict_size": latent},
                               fista_iters=fista_iters, fista_backend=fista_backend,
-                              persist_hessian=persist_hessian, basis_normalize=basis_normalize, fista_eta=fista_eta)
+                              persist_hessian=persist_hessian, basis_normalize=basis_normalize, fista_eta=fista_eta,
+                              dist=info, parallel=parallel)
     rows_max = max(folder.meta(i)[0][0] for i in folder.indices)
     fused = trainer.kind.startswith("fused")
     ring = DeviceRing(rows_max, d, device=device, dtype=torch.bfloat16 if fused else torch.float32, seed=seed)
@@ -109,19 +120,23 @@ def basic_l1_sweep(dataset_dir: str, output_dir: str, ratio: float, l1_values=np
                 handle = folder.prefetch(int(order[ci + 1]))
             ring.size = ring.head = 0
             ring.push(host.to(device, non_blocking=True))
-            n = ring.batches_per_epoch(batch_size)
+            n = ring.batches_per_epoch(batch_size * world)
             if max_batches is not None:
                 n = min(n, max_batches)
-            bar = ProgressBar(n, ci, n_chunks, epoch, n_repetitions, enabled=progress)
-            ensemble_train_loop(trainer, ring, batch_size, n, progress=bar)
+            bar = ProgressBar(n, ci, n_chunks, epoch, n_repetitions, enabled=progress and rank == 0)
+            ensemble_train_loop(trainer, ring, batch_size, n, progress=bar, rank=rank, world=world)
             bar.close()
             if save_after_every:
                 path = os.path.join(output_dir, f"learned_dicts_epoch_{epoch}_chunk_{ci}.pt")
-                ckpt.save_learned_dicts(trainer.to_learned_dicts(["dict_size"], ["l1_alpha"]), path)
+                lds = trainer.to_learned_dicts(["dict_size"], ["l1_alpha"])  # collective under "es"
+                if rank == 0:
+                    ckpt.save_learned_dicts(lds, path)
                 written.append(path)
         if not save_after_every:
             path = os.path.join(output_dir, f"learned_dicts_epoch_{epoch}.pt")
-            ckpt.save_learned_dicts(trainer.to_learned_dicts(["dict_size"], ["l1_alpha"]), path)
+            lds = trainer.to_learned_dicts(["dict_size"], ["l1_alpha"])
+            if rank == 0:
+                ckpt.save_learned_dicts(lds, path)
             written.append(path)
     return written
 
@@ -132,7 +147,7 @@ def main(argv=None):
     basic_l1_sweep(args.dataset_dir, args.output_dir, args.ratio, l1_values, args.batch_size, args.device,
                    args.adam_lr, args.n_repetitions, args.save_after_every, args.signature, args.fista_iters,
                    args.fista_backend, args.persist_hessian, args.basis_normalize, args.engine, args.seed,
-                   fista_eta=args.fista_eta)
+                   fista_eta=args.fista_eta, parallel=args.parallel)
     return 0
 
 

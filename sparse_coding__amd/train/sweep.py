@@ -48,11 +48,11 @@ def ensemble_train_loop(trainer: EnsembleTrainer, ring: DeviceRing, batch_size: 
     n = n_batches if n_batches is not None else ring.batches_per_epoch(batch_size * world)
     fused = trainer.kind.startswith("fused")
     xbuf = None
-    if trainer.kind == "fused-sae" and getattr(trainer.impl, "use_graph", False):
+    if trainer.kind == "fused-sae" and getattr(trainer.impl, "use_graph", False) and trainer.es is None:
         xbuf = trainer.impl.x_static
     elif fused and ring.dtype == torch.bfloat16:
         xbuf = torch.empty(batch_size, ring.d, device=ring.device, dtype=ring.dtype)
-    hp = trainer.hyperparams(ensemble_hparams, buffer_hparams)
+    hp = trainer.hyperparams(ensemble_hparams, buffer_hparams, local=True)
     for i in range(n):
         with trace_range("sample"):
             x = ring.sample_shard(batch_size, rank, world, out=xbuf) if xbuf is not None else \

@@ -285,6 +285,7 @@ class SweepArgs(EnsembleArgs):
     persist_hessian: bool = False     # reference quirk B#3 (throwaway EMA) by default
     basis_normalize: str = "column"   # reference quirk B#4 by default
     signature: str = "fista"          # fista | sae | tied
+    parallel: str = "none"            # "es": ensemble-axis sharding over torchrun ranks
 
 
 def make_hyperparam_name(values: Dict[str, Any]) -> str:

@@ -521,3 +521,50 @@ def test_ensemble_sharded_gloo_matches_global_batch():
     for k in single.params:
         np.testing.assert_array_equal(res[0][k], res[1][k])
         np.testing.assert_allclose(res[0][k], single.params[k].numpy(), atol=2e-5, rtol=1e-4)
+
+
+def _trainer_es_worker(rank, world, port, xs, init, out_q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
+
+    info = init_distributed("gloo")
+    tr = EnsembleTrainer(init, FunctionalSAE, lr=1e-2, batch_size=xs[0].shape[0] // world, device="cpu",
+                         dist=info, parallel="es", args={"dict_size": 32})
+    assert tr.kind == "analytic" and tr.impl.n_models == len(init) // world
+    for x in xs:
+        tr.step(x.chunk(world)[rank])
+    lds = tr.to_learned_dicts(["dict_size"], ["l1_alpha"])
+    out_q.put((rank, [ld.encoder.numpy().copy() for ld, _ in lds], [hp for _, hp in lds]))
+    shutdown(info)
+
+
+def test_trainer_ensemble_sharded_gloo():
+    """EnsembleTrainer(parallel="es") over two gloo ranks == one process training every
+    model on the global batch; LearnedDicts and hyper-parameters come back for all models."""
+    from sparse_coding__amd.engine.analytic import AnalyticSAEEnsemble
+
+    torch.manual_seed(1)
+    init = [FunctionalSAE.init(16, 32, l1) for l1 in (1e-4, 3e-4, 1e-3, 3e-3)]
+    xs = [torch.randn(64, 16) for _ in range(3)]
+    single = AnalyticSAEEnsemble([(dict(p), dict(b)) for p, b in init], FunctionalSAE, lr=1e-2)
+    for x in xs:
+        single.step_batch(x)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_es_worker, args=(r, 2, port, xs, init, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, encs, hps = q.get(timeout=180)
+        res[r] = (encs, hps)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    encs, hps = res[0]
+    assert len(encs) == 4 and [h["l1_alpha"] for h in hps] == pytest.approx([1e-4, 3e-4, 1e-3, 3e-3])
+    for g in range(4):
+        np.testing.assert_array_equal(encs[g], res[1][0][g])
+        np.testing.assert_allclose(encs[g], single.params["encoder"][g].numpy(), atol=2e-5, rtol=1e-4)
