@@ -84,7 +84,7 @@ def basic_l1_sweep(dataset_dir: str, output_dir: str, ratio: float, l1_values=np
     if parallel == "es":
         from ..parallel.dist import init_distributed
 
-        info = init_distributed()
+        info = init_distributed(force=True)  # a process group even for one rank (same code path)
         rank, world = info.rank, info.world_size
         device = info.device
     device = torch.device(device or ("cuda:0" if torch.cuda.is_available() else "cpu"))
@@ -138,6 +138,10 @@ def basic_l1_sweep(dataset_dir: str, output_dir: str, ratio: float, l1_values=np
             if rank == 0:
                 ckpt.save_learned_dicts(lds, path)
             written.append(path)
+    if info is not None:
+        from ..parallel.dist import shutdown
+
+        shutdown(info)
     return written
 
 

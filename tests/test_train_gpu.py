@@ -186,3 +186,24 @@ def test_chunked_dp_fused_two_ranks_one_gpu():
     du, dr = (res[0] - init_dec).ravel(), (want - init_dec).ravel()
     cos = float(du @ dr / (np.linalg.norm(du) * np.linalg.norm(dr)))
     assert cos > 0.99, cos
+
+
+def test_sweep_cli_ensemble_sharded_rccl(tmp_path):
+    """basic_l1_sweep --parallel es under torch.distributed.run (one rank: the sharded path
+    with real RCCL collectives -- batch all-gather, parameter gather for the checkpoint)."""
+    import subprocess
+    import sys
+
+    g = torch.Generator().manual_seed(0)
+    for i in range(2):
+        save_chunk(torch.randn(4096, 256, generator=g), str(tmp_path / "d"), i)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", "29561", "-m", "sparse_coding__amd.train.basic_l1_sweep",
+           "--dataset_dir", str(tmp_path / "d"), "--output_dir", str(tmp_path / "o"), "--ratio", "2.0",
+           "--l1_value_n", "2", "--signature", "sae", "--batch_size", "256", "--parallel", "es",
+           "--save_after_every", "false"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lds = ckpt.load_learned_dicts(str(tmp_path / "o" / "learned_dicts_epoch_0.pt"))
+    assert len(lds) == 2 and all(torch.isfinite(ld.get_learned_dict()).all() for ld, _ in lds)
