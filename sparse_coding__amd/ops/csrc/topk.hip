@@ -325,6 +325,180 @@ __global__ __launch_bounds__(256) void topk_wave_kernel(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Block-per-row bisection for long rows (4096 < n <= 256 * PL): the same algorithm as
+// topk_wave_kernel with the row spread over 4 waves (PL keys per thread), so every
+// full-scan step costs PL compares per lane plus a DPP wave total and one LDS exchange
+// (parity-double-buffered slots: one barrier per step).  After S1 = 12 bits the bucket
+// (keys sharing t's top bits) is compacted into LDS and -- when it holds <= 64 keys,
+// the usual case -- wave 0 resolves the last 20 bits with ballots alone.
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
+  const int r2 = __builtin_amdgcn_readlane(v, 47);
+  return v + (lane < 16 ? 0 : lane < 32 ? r0 : lane < 48 ? r0 + r1 : r0 + r1 + r2);
+}
+
+template <int PL>
+__global__ __launch_bounds__(256) void topk_block_kernel(const float* __restrict__ scores, const int* __restrict__ kv,
+                                                       int* __restrict__ idx, float* __restrict__ val, int B, int n,
+                                                       int kmax, int absolute, int relu) {
+  constexpr int S1 = 12, LOW = 32 - S1;
+  __shared__ int red[2][4];
+  __shared__ int wsum[2][4];
+  __shared__ uint32_t cbuf[256];
+  __shared__ uint32_t res[2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long row = blockIdx.x;
+  const int g = (int)(row / B);
+  const int k = min(kv[g], n);
+  const float* S = reinterpret_cast<const float*>(__builtin_assume_aligned(scores + row * n, 16));
+  int* I = idx + row * kmax;
+  float* V = val + row * kmax;
+  uint32_t key[PL];
+#pragma unroll
+  for (int i = 0; i < PL / 4; ++i) {
+    const int c = (i * 256 + tid) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(__builtin_assume_aligned(S + (min(c, n - 4) & ~3), 16));
+    const uint32_t live = 0u - (uint32_t)(c < n);
+    const float f[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) key[4 * i + j] = order_key(absolute ? fabsf(f[j]) : f[j]) & live;
+  }
+  int par = 0;
+  auto block_total = [&](int c) {  // one barrier: per-wave DPP totals through parity slots
+    c = wave_total(c);
+    if (lane == 0) red[par][w] = c;
+    __syncthreads();
+    const int tot = red[par][0] + red[par][1] + red[par][2] + red[par][3];
+    par ^= 1;
+    return tot;
+  };
+  if (k > 0) {
+    uint32_t t = 0;
+#pragma unroll 1
+    for (int b = 31; b >= LOW; --b) {
+      const uint32_t cand = t | (1u << b);
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
+      if (block_total(cnt) >= k) t = cand;
+    }
+    const uint32_t hi = t >> LOW;
+    int above = 0, inb = 0;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) {
+      const uint32_t h = key[i] >> LOW;
+      above += h > hi ? 1 : 0;
+      inb += h == hi ? 1 : 0;
+    }
+    const int n_above = block_total(above);
+    const int nb = block_total(inb);
+    int gt;
+    if (nb <= 64) {
+      // compact the bucket (block exclusive scan of the per-thread counts), then wave 0
+      // finishes the bisection with ballots
+      const int incl = wave_incl_scan(inb, lane);
+      if (lane == 63) wsum[par][w] = incl;
+      __syncthreads();
+      int off = incl - inb;
+      for (int ww = 0; ww < w; ++ww) off += wsum[par][ww];
+      par ^= 1;
+#pragma unroll
+      for (int i = 0; i < PL; ++i)
+        if ((key[i] >> LOW) == hi) cbuf[off++] = key[i];
+      __syncthreads();
+      if (w == 0) {
+        const bool valid = lane < nb;
+        const uint32_t ck = valid ? cbuf[lane] : 0u;
+        uint32_t tt = t;
+#pragma unroll 1
+        for (int b = LOW - 1; b >= 0; --b) {
+          const uint32_t cand = tt | (1u << b);
+          if (n_above + (int)__popcll(__ballot(valid && ck >= cand)) >= k) tt = cand;
+        }
+        const int gtv = n_above + (int)__popcll(__ballot(valid && ck > tt));  // all lanes vote
+        if (lane == 0) {
+          res[0] = tt;
+          res[1] = (uint32_t)gtv;
+        }
+      }
+      __syncthreads();
+      t = res[0];
+      gt = (int)res[1];
+    } else {  // crowded bucket: finish by full scans
+#pragma unroll 1
+      for (int b = LOW - 1; b >= 0; --b) {
+        const uint32_t cand = t | (1u << b);
+        int cnt = 0;
+#pragma unroll
+        for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
+        if (block_total(cnt) >= k) t = cand;
+      }
+      int c2 = 0;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) c2 += key[i] > t ? 1 : 0;
+      gt = block_total(c2);
+    }
+    const int need_ties = k - gt;
+    // output in column order: chunk i = columns [1024 i, 1024 i + 1024), thread t owns
+    // 4 t .. 4 t + 3 of it; block scans of the tie and take counts give each thread its slots
+    int base = 0, ties_seen = 0;
+#pragma unroll
+    for (int i = 0; i < PL / 4; ++i) {
+      int neq = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) neq += key[4 * i + j] == t ? 1 : 0;
+      int ie = wave_incl_scan(neq, lane);
+      if (lane == 63) wsum[par][w] = ie;
+      __syncthreads();
+      int tie_rank = ties_seen + ie - neq, tie_tot = 0;
+      for (int ww = 0; ww < 4; ++ww) {
+        if (ww < w) tie_rank += wsum[par][ww];
+        tie_tot += wsum[par][ww];
+      }
+      par ^= 1;
+      bool take[4];
+      int ns = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t kk = key[4 * i + j];
+        take[j] = kk > t || (kk == t && tie_rank < need_ties);
+        tie_rank += kk == t ? 1 : 0;
+        ns += take[j] ? 1 : 0;
+      }
+      int is = wave_incl_scan(ns, lane);
+      if (lane == 63) wsum[par][w] = is;
+      __syncthreads();
+      int pos = base + is - ns, tot = 0;
+      for (int ww = 0; ww < 4; ++ww) {
+        if (ww < w) pos += wsum[par][ww];
+        tot += wsum[par][ww];
+      }
+      par ^= 1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (take[j]) {
+          const int c = (i * 256 + tid) * 4 + j;
+          const float sv = S[c];
+          I[pos] = c;
+          V[pos] = relu ? fmaxf(sv, 0.f) : sv;
+          ++pos;
+        }
+      }
+      base += tot;
+      ties_seen += tie_tot;
+    }
+  }
+  for (int j = k + tid; j < kmax; j += 256) {
+    I[j] = 0;
+    V[j] = 0.f;
+  }
+}
+
 // One wave per (model, row).  D: [G][n][d] bf16 normalised dictionary (gathered rows).
 // Decode gathers the k dictionary rows four at a time (indices and values are
 // wave-uniform scalar loads issued ahead of the row loads).  The k code gradients
@@ -477,6 +651,15 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
       return hipGetLastError() == hipSuccess ? 0 : 3; }
     SC_W(16) SC_W(32) SC_W(64)
 #undef SC_W
+  }
+  if (n % 4 == 0 && n <= 256 * 64 && !getenv("SC_TOPK_RADIX")) {  // long rows: a block per row
+    dim3 bgrid((unsigned)G * B);
+#define SC_BK(P) \
+    if (n <= 256 * P) { hipLaunchKernelGGL((topk_block_kernel<P>), bgrid, dim3(256), 0, stream, scores, k, idx, val, B, n, \
+                                           kmax, absolute, relu); \
+      return hipGetLastError() == hipSuccess ? 0 : 3; }
+    SC_BK(24) SC_BK(32) SC_BK(48) SC_BK(64)
+#undef SC_BK
   }
   const int per = (n + 255) / 256;
   dim3 grid((unsigned)G * B);

@@ -271,7 +271,7 @@ def test_fused_adam_epilogue_matches_separate_adam():
 
 
 @pytest.mark.parametrize("radix", [False, True])
-@pytest.mark.parametrize("n", [6144, 1000])
+@pytest.mark.parametrize("n", [6144, 1000, 12288])  # block-per-row, wave-per-row, block (PL=48)
 def test_topk_select_exact(radix, n, monkeypatch):
     from sparse_coding__amd.ops import topk as T
 
