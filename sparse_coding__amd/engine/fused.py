@@ -18,7 +18,11 @@ ever recomputes norms); per-model hyper-parameters as device vectors
 
 Supported kinds: ``untied`` (FunctionalSAE / FunctionalMaskedSAE / FunctionalFista's
 SAE loss) and ``tied`` (FunctionalTiedSAE with identity centering /
-FunctionalMaskedTiedSAE).  Masked models pass per-model ``dict_size``.
+FunctionalMaskedTiedSAE), plus the tied activation variants ``reverse``
+(FunctionalReverseSAE, codes 1[pre > 0](pre - b)) and ``threshold``
+(FunctionalThresholdingSAE, learned scale / gain / centering), which run the
+same kernels with the ENC_ACT / DC_ACT epilogues.  Masked models pass per-model
+``dict_size``.
 """
 
 from __future__ import annotations
@@ -33,6 +37,11 @@ from ..ops import adam as adam_ops
 from ..ops import gemm as gemm_ops
 
 
+# engine kind -> code activation of the encoder / code-gradient epilogues
+_ACTS = {"untied": gemm_ops.ACT_RELU, "tied": gemm_ops.ACT_RELU, "reverse": gemm_ops.ACT_REVERSE,
+         "threshold": gemm_ops.ACT_THRESHOLD}
+
+
 def _stack(models, key, which=0, device=None):
     return torch.stack([m[which][key].detach().float() for m in models]).to(device).contiguous()
 
@@ -45,8 +54,15 @@ class FusedSAEEnsemble:
                  count_every: int = 8, wgrad_split="auto"):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
-        if self.kind not in ("untied", "tied"):
+        if self.kind not in _ACTS:
             raise ValueError(f"signature {sig} has no fused implementation")
+        # code activation of the encoder / code-gradient epilogues: reverse and threshold
+        # SAEs are tied dictionaries with another activation (sae_ensemble.py:230-303, 445-501)
+        self.act = _ACTS[self.kind]
+        if self.act and fuse_adam:
+            raise ValueError(f"fuse_adam is not implemented for {self.kind} SAEs")
+        # the per-feature vector that plays the encoder bias (threshold SAEs: the gain)
+        self._bkey = "activation_gain" if self.kind == "threshold" else "encoder_bias"
         self.device = torch.device(device)
         self.n_models = G = len(models)
         self.batch_size = B = int(batch_size)
@@ -83,9 +99,13 @@ class FusedSAEEnsemble:
 
         # ----- parameters (fp32 masters) and Adam state
         self.params: Dict[str, torch.Tensor] = {"encoder": _stack(models, "encoder", 0, dev),
-                                                "encoder_bias": _stack(models, "encoder_bias", 0, dev)}
+                                                self._bkey: _stack(models, self._bkey, 0, dev)}
         if self.kind == "untied":
             self.params["decoder"] = _stack(models, "decoder", 0, dev)
+        if self.kind == "threshold":
+            # learned per-feature scale s (codes scale with s^2) and input centering vector
+            self.params["activation_scale"] = _stack(models, "activation_scale", 0, dev)
+            self.params["centering"] = _stack(models, "centering", 0, dev)
         self.m = {k: torch.zeros_like(v) for k, v in self.params.items()}
         self.v = {k: torch.zeros_like(v) for k, v in self.params.items()}
         # ----- per-model hyper-parameters as device vectors
@@ -163,9 +183,12 @@ class FusedSAEEnsemble:
         self.sqpart = torch.zeros(G, n, d // 128, device=dev)   # updated-row |w|^2 partials
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)  # graph input buffer
         self._static_inputs = [self.x_static]
-        if self.centering is not None:
+        if self.centering is not None or self.kind == "threshold":
             self._xr = torch.empty(G, B, d, device=dev)              # x R^T (fp32)
             self.x_c = torch.empty(G, B, d, device=dev, dtype=bf)    # centred input per model
+        if self.kind == "threshold":
+            self.s2 = torch.empty(G, n, device=dev)                  # s^2 read by the epilogues
+            self._gsum = torch.empty(G, n, device=dev)
 
     # ------------------------------------------------------------------ helpers
     def refresh_shadows(self):
@@ -178,7 +201,12 @@ class FusedSAEEnsemble:
 
     def prepare(self, x):
         """The kernels' input: ``x`` itself, or its per-model centred copy for tied SAEs
-        with non-identity centering."""
+        with non-identity centering (threshold SAEs: x - centering, learned)."""
+        if self.kind == "threshold":
+            torch.sub(x.unsqueeze(0), self.params["centering"].unsqueeze(1), out=self._xr)
+            self.x_c.copy_(self._xr)
+            torch.mul(self.params["activation_scale"], self.params["activation_scale"], out=self.s2)
+            return self.x_c
         if self.centering is None:
             return x
         c = self.centering
@@ -199,15 +227,24 @@ class FusedSAEEnsemble:
     def _counting(self):
         return self.track_feature_counts and (self.step_count % self.count_every == 0)
 
-    def forward(self, x, count=None):
-        """Kernels 1-3: codes (+L1/L0), residual (+MSE), code gradient (+bias-grad partials)."""
+    def forward(self, x, count=None, target=None):
+        """Kernels 1-3: codes (+L1/L0), residual (+MSE), code gradient (+bias-grad partials).
+        ``target``: the reconstruction target when it differs from the encoder input ``x``
+        (threshold SAEs reconstruct the uncentred batch)."""
         if x.shape[-2] != self.batch_size:
             raise ValueError(f"batch has {x.shape[-2]} rows, engine was built for {self.batch_size}")
         count = self._counting() if count is None else count
         self._counted = count
-        gemm_ops.encode_relu(x, self.enc_shadow, self.params["encoder_bias"], self.c, self.enc_part,
-                             self.cnt_part if count else None, self.nactive, mask_out=self.cmask)
-        gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
+        ascale = self.s2 if self.kind == "threshold" else None
+        gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part,
+                             self.cnt_part if count else None, self.nactive, mask_out=self.cmask,
+                             act=self.act, ascale=ascale)
+        gemm_ops.decode_residual(self.c, self.dec_shadow, x if target is None else target, self.r, self.dec_part)
+        if self.act:
+            gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
+                               dotpart=self.dotpart if self.kind == "threshold" else None, mask=self.cmask,
+                               act=self.act, ascale=ascale)
+            return
         gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                            dotpart=self.dotpart if self.fuse_adam else None,
                            tied_bias=self.params["encoder_bias"] if (self.fuse_adam and self.kind == "tied") else None,
@@ -312,7 +349,30 @@ class FusedSAEEnsemble:
         if not self.fuse_adam:  # with fuse_adam the weights were already updated in wgrad_adam
             adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
                                step_dev=self.step_dev, **self._adam_split_kw())
+        if self.kind == "threshold":
+            self._threshold_extra_adam()
         self._bias_loss(update=True, reduced=False)
+
+    def _threshold_extra_adam(self):
+        """Scale and centering of the threshold SAE (small vectors; before the bias / loss
+        kernel, which advances the device step counter):
+        dL/ds = 2 s alpha sum(dotpart), dL/dcentering = -alpha (sum_b dL/dpre) W_hat."""
+        a = self._alpha
+        s = self.params["activation_scale"]
+        torch.sum(self.dotpart, dim=1, out=self._gsum)
+        g_s = self._gsum * s * (2.0 * a)
+        torch.sum(self.colpart, dim=1, out=self._gsum)
+        g_c = torch.bmm(self._gsum.unsqueeze(1).to(torch.bfloat16), self.enc_shadow).squeeze(1).float() * (-a)
+        t = self.step_dev.float() + 1.0
+        b1, b2 = self.betas
+        bc1 = 1.0 - torch.pow(b1, t)
+        bc2 = 1.0 - torch.pow(b2, t)
+        lr = self.lr.unsqueeze(1)
+        for k, g in (("activation_scale", g_s), ("centering", g_c)):
+            p, m, v = self.params[k], self.m[k], self.v[k]
+            m.mul_(b1).add_(g, alpha=1.0 - b1)
+            v.mul_(b2).addcmul_(g, g, value=1.0 - b2)
+            p.sub_(lr * (m / bc1) / ((v / bc2).sqrt() + self.eps))
 
     def _host_step(self):
         if self._counted:
@@ -326,7 +386,7 @@ class FusedSAEEnsemble:
             colpart, tm, gscale = self.g_bias, 1, 1.0
         else:
             colpart, tm, gscale = self.colpart, B // 128, self._alpha
-        adam_ops.bias_loss(self.params["encoder_bias"], self.m["encoder_bias"], self.v["encoder_bias"],
+        adam_ops.bias_loss(self.params[self._bkey], self.m[self._bkey], self.v[self._bkey],
                            colpart, tm, self.enc_part, self.enc_part.shape[1], self.dec_part,
                            self.dec_part.shape[1], self.l1, self.bias_decay, self.lr, self.out, B, d,
                            self.step_count + 1, gscale=gscale,
@@ -362,6 +422,7 @@ class FusedSAEEnsemble:
     def _step_kernels(self, x, count=None):
         """All kernels of one step.  Optionally (``overlap_adam``) untied models overlap the
         memory-bound decoder Adam (side stream) with the compute-bound encoder wgrad GEMM."""
+        target = x if self.kind == "threshold" else None
         x = self.prepare(x)
         if (self.kind == "untied" and self.overlap_adam and not self.fuse_adam
                 and os.environ.get("SC_SERIALIZE_STREAMS", "0") in ("", "0")):
@@ -379,7 +440,7 @@ class FusedSAEEnsemble:
             main.wait_stream(self._side)  # join before the step counter advances
             self._bias_loss(update=True, reduced=False)
         else:
-            self.forward(x, count)
+            self.forward(x, count, target)
             self.backward_weights(x)
             self._apply_update_kernels()
 
@@ -432,9 +493,13 @@ class FusedSAEEnsemble:
         s1 = torch.zeros(G, self.d, device=self.device, dtype=torch.float64)
         s2 = torch.zeros(G, device=self.device, dtype=torch.float64)
         for i in range(0, N, B):
-            x = self.prepare(self._x_bf16(rows[i:i + B]))
-            gemm_ops.encode_relu(x, self.enc_shadow, self.params["encoder_bias"], self.c, self.enc_part, None,
-                                 self.nactive)
+            xin = self._x_bf16(rows[i:i + B])
+            x = self.prepare(xin)
+            gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part, None,
+                                 self.nactive, mask_out=self.cmask, act=self.act,
+                                 ascale=self.s2 if self.kind == "threshold" else None)
+            if self.kind == "threshold":  # reconstructs the uncentred rows
+                x = xin
             gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
             se += self.dec_part.sum(1).double()
             l0 += self.enc_part[..., 1].sum(1).double()

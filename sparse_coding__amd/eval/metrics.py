@@ -79,9 +79,26 @@ def batched_fvu_l0(model: LearnedDict, activations: torch.Tensor, batch_size: in
 
 
 # ------------------------------------------------------------------ dictionary similarity
+# Above this many similarity entries, GPU max-cosine reductions run on the fused
+# EPI_ROWMAX kernel (bf16 MFMA, the [n1, n2] matrix never materialised; 16k x 16k fp32
+# would be 1 GiB); below it the exact fp32 torch product is cheap enough.
+ROWMAX_MIN_ENTRIES = 1 << 24
+
+
+def max_cosine(rows: torch.Tensor, against: torch.Tensor, fused: bool | None = None) -> torch.Tensor:
+    """max_j <rows_i, against_j> for every row (inputs already unit-norm)."""
+    if fused is None:
+        fused = rows.is_cuda and rows.shape[0] * against.shape[0] >= ROWMAX_MIN_ENTRIES
+    if fused:
+        from ..ops import gemm
+
+        return gemm.rowmax_nt(rows.to(torch.bfloat16).contiguous(), against.to(torch.bfloat16).contiguous())
+    return (rows @ against.T).max(dim=-1).values
+
+
 def mcs_duplicates(ground: LearnedDict, model: LearnedDict) -> torch.Tensor:
     """Max cosine similarity of each ``model`` atom to the ``ground`` atoms (reference :268-272)."""
-    return (model.get_learned_dict() @ ground.get_learned_dict().T).max(dim=-1).values
+    return max_cosine(model.get_learned_dict(), ground.get_learned_dict())
 
 
 def mmcs(model: LearnedDict, model2: LearnedDict) -> torch.Tensor:
@@ -89,7 +106,7 @@ def mmcs(model: LearnedDict, model2: LearnedDict) -> torch.Tensor:
 
 
 def mcs_to_fixed(model: LearnedDict, truth: torch.Tensor) -> torch.Tensor:
-    return (model.get_learned_dict() @ truth.T).max(dim=-1).values
+    return max_cosine(model.get_learned_dict(), truth)
 
 
 def mmcs_to_fixed(model: LearnedDict, truth: torch.Tensor) -> torch.Tensor:

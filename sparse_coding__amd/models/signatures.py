@@ -204,7 +204,10 @@ class FunctionalThresholdingSAE(DictSignature):
 
     fix B#10: the reference encodes with ``params["centering"]`` which ``init`` never
     creates; we add a zero-initialised learned ``centering`` vector so the model runs.
+    Fused engine: ``FusedSAEEnsemble`` kind "threshold" (EPI_ENC_ACT / EPI_DC_ACT, act 2).
     """
+
+    fused_kind = "threshold"
 
     @staticmethod
     def init(activation_size, n_dict_components, l1_alpha, device=None, dtype=None):
@@ -326,7 +329,10 @@ class FunctionalMaskedSAE(DictSignature):
 
 # --------------------------------------------------------------------------- reverse
 class FunctionalReverseSAE(DictSignature):
-    """Tied SAE that subtracts the bias from active codes before decoding (reference :445-501)."""
+    """Tied SAE that subtracts the bias from active codes before decoding (reference :445-501).
+    Fused engine: ``FusedSAEEnsemble`` kind "reverse" (EPI_ENC_ACT / EPI_DC_ACT, act 1)."""
+
+    fused_kind = "reverse"
 
     @staticmethod
     def init(activation_size, n_dict_components, l1_alpha, bias_decay=0.0, device=None, dtype=None):

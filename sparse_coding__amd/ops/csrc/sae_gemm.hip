@@ -15,6 +15,12 @@
 //             partials for the bias gradient (autograd of :54-64, Appendix A of SURVEY)
 //   EPI_F32 : C = alpha * acc (fp32), used for dW = c^T R and dW_e = dpre^T x
 //   EPI_BF16: C = alpha * acc (bf16), generic inference GEMM
+//   EPI_ENC_ACT / EPI_DC_ACT: EPI_ENC / EPI_DC_MASK for the other code activations
+//             (GemmParams::act): 1 = reverse SAE, codes 1[pre > 0] (pre - b)
+//             (sae_ensemble.py:481-482); 2 = smooth threshold
+//             s^2 thr((pre)/s^2), thr(u) = relu6(60(u - 0.9))/6 + relu(u - 1) (:254-257)
+//   EPI_ROWMAX: per-row max of alpha * A B^T over column tiles (max cosine similarity /
+//             MMCS, standard_metrics.py:268-301) -- the [M, N] product never reaches HBM
 //
 // Tiling (template "shape"): a WGM x WGN grid of waves, each owning a
 // (16 WI) x (16 WJ) sub-tile = WI x WJ v_mfma_f32_16x16x32_bf16 accumulators:
@@ -53,7 +59,7 @@ using S256 = Shape<2, 4, 8, 4>;
 constexpr int PT = 128;
 
 enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5, EPI_ENC_CNT = 6,
-       EPI_DC_MASK = 7 };
+       EPI_DC_MASK = 7, EPI_ENC_ACT = 8, EPI_DC_ACT = 9, EPI_ROWMAX = 10 };
 
 // Activity bitmask of the codes, in MFMA-fragment order: for the 16x16 output fragment at
 // (row/16, col/16) the encoder epilogue stores its four wave ballots (bit l of word r: lane
@@ -123,6 +129,9 @@ struct GemmParams {
   // (the consumer -- the Adam kernel for weight gradients -- sums the slabs).
   int ksplit;
   long split_stride;
+  // --- EPI_ENC_ACT / EPI_DC_ACT: activation mode and the threshold SAE's per-feature s^2
+  int act;
+  const float* ascale;  // [G][N] (group stride sbias)
 };
 
 // LDS image of a K-major tile [128 rows][BKT k] bf16.
@@ -277,7 +286,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   // Only the weight-gradient style epilogues take a second K segment (K-concat);
   // the fused forward epilogues never do, and skipping its offsets saves VGPRs.
   constexpr bool SEG2 = (EPI == EPI_F32 || EPI == EPI_BF16 || EPI == EPI_ADAM);
-  constexpr bool ENC = (EPI == EPI_ENC || EPI == EPI_ENC_CNT);
+  constexpr bool ENC = (EPI == EPI_ENC || EPI == EPI_ENC_CNT || EPI == EPI_ENC_ACT);
   const int nk1 = p.K1 / BKT, nk_all = nk1 + (SEG2 ? p.K2 / BKT : 0);
   // this block's K-tile range [kbeg, nk) (the whole range unless split-K)
   const int kbeg = (int)(((long)ksi * nk_all) / p.ksplit);
@@ -323,7 +332,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   // The DEC / DC epilogues read a bf16 tile of x / c at the output positions:
   // fetch it before the K loop so its HBM latency hides under the MFMAs (small
   // per-wave tiles only; at 128x64 per wave the registers are needed by the loop).
-  constexpr bool AUX_EARLY = (EPI == EPI_DEC || EPI == EPI_DC) && WI * WJ <= 16;
+  constexpr bool AUX_EARLY = (EPI == EPI_DEC || EPI == EPI_DC || EPI == EPI_DC_ACT) && WI * WJ <= 16;
   uint2 auxv[WI][WJ];
   if constexpr (AUX_EARLY) {
     const uint16_t* X = p.aux + (long)g * p.saux;
@@ -446,34 +455,69 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     const float* bias = p.bias + (long)g * p.sbias;
     const int nact = p.nactive ? p.nactive[g] : p.N;  // masked SAEs: live columns [0, nact)
-    constexpr bool counting = EPI == EPI_ENC_CNT;
+    constexpr bool ACTV = EPI == EPI_ENC_ACT;
+    const int act = ACTV ? p.act : 0;  // compile-time 0 for the plain ReLU instantiations
+    const bool counting = EPI == EPI_ENC_CNT || (ACTV && p.colpart != nullptr);
     float l1 = 0.f, l0 = 0.f;
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
       const int col = colb + j * 16;
       const f32x4_t bj = *reinterpret_cast<const f32x4_t*>(bias + col);
+      f32x4_t s2 = f32x4_t{1.f, 1.f, 1.f, 1.f}, is2 = s2;
+      if (ACTV && act == 2) {
+        s2 = *reinterpret_cast<const f32x4_t*>(p.ascale + (long)g * p.sbias + col);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) is2[r] = 1.f / fmaxf(s2[r], 1e-8f);
+      }
       f32x4_t cnt = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < WI; ++i) {
         f32x4_t v;
+        bool on[4];
+        if constexpr (ACTV) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[i][j][r] + bj[r], 0.f);
-        // branch-free (a block-uniform `if (masked)` made hipcc version the whole
-        // epilogue and spill at 128x64 per wave)
+          for (int r = 0; r < 4; ++r) {
+            const float pre = acc[i][j][r] + bj[r];
+            if (act == 1) {
+              v[r] = pre > 0.f ? acc[i][j][r] : 0.f;  // relu(pre) - b on the active codes
+            } else if (act == 2) {
+              const float u = pre * is2[r];
+              v[r] = (fminf(fmaxf(10.f * (u - 0.9f), 0.f), 1.f) + fmaxf(u - 1.f, 0.f)) * s2[r];
+            } else {
+              v[r] = fmaxf(pre, 0.f);
+            }
+            const bool live = col + r < nact;
+            on[r] = live && (act == 1 ? pre > 0.f : v[r] > 0.f);
+            v[r] = live ? v[r] : 0.f;
+          }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (col + r < nact) ? v[r] : 0.f;
+          for (int r = 0; r < 4; ++r) {
+            l1 += fabsf(v[r]);
+            const float onf = on[r] ? 1.f : 0.f;
+            l0 += onf;
+            cnt[r] += onf;
+          }
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          l1 += v[r];
-          const float on = v[r] > 0.f ? 1.f : 0.f;
-          l0 += on;
-          cnt[r] += on;
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[i][j][r] + bj[r], 0.f);
+          // branch-free (a block-uniform `if (masked)` made hipcc version the whole
+          // epilogue and spill at 128x64 per wave)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (col + r < nact) ? v[r] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            l1 += v[r];
+            on[r] = v[r] > 0.f;
+            const float onf = on[r] ? 1.f : 0.f;
+            l0 += onf;
+            cnt[r] += onf;
+          }
         }
         *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + col) =
             make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
         if (p.cmask) {  // block-uniform
-          const uint64_t b0 = __ballot(v[0] > 0.f), b1 = __ballot(v[1] > 0.f);
-          const uint64_t b2 = __ballot(v[2] > 0.f), b3 = __ballot(v[3] > 0.f);
+          const uint64_t b0 = __ballot(on[0]), b1 = __ballot(on[1]);
+          const uint64_t b2 = __ballot(on[2]), b3 = __ballot(on[3]);
           const long frag = ((long)g * (p.M >> 4) + ((rowb + i * 16) >> 4)) * (p.N >> 4) + ((colb + j * 16) >> 4);
           if (lane == 0) {
             u32x4_t* dst = reinterpret_cast<u32x4_t*>(p.cmask + frag * 4);
@@ -482,11 +526,11 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
           }
         }
       }
-      if constexpr (counting) colred_lane(cnt, j, 0);
+      if (counting) colred_lane(cnt, j, 0);
     }
     l1 = block_sum<NW>(l1, red + 4096);  // its barriers also publish the colred_lane writes
     l0 = block_sum<NW>(l0, red + 4096);
-    if constexpr (counting) colred_store(p.colpart, 0);
+    if (counting) colred_store(p.colpart, 0);
     scalar_partial(p.part, 2, 0, l1);
     scalar_partial(p.part, 2, 1, l0);
     return;
@@ -578,6 +622,82 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
     }
     __syncthreads();
     colred_store(p.colpart, 0);
+    return;
+  }
+  if constexpr (EPI == EPI_DC_ACT) {
+    // Code gradient of the reverse / threshold activations: activity from the encoder's
+    // bitmask, the codes themselves (aux) for the L1 sign (reverse codes can be negative)
+    // and the threshold's slope.  Threshold: thr' = 10 on the ramp (c / s^2 < 1), 1 above;
+    // region 1 collects sum_b dL/dc * (thr - u thr') = -9 dL/dc on the ramp (the s^2
+    // gradient: dL/ds = 2 s * that); reverse SAEs get no bias gradient (column sums 0).
+    uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
+    const float add = p.l1[g] * p.l1_add_scale;
+    const int act = p.act;
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) {
+      f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f}, ds = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int col = colb + j * 16;
+      f32x4_t is2 = f32x4_t{1.f, 1.f, 1.f, 1.f};
+      if (act == 2) {
+        const f32x4_t s2 = *reinterpret_cast<const f32x4_t*>(p.ascale + (long)g * p.sbias + col);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) is2[r] = 1.f / fmaxf(s2[r], 1e-8f);
+      }
+#pragma unroll
+      for (int i = 0; i < WI; ++i) {
+        const long row = rowb + i * 16;
+        const long frag = ((long)g * (p.M >> 4) + (row >> 4)) * (p.N >> 4) + (col >> 4);
+        const uint64_t* mk = p.cmask + frag * 4;  // wave-uniform address
+        const uint2 cv = AUX_EARLY ? auxv[i][j]
+                                   : *reinterpret_cast<const uint2*>(p.aux + (long)g * p.saux + row * p.ldaux + col);
+        const uint16_t cvs[4] = {(uint16_t)(cv.x & 0xFFFF), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xFFFF),
+                                 (uint16_t)(cv.y >> 16)};
+        f32x4_t dv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool on = (mk[r] >> lane) & 1ull;
+          const float c = bf2f(cvs[r]);
+          if (act == 1) {
+            const float sgn = c > 0.f ? 1.f : (c < 0.f ? -1.f : 0.f);
+            dv[r] = on ? acc[i][j][r] + add * sgn : 0.f;
+          } else if (act == 2) {
+            const float dc = acc[i][j][r] + add;
+            const bool ramp = c * is2[r] < 1.f;
+            dv[r] = on ? dc * (ramp ? 10.f : 1.f) : 0.f;
+            cs[r] += dv[r];
+            ds[r] += (on && ramp) ? -9.f * dc : 0.f;
+          } else {
+            dv[r] = on ? acc[i][j][r] + add : 0.f;
+            cs[r] += dv[r];
+          }
+        }
+        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
+            make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
+      }
+      colred_lane(cs, j, 0);
+      colred_lane(ds, j, 1);
+    }
+    __syncthreads();
+    colred_store(p.colpart, 0);
+    if (p.dotpart) colred_store(p.dotpart, 1);
+    return;
+  }
+  if constexpr (EPI == EPI_ROWMAX) {
+    // max over this wave's columns of each output row, then over the four 16-lane groups
+    // holding the same row; one partial per (row, wave column) -> C[g][row][tn * WGN + wc]
+    float* C = reinterpret_cast<float*>(cptr) + (long)g * p.sc;
+    const long ldp = (long)tiles_n * WGN;
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+      float mx = -3.0e38f;
+#pragma unroll
+      for (int j = 0; j < WJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, alpha * acc[i][j][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      if (lane < 16) C[(long)(rowb + i * 16) * ldp + tn * WGN + wc] = mx;
+    }
     return;
   }
   if constexpr (EPI == EPI_ADAM) {
@@ -683,7 +803,7 @@ template <class S, int BKT, int NST, bool FULL = true>
 int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
   const dim3 grid((unsigned)(n_blocks<S>(p.M, p.N, p.G, nprob) * p.ksplit)), block(S::NT);
   if constexpr (!FULL) {
-    if (epi == EPI_ADAM || epi == EPI_BF16 || (epi == EPI_F32 && (ak || bk))) return 8;
+    if (epi == EPI_ADAM || epi == EPI_BF16 || epi >= EPI_ENC_ACT || (epi == EPI_F32 && (ak || bk))) return 8;
   }
 #define SC_L(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_kernel<S, AKV, BKV, E, BKT, NST>), grid, block, 0, stream, p)
   // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
@@ -694,6 +814,15 @@ int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_
     case EPI_DEC: if (!(ak && !bk)) return 5; SC_L(true, false, EPI_DEC); break;
     case EPI_DC: if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC); break;
     case EPI_DC_MASK: if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC_MASK); break;
+    case EPI_ENC_ACT:
+      if constexpr (FULL) { if (!(ak && bk)) return 5; SC_L(true, true, EPI_ENC_ACT); }
+      break;
+    case EPI_DC_ACT:
+      if constexpr (FULL) { if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC_ACT); }
+      break;
+    case EPI_ROWMAX:
+      if constexpr (FULL) { if (!(ak && bk)) return 5; SC_L(true, true, EPI_ROWMAX); }
+      break;
     case EPI_ADAM:
       if constexpr (FULL) { if (ak || bk) return 5; SC_L(false, false, EPI_ADAM); }
       break;
@@ -761,9 +890,12 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             long saux, float* part, float* colpart, const float* l1, float l1_add_scale,
             float* dotpart, int dc_tied, const ScAdamEpi* adam /* [nprob] or null */, const float* lr,
             const int* step, float b1, float b2, float eps, int dot_tm, float dot_scale,
-            int cfg, int ksplit, long split_stride, void* cmask, hipStream_t stream) {
+            int cfg, int ksplit, long split_stride, void* cmask, int act, const float* ascale,
+            hipStream_t stream) {
   if (M % PT || N % PT || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
-  if (epi == EPI_DC_MASK && !cmask) return 4;
+  if ((epi == EPI_DC_MASK || epi == EPI_DC_ACT) && !cmask) return 4;
+  if (epi == EPI_DC_ACT && (!aux || !colpart || !l1)) return 4;
+  if ((epi == EPI_ENC_ACT || epi == EPI_DC_ACT) && (act < 0 || act > 2 || (act == 2 && !ascale))) return 4;
   if (ksplit < 1 || ksplit > (K1 + K2) / 64 || (ksplit > 1 && epi != EPI_F32 && epi != EPI_BF16)) return 7;
   GemmParams p;
   for (int i = 0; i < nprob; ++i) {
@@ -792,6 +924,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   if (epi == EPI_ADAM && (!adam || !lr || !step)) return 4;
   p.lr = lr; p.step = step; p.b1 = b1; p.b2 = b2; p.eps = eps; p.dot_tm = dot_tm; p.dot_scale = dot_scale;
   p.ksplit = ksplit; p.split_stride = split_stride;
+  p.act = act; p.ascale = ascale;
   const bool ak = layout & 1, bk = layout & 2;
   int shape = cfg & 3;
   const int pipe = (cfg >> 2) & 3;  // 0: BK64 x 2 stages, 1: BK32 x 4, 2: BK32 x 2, 3: BK32 x 3

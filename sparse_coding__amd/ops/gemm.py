@@ -18,6 +18,9 @@ import torch
 from . import _lib
 
 EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16, EPI_ADAM, EPI_ENC_CNT, EPI_DC_MASK = 0, 1, 2, 3, 4, 5, 6, 7
+EPI_ENC_ACT, EPI_DC_ACT, EPI_ROWMAX = 8, 9, 10
+# code activations of the ENC_ACT / DC_ACT epilogues
+ACT_RELU, ACT_REVERSE, ACT_THRESHOLD = 0, 1, 2
 TILE_M, TILE_N, TILE_K = 128, 128, 64
 
 # Block shapes of the kernel (BK64 x 2-stage LDS-DMA ring for all of them):
@@ -31,7 +34,7 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 # with the other's MFMA loop: enc 61 vs 84 us on 256x256), the plain fp32 weight-gradient
 # GEMM (K = B = 2048) on 256x256 blocks (65 vs 74 us) -- "auto" picks that.
 _CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 1, EPI_ENC_CNT: 1,
-                EPI_DC_MASK: 1}
+                EPI_DC_MASK: 1, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
 _CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 # cfg bits 2-3 select the K pipeline: 0 BK64 x 2-stage LDS ring (default), 1 BK32 x 4,
@@ -84,7 +87,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
             bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
             colpart=None, l1=None, l1_add_scale=0.0, dotpart=None, dc_tied=False, adam=None,
             lr=None, step=None, betas=(0.9, 0.999), eps=1e-8, dot_tm=0, dot_scale=0.0, cfg=None,
-            ksplit=1, split_stride=0, cmask=None):
+            ksplit=1, split_stride=0, cmask=None, act=0, ascale=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
@@ -100,7 +103,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
         _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1), float(l1_add_scale),
         _lib.ptr(dotpart), int(bool(dc_tied)), adam, _lib.ptr(lr), _lib.ptr(step),
         float(betas[0]), float(betas[1]), float(eps), int(dot_tm), float(dot_scale),
-        cfg, int(ksplit), int(split_stride), _lib.ptr(cmask),
+        cfg, int(ksplit), int(split_stride), _lib.ptr(cmask), int(act), _lib.ptr(ascale),
         _lib.stream_handle(),
     )
     _lib.check(rc, f"sc_gemm(epi={epi})")
@@ -120,8 +123,13 @@ def code_mask_shape(G, B, n):
     return (G, B // 16, n // 16, 4)
 
 
-def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=None):
+def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=None, act=ACT_RELU, ascale=None):
     """c[g] = relu(x[g] @ w[g]^T + bias[g]) with L1/L0 partials.
+
+    ``act`` selects another code activation of the same GEMM:
+    ``ACT_REVERSE`` c = 1[pre > 0] (pre - bias) (L1 partial = sum |c|, L0 = active count);
+    ``ACT_THRESHOLD`` c = s2 thr(pre / s2) with ``ascale`` = s2 [G, n] fp32 and ``bias``
+    the per-feature gain.
 
     x: [B, d] or [G, B, d] bf16; w: [G, n, d] bf16; bias: [G, n] fp32;
     c_out: [G, B, n] bf16; part: [G, (B/128)*(n/128), 2] fp32;
@@ -143,10 +151,15 @@ def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=No
     if mask_out is not None:
         _need(mask_out.dtype == torch.int64 and tuple(mask_out.shape) == code_mask_shape(G, B, n)
               and mask_out.is_contiguous(), "mask_out must be contiguous int64 code_mask_shape(G, B, n)")
+    if act == ACT_THRESHOLD:
+        _need(ascale is not None and tuple(ascale.shape) == (G, n) and ascale.dtype == torch.float32
+              and ascale.is_contiguous(), "threshold activation needs ascale fp32 [G, n]")
     a = [_op(x, d, sx), _op(x, d, sx)]
     b = [_op(w, d, n * d), _op(w, d, n * d)]
-    _launch(EPI_ENC_CNT if colpart is not None else EPI_ENC, 3, B, n, d, 0, G, a, b, [c_out], [1.0], n, B * n,
-            bias=bias, sbias=n, nactive=nactive, part=part, colpart=colpart, cmask=mask_out)
+    epi = EPI_ENC_ACT if act != ACT_RELU else (EPI_ENC_CNT if colpart is not None else EPI_ENC)
+    _launch(epi, 3, B, n, d, 0, G, a, b, [c_out], [1.0], n, B * n,
+            bias=bias, sbias=n, nactive=nactive, part=part, colpart=colpart, cmask=mask_out, act=act,
+            ascale=ascale)
 
 
 def decode_residual(c, w_hat, x, r_out, part):
@@ -167,7 +180,8 @@ def decode_residual(c, w_hat, x, r_out, part):
             aux=x, ldaux=d, saux=sx, part=part)
 
 
-def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, mask=None):
+def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, mask=None, act=ACT_RELU,
+              ascale=None):
     """dpre_s[g] = 1[c>0] * (r[g] @ w_hat[g]^T + l1[g] * d / 2).
 
     dpre_s is the code gradient in units of the residual: dL/dpre = 2/(B d) * dpre_s.
@@ -176,6 +190,12 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, 
     <w_hat_j, dL/dw_hat_j> (in units of 2/(B d)); ``tied_bias`` ([G, n]) adds the tied
     dictionary's encoder-path term.  ``mask`` (the encoder's ``mask_out``) replaces the
     read of ``c`` by the 16x smaller activity bitmask when no dots are requested.
+
+    With ``act`` (ACT_REVERSE / ACT_THRESHOLD, needs ``mask``): the code gradient of that
+    activation.  Reverse: dpre_s = active * (r w^T + l1 d/2 sign(c)) and zero column sums
+    (the bias gets no gradient through the codes).  Threshold (``ascale`` = s2): dpre_s =
+    active * (r w^T + l1 d/2) thr', column sums = gain gradient, and ``dotpart`` receives
+    the partials of sum_b dL/dc (thr - u thr') (x 2 s: the scale gradient).
     """
     G, B, d = r.shape
     n = w_hat.shape[1]
@@ -187,6 +207,16 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, 
     b = [_op(w_hat, d, n * d)] * 2
     if dotpart is not None:
         _need(dotpart.numel() >= G * (B // 128) * n, "dotpart too small")
+    if act != ACT_RELU:
+        _need(mask is not None and mask.dtype == torch.int64 and tuple(mask.shape) == code_mask_shape(G, B, n),
+              "activation code gradient needs the encoder's mask")
+        if act == ACT_THRESHOLD:
+            _need(ascale is not None and tuple(ascale.shape) == (G, n) and ascale.dtype == torch.float32
+                  and ascale.is_contiguous(), "threshold activation needs ascale fp32 [G, n]")
+        _launch(EPI_DC_ACT, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
+                aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0,
+                dotpart=dotpart, cmask=mask, act=act, ascale=ascale, sbias=n)
+        return
     if mask is not None and dotpart is None:
         _need(mask.dtype == torch.int64 and tuple(mask.shape) == code_mask_shape(G, B, n), "mask shape")
         _launch(EPI_DC_MASK, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
@@ -293,6 +323,36 @@ def weight_grads_adam(pairs, states, alpha, lr, step_dev, betas=(0.9, 0.999), ep
     _launch(EPI_ADAM, 0, n, d, K1, K2, G, a_ops, b_ops, [st["p"] for st in states], [alpha] * len(states),
             d, n * d, adam=eps_arr, lr=lr, step=step_dev, betas=betas, eps=eps, dot_tm=dot_tm,
             dot_scale=alpha)
+
+
+def rowmax_nt(a, b, alpha=1.0):
+    """max_j alpha <a[g, i], b[g, j]> for every row i: [G, M, K] x [G, N, K] -> [G, M] fp32.
+
+    The max-cosine-similarity reduction behind MMCS: the [M, N] similarity
+    matrix stays in registers (EPI_ROWMAX partials per 64-column wave tile, a tiny max on
+    the host side).  Any shapes: rows / columns / K are padded here (extra columns repeat
+    b's first row, so they never change a max; K is zero-padded).
+    """
+    squeeze = a.dim() == 2
+    if squeeze:
+        a, b = a.unsqueeze(0), b.unsqueeze(0)
+    G, M, K = a.shape
+    N = b.shape[1]
+    _need(b.shape[0] == G and b.shape[2] == K, f"shapes {tuple(a.shape)} x {tuple(b.shape)}")
+    Mp, Np, Kp = -(-M // 128) * 128, -(-N // 128) * 128, -(-K // 64) * 64
+    bf = torch.bfloat16
+    ap = torch.zeros(G, Mp, Kp, device=a.device, dtype=bf)
+    ap[:, :M, :K] = a
+    bp = torch.zeros(G, Np, Kp, device=a.device, dtype=bf)
+    bp[:, :N, :K] = b
+    if Np > N:
+        bp[:, N:, :K] = b[:, :1]
+    tiles = (Np // 128) * 2  # 128x128 blocks of two 64-column waves
+    part = torch.empty(G, Mp, tiles, device=a.device, dtype=torch.float32)
+    _launch(EPI_ROWMAX, 3, Mp, Np, Kp, 0, G, [_op(ap, Kp, Mp * Kp)] * 2, [_op(bp, Kp, Np * Kp)] * 2, [part],
+            [float(alpha)], tiles, Mp * tiles, cfg=1)
+    out = part.amax(dim=-1)[:, :M]
+    return out[0] if squeeze else out
 
 
 def matmul_nt(a, b, out, alpha=1.0):

@@ -30,10 +30,18 @@ from torch.utils import _pytree as pytree
 from .dist import DistInfo
 
 
+def _check_kind(engine):
+    # the threshold SAE's scale / centering gradients are reduced inside the engine's own
+    # update, not through the flat gradient buffer these wrappers all-reduce
+    if getattr(engine, "kind", None) == "threshold":
+        raise NotImplementedError("data-parallel threshold SAEs: use ensemble sharding (parallel='es')")
+
+
 class DataParallelFused:
     """Wraps a ``FusedSAEEnsemble``; identical parameters on every rank after each step."""
 
     def __init__(self, engine, info: DistInfo, grad_dtype: torch.dtype = torch.float32):
+        _check_kind(engine)
         self.engine = engine
         self.info = info
         self.grad_dtype = grad_dtype
@@ -136,6 +144,7 @@ class FusedChunk:
     """Adapter: one ``FusedSAEEnsemble`` (a chunk of the ensemble's models) as a pipeline stage."""
 
     def __init__(self, engine):
+        _check_kind(engine)
         self.engine = engine
         engine.fuse_adam = False  # gradients are reduced before Adam
 

@@ -526,3 +526,84 @@ def test_fista_gram_row_tiles_match(n, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(A1, A2)
     assert A1.abs().sum() > 0
+
+
+@pytest.mark.parametrize("kind", ["reverse", "threshold"])
+def test_fused_activation_variants_match_functional_ensemble(kind):
+    """Reverse (K10) and smooth-threshold (K11) SAEs on the fused engine vs the eager
+    autograd ensemble: losses per step and the direction of every parameter's update."""
+    from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.engine.optim import adam
+    from sparse_coding__amd.models.signatures import FunctionalReverseSAE, FunctionalThresholdingSAE
+
+    torch.manual_seed(5)
+    sig = FunctionalReverseSAE if kind == "reverse" else FunctionalThresholdingSAE
+    d, n, B = 256, 512, 256
+    models = [sig.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3, 1e-2)]
+    for p, _ in models:
+        if kind == "reverse":
+            p["encoder_bias"].uniform_(-0.2, 0.2)
+        else:
+            p["activation_scale"].uniform_(0.7, 1.3)
+            p["activation_gain"].uniform_(-0.2, 0.4)
+            p["centering"].normal_(0.0, 0.05)
+    ref = FunctionalEnsemble([({k: v.clone() for k, v in p.items()}, b) for p, b in models], sig, adam,
+                             {"lr": 1e-3}, device=DEV)
+    fused = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=DEV)
+    assert fused.kind == kind
+    feats = torch.nn.functional.normalize(torch.randn(1024, d, device=DEV), dim=-1)
+    for step in range(5):
+        codes = torch.relu(torch.randn(B, 1024, device=DEV) - 1.5) * 3.0
+        x = (codes @ feats).to(torch.bfloat16)
+        loss_ref, _ = ref.step_batch(x.float())
+        out = fused.step_batch(x)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(out[:, 1], loss_ref["l_reconstruction"], rtol=3e-2, atol=1e-4)
+        torch.testing.assert_close(out[:, 2], loss_ref["l_l1"], rtol=5e-2, atol=1e-5)
+        assert float(out[:, 4].min()) > 0.5, "codes must be active for the test to mean anything"
+    for k, v in fused.params.items():
+        init = torch.stack([m[0][k] for m in models]).to(DEV)
+        mv_f, mv_r = (v - init).flatten(), (ref.params[k] - init).flatten()
+        if mv_r.abs().max() == 0:  # reverse SAE bias: no gradient through the codes, no decay
+            assert mv_f.abs().max() == 0, k
+            continue
+        cos = torch.nn.functional.cosine_similarity(mv_f, mv_r, dim=0).item()
+        rel = ((mv_f - mv_r).abs().mean() / mv_r.abs().mean()).item()
+        assert cos > 0.95 and rel < 0.25, (k, cos, rel)
+    # evaluate() uses the same epilogues
+    fvu, l0 = fused.evaluate(x)
+    for g, ld in enumerate(fused.to_learned_dicts(DEV)):
+        xf = x.float()
+        x_hat = ld.predict(xf)
+        f_ref = float((x_hat - xf).pow(2).sum() / (xf - xf.mean(0)).pow(2).sum())
+        assert abs(float(fvu[g]) - f_ref) < 0.02 + 0.03 * f_ref, (g, float(fvu[g]), f_ref)
+
+
+@pytest.mark.parametrize("G,M,N,K", [(1, 128, 128, 64), (3, 300, 517, 200), (2, 1024, 256, 512)])
+def test_rowmax_nt_matches_torch(G, M, N, K):
+    """EPI_ROWMAX (max cosine similarity, K20) against a torch fp32 max over A B^T."""
+    from sparse_coding__amd.ops import gemm
+
+    a = torch.nn.functional.normalize(torch.randn(G, M, K, device=DEV), dim=-1).to(torch.bfloat16)
+    b = torch.nn.functional.normalize(torch.randn(G, N, K, device=DEV), dim=-1).to(torch.bfloat16)
+    ref = torch.bmm(a.float(), b.float().transpose(1, 2)).amax(-1)
+    got = gemm.rowmax_nt(a, b)
+    assert got.shape == (G, M)
+    torch.testing.assert_close(got, ref, rtol=1e-3, atol=1e-3)
+    got2 = gemm.rowmax_nt(a[0], b[0], alpha=-1.0)  # 2-D form; alpha flips to a row min
+    torch.testing.assert_close(got2, -torch.mm(a[0].float(), b[0].float().T).amin(-1), rtol=1e-3, atol=1e-3)
+
+
+def test_mmcs_fused_path_matches_fp32():
+    from sparse_coding__amd.eval import metrics
+    from sparse_coding__amd.models.learned_dict import UntiedSAE
+
+    torch.manual_seed(2)
+    d = 512
+    lds = [UntiedSAE(torch.randn(4096, d, device=DEV), torch.randn(4096, d, device=DEV),
+                     torch.zeros(4096, device=DEV)) for _ in range(2)]
+    exact = metrics.max_cosine(lds[0].get_learned_dict(), lds[1].get_learned_dict(), fused=False)
+    fused = metrics.max_cosine(lds[0].get_learned_dict(), lds[1].get_learned_dict(), fused=True)
+    torch.testing.assert_close(fused, exact, rtol=0, atol=6e-3)
+    assert abs(float(metrics.mmcs(lds[0], lds[1])) - float(exact.mean())) < 2e-3
