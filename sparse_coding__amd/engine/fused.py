@@ -54,6 +54,13 @@ class FusedSAEEnsemble:
                  count_every: int = 8, wgrad_split="auto"):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
+        # FunctionalTiedCenteredSAE (sae_ensemble.py:162-228): the tied kernels on x - center
+        # with a learned center vector (updated by a small extra Adam step)
+        self.learned_center = self.kind == "tied_centered"
+        if self.learned_center:
+            self.kind = "tied"
+            if fuse_adam:
+                raise ValueError("fuse_adam is not implemented for learned-centering SAEs")
         if self.kind not in _ACTS:
             raise ValueError(f"signature {sig} has no fused implementation")
         # code activation of the encoder / code-gradient epilogues: reverse and threshold
@@ -106,6 +113,8 @@ class FusedSAEEnsemble:
             # learned per-feature scale s (codes scale with s^2) and input centering vector
             self.params["activation_scale"] = _stack(models, "activation_scale", 0, dev)
             self.params["centering"] = _stack(models, "centering", 0, dev)
+        if self.learned_center:
+            self.params["center"] = _stack(models, "center", 0, dev)
         self.m = {k: torch.zeros_like(v) for k, v in self.params.items()}
         self.v = {k: torch.zeros_like(v) for k, v in self.params.items()}
         # ----- per-model hyper-parameters as device vectors
@@ -183,10 +192,10 @@ class FusedSAEEnsemble:
         self.sqpart = torch.zeros(G, n, d // 128, device=dev)   # updated-row |w|^2 partials
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)  # graph input buffer
         self._static_inputs = [self.x_static]
-        if self.centering is not None or self.kind == "threshold":
+        if self.centering is not None or self.kind == "threshold" or self.learned_center:
             self._xr = torch.empty(G, B, d, device=dev)              # x R^T (fp32)
             self.x_c = torch.empty(G, B, d, device=dev, dtype=bf)    # centred input per model
-        if self.kind == "threshold":
+        if self.kind == "threshold" or self.learned_center:
             self.s2 = torch.empty(G, n, device=dev)                  # s^2 read by the epilogues
             self._gsum = torch.empty(G, n, device=dev)
 
@@ -206,6 +215,10 @@ class FusedSAEEnsemble:
             torch.sub(x.unsqueeze(0), self.params["centering"].unsqueeze(1), out=self._xr)
             self.x_c.copy_(self._xr)
             torch.mul(self.params["activation_scale"], self.params["activation_scale"], out=self.s2)
+            return self.x_c
+        if self.learned_center:
+            torch.sub(x.unsqueeze(0), self.params["center"].unsqueeze(1), out=self._xr)
+            self.x_c.copy_(self._xr)
             return self.x_c
         if self.centering is None:
             return x
@@ -349,26 +362,38 @@ class FusedSAEEnsemble:
         if not self.fuse_adam:  # with fuse_adam the weights were already updated in wgrad_adam
             adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
                                step_dev=self.step_dev, **self._adam_split_kw())
-        if self.kind == "threshold":
+        if self.kind == "threshold" or self.learned_center:
             self._threshold_extra_adam()
         self._bias_loss(update=True, reduced=False)
 
     def _threshold_extra_adam(self):
         """Scale and centering of the threshold SAE (small vectors; before the bias / loss
         kernel, which advances the device step counter):
-        dL/ds = 2 s alpha sum(dotpart), dL/dcentering = -alpha (sum_b dL/dpre) W_hat."""
+        dL/ds = 2 s alpha sum(dotpart), dL/dcentering = -alpha (sum_b dL/dpre) W_hat.
+        Learned-centering tied SAEs also reconstruct x - center, so their center gradient
+        gains the direct residual term + alpha sum_b R."""
         a = self._alpha
-        s = self.params["activation_scale"]
-        torch.sum(self.dotpart, dim=1, out=self._gsum)
-        g_s = self._gsum * s * (2.0 * a)
         torch.sum(self.colpart, dim=1, out=self._gsum)
-        g_c = torch.bmm(self._gsum.unsqueeze(1).to(torch.bfloat16), self.enc_shadow).squeeze(1).float() * (-a)
+        if self.learned_center:
+            # the two terms largely cancel (the residual's component outside the active
+            # atoms' span survives): keep the column sums in fp32
+            g_c = torch.bmm(self._gsum.unsqueeze(1), self.enc_shadow.float()).squeeze(1) * (-a)
+            g_c += self.r.float().sum(dim=1) * a
+        else:
+            g_c = torch.bmm(self._gsum.unsqueeze(1).to(torch.bfloat16), self.enc_shadow).squeeze(1).float() * (-a)
+        if self.learned_center:
+            upd = (("center", g_c),)
+        else:
+            s = self.params["activation_scale"]
+            torch.sum(self.dotpart, dim=1, out=self._gsum)
+            g_s = self._gsum * s * (2.0 * a)
+            upd = (("activation_scale", g_s), ("centering", g_c))
         t = self.step_dev.float() + 1.0
         b1, b2 = self.betas
         bc1 = 1.0 - torch.pow(b1, t)
         bc2 = 1.0 - torch.pow(b2, t)
         lr = self.lr.unsqueeze(1)
-        for k, g in (("activation_scale", g_s), ("centering", g_c)):
+        for k, g in upd:
             p, m, v = self.params[k], self.m[k], self.v[k]
             m.mul_(b1).add_(g, alpha=1.0 - b1)
             v.mul_(b2).addcmul_(g, g, value=1.0 - b2)

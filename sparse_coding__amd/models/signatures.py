@@ -168,7 +168,10 @@ class FunctionalTiedSAE(DictSignature):
 
 
 class FunctionalTiedCenteredSAE(DictSignature):
-    """Tied SAE with a *learned* centering vector (reference sae_ensemble.py:162-228)."""
+    """Tied SAE with a *learned* centering vector (reference sae_ensemble.py:162-228).
+    Fused engine: ``FusedSAEEnsemble`` kind "tied_centered" (tied kernels on x - center)."""
+
+    fused_kind = "tied_centered"
 
     @staticmethod
     def init(activation_size, n_dict_components, l1_alpha, center=None, device=None, dtype=None):

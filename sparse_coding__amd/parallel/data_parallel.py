@@ -33,7 +33,7 @@ from .dist import DistInfo
 def _check_kind(engine):
     # the threshold SAE's scale / centering gradients are reduced inside the engine's own
     # update, not through the flat gradient buffer these wrappers all-reduce
-    if getattr(engine, "kind", None) == "threshold":
+    if getattr(engine, "kind", None) == "threshold" or getattr(engine, "learned_center", False):
         raise NotImplementedError("data-parallel threshold SAEs: use ensemble sharding (parallel='es')")
 
 

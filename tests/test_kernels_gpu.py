@@ -528,22 +528,30 @@ def test_fista_gram_row_tiles_match(n, monkeypatch):
     assert A1.abs().sum() > 0
 
 
-@pytest.mark.parametrize("kind", ["reverse", "threshold"])
+@pytest.mark.parametrize("kind", ["reverse", "threshold", "tied_centered"])
 def test_fused_activation_variants_match_functional_ensemble(kind):
-    """Reverse (K10) and smooth-threshold (K11) SAEs on the fused engine vs the eager
-    autograd ensemble: losses per step and the direction of every parameter's update."""
+    """Reverse (K10), smooth-threshold (K11) and learned-centering tied (C8) SAEs on the
+    fused engine vs the eager autograd ensemble: losses per step and the direction of
+    every parameter's update."""
     from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
     from sparse_coding__amd.engine.fused import FusedSAEEnsemble
     from sparse_coding__amd.engine.optim import adam
-    from sparse_coding__amd.models.signatures import FunctionalReverseSAE, FunctionalThresholdingSAE
+    from sparse_coding__amd.models.signatures import (FunctionalReverseSAE, FunctionalThresholdingSAE,
+                                                      FunctionalTiedCenteredSAE)
 
     torch.manual_seed(5)
-    sig = FunctionalReverseSAE if kind == "reverse" else FunctionalThresholdingSAE
+    sig = {"reverse": FunctionalReverseSAE, "threshold": FunctionalThresholdingSAE,
+           "tied_centered": FunctionalTiedCenteredSAE}[kind]
     d, n, B = 256, 512, 256
     models = [sig.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3, 1e-2)]
     for p, _ in models:
         if kind == "reverse":
             p["encoder_bias"].uniform_(-0.2, 0.2)
+        elif kind == "tied_centered":
+            # sparse codes: with ~half the 512 atoms active their span covers all of d = 256
+            # and the two terms of the center gradient cancel to bf16 noise
+            p["encoder_bias"].uniform_(-1.2, -0.8)
+            p["center"].normal_(0.0, 0.3)
         else:
             p["activation_scale"].uniform_(0.7, 1.3)
             p["activation_gain"].uniform_(-0.2, 0.4)
@@ -551,7 +559,8 @@ def test_fused_activation_variants_match_functional_ensemble(kind):
     ref = FunctionalEnsemble([({k: v.clone() for k, v in p.items()}, b) for p, b in models], sig, adam,
                              {"lr": 1e-3}, device=DEV)
     fused = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=DEV)
-    assert fused.kind == kind
+    assert fused.kind == ("tied" if kind == "tied_centered" else kind)
+    assert fused.learned_center == (kind == "tied_centered")
     feats = torch.nn.functional.normalize(torch.randn(1024, d, device=DEV), dim=-1)
     for step in range(5):
         codes = torch.relu(torch.randn(B, 1024, device=DEV) - 1.5) * 3.0
@@ -570,6 +579,7 @@ def test_fused_activation_variants_match_functional_ensemble(kind):
             continue
         cos = torch.nn.functional.cosine_similarity(mv_f, mv_r, dim=0).item()
         rel = ((mv_f - mv_r).abs().mean() / mv_r.abs().mean()).item()
+        print(kind, k, "cos", round(cos, 4), "rel", round(rel, 4))
         assert cos > 0.95 and rel < 0.25, (k, cos, rel)
     # evaluate() uses the same epilogues
     fvu, l0 = fused.evaluate(x)
