@@ -325,7 +325,7 @@ def weight_grads_adam(pairs, states, alpha, lr, step_dev, betas=(0.9, 0.999), ep
             dot_scale=alpha)
 
 
-def rowmax_nt(a, b, alpha=1.0):
+def rowmax_nt(a, b, alpha=1.0, cfg=None):
     """max_j alpha <a[g, i], b[g, j]> for every row i: [G, M, K] x [G, N, K] -> [G, M] fp32.
 
     The max-cosine-similarity reduction behind MMCS: the [M, N] similarity
@@ -339,7 +339,12 @@ def rowmax_nt(a, b, alpha=1.0):
     G, M, K = a.shape
     N = b.shape[1]
     _need(b.shape[0] == G and b.shape[2] == K, f"shapes {tuple(a.shape)} x {tuple(b.shape)}")
-    Mp, Np, Kp = -(-M // 128) * 128, -(-N // 128) * 128, -(-K // 64) * 64
+    # 256x256 blocks (128x64 per wave) from 16M similarity entries on: 0.29 vs 0.37 ms at
+    # 16k x 16k x 512, 3.72 vs 4.65 ms at 32k x 32k x 2048 (profiles/mmcs_bench_r1.jsonl)
+    if cfg is None:
+        cfg = 3 if M * N >= (1 << 24) else 1
+    blk = 256 if cfg == 3 else 128
+    Mp, Np, Kp = -(-M // blk) * blk, -(-N // blk) * blk, -(-K // 64) * 64
     bf = torch.bfloat16
     ap = torch.zeros(G, Mp, Kp, device=a.device, dtype=bf)
     ap[:, :M, :K] = a
@@ -350,7 +355,7 @@ def rowmax_nt(a, b, alpha=1.0):
     tiles = (Np // 128) * 2  # 128x128 blocks of two 64-column waves
     part = torch.empty(G, Mp, tiles, device=a.device, dtype=torch.float32)
     _launch(EPI_ROWMAX, 3, Mp, Np, Kp, 0, G, [_op(ap, Kp, Mp * Kp)] * 2, [_op(bp, Kp, Np * Kp)] * 2, [part],
-            [float(alpha)], tiles, Mp * tiles, cfg=1)
+            [float(alpha)], tiles, Mp * tiles, cfg=cfg)
     out = part.amax(dim=-1)[:, :M]
     return out[0] if squeeze else out
 

@@ -617,3 +617,16 @@ def test_mmcs_fused_path_matches_fp32():
     fused = metrics.max_cosine(lds[0].get_learned_dict(), lds[1].get_learned_dict(), fused=True)
     torch.testing.assert_close(fused, exact, rtol=0, atol=6e-3)
     assert abs(float(metrics.mmcs(lds[0], lds[1])) - float(exact.mean())) < 2e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 517, 200), (4096, 4100, 512)])
+def test_rowmax_nt_256_blocks(M, N, K):
+    """The 256x256-block EPI_ROWMAX path (padding to 256; auto-selected from 16M entries)."""
+    from sparse_coding__amd.ops import gemm
+
+    torch.manual_seed(3)
+    a = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
+    b = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
+    ref = torch.mm(a.float(), b.float().T).amax(-1)
+    torch.testing.assert_close(gemm.rowmax_nt(a, b, cfg=3), ref, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(gemm.rowmax_nt(a, b), ref, rtol=1e-3, atol=1e-3)
