@@ -6,8 +6,18 @@ with fp32 master weights and fp32 Adam, trained on synthetic Pythia-70m-shaped
 activations (sparse mixture of 4096 unit-norm features, held in an HBM ring
 buffer; no network, so no real harvest).  Every timed step does the full work:
 device-side random batch gather, encoder/decoder forward, backward, Adam on all
-8 models.  With N > 1 GPUs it is data parallel (per-GPU batch fixed, i.e. weak
-scaling) with RCCL gradient all-reduce overlapped with the encoder wgrad/Adam.
+8 models (one HIP graph per step on one GPU).
+
+N > 1 GPUs (weak scaling: 2048 rows per GPU per step), ``--parallelism``:
+  es  (default) ensemble-axis sharding: rank r owns models [r G/N, (r+1) G/N) and trains
+      them on the all-gathered global batch -- per model the same update as data parallel
+      on the global batch, but 2 MB of batch cross xGMI per step instead of 67 MB of
+      gradients;
+  dp  data parallel: every rank holds all 8 models, gradients are all-reduced (RCCL over
+      xGMI) in model chunks overlapped with the next chunk's compute (BASELINE config 3's
+      mechanism).
+The run times the other strategy too (untimed for the headline) and reports it under
+``alt_parallelism`` in the JSON line.
 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N bench.py --gpus N ...
@@ -30,6 +40,10 @@ import torch
 # vmap(grad)+Adam) -- the only measured throughput for this exact config (no GPU number
 # is published, BASELINE.json "published": {}).
 BASELINE_ACT_PER_S = 1.86e3
+# This repo's PyTorch-eager engine (FunctionalEnsemble: torch.func vmap(grad(loss)) + vmapped
+# Adam, fp32, the reference's algorithm) on ONE MI355X at the same config
+# (profiles/bench_eager_r2.json); None until measured.
+EAGER_SAME_BOX_ACT_PER_S = None
 METRIC = "activations/sec (ensemble train) + FVU@L0, Pythia-70m resid SAE at 1/2/4/8 GPU"
 
 
@@ -72,6 +86,9 @@ def parse(argv=None):
                     help="create the process group even at N=1 and run the N>1 code path (rehearses the "
                          "sharded step with real RCCL collectives on a one-GPU box)")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--compare-parallelism", type=int, default=1,
+                    help="N>1: after the headline run, also time the other strategy (es <-> dp) and report it "
+                         "under alt_parallelism")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of a HIP graph")
     return ap.parse_args(argv)
 
@@ -97,9 +114,87 @@ def fvu_l0(dicts, x):
     return [(float(mean_l0(ld, x)), float(fraction_variance_unexplained(ld, x))) for ld in dicts]
 
 
+class Runner:
+    """One training configuration: ``step()`` (one full optimizer step on a fresh device batch),
+    ``finish()`` (complete cross-step work), ``dicts()`` (LearnedDicts), ``close()``."""
+
+    def __init__(self, step, dicts, finish=None, close=None):
+        self.step, self.dicts = step, dicts
+        self.finish = finish or (lambda: None)
+        self.close = close or (lambda: None)
+
+
+def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
+    B = args.batch
+    distributed = info.world_size > 1 or args.force_dist
+    if args.engine == "fused" and par == "es":
+        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+        from sparse_coding__amd.parallel.ensemble_shard import EnsembleSharded
+
+        es = EnsembleSharded(models, lambda m, bs: FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=bs, device=device),
+                             info, batch_per_rank=B, d=args.d)
+        if not args.no_graph:
+            es.enable_graph()
+        metas = [b for _, b in models]
+
+        def sample(out):
+            return ring.sample_shard(B, info.rank, info.world_size, out=out)
+
+        return Runner(lambda: es.step_sampled(sample), lambda: es.to_learned_dicts(metas, sig, device),
+                      close=es.flush)
+    if args.engine == "fused" and distributed:
+        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+        from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
+
+        engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device)
+                   for m in split_models(models, args.dp_chunks)]
+        # cross-step: the last chunk's all-reduce overlaps the next step's first (encoder) GEMMs
+        trainer = ChunkedDataParallel([FusedChunk(e) for e in engines], info, grad_dtype, cross_step=True)
+        xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
+        return Runner(lambda: trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf)),
+                      lambda: [ld for e in engines for ld in e.to_learned_dicts(device)],
+                      finish=trainer.flush, close=trainer.flush)
+    if args.engine == "fused":
+        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+
+        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
+        if not args.no_graph:
+            eng.enable_graph()  # whole step = one HIP graph replay
+
+        def step():
+            ring.sample_shard(B, 0, 1, out=eng.x_static)
+            eng.step_static() if not args.no_graph else eng.step_batch(eng.x_static)
+
+        return Runner(step, lambda: eng.to_learned_dicts(device))
+    from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
+    from sparse_coding__amd.engine.optim import adam
+    from sparse_coding__amd.parallel.data_parallel import DataParallelEnsemble
+
+    ens = FunctionalEnsemble(models, sig, adam, {"lr": 1e-3}, device=device)
+    trainer = DataParallelEnsemble(ens, info)
+    return Runner(lambda: trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size).float()),
+                  lambda: ens.to_learned_dicts(device))
+
+
+def timed(runner, steps, info, B):
+    """Exactly ``steps`` steps between barrier + synchronize on both sides; max over ranks."""
+    from sparse_coding__amd.parallel.dist import all_reduce_max, barrier
+
+    barrier(info)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        runner.step()
+    runner.finish()  # work the last timed step still has in flight (cross-step pipelining)
+    torch.cuda.synchronize()
+    barrier(info)
+    elapsed = all_reduce_max(time.perf_counter() - t0, info)
+    return 1e3 * elapsed / steps, B * info.world_size * steps / elapsed
+
+
 def main(argv=None):
     args = parse(argv)
-    from sparse_coding__amd.parallel.dist import all_reduce_max, barrier, init_distributed, shutdown
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
 
     info = init_distributed(None if args.dist_backend == "auto" else args.dist_backend,
                             device="cuda:0" if args.shared_gpu else None, force=args.force_dist)
@@ -118,115 +213,47 @@ def main(argv=None):
     B = args.batch
 
     grad_dtype = torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32
-
-    def finish():
-        return None
-
+    distributed = info.world_size > 1 or args.force_dist
     par = args.parallelism
     if par == "auto":
-        par = "es" if (info.world_size > 1 and args.models % info.world_size == 0) else "dp"
-    if args.force_dist and args.parallelism == "auto":
-        par = "es"
-    if info.world_size == 1 and not args.force_dist:
-        par = "dp"
-    if args.engine == "fused" and par == "es":
-        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
-        from sparse_coding__amd.parallel.ensemble_shard import EnsembleSharded
+        # N > 1: ensemble-axis sharding (per model identical to data parallel on the global batch;
+        # moves the 2 MB batch instead of 67 MB of gradients per step)
+        par = "es" if (distributed and args.models % info.world_size == 0) else "dp"
+    if not distributed:
+        par = "dp"  # one GPU: the plain fused step (no collectives)
 
-        es = EnsembleSharded(models, lambda m, bs: FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=bs, device=device),
-                             info, batch_per_rank=B, d=args.d)
-        if not args.no_graph:
-            es.enable_graph()
-        metas = [b for _, b in models]
-
-        def sample(out):
-            return ring.sample_shard(B, info.rank, info.world_size, out=out)
-
-        def step():
-            es.step_sampled(sample)
-
-        def dicts():
-            return es.to_learned_dicts(metas, sig, device)
-    elif args.engine == "fused" and (info.world_size > 1 or args.force_dist):
-        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
-        from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
-
-        engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device)
-                   for m in split_models(models, args.dp_chunks)]
-        # cross-step: the last chunk's all-reduce overlaps the next step's first (encoder) GEMMs
-        trainer = ChunkedDataParallel([FusedChunk(e) for e in engines], info, grad_dtype, cross_step=True)
-        xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
-
-        def step():
-            trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf))
-
-        finish = trainer.flush
-
-        def dicts():
-            return [ld for e in engines for ld in e.to_learned_dicts(device)]
-    elif args.engine == "fused":
-        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
-        from sparse_coding__amd.parallel.data_parallel import DataParallelFused
-
-        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
-        trainer = DataParallelFused(eng, info, grad_dtype)
-        if info.world_size == 1 and not args.no_graph:
-            eng.enable_graph()  # whole step = one HIP graph replay
-
-            def step():
-                ring.sample_shard(B, 0, 1, out=eng.x_static)
-                eng.step_static()
-        else:
-            xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
-
-            def step():
-                trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf))
-
-        def dicts():
-            return eng.to_learned_dicts(device)
-    else:
-        from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
-        from sparse_coding__amd.engine.optim import adam
-        from sparse_coding__amd.parallel.data_parallel import DataParallelEnsemble
-
-        ens = FunctionalEnsemble(models, sig, adam, {"lr": 1e-3}, device=device)
-        trainer = DataParallelEnsemble(ens, info)
-
-        def step():
-            trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size).float())
-
-        def dicts():
-            return ens.to_learned_dicts(device)
-
+    runner = make_runner(par, args, info, sig, models, ring, device, grad_dtype)
     for _ in range(args.warmup):
-        step()
-    barrier(info)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    finish()  # work the last timed step still has in flight (cross-step pipelining)
-    torch.cuda.synchronize()
-    barrier(info)
-    elapsed = time.perf_counter() - t0
-    elapsed = all_reduce_max(elapsed, info)
-    ms = 1e3 * elapsed / args.steps
-    total_rows = B * info.world_size * args.steps
-    value = total_rows / elapsed
+        runner.step()
+    ms, value = timed(runner, args.steps, info, B)
 
     quality = None
     trained = args.warmup + args.steps
     if not args.no_eval:
         while trained < args.quality_steps:  # untimed: train on toward convergence before evaluating
-            step()
+            runner.step()
             trained += 1
-        finish()
+        runner.finish()
         torch.cuda.synchronize()
-        lds = dicts()  # collective in the sharded mode: every rank takes part
+        lds = runner.dicts()  # collective in the sharded mode: every rank takes part
         if info.is_main:
             quality = fvu_l0(lds, held_out.float())
-    if par == "es":
-        es.flush()
+    runner.close()
+
+    # N > 1: also time the other multi-GPU strategy on the same models (untimed for the
+    # headline; reported under "alt_parallelism" so both the gradient all-reduce path --
+    # BASELINE config 3's mechanism -- and the ensemble-sharded path are on record)
+    alt = None
+    if distributed and args.compare_parallelism and args.models % info.world_size == 0:
+        other = "dp" if par == "es" else "es"
+        alt_models = [sig.init(args.d, n, float(l1), device=device) for l1 in l1s]
+        alt_runner = make_runner(other, args, info, sig, alt_models, ring, device, grad_dtype)
+        for _ in range(args.warmup):
+            alt_runner.step()
+        a_ms, a_value = timed(alt_runner, args.steps, info, B)
+        alt_runner.close()
+        alt = {"parallelism": f"{other}{info.world_size}", "value": round(a_value, 1), "ms_per_step": round(a_ms, 4),
+               "dp_chunks": args.dp_chunks if other == "dp" else None}
 
     if info.is_main:
         rec = {
@@ -251,13 +278,20 @@ def main(argv=None):
                 "per_gpu_batch": B,
                 "parallelism": f"{par}{info.world_size}",
                 "engine": args.engine,
-                "dp_chunks": args.dp_chunks if par == "dp" and info.world_size > 1 else None,
+                "dp_chunks": args.dp_chunks if par == "dp" and distributed else None,
                 "grad_allreduce_dtype": args.grad_dtype,
             },
             "model_activations_per_s": round(value * args.models, 1),
             "baseline_note": "vs_baseline divides by BASELINE.md row 12 (reference math, same shapes, "
-                             "1.86k act/s); no published GPU throughput exists",
+                             "1.86k act/s, 8-vCPU sandbox); no published GPU throughput exists.  "
+                             "vs_eager_same_box divides by this repo's PyTorch-eager vmap(grad)+Adam "
+                             "engine on the same MI355X (profiles/bench_eager_r2.json)",
+            "vs_eager_same_box": round(value / (EAGER_SAME_BOX_ACT_PER_S * info.world_size), 2)
+            if EAGER_SAME_BOX_ACT_PER_S and args.engine == "fused" and args.d == 512 and args.ratio == 4
+            and args.models == 8 and B == 2048 else None,
         }
+        if alt is not None:
+            rec["alt_parallelism"] = alt
         if quality is not None:
             rec["fvu_at_l0"] = [{"l1": float(l), "l0": round(a, 2), "fvu": round(b, 4)}
                                 for l, (a, b) in zip(l1s, quality)]

@@ -1,5 +1,5 @@
 """Runs each kernel of the fused SAE step (config 2 shapes) a few times, plus the top-k
-select of config 4, for rocprofv3 counter collection (scripts/gpu_pmc2.sh)."""
+select of config 4, for rocprofv3 counter collection (scripts/gpu.sh pmc)."""
 import os
 import sys
 

@@ -142,6 +142,9 @@ class FusedSAEEnsemble:
         # activity bitmask of c written by the encoder epilogue, read by the code-gradient
         # epilogue instead of c itself (1/16 of the bytes)
         self.cmask = torch.empty(gemm_ops.code_mask_shape(G, B, n), device=dev, dtype=torch.int64)
+        # threshold SAEs: second bitmask, 1 on the activation's ramp (decided on the fp32
+        # pre-activation in the encoder epilogue, read by the code gradient)
+        self.cmask2 = torch.empty_like(self.cmask) if self.kind == "threshold" else None
         # gradient buffers; the last-produced weight gradient shares one flat buffer with the
         # reduced bias gradient so data-parallel runs all-reduce both with a single collective
         if self.kind == "untied":
@@ -198,6 +201,9 @@ class FusedSAEEnsemble:
         if self.kind == "threshold" or self.learned_center:
             self.s2 = torch.empty(G, n, device=dev)                  # s^2 read by the epilogues
             self._gsum = torch.empty(G, n, device=dev)
+        # learned centering: fp32 column sums of the residual from the decoder epilogue (the
+        # center gradient's direct term, taken before the bf16 rounding of R)
+        self.rcol = torch.zeros(G, tm, d, device=dev) if self.learned_center else None
 
     # ------------------------------------------------------------------ helpers
     def refresh_shadows(self):
@@ -251,12 +257,13 @@ class FusedSAEEnsemble:
         ascale = self.s2 if self.kind == "threshold" else None
         gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part,
                              self.cnt_part if count else None, self.nactive, mask_out=self.cmask,
-                             act=self.act, ascale=ascale)
-        gemm_ops.decode_residual(self.c, self.dec_shadow, x if target is None else target, self.r, self.dec_part)
+                             act=self.act, ascale=ascale, mask2_out=self.cmask2)
+        gemm_ops.decode_residual(self.c, self.dec_shadow, x if target is None else target, self.r, self.dec_part,
+                                 rcol=self.rcol)
         if self.act:
             gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                                dotpart=self.dotpart if self.kind == "threshold" else None, mask=self.cmask,
-                               act=self.act, ascale=ascale)
+                               act=self.act, ascale=ascale, mask2=self.cmask2)
             return
         gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                            dotpart=self.dotpart if self.fuse_adam else None,
@@ -375,10 +382,12 @@ class FusedSAEEnsemble:
         a = self._alpha
         torch.sum(self.colpart, dim=1, out=self._gsum)
         if self.learned_center:
-            # the two terms largely cancel (the residual's component outside the active
-            # atoms' span survives): keep the column sums in fp32
-            g_c = torch.bmm(self._gsum.unsqueeze(1), self.enc_shadow.float()).squeeze(1) * (-a)
-            g_c += self.r.float().sum(dim=1) * a
+            # the two terms largely cancel (dense codes: the residual's component outside the
+            # active atoms' span survives), so both come from fp32 data: the decoder epilogue's
+            # fp32 column sums of R (before its bf16 rounding) and the fp32 normalised masters
+            w_hat = self.params["encoder"] / self.norms.unsqueeze(-1)
+            g_c = torch.bmm(self._gsum.unsqueeze(1), w_hat).squeeze(1) * (-a)
+            g_c += self.rcol.sum(dim=1) * a
         else:
             g_c = torch.bmm(self._gsum.unsqueeze(1).to(torch.bfloat16), self.enc_shadow).squeeze(1).float() * (-a)
         if self.learned_center:

@@ -78,7 +78,9 @@ class FusedTopKEnsemble:
         scores = torch.empty(self.n_models, x.shape[0], self.n, device=self.device)
         gemm_ops.matmul_nt(xb, self.shadow, scores)
         idx, val = topk_ops.topk_select(scores, self.k, self.kmax)
-        return torch.zeros_like(scores).scatter_(-1, idx.long(), val)
+        # slots >= k[g] are padded with (index 0, value 0): scatter_add keeps a real pick of
+        # feature 0 intact (real indices are unique, the padded values add 0)
+        return torch.zeros_like(scores).scatter_add_(-1, idx.long(), val)
 
     def unstack(self, device="cpu"):
         return [({"dict": self.params["dict"][i].detach().to(device).clone()},

@@ -212,8 +212,11 @@ class EnsembleTrainer:
         return list(zip(lds, self.hyperparams(ensemble_hyperparams, buffer_hyperparams)))
 
     def losses_host(self) -> List[Dict[str, float]]:
+        """Per-model loss dicts of the last step.  Under ensemble sharding only this rank's
+        models (``self.local``) have losses here, matching ``hyperparams(local=True)``."""
         host = {k: v.detach().float().cpu() for k, v in self.last_losses.items() if torch.is_tensor(v)}
-        return [{k: float(v[i]) for k, v in host.items()} for i in range(self.n_models)]
+        count = (self.local.stop - self.local.start) if self.es is not None else self.n_models
+        return [{k: float(v[i]) for k, v in host.items()} for i in range(count)]
 
     def state_dict(self) -> Dict[str, Any]:
         st = {"kind": self.kind, "steps": self.steps, "name": self.name, "args": self.args}

@@ -40,209 +40,9 @@
 // gfx950 transposing read ds_read_b64_tr_b16, so c^T R style products need no
 // transposed copies in HBM.  Both LDS images are XOR-swizzled to avoid bank
 // conflicts.
-#include "common.h"
+#include "gemm_tiles.h"
 
 namespace scamd {
-
-template <int WGM_, int WGN_, int WI_, int WJ_>
-struct Shape {
-  static constexpr int WGM = WGM_, WGN = WGN_, WI = WI_, WJ = WJ_;
-  static constexpr int NW = WGM * WGN, NT = NW * 64;
-  static constexpr int BM = WGM * WI * 16, BN = WGN * WJ * 16;
-};
-using S128 = Shape<2, 2, 4, 4>;
-using S256x128 = Shape<2, 2, 8, 4>;
-using S256 = Shape<2, 4, 8, 4>;
-// Partial-sum buffers (scalar parts, column parts, row-dot parts, squared-norm
-// parts) are laid out on a 128x128 sub-tile grid whatever the block shape, so the
-// consumers (loss / bias / Adam kernels) do not depend on the GEMM configuration.
-constexpr int PT = 128;
-
-enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5, EPI_ENC_CNT = 6,
-       EPI_DC_MASK = 7, EPI_ENC_ACT = 8, EPI_DC_ACT = 9, EPI_ROWMAX = 10 };
-
-// Activity bitmask of the codes, in MFMA-fragment order: for the 16x16 output fragment at
-// (row/16, col/16) the encoder epilogue stores its four wave ballots (bit l of word r: lane
-// l's value r, i.e. output row 16 i + (l & 15), column 16 j + 4 (l >> 4) + r, is > 0).  The
-// code-gradient epilogue only needs 1[c > 0]: reading these 32 bytes per fragment instead
-// of the bf16 codes (512 bytes) removes B n G x 2 bytes of HBM reads per step.
-// Layout [G][B/16][n/16][4] uint64; every GEMM block shape uses the same fragment map.
-
-struct Operand {
-  const uint16_t* ptr;
-  long ld;  // leading dimension (elements)
-  long sg;  // stride between groups (elements); 0 = shared by all groups
-};
-
-struct Problem {
-  Operand a[2];  // two K segments (second used when k2 > 0)
-  Operand b[2];
-  void* c;
-  float alpha;
-};
-
-// Per-problem state for EPI_ADAM.  mode 1 = row-normalised parameter (decoder /
-// tied dictionary): the gradient reaching the raw rows goes through the norm
-// Jacobian, using the row dots accumulated by the code-gradient epilogue and
-// the current row norms; the updated rows are written unnormalised to the bf16
-// shadow together with per-(row, column-tile) partial squared norms, and a
-// small normalize pass finishes the shadow.
-struct AdamEpi {
-  float* p;
-  float* m;
-  float* v;
-  uint16_t* sh;
-  const float* dotpart;
-  const float* norms;
-  float* sqpart;
-  int mode;
-};
-
-struct GemmParams {
-  Problem prob[2];
-  int nprob;
-  int M, N, K1, K2;
-  int G;
-  long ldc, sc;  // output leading dim / group stride (elements)
-  // --- epilogue auxiliaries -------------------------------------------------
-  const float* bias;  // ENC: [G][N] fp32
-  long sbias;
-  const int* nactive;  // ENC: per-group number of live columns (masked SAEs), may be null
-  const uint16_t* aux; // DEC: x (bf16); DC: c (bf16)
-  long ldaux, saux;
-  float* part;         // per-block scalar partials [G][tiles] x nstat
-  float* colpart;      // per-(tile_m, column) partials [G][tiles_m][N] (DC: bias grad, ENC: counts)
-  const float* l1;     // DC: l1 coefficient per group
-  float l1_add_scale;  // DC: multiplies l1[g] (= d/2 so dpre is in units of R)
-  float* dotpart;      // DC (optional): [G][tiles_m][N] partials of the norm-Jacobian row dots
-  int dc_tied;         // DC: tied dictionary -> dot also gets dpre * (c - b) (uses bias)
-  // --- EPI_ADAM: Adam fused into the weight-gradient epilogue -----------------
-  AdamEpi adam[2];
-  const float* lr;     // [G]
-  const int* step;     // device count of completed steps (t = *step + 1)
-  float b1, b2, eps;
-  int dot_tm;          // row tiles in dotpart
-  float dot_scale;     // converts dotpart sums to <w_hat, dL/dw_hat>
-  uint64_t* cmask;     // ENC: optional activity-bitmask output; DC_MASK: its input
-  // --- split-K (plain F32 / BF16 epilogues only): K-tile range split over `ksplit`
-  // blocks per output tile; split s writes its partial product at c + s * split_stride
-  // (the consumer -- the Adam kernel for weight gradients -- sums the slabs).
-  int ksplit;
-  long split_stride;
-  // --- EPI_ENC_ACT / EPI_DC_ACT: activation mode and the threshold SAE's per-feature s^2
-  int act;
-  const float* ascale;  // [G][N] (group stride sbias)
-};
-
-// LDS image of a K-major tile [128 rows][BKT k] bf16.
-//  BKT=64: 128-byte rows (8 chunks of 16 B), chunk ^= (row>>1)&7
-//  BKT=32:  64-byte rows (4 chunks),         chunk ^= ((row>>2)&1)<<1
-// Both keep the 16-lane groups of ds_read_b128 conflict free for the MFMA
-// fragment reads (lane = row, chunk = k/8).
-template <int BKT>
-__device__ __forceinline__ int kmaj_off(int row, int ch) {
-  if constexpr (BKT == 64) return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4);
-  else return row * 64 + ((ch ^ (((row >> 2) & 1) << 1)) << 4);
-}
-// LDS image of an M/N-major tile [BKT k][128 cols] bf16: 256-byte rows, 16
-// chunks, swizzle that keeps the transposed 4x16 block reads conflict free.
-__device__ __forceinline__ int mmaj_off(int row, int ch) {
-  return row * 256 + ((ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) << 4);
-}
-
-// s_waitcnt vmcnt(N) only (expcnt/lgkmcnt left at their maxima).
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Per-lane byte offsets (relative to the operand's group base) of the 1 KiB
-// LDS-DMA pieces this wave fills for K-tile 0; later tiles add a scalar soffset.
-// An M/N-major tile wider than 128 is stored as 128-column halves, each its own
-// [BKT][128] swizzled image (BKT/4 pieces per half).
-// The LDS destination of a piece is lane-linear, so the swizzle is applied to
-// the SOURCE: lane L fills physical slot L and fetches the logical chunk the
-// image places there (the XOR swizzles are involutions).
-template <bool KMAJ, int BKT, int PPW>
-__device__ __forceinline__ void piece_offsets(uint32_t (&voff)[PPW], long ld, int r0, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int piece = wid * PPW + i;
-    if constexpr (KMAJ) {
-      constexpr int LPR = BKT / 8;         // lanes (16-B chunks) per row
-      constexpr int RPP = 64 / LPR;        // rows per 1 KiB piece
-      const int row = piece * RPP + lane / LPR;
-      const int slot = lane % LPR;
-      const int ch = (BKT == 64) ? (slot ^ ((row >> 1) & 7)) : (slot ^ (((row >> 2) & 1) << 1));
-      voff[i] = (uint32_t)(((long)(r0 + row) * ld + ch * 8) * 2);
-    } else {
-      constexpr int PPH = BKT / 4;  // pieces per 128-column half
-      const int half = piece / PPH;
-      const int row = (piece % PPH) * 4 + (lane >> 4);
-      const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-      voff[i] = (uint32_t)(((long)row * ld + r0 + half * 128 + ch * 8) * 2);
-    }
-  }
-}
-
-// Buffer resource (V#) as four SGPR words for inline asm: base, stride 0,
-// num_records, gfx950 raw-buffer flags.
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4_t make_rsrc(const uint16_t* base) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  i32x4_t r;
-  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-  r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) & 0xFFFF);
-  r[2] = 0x7FFFFFFF;
-  r[3] = 0x00020000;
-  return r;
-}
-
-// The LDS-DMA is issued from inline asm on purpose: when hipcc sees a
-// buffer_load...lds it conservatively waits vmcnt(0) before the next ds_read of
-// the same LDS array, which would drain the prefetch of tile kt+1 before tile
-// kt's MFMAs and serialise the pipeline.  Hidden in asm, the DMAs are waited for
-// only by the explicit counted vmcnt before each barrier.
-template <int PPW>
-__device__ __forceinline__ void issue_pieces(const i32x4_t& rs, const uint32_t* voff, uint32_t soff, char* lds_tile,
-                                             int wid) {
-  const uint32_t base = (uint32_t)reinterpret_cast<uintptr_t>(lds_tile) + (uint32_t)(wid * PPW * 1024);
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    asm volatile(
-        "s_mov_b32 m0, %0\n\t"
-        "s_nop 0\n\t"
-        "buffer_load_dwordx4 %1, %2, %3 offen lds"
-        :
-        : "s"(base + i * 1024), "v"(voff[i]), "s"(rs), "s"(soff)
-        : "memory", "m0");
-  }
-}
-
-// Fragment for v_mfma_f32_16x16x32_bf16: lane l holds X[r = rbase + (l&15)][k = 32 ks + 8(l>>4) + j].
-template <bool KMAJ, int BKT>
-__device__ __forceinline__ bf16x8_t load_frag(const char* lds, int rbase, int ks, int lane) {
-  if constexpr (KMAJ) {
-    const int row = rbase + (lane & 15);
-    const int ch = ks * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8_t*>(lds + kmaj_off<BKT>(row, ch));
-  } else {
-    // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group addresses row q,
-    // columns 4p..4p+3 of a 4x16 block; lane i receives column i.
-    lds += (rbase >> 7) * (BKT * 256);  // 128-column half image
-    rbase &= 127;
-    const int li = lane & 15, q = li >> 2, p = li & 3, g = lane >> 4;
-    const int ch = (rbase >> 3) + (p >> 1);
-    const int within = (p & 1) * 8;
-    const int row0 = ks * 32 + 8 * g + q;
-    i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(SC_LDS(i16x4_t, lds + mmaj_off(row0, ch) + within));
-    i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(SC_LDS(i16x4_t, lds + mmaj_off(row0 + 4, ch) + within));
-    typedef short i16x8_t __attribute__((ext_vector_type(8)));
-    i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8_t, v);
-  }
-}
-
 
 template <class S, bool AK, bool BKM, int EPI, int BKT, int NST>
 __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
@@ -473,7 +273,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
 #pragma unroll
       for (int i = 0; i < WI; ++i) {
         f32x4_t v;
-        bool on[4];
+        bool on[4], rampv[4] = {false, false, false, false};
         if constexpr (ACTV) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -483,11 +283,13 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
             } else if (act == 2) {
               const float u = pre * is2[r];
               v[r] = (fminf(fmaxf(10.f * (u - 0.9f), 0.f), 1.f) + fmaxf(u - 1.f, 0.f)) * s2[r];
+              rampv[r] = u < 1.f;
             } else {
               v[r] = fmaxf(pre, 0.f);
             }
             const bool live = col + r < nact;
             on[r] = live && (act == 1 ? pre > 0.f : v[r] > 0.f);
+            rampv[r] = rampv[r] && on[r];
             v[r] = live ? v[r] : 0.f;
           }
 #pragma unroll
@@ -524,6 +326,15 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
             dst[0] = u32x4_t{(uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32)};
             dst[1] = u32x4_t{(uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32)};
           }
+          if (ACTV && act == 2 && p.cmask2) {  // ramp bits of the threshold activation
+            const uint64_t q0 = __ballot(rampv[0]), q1 = __ballot(rampv[1]);
+            const uint64_t q2 = __ballot(rampv[2]), q3 = __ballot(rampv[3]);
+            if (lane == 0) {
+              u32x4_t* dst = reinterpret_cast<u32x4_t*>(p.cmask2 + frag * 4);
+              dst[0] = u32x4_t{(uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32)};
+              dst[1] = u32x4_t{(uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)q3, (uint32_t)(q3 >> 32)};
+            }
+          }
         }
       }
       if (counting) colred_lane(cnt, j, 0);
@@ -538,10 +349,12 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   if constexpr (EPI == EPI_DEC) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     float se = 0.f;
+    const bool rcol = p.rcol != nullptr;  // fp32 column sums of R (learned-centering gradient)
 #pragma unroll
-    for (int i = 0; i < WI; ++i)
+    for (int j = 0; j < WJ; ++j) {
+      f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < WJ; ++j) {
+      for (int i = 0; i < WI; ++i) {
         const long row = rowb + i * 16;
         const int col = colb + j * 16;
         const uint2 xv = AUX_EARLY ? auxv[i][j]
@@ -550,8 +363,12 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
         const float r2 = acc[i][j][2] - bf2f(xv.y & 0xFFFF), r3 = acc[i][j][3] - bf2f(xv.y >> 16);
         *reinterpret_cast<ushort4*>(C + row * p.ldc + col) = make_ushort4(f2bf(r0), f2bf(r1), f2bf(r2), f2bf(r3));
         se += r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
+        cs[0] += r0; cs[1] += r1; cs[2] += r2; cs[3] += r3;
       }
-    se = block_sum<NW>(se, red);
+      if (rcol) colred_lane(cs, j, 0);
+    }
+    se = block_sum<NW>(se, red + 8192);  // its barriers also publish the colred_lane writes
+    if (rcol) colred_store(p.rcol, 0);
     scalar_partial(p.part, 1, 0, se);
     return;
   }
@@ -662,7 +479,8 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
             dv[r] = on ? acc[i][j][r] + add * sgn : 0.f;
           } else if (act == 2) {
             const float dc = acc[i][j][r] + add;
-            const bool ramp = c * is2[r] < 1.f;
+            // ramp bit from the encoder's fp32 decision; without it, from the bf16 code
+            const bool ramp = p.cmask2 ? (bool)((p.cmask2[frag * 4 + r] >> lane) & 1ull) : c * is2[r] < 1.f;
             dv[r] = on ? dc * (ramp ? 10.f : 1.f) : 0.f;
             cs[r] += dv[r];
             ds[r] += (on && ramp) ? -9.f * dc : 0.f;
@@ -891,7 +709,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             float* dotpart, int dc_tied, const ScAdamEpi* adam /* [nprob] or null */, const float* lr,
             const int* step, float b1, float b2, float eps, int dot_tm, float dot_scale,
             int cfg, int ksplit, long split_stride, void* cmask, int act, const float* ascale,
-            hipStream_t stream) {
+            void* cmask2, float* rcol, hipStream_t stream) {
   if (M % PT || N % PT || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
   if ((epi == EPI_DC_MASK || epi == EPI_DC_ACT) && !cmask) return 4;
   if (epi == EPI_DC_ACT && (!aux || !colpart || !l1)) return 4;
@@ -925,6 +743,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.lr = lr; p.step = step; p.b1 = b1; p.b2 = b2; p.eps = eps; p.dot_tm = dot_tm; p.dot_scale = dot_scale;
   p.ksplit = ksplit; p.split_stride = split_stride;
   p.act = act; p.ascale = ascale;
+  p.cmask2 = reinterpret_cast<uint64_t*>(cmask2); p.rcol = rcol;
   const bool ak = layout & 1, bk = layout & 2;
   int shape = cfg & 3;
   const int pipe = (cfg >> 2) & 3;  // 0: BK64 x 2 stages, 1: BK32 x 4, 2: BK32 x 2, 3: BK32 x 3

@@ -47,6 +47,55 @@ def set_config(epi: int, cfg: int):
     _CFG_DEFAULT[epi] = int(cfg)
 
 
+# Persistent, wave-specialised kernel (csrc/sae_gemm_p.hip): 4 MFMA waves + 4 epilogue waves per
+# CU, the previous tile's fused epilogue overlapped with the current tile's MFMAs.  Opt-in
+# (SC_GEMM_PERSIST=1 / force_persistent): on MI355X its single MFMA wave per SIMD issues the
+# LDS-DMA and the fragment reads itself and loses to two tile-kernel workgroups per CU on every
+# step GEMM (enc 80 vs 59 us, wgrad 114 vs 64 us; profiles/gemm_lab_r2_v1.jsonl), although its
+# outputs are bit-identical (tests/test_gemm_persistent_gpu.py).
+_PERSIST = os.environ.get("SC_GEMM_PERSIST", "0") not in ("", "0")
+_P_EPIS = {EPI_F32, EPI_BF16, EPI_ENC, EPI_ENC_CNT, EPI_ENC_ACT, EPI_DEC, EPI_DC_MASK, EPI_DC_ACT}
+_P_NST = int(os.environ.get("SC_GEMM_NST", "3"))
+_P_MAX_BLOCKS = 0
+
+
+class force_persistent:
+    """Context manager: route eligible GEMMs to the persistent kernel (``on``) or to the tile
+    kernel; ``max_blocks`` caps the grid (tests: several tiles per workgroup); ``nst`` sets
+    the LDS ring depth (3 or 4)."""
+
+    def __init__(self, on: bool = True, max_blocks: int = 0, nst: int | None = None):
+        self.on, self.max_blocks, self.nst = bool(on), int(max_blocks), nst
+
+    def __enter__(self):
+        global _PERSIST, _P_MAX_BLOCKS, _P_NST
+        self._old = (_PERSIST, _P_MAX_BLOCKS, _P_NST)
+        _PERSIST, _P_MAX_BLOCKS = self.on, self.max_blocks
+        if self.nst is not None:
+            _P_NST = int(self.nst)
+        return self
+
+    def __exit__(self, *exc):
+        global _PERSIST, _P_MAX_BLOCKS, _P_NST
+        _PERSIST, _P_MAX_BLOCKS, _P_NST = self._old
+
+
+def _persistent_ok(epi, layout, K1, K2, nprob, cfg, ksplit, cmask, act=0, cmask2=None):
+    if not _PERSIST or epi not in _P_EPIS or ksplit != 1 or cfg is not None or _CFG_OVERRIDE is not None:
+        return False
+    if K1 + K2 < 512:
+        return False
+    if K2 and (epi != EPI_F32 or layout != 0):
+        return False
+    if epi in (EPI_ENC, EPI_ENC_CNT, EPI_ENC_ACT, EPI_DC_MASK, EPI_DC_ACT) and (cmask is None or layout != 3):
+        return False
+    if epi == EPI_DEC and layout != 1:
+        return False
+    if act == ACT_THRESHOLD and epi in (EPI_ENC_ACT, EPI_DC_ACT) and cmask2 is None:
+        return False  # the persistent kernel takes the ramp bits from the encoder's fp32 decision
+    return _lib.lib() is not None and hasattr(_lib.lib(), "sc_gemm_p")
+
+
 class force_shape:
     """Context manager: run every GEMM with block shape ``cfg`` (tests / A-B timing)."""
 
@@ -87,12 +136,35 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
             bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
             colpart=None, l1=None, l1_add_scale=0.0, dotpart=None, dc_tied=False, adam=None,
             lr=None, step=None, betas=(0.9, 0.999), eps=1e-8, dot_tm=0, dot_scale=0.0, cfg=None,
-            ksplit=1, split_stride=0, cmask=None, act=0, ascale=None):
+            ksplit=1, split_stride=0, cmask=None, act=0, ascale=None, cmask2=None, rcol=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
+    cfg_explicit = cfg
     cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
     _need((cfg & 3) == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg & 3)} does not tile M={M}, N={N}")
     nprob = len(outs)
+    if _persistent_ok(epi, layout, K1, K2, nprob, cfg_explicit, ksplit, cmask, act, cmask2):
+        args = _lib.ScGemmArgs()
+        args.epi, args.layout, args.nprob = epi, layout, nprob
+        args.M, args.N, args.K1, args.K2, args.G = M, N, K1, K2, G
+        for i, op in enumerate(a_ops):
+            args.a[i] = op
+        for i, op in enumerate(b_ops):
+            args.b[i] = op
+        for i, o in enumerate(outs):
+            args.c[i] = _lib.ptr(o)
+            args.alpha[i] = float(alphas[i])
+        args.ldc, args.sc = ldc, sc
+        args.bias, args.sbias, args.nactive = _lib.ptr(bias), sbias, _lib.ptr(nactive)
+        args.aux, args.ldaux, args.saux = _lib.ptr(aux), ldaux, saux
+        args.part, args.colpart, args.l1 = _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1)
+        args.l1_add_scale, args.dotpart = float(l1_add_scale), _lib.ptr(dotpart)
+        args.cmask, args.cmask2, args.rcol = _lib.ptr(cmask), _lib.ptr(cmask2), _lib.ptr(rcol)
+        args.act, args.ascale = int(act), _lib.ptr(ascale)
+        args.nst, args.max_blocks = _P_NST, _P_MAX_BLOCKS
+        rc = _lib.lib().sc_gemm_p(C.byref(args), _lib.stream_handle())
+        _lib.check(rc, f"sc_gemm_p(epi={epi})")
+        return
     A = (_lib.ScOperand * (2 * nprob))(*a_ops)
     Bo = (_lib.ScOperand * (2 * nprob))(*b_ops)
     Cp = (C.c_void_p * nprob)(*[_lib.ptr(o) for o in outs])
@@ -104,7 +176,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
         _lib.ptr(dotpart), int(bool(dc_tied)), adam, _lib.ptr(lr), _lib.ptr(step),
         float(betas[0]), float(betas[1]), float(eps), int(dot_tm), float(dot_scale),
         cfg, int(ksplit), int(split_stride), _lib.ptr(cmask), int(act), _lib.ptr(ascale),
-        _lib.stream_handle(),
+        _lib.ptr(cmask2), _lib.ptr(rcol), _lib.stream_handle(),
     )
     _lib.check(rc, f"sc_gemm(epi={epi})")
 
@@ -123,7 +195,8 @@ def code_mask_shape(G, B, n):
     return (G, B // 16, n // 16, 4)
 
 
-def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=None, act=ACT_RELU, ascale=None):
+def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=None, act=ACT_RELU, ascale=None,
+                mask2_out=None):
     """c[g] = relu(x[g] @ w[g]^T + bias[g]) with L1/L0 partials.
 
     ``act`` selects another code activation of the same GEMM:
@@ -136,6 +209,8 @@ def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=No
     colpart (optional): [G, B/128, n] fp32 per-feature on-counts;
     mask_out (optional): int64 ``code_mask_shape(G, B, n)``: the activity bitmask ``code_grad``
     can read instead of the codes.
+    mask2_out (``ACT_THRESHOLD``): the same layout, 1 where the code is on the threshold's ramp
+    (decided on the fp32 pre-activation; ``code_grad(mask2=...)`` reads it).
     """
     G, n, d = w.shape
     B = c_out.shape[1]
@@ -154,19 +229,25 @@ def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=No
     if act == ACT_THRESHOLD:
         _need(ascale is not None and tuple(ascale.shape) == (G, n) and ascale.dtype == torch.float32
               and ascale.is_contiguous(), "threshold activation needs ascale fp32 [G, n]")
+    if mask2_out is not None:
+        _need(act == ACT_THRESHOLD and mask2_out.dtype == torch.int64
+              and tuple(mask2_out.shape) == code_mask_shape(G, B, n) and mask2_out.is_contiguous(),
+              "mask2_out: int64 code_mask_shape(G, B, n), threshold activation only")
     a = [_op(x, d, sx), _op(x, d, sx)]
     b = [_op(w, d, n * d), _op(w, d, n * d)]
     epi = EPI_ENC_ACT if act != ACT_RELU else (EPI_ENC_CNT if colpart is not None else EPI_ENC)
     _launch(epi, 3, B, n, d, 0, G, a, b, [c_out], [1.0], n, B * n,
             bias=bias, sbias=n, nactive=nactive, part=part, colpart=colpart, cmask=mask_out, act=act,
-            ascale=ascale)
+            ascale=ascale, cmask2=mask2_out)
 
 
-def decode_residual(c, w_hat, x, r_out, part):
+def decode_residual(c, w_hat, x, r_out, part, rcol=None):
     """r[g] = c[g] @ w_hat[g] - x[g]  (bf16 out) with sum(r^2) partials.
 
     c: [G, B, n] bf16; w_hat: [G, n, d] bf16 (row-normalised dictionary);
-    x: [B, d] or [G, B, d] bf16; r_out: [G, B, d] bf16; part: [G, (B/128)*(d/128)].
+    x: [B, d] or [G, B, d] bf16; r_out: [G, B, d] bf16; part: [G, (B/128)*(d/128)];
+    rcol (optional): [G, B/128, d] fp32 column sums of the residual per 128-row tile, taken
+    before the bf16 rounding.
     """
     G, B, n = c.shape
     d = w_hat.shape[2]
@@ -174,14 +255,17 @@ def decode_residual(c, w_hat, x, r_out, part):
     sx = _x_stride(x, B, d, G)
     _need(tuple(w_hat.shape) == (G, n, d), "w_hat shape")
     _need(part.numel() >= G * (B // 128) * (d // 128), "part too small")
+    if rcol is not None:
+        _need(rcol.dtype == torch.float32 and rcol.numel() >= G * (B // 128) * d and rcol.is_contiguous(),
+              "rcol must be fp32 [G, B/128, d]")
     a = [_op(c, n, B * n)] * 2
     b = [_op(w_hat, d, n * d)] * 2  # stored [K=n][N=d] -> N-major
     _launch(EPI_DEC, 1, B, d, n, 0, G, a, b, [r_out], [1.0], d, B * d,
-            aux=x, ldaux=d, saux=sx, part=part)
+            aux=x, ldaux=d, saux=sx, part=part, rcol=rcol)
 
 
 def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, mask=None, act=ACT_RELU,
-              ascale=None):
+              ascale=None, mask2=None):
     """dpre_s[g] = 1[c>0] * (r[g] @ w_hat[g]^T + l1[g] * d / 2).
 
     dpre_s is the code gradient in units of the residual: dL/dpre = 2/(B d) * dpre_s.
@@ -213,9 +297,12 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, 
         if act == ACT_THRESHOLD:
             _need(ascale is not None and tuple(ascale.shape) == (G, n) and ascale.dtype == torch.float32
                   and ascale.is_contiguous(), "threshold activation needs ascale fp32 [G, n]")
+        if mask2 is not None:
+            _need(act == ACT_THRESHOLD and mask2.dtype == torch.int64
+                  and tuple(mask2.shape) == code_mask_shape(G, B, n), "mask2 must match the encoder's mask2_out")
         _launch(EPI_DC_ACT, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
                 aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0,
-                dotpart=dotpart, cmask=mask, act=act, ascale=ascale, sbias=n)
+                dotpart=dotpart, cmask=mask, act=act, ascale=ascale, sbias=n, cmask2=mask2)
         return
     if mask is not None and dotpart is None:
         _need(mask.dtype == torch.int64 and tuple(mask.shape) == code_mask_shape(G, B, n), "mask shape")

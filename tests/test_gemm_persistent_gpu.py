@@ -1,0 +1,227 @@
+"""The persistent wave-specialised GEMM (csrc/sae_gemm_p.hip) against fp32 PyTorch and the
+tile kernel (csrc/sae_gemm.hip).
+
+Every case runs with the grid capped to a few workgroups too (``max_blocks``), so each
+workgroup walks several tiles and the cross-tile paths are exercised: the LDS-DMA ring running
+into the next tile, the staged hand-off of the previous tile's fragments, the epilogue waves'
+deferred partial-sum flush.  Outputs (codes, residuals, code gradients, activity bitmasks)
+must be bit-identical to the tile kernel's -- both accumulate the same MFMA fragments in the
+same K order; partial sums are compared with a tolerance (different summation order).
+"""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+GRIDS = [0, 1, 3]  # 0: one workgroup per CU; 1 and 3: every workgroup walks many tiles
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from sparse_coding__amd.ops import _lib as L
+
+    L.lib()
+    assert hasattr(L.lib(), "sc_gemm_p"), "persistent GEMM missing from the kernel library"
+    yield
+
+
+def _bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(torch.bfloat16)
+
+
+def _close(a, b, rtol=2e-2, atol=1e-2):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item()
+    assert err <= atol + rtol * ref, f"max err {err} vs ref scale {ref}"
+
+
+@pytest.mark.parametrize("grid", GRIDS)
+@pytest.mark.parametrize("G,M,N,K", [(1, 128, 128, 512), (2, 256, 384, 512), (3, 384, 256, 1024)])
+def test_plain_layouts(G, M, N, K, grid):
+    from sparse_coding__amd.ops import gemm
+
+    torch.manual_seed(0)
+    a = _bf(G, M, K)
+    b = _bf(G, N, K)
+    bn = _bf(G, K, N)
+    at = _bf(G, K, M)
+    with gemm.force_persistent(True, max_blocks=grid):
+        out = torch.empty(G, M, N, device=DEV)
+        gemm.matmul_nt(a, b, out)
+        _close(out, a.float() @ b.float().transpose(1, 2), rtol=1e-3, atol=1e-3)
+        gemm.matmul_nn(a, bn, out)
+        _close(out, a.float() @ bn.float(), rtol=1e-3, atol=1e-3)
+        gemm.matmul_tn(at, bn, out, alpha=0.5)
+        _close(out, 0.5 * at.float().transpose(1, 2) @ bn.float(), rtol=1e-3, atol=1e-3)
+        out16 = torch.empty(G, M, N, device=DEV, dtype=torch.bfloat16)
+        gemm.matmul_nt(a, b, out16)
+    ref16 = torch.empty_like(out16)
+    with gemm.force_persistent(False):
+        gemm.matmul_nt(a, b, ref16)
+    assert torch.equal(out16, ref16)  # 16-byte permlane-swapped stores land where the tile kernel's do
+
+
+def test_identity_asymmetric_persistent():
+    """A = I with an asymmetric B catches a transposed or column-swapped C write."""
+    from sparse_coding__amd.ops import gemm
+
+    M, K, N = 128, 512, 256
+    a = torch.eye(M, K, device=DEV).to(torch.bfloat16)[None]
+    b = torch.arange(N * K, device=DEV, dtype=torch.float32).reshape(1, N, K).remainder(97).to(torch.bfloat16)
+    with gemm.force_persistent(True, max_blocks=1):
+        out = torch.empty(1, M, N, device=DEV)
+        gemm.matmul_nt(a, b, out)
+        torch.testing.assert_close(out, b.float().transpose(1, 2)[:, :M, :], rtol=0, atol=0)
+        out16 = torch.empty(1, M, N, device=DEV, dtype=torch.bfloat16)
+        gemm.matmul_nt(a, b, out16)
+        torch.testing.assert_close(out16.float(), b.float().transpose(1, 2)[:, :M, :], rtol=0, atol=0)
+
+
+def _run_step_epilogues(G, B, d, n, nactive, grid, persistent):
+    from sparse_coding__amd.ops import gemm
+
+    torch.manual_seed(1)
+    x = _bf(B, d)
+    we = _bf(G, n, d, scale=0.05)
+    wd = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1).to(torch.bfloat16)
+    bias = torch.randn(G, n, device=DEV) * 0.1
+    l1 = torch.tensor([1e-3, 3e-3, 1e-2][:G], device=DEV)
+    out = {}
+    with gemm.force_persistent(persistent, max_blocks=grid):
+        c = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
+        part = torch.zeros(G, (B // 128) * (n // 128), 2, device=DEV)
+        cnt = torch.zeros(G, B // 128, n, device=DEV)
+        cmask = torch.zeros(gemm.code_mask_shape(G, B, n), device=DEV, dtype=torch.int64)
+        gemm.encode_relu(x, we, bias, c, part, cnt, nactive, mask_out=cmask)
+        r = torch.empty(G, B, d, device=DEV, dtype=torch.bfloat16)
+        dpart = torch.zeros(G, (B // 128) * (d // 128), device=DEV)
+        gemm.decode_residual(c, wd, x, r, dpart)
+        dpre = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
+        colpart = torch.zeros(G, B // 128, n, device=DEV)
+        gemm.code_grad(r, wd, c, l1, dpre, colpart, mask=cmask)
+        gd = torch.empty(G, n, d, device=DEV)
+        ge = torch.empty(G, n, d, device=DEV)
+        alpha = 2.0 / (B * d)
+        gemm.weight_grads([[(c, r)], [(dpre, x)]], [gd, ge], alpha)
+        gt = torch.empty(G, n, d, device=DEV)
+        gemm.weight_grads([[(c, r), (dpre, x)]], [gt], alpha)
+    torch.cuda.synchronize()
+    out.update(x=x, we=we, wd=wd, bias=bias, l1=l1, c=c, part=part, cnt=cnt, cmask=cmask, r=r, dpart=dpart,
+               dpre=dpre, colpart=colpart, gd=gd, ge=ge, gt=gt, alpha=alpha)
+    return out
+
+
+@pytest.mark.parametrize("grid", GRIDS)
+def test_step_epilogues_match_reference_and_tile_kernel(grid):
+    G, B, d, n = 3, 512, 512, 384
+    nactive = torch.tensor([n, 256, 128], device=DEV, dtype=torch.int32)
+    o = _run_step_epilogues(G, B, d, n, nactive, grid, True)
+    x, we, wd, bias, l1 = o["x"], o["we"], o["wd"], o["bias"], o["l1"]
+    ref = torch.relu(x.float() @ we.float().transpose(1, 2) + bias[:, None, :])
+    for g in range(G):
+        ref[g, :, int(nactive[g]):] = 0
+    _close(o["c"], ref)
+    cf = o["c"].float()
+    torch.testing.assert_close(o["part"][..., 0].sum(1), ref.sum((1, 2)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(o["part"][..., 1].sum(1), (cf > 0).float().sum((1, 2)), rtol=0, atol=0)
+    torch.testing.assert_close(o["cnt"].sum(1), (cf > 0).float().sum(1), rtol=0, atol=0)
+    rref = cf @ wd.float() - x.float()
+    _close(o["r"], rref)
+    torch.testing.assert_close(o["dpart"].sum(1), (rref ** 2).sum((1, 2)), rtol=2e-2, atol=1e-1)
+    dref = (o["r"].float() @ wd.float().transpose(1, 2) + (l1 * d / 2)[:, None, None]) * (cf > 0)
+    _close(o["dpre"], dref)
+    _close(o["colpart"].sum(1), dref.sum(1), rtol=1e-2, atol=1e-2)
+    a = o["alpha"]
+    _close(o["gd"], a * cf.transpose(1, 2) @ o["r"].float(), rtol=1e-3, atol=1e-6)
+    _close(o["ge"], a * o["dpre"].float().transpose(1, 2) @ x.float(), rtol=1e-3, atol=1e-6)
+    _close(o["gt"], o["gd"] + o["ge"], rtol=1e-3, atol=1e-6)
+
+    t = _run_step_epilogues(G, B, d, n, nactive, 0, False)  # the tile kernel on the same inputs
+    for k in ("c", "cmask", "r", "dpre"):
+        assert torch.equal(o[k], t[k]), k
+    torch.testing.assert_close(o["cnt"], t["cnt"], rtol=0, atol=0)
+    for k in ("part", "dpart", "colpart"):
+        torch.testing.assert_close(o[k], t[k], rtol=1e-4, atol=1e-3)
+    for k in ("gd", "ge", "gt"):
+        torch.testing.assert_close(o[k], t[k], rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("act", [1, 2])
+@pytest.mark.parametrize("grid", [0, 2])
+def test_activation_epilogues(act, grid):
+    """Reverse (act 1) and smooth-threshold (act 2) encoder / code-gradient epilogues against
+    fp32 formulas; the threshold ramp bit is decided on the fp32 pre-activation."""
+    from sparse_coding__amd.ops import gemm
+
+    torch.manual_seed(7)
+    G, B, d, n = 2, 256, 512, 256
+    x = _bf(B, d)
+    w = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1).to(torch.bfloat16)
+    gain = torch.randn(G, n, device=DEV) * 0.2
+    s2 = (torch.rand(G, n, device=DEV) * 0.5 + 0.75) if act == 2 else None
+    l1 = torch.tensor([2e-3, 5e-3], device=DEV)
+    with gemm.force_persistent(True, max_blocks=grid):
+        c = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
+        part = torch.zeros(G, (B // 128) * (n // 128), 2, device=DEV)
+        cmask = torch.zeros(gemm.code_mask_shape(G, B, n), device=DEV, dtype=torch.int64)
+        cmask2 = torch.zeros_like(cmask) if act == 2 else None
+        gemm.encode_relu(x, w, gain, c, part, None, None, mask_out=cmask, act=act, ascale=s2, mask2_out=cmask2)
+        r = _bf(G, B, d, scale=0.3)
+        dpre = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
+        colpart = torch.zeros(G, B // 128, n, device=DEV)
+        dotpart = torch.zeros(G, B // 128, n, device=DEV)
+        gemm.code_grad(r, w, c, l1, dpre, colpart, dotpart=dotpart if act == 2 else None, mask=cmask, act=act,
+                       ascale=s2, mask2=cmask2)
+    torch.cuda.synchronize()
+    pre = x.float() @ w.float().transpose(1, 2) + gain[:, None, :]
+    if act == 1:
+        cref = torch.where(pre > 0, pre - gain[:, None, :], torch.zeros_like(pre))
+        on = pre > 0
+    else:
+        u = pre / s2[:, None, :]
+        cref = (torch.clamp(10 * (u - 0.9), 0, 1) + torch.relu(u - 1)) * s2[:, None, :]
+        on = cref > 0
+    _close(c, cref)
+    gdc = r.float() @ w.float().transpose(1, 2) + (l1 * d / 2)[:, None, None] * (
+        torch.sign(c.float()) if act == 1 else 1.0)
+    if act == 1:
+        dref = gdc * on
+    else:
+        ramp = on & (u < 1)
+        dref = gdc * on * torch.where(ramp, 10.0, 1.0)
+        # the ramp bit is decided on the kernel's own fp32 pre-activation: within a few ulps of
+        # u = 1 it may fall either way (bf16 MFMA vs torch accumulation order), so those
+        # elements may contribute -9 dL/dc or not
+        amb = on & ((u - 1).abs() < 2e-3)
+        certain = (-9.0 * gdc * (ramp & ~amb)).sum(1)
+        slack = (9.0 * gdc.abs() * amb).sum(1)
+        assert bool(((dotpart.sum(1) - certain).abs() <= slack + 2e-2 + 2e-2 * certain.abs()).all())
+        dref = torch.where(amb, dpre.float(), dref)
+    _close(dpre, dref, rtol=3e-2, atol=3e-2)
+    if act == 2:
+        _close(colpart.sum(1), dref.sum(1), rtol=2e-2, atol=2e-2)
+    else:
+        assert float(colpart.abs().max()) == 0.0
+
+
+def test_decoder_fp32_residual_column_sums():
+    """The decoder epilogue's optional fp32 column sums of R (learned-centering gradient)."""
+    from sparse_coding__amd.ops import gemm
+
+    torch.manual_seed(9)
+    G, B, d, n = 2, 384, 512, 512
+    c = torch.relu(_bf(G, B, n).float()).to(torch.bfloat16)
+    wd = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1).to(torch.bfloat16)
+    x = _bf(B, d)
+    r = torch.empty(G, B, d, device=DEV, dtype=torch.bfloat16)
+    part = torch.zeros(G, (B // 128) * (d // 128), device=DEV)
+    rcol = torch.zeros(G, B // 128, d, device=DEV)
+    for persistent in (True, False):
+        rcol.zero_()
+        with gemm.force_persistent(persistent, max_blocks=2):
+            gemm.decode_residual(c, wd, x, r, part, rcol=rcol)
+        ref = (c.float() @ wd.float() - x.float()).sum(1)
+        torch.testing.assert_close(rcol.sum(1), ref, rtol=1e-3, atol=5e-2)
