@@ -106,10 +106,17 @@ def main():
         "ntbf16": (lambda: gemm.matmul_nt(x, we, c), fl),
     }
     gemm.encode_relu(x, we, bias, c, part, None, None, mask_out=cmask)
+    modes = [("tile", lambda: gemm.force_persistent(False)),
+             ("p3", lambda: gemm.force_persistent(True, nst=3)),
+             ("p4", lambda: gemm.force_persistent(True, nst=4))]
+    if a.cfgs:  # explicit tile-kernel configurations (block shape | pipeline << 2) instead
+        modes = [(f"cfg{c}", lambda c=int(c): gemm.force_shape(c)) for c in a.cfgs.split(",")]
+    cases["step_torch_enc"] = (lambda: torch.matmul(x, we.transpose(1, 2), out=c), fl)
+    cases["step_torch_dec"] = (lambda: torch.matmul(c, wd, out=r), fl)
+    cases["step_torch_wgrad"] = (lambda: (torch.matmul(c.transpose(1, 2), r),
+                                          torch.matmul(dpre.transpose(1, 2), x)), 2 * fl)
     for name, (fn, f) in step_ops.items():
-        for mode, ctx in (("tile", lambda: gemm.force_persistent(False)),
-                          ("p3", lambda: gemm.force_persistent(True, nst=3)),
-                          ("p4", lambda: gemm.force_persistent(True, nst=4))):
+        for mode, ctx in modes:
             def run(fn=fn, ctx=ctx):
                 with ctx():
                     fn()
@@ -117,8 +124,12 @@ def main():
     names = [k for k in cases if not a.which or any(k.startswith(w) for w in a.which.split(","))]
     res = {k: [] for k in names}
     for _ in range(a.rounds):
-        for k in names:
-            res[k].append(timeit(cases[k][0]))
+        for k in list(names):
+            try:
+                res[k].append(timeit(cases[k][0]))
+            except Exception as e:  # a configuration the library does not instantiate
+                print(json.dumps({"case": k, "error": str(e)[:120]}), flush=True)
+                names.remove(k)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         for k in names:

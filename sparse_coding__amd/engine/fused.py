@@ -155,11 +155,27 @@ class FusedSAEEnsemble:
             self._g_flat = self.grad_all[G * n * d:]
             self.g_enc = self._g_flat[: G * n * d].view(G, n, d)
         else:
-            self._g_flat = torch.empty(G * n * d + G * n, device=dev, dtype=torch.float32)
+            # threshold / learned-centering SAEs append their small extra gradient sources (raw
+            # column sums, scaled by alpha at the update) so data-parallel runs reduce them in
+            # the same collective: [g_dec | g_bias | code-grad column sums | scale sums | R sums]
+            self._n_extra = 0
+            if self.kind == "threshold" or self.learned_center:
+                self._n_extra = G * n + (G * n if self.kind == "threshold" else 0) + (G * d if self.learned_center else 0)
+            self._g_flat = torch.empty(G * n * d + G * n + self._n_extra, device=dev, dtype=torch.float32)
             self.grad_all = self._g_flat
             self.g_dec = self._g_flat[: G * n * d].view(G, n, d)
             self.g_enc = None
-        self.g_bias = self._g_flat[G * n * d:].view(G, 1, n)
+        self.g_bias = self._g_flat[G * n * d: G * n * d + G * n].view(G, 1, n)
+        self._x_gsum = self._x_dsum = self._x_rsum = None
+        if getattr(self, "_n_extra", 0):
+            off = G * n * d + G * n
+            self._x_gsum = self._g_flat[off: off + G * n].view(G, n)
+            off += G * n
+            if self.kind == "threshold":
+                self._x_dsum = self._g_flat[off: off + G * n].view(G, n)
+                off += G * n
+            if self.learned_center:
+                self._x_rsum = self._g_flat[off: off + G * d].view(G, d)
         # Split-K of the single-device weight-gradient GEMM: with few models on a large
         # batch (ensemble sharding gives each GPU G/N models on N*B rows) the 256x256 grid
         # has fewer blocks than CUs, so the K = B reduction is split over blocks and the
@@ -311,6 +327,12 @@ class FusedSAEEnsemble:
     def _reduce_bias_grad(self):
         torch.sum(self.colpart, dim=1, keepdim=True, out=self.g_bias)
         self.g_bias.mul_(self._alpha)
+        if self._x_gsum is not None:  # raw sums for the scale / centering updates (reduced with g_bias)
+            torch.sum(self.colpart, dim=1, out=self._x_gsum)
+            if self._x_dsum is not None:
+                torch.sum(self.dotpart, dim=1, out=self._x_dsum)
+            if self._x_rsum is not None:
+                torch.sum(self.rcol, dim=1, out=self._x_rsum)
 
     def forward_backward(self, x):
         """Kernels 1-4 for the single-device step (both weight gradients in one launch).
@@ -357,6 +379,8 @@ class FusedSAEEnsemble:
         if self.kind == "untied":
             adam_ops.adam_rows(self._adam_sets()[1:], self.lr, self.step_count + 1, *self.betas, self.eps,
                                step_dev=self.step_dev)
+        if self.kind == "threshold" or self.learned_center:
+            self._threshold_extra_adam(reduced=reduced_bias)
         self._bias_loss(update=True, reduced=reduced_bias)
         self._host_step()
 
@@ -373,28 +397,35 @@ class FusedSAEEnsemble:
             self._threshold_extra_adam()
         self._bias_loss(update=True, reduced=False)
 
-    def _threshold_extra_adam(self):
+    def _threshold_extra_adam(self, reduced: bool = False):
         """Scale and centering of the threshold SAE (small vectors; before the bias / loss
         kernel, which advances the device step counter):
         dL/ds = 2 s alpha sum(dotpart), dL/dcentering = -alpha (sum_b dL/dpre) W_hat.
         Learned-centering tied SAEs also reconstruct x - center, so their center gradient
-        gains the direct residual term + alpha sum_b R."""
+        gains the direct residual term + alpha sum_b R.  ``reduced``: take the column sums
+        from the (data-parallel all-reduced) gradient buffer instead of this rank's partials."""
         a = self._alpha
-        torch.sum(self.colpart, dim=1, out=self._gsum)
+        if reduced:
+            self._gsum.copy_(self._x_gsum)
+        else:
+            torch.sum(self.colpart, dim=1, out=self._gsum)
         if self.learned_center:
             # the two terms largely cancel (dense codes: the residual's component outside the
             # active atoms' span survives), so both come from fp32 data: the decoder epilogue's
             # fp32 column sums of R (before its bf16 rounding) and the fp32 normalised masters
             w_hat = self.params["encoder"] / self.norms.unsqueeze(-1)
             g_c = torch.bmm(self._gsum.unsqueeze(1), w_hat).squeeze(1) * (-a)
-            g_c += self.rcol.sum(dim=1) * a
+            g_c += (self._x_rsum if reduced else self.rcol.sum(dim=1)) * a
         else:
             g_c = torch.bmm(self._gsum.unsqueeze(1).to(torch.bfloat16), self.enc_shadow).squeeze(1).float() * (-a)
         if self.learned_center:
             upd = (("center", g_c),)
         else:
             s = self.params["activation_scale"]
-            torch.sum(self.dotpart, dim=1, out=self._gsum)
+            if reduced:
+                self._gsum.copy_(self._x_dsum)
+            else:
+                torch.sum(self.dotpart, dim=1, out=self._gsum)
             g_s = self._gsum * s * (2.0 * a)
             upd = (("activation_scale", g_s), ("centering", g_c))
         t = self.step_dev.float() + 1.0

@@ -57,6 +57,12 @@ def _stale(target: Path, deps) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
+# Per-source extra flags.  sae_gemm.hip (128x128 blocks, software-pipelined K loop with two
+# MFMA groups per iteration) uses the VGPR form of the MFMA: with AGPR accumulators the
+# register allocator rotated them through v_accvgpr copies every iteration.
+EXTRA_FLAGS = {"sae_gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _compile_one(src: Path, force: bool) -> Path:
     obj = BUILD / (src.stem + ".o")
     if not force and not _stale(obj, [src, *_headers()]):
@@ -69,6 +75,7 @@ def _compile_one(src: Path, force: bool) -> Path:
         "-fPIC",
         "-munsafe-fp-atomics",
         f"-I{CSRC}",
+        *EXTRA_FLAGS.get(src.name, []),
         "-c",
         str(src),
         "-o",

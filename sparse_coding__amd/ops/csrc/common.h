@@ -85,6 +85,27 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return r;
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not for its
+// global stores / loads / LDS-DMAs (a __syncthreads() would drain vmcnt too).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// block_sum with LDS-only barriers (see lds_barrier); `red` must hold >= NW floats.
+template <int NW>
+__device__ __forceinline__ float block_sum_lds(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  lds_barrier();
+  if (lane == 0) red[w] = v;
+  lds_barrier();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r += red[i];
+  lds_barrier();
+  return r;
+}
+
 // Bijective XCD-aware block remap (MI355X has 8 XCDs, each with its own L2).
 // Hardware hands consecutive block ids to different XCDs round-robin; this
 // gives each XCD a contiguous run of logical tiles so neighbouring tiles that

@@ -91,6 +91,7 @@ struct GemmParams {
   // (the consumer -- the Adam kernel for weight gradients -- sums the slabs).
   int ksplit;
   long split_stride;
+  int dbg;  // diagnostics (SC_GEMM_DBG): bit 0 = EPI_BF16 skips its output stores
   // --- EPI_ENC_ACT / EPI_DC_ACT: activation mode and the threshold SAE's per-feature s^2
   int act;
   const float* ascale;  // [G][N] (group stride sbias)

@@ -1,670 +1,44 @@
-// Grouped bf16 MFMA GEMM with fused sparse-autoencoder epilogues (gfx950).
-//
-// One launch covers every model of an ensemble (the "group" axis G) and, for
-// the weight-gradient pass, two independent problems at once.  This replaces
-// the reference's torch.vmap(torch.func.grad(loss)) over stacked parameters
-// (reference autoencoders/ensemble.py:119-123) with explicit kernels:
-//
-//   EPI_ENC : c = relu(x W_e^T + b)  (+ masked tail), bf16 store, L1/L0 partials
-//   EPI_ENC_CNT: EPI_ENC + per-feature fire counts (a separate instantiation: the
-//             count reduction costs ~10% of the kernel and runs only on sampled steps)
-//             (autoencoders/sae_ensemble.py:54-56, :354 masked_fill_)
-//   EPI_DEC : R = c W_hat - x, bf16 store, sum(R^2) partials
-//             (autoencoders/sae_ensemble.py:58-62)
-//   EPI_DC  : dpre_s = 1[c>0] * (R W_hat^T + lambda*d/2), bf16 store, column-sum
-//             partials for the bias gradient (autograd of :54-64, Appendix A of SURVEY)
-//   EPI_F32 : C = alpha * acc (fp32), used for dW = c^T R and dW_e = dpre^T x
-//   EPI_BF16: C = alpha * acc (bf16), generic inference GEMM
-//   EPI_ENC_ACT / EPI_DC_ACT: EPI_ENC / EPI_DC_MASK for the other code activations
-//             (GemmParams::act): 1 = reverse SAE, codes 1[pre > 0] (pre - b)
-//             (sae_ensemble.py:481-482); 2 = smooth threshold
-//             s^2 thr((pre)/s^2), thr(u) = relu6(60(u - 0.9))/6 + relu(u - 1) (:254-257)
-//   EPI_ROWMAX: per-row max of alpha * A B^T over column tiles (max cosine similarity /
-//             MMCS, standard_metrics.py:268-301) -- the [M, N] product never reaches HBM
-//
-// Tiling (template "shape"): a WGM x WGN grid of waves, each owning a
-// (16 WI) x (16 WJ) sub-tile = WI x WJ v_mfma_f32_16x16x32_bf16 accumulators:
-//   S128   : 2x2 waves of 64x64   -> 128x128 block, 256 threads
-//   S256x128: 2x2 waves of 128x64 -> 256x128 block, 256 threads
-//   S256   : 2x4 waves of 128x64  -> 256x256 block, 512 threads, 1 block/CU
-// Bigger tiles raise FLOPs per staged byte (64 -> 85 -> 128 FLOP/B) and per LDS
-// fragment read (per-wave 128x64 reads 12 fragments per 32 MFMAs instead of 8 per
-// 16), which is what limits the short-K (K = d = 512) step GEMMs.  Operands
-// are staged global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds) into an
-// NST-deep ring of BKT-deep K-tiles (configurations: BK64 x 2 stages, BK32 x 3
-// or 4 stages).  Per-lane source offsets are computed once; the K loop only
-// advances a scalar soffset, so the main loop is MFMA + ds_read + a handful of
-// SALU.  One raw s_barrier per K-tile with a counted vmcnt keeps NST-2 tiles in
-// flight across it.
-// K-major operands are read with ds_read_b128, M/N-major operands with the
-// gfx950 transposing read ds_read_b64_tr_b16, so c^T R style products need no
-// transposed copies in HBM.  Both LDS images are XOR-swizzled to avoid bank
-// conflicts.
-#include "gemm_tiles.h"
+// Grouped bf16 MFMA GEMM with fused sparse-autoencoder epilogues (gfx950): C ABI and the
+// 128x128-block launches.  The kernel itself and the epilogue catalogue are in
+// sae_gemm_kernel.h; the 256-row block shapes are instantiated in sae_gemm_big.hip.
+#include "sae_gemm_kernel.h"
 
-namespace scamd {
-
-template <class S, bool AK, bool BKM, int EPI, int BKT, int NST>
-__global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
-  constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
-  constexpr int TA = BM * BKT * 2, TBB = BN * BKT * 2;  // bytes per operand tile
-  constexpr int PPWA = TA / 1024 / NW, PPWB = TBB / 1024 / NW;  // LDS-DMA pieces per wave
-  constexpr int LPT = PPWA + PPWB;                       // DMA instructions per wave per K-tile
-  constexpr int STG = TA + TBB;
-  static_assert(PPWA * NW * 1024 == TA && PPWB * NW * 1024 == TBB, "tile must split into whole pieces");
-  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid / WGN, wc = wid % WGN;
-  const int tiles_m = p.M / BM, tiles_n = p.N / BN;
-  const int ptm = p.M / PT, ptn = p.N / PT;  // partial-buffer grid (128 x 128 sub-tiles)
-  const int per_split = tiles_m * tiles_n * p.G;
-  const int per_prob = per_split * p.ksplit;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int pi = bid / per_prob;
-  int rem = bid - pi * per_prob;
-  const int ksi = rem / per_split;
-  rem -= ksi * per_split;
-  const int g = rem / (tiles_m * tiles_n);
-  rem -= g * tiles_m * tiles_n;
-  const int tm = rem / tiles_n, tn = rem - tm * tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  // Resolve the problem's operands with selects (a dynamically indexed kernarg
-  // struct would be copied to scratch).
-  const bool p1 = pi != 0;
-  const Operand oa0 = p1 ? p.prob[1].a[0] : p.prob[0].a[0];
-  const Operand oa1 = p1 ? p.prob[1].a[1] : p.prob[0].a[1];
-  const Operand ob0 = p1 ? p.prob[1].b[0] : p.prob[0].b[0];
-  const Operand ob1 = p1 ? p.prob[1].b[1] : p.prob[0].b[1];
-  void* cptr = p1 ? p.prob[1].c : p.prob[0].c;
-  if constexpr (EPI == EPI_F32) cptr = reinterpret_cast<float*>(cptr) + ksi * p.split_stride;
-  if constexpr (EPI == EPI_BF16) cptr = reinterpret_cast<uint16_t*>(cptr) + ksi * p.split_stride;
-  const float alpha = p1 ? p.prob[1].alpha : p.prob[0].alpha;
-
-  // Only the weight-gradient style epilogues take a second K segment (K-concat);
-  // the fused forward epilogues never do, and skipping its offsets saves VGPRs.
-  constexpr bool SEG2 = (EPI == EPI_F32 || EPI == EPI_BF16 || EPI == EPI_ADAM);
-  constexpr bool ENC = (EPI == EPI_ENC || EPI == EPI_ENC_CNT || EPI == EPI_ENC_ACT);
-  const int nk1 = p.K1 / BKT, nk_all = nk1 + (SEG2 ? p.K2 / BKT : 0);
-  // this block's K-tile range [kbeg, nk) (the whole range unless split-K)
-  const int kbeg = (int)(((long)ksi * nk_all) / p.ksplit);
-  const int nk = (int)(((long)(ksi + 1) * nk_all) / p.ksplit);
-  // per-lane DMA source offsets for both K segments
-  uint32_t va0[PPWA], vb0[PPWB], va1[SEG2 ? PPWA : 1], vb1[SEG2 ? PPWB : 1];
-  piece_offsets<AK, BKT, PPWA>(va0, oa0.ld, m0, wid, lane);
-  piece_offsets<BKM, BKT, PPWB>(vb0, ob0.ld, n0, wid, lane);
-  if constexpr (SEG2) {
-    piece_offsets<AK, BKT, PPWA>(va1, oa1.ld, m0, wid, lane);
-    piece_offsets<BKM, BKT, PPWB>(vb1, ob1.ld, n0, wid, lane);
-  }
-  const i32x4_t ra0 = make_rsrc(oa0.ptr + (long)g * oa0.sg);
-  const i32x4_t rb0 = make_rsrc(ob0.ptr + (long)g * ob0.sg);
-  const i32x4_t ra1 = make_rsrc(oa1.ptr + (long)g * oa1.sg);
-  const i32x4_t rb1 = make_rsrc(ob1.ptr + (long)g * ob1.sg);
-  // soffset advance per K-tile: K-major operands step BKT elements, M/N-major BKT rows
-  const uint32_t sa0 = AK ? BKT * 2 : (uint32_t)(BKT * oa0.ld * 2), sa1 = AK ? BKT * 2 : (uint32_t)(BKT * oa1.ld * 2);
-  const uint32_t sb0 = BKM ? BKT * 2 : (uint32_t)(BKT * ob0.ld * 2), sb1 = BKM ? BKT * 2 : (uint32_t)(BKT * ob1.ld * 2);
-
-#define SC_ISSUE(t)                                                              \
-  do {                                                                           \
-    char* dst_ = smem + ((t) % NST) * STG;                                       \
-    if (!SEG2 || (t) < nk1) {                                                    \
-      issue_pieces<PPWA>(ra0, va0, (uint32_t)(t) * sa0, dst_, wid);              \
-      issue_pieces<PPWB>(rb0, vb0, (uint32_t)(t) * sb0, dst_ + TA, wid);         \
-    } else if constexpr (SEG2) {                                                 \
-      issue_pieces<PPWA>(ra1, va1, (uint32_t)((t) - nk1) * sa1, dst_, wid);      \
-      issue_pieces<PPWB>(rb1, vb1, (uint32_t)((t) - nk1) * sb1, dst_ + TA, wid); \
-    }                                                                            \
-  } while (0)
-
-  f32x4_t acc[WI][WJ];
-#pragma unroll
-  for (int i = 0; i < WI; ++i)
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  // acc[i][j][r] = C[row][col0 + r] with row = m0 + wr*16WI + i*16 + (lane&15),
-  // col0 = n0 + wc*16WJ + j*16 + 4*(lane>>4).
-  const int rowb = m0 + wr * (WI * 16) + (lane & 15);
-  const int colb = n0 + wc * (WJ * 16) + 4 * (lane >> 4);
-  // The DEC / DC epilogues read a bf16 tile of x / c at the output positions:
-  // fetch it before the K loop so its HBM latency hides under the MFMAs (small
-  // per-wave tiles only; at 128x64 per wave the registers are needed by the loop).
-  constexpr bool AUX_EARLY = (EPI == EPI_DEC || EPI == EPI_DC || EPI == EPI_DC_ACT) && WI * WJ <= 16;
-  uint2 auxv[WI][WJ];
-  if constexpr (AUX_EARLY) {
-    const uint16_t* X = p.aux + (long)g * p.saux;
-#pragma unroll
-    for (int i = 0; i < WI; ++i)
-#pragma unroll
-      for (int j = 0; j < WJ; ++j)
-        auxv[i][j] = *reinterpret_cast<const uint2*>(X + (long)(rowb + i * 16) * p.ldaux + colb + j * 16);
-  }
-
-#pragma unroll
-  for (int t = 0; t < NST - 1; ++t)
-    if (kbeg + t < nk) SC_ISSUE(kbeg + t);
-
-  for (int kt = kbeg; kt < nk; ++kt) {
-    // Tile kt must have landed; tiles kt+1 .. kt+NST-2 may stay in flight.
-    const int younger = min(NST - 2, nk - 1 - kt);
-    if constexpr (NST >= 4) {
-      if (younger >= 2) wait_vmcnt<2 * LPT>();
-      else if (younger == 1) wait_vmcnt<LPT>();
-      else wait_vmcnt<0>();
-    } else if constexpr (NST == 3) {
-      if (younger >= 1) wait_vmcnt<LPT>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    // lgkmcnt(0): this wave's reads of the stage being recycled are done; raw barrier
-    // (no implicit vmcnt(0)) so younger DMAs stay in flight; "memory" keeps hipcc from
-    // moving LDS reads across it.
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (kt + NST - 1 < nk) SC_ISSUE(kt + NST - 1);
-    const char* la = smem + (kt % NST) * STG;
-    const char* lb = la + TA;
-#pragma unroll
-    for (int ks = 0; ks < BKT / 32; ++ks) {
-      bf16x8_t fa[WI], fb[WJ];
-#pragma unroll
-      for (int j = 0; j < WJ; ++j) fb[j] = load_frag<BKM, BKT>(lb, wc * (WJ * 16) + j * 16, ks, lane);
-#pragma unroll
-      for (int i = 0; i < WI; ++i) fa[i] = load_frag<AK, BKT>(la, wr * (WI * 16) + i * 16, ks, lane);
-      // Operands swapped (B-side rows as the MFMA's A): each lane then holds
-      // 4 consecutive OUTPUT COLUMNS of one output row, so the epilogue
-      // issues 8/16-byte vector stores instead of 2-byte scatters.
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < WI; ++i)
-#pragma unroll
-        for (int j = 0; j < WJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  }
-#undef SC_ISSUE
-  __syncthreads();  // all reads of the ring done before smem is reused below
-
-  // ------------------------------------------------------------------ epilogue
-  float* red = reinterpret_cast<float*>(smem);  // free after the barrier above
-
-  if constexpr (EPI == EPI_F32) {
-    float* C = reinterpret_cast<float*>(cptr) + (long)g * p.sc;
-#pragma unroll
-    for (int i = 0; i < WI; ++i)
-#pragma unroll
-      for (int j = 0; j < WJ; ++j) {
-        const f32x4_t v = acc[i][j] * alpha;
-        *reinterpret_cast<f32x4_t*>(C + (long)(rowb + i * 16) * p.ldc + colb + j * 16) = v;
-      }
-    return;
-  }
-  if constexpr (EPI == EPI_BF16) {
-    uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-#pragma unroll
-    for (int i = 0; i < WI; ++i)
-#pragma unroll
-      for (int j = 0; j < WJ; ++j) {
-        ushort4 h;
-        h.x = f2bf(alpha * acc[i][j][0]); h.y = f2bf(alpha * acc[i][j][1]);
-        h.z = f2bf(alpha * acc[i][j][2]); h.w = f2bf(alpha * acc[i][j][3]);
-        *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + colb + j * 16) = h;
-      }
-    return;
-  }
-  // Column partial sums (ENC: on-counts, DC: bias gradient) per 128-row slot, in
-  // two steps so no per-column array stays live across the epilogue: (1) right
-  // after fragment column j is produced, reduce its 4 columns over the lane's
-  // rows and the 16 lanes sharing them (xor shuffles) and park the result in LDS
-  // (region `slot` of `red`); (2) after a barrier, sum the wave rows of each
-  // 128-row slot and store one value per (slot, column).  Deterministic.
-  constexpr int WPS = PT / (WI * 16);  // wave rows per 128-row slot
-  auto colred_lane = [&](f32x4_t v, int j, int region) {
-    // sum over the 16 lanes of a DPP row (the fragment's 16 output rows): lane 15 ends
-    // with the total -- four DPP adds per value instead of four ds_bpermute shuffles
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = row16_scan(v[r]);
-    if ((lane & 15) == 15)
-      *reinterpret_cast<f32x4_t*>(red + region * (S::WGM * BN) + wr * BN + wc * (WJ * 16) + j * 16 +
-                                  4 * (lane >> 4)) = v;
-  };
-  auto colred_store = [&](float* dst, int region) {
-    const float* rr = red + region * (S::WGM * BN);
-    for (int idx = tid; idx < (BM / PT) * BN; idx += NT) {
-      const int s = idx / BN, col = idx - s * BN;
-      float v = 0.f;
-#pragma unroll
-      for (int w = 0; w < WPS; ++w) v += rr[(s * WPS + w) * BN + col];
-      dst[((long)g * ptm + m0 / PT + s) * p.N + n0 + col] = v;
-    }
-  };
-  // Scalar partials live on the 128x128 grid: the block total goes to its first
-  // sub-tile, the block's other sub-tiles get zero (consumers sum them all).
-  auto scalar_partial = [&](float* base, int nstat, int stat, float v) {
-    if (tid < (BM / PT) * (BN / PT)) {
-      const int sm = tid / (BN / PT), sn = tid - sm * (BN / PT);
-      base[((long)g * ptm * ptn + (m0 / PT + sm) * ptn + n0 / PT + sn) * nstat + stat] = tid == 0 ? v : 0.f;
-    }
-  };
-
-  if constexpr (ENC) {
-    uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-    const float* bias = p.bias + (long)g * p.sbias;
-    const int nact = p.nactive ? p.nactive[g] : p.N;  // masked SAEs: live columns [0, nact)
-    constexpr bool ACTV = EPI == EPI_ENC_ACT;
-    const int act = ACTV ? p.act : 0;  // compile-time 0 for the plain ReLU instantiations
-    const bool counting = EPI == EPI_ENC_CNT || (ACTV && p.colpart != nullptr);
-    float l1 = 0.f, l0 = 0.f;
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) {
-      const int col = colb + j * 16;
-      const f32x4_t bj = *reinterpret_cast<const f32x4_t*>(bias + col);
-      f32x4_t s2 = f32x4_t{1.f, 1.f, 1.f, 1.f}, is2 = s2;
-      if (ACTV && act == 2) {
-        s2 = *reinterpret_cast<const f32x4_t*>(p.ascale + (long)g * p.sbias + col);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) is2[r] = 1.f / fmaxf(s2[r], 1e-8f);
-      }
-      f32x4_t cnt = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < WI; ++i) {
-        f32x4_t v;
-        bool on[4], rampv[4] = {false, false, false, false};
-        if constexpr (ACTV) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pre = acc[i][j][r] + bj[r];
-            if (act == 1) {
-              v[r] = pre > 0.f ? acc[i][j][r] : 0.f;  // relu(pre) - b on the active codes
-            } else if (act == 2) {
-              const float u = pre * is2[r];
-              v[r] = (fminf(fmaxf(10.f * (u - 0.9f), 0.f), 1.f) + fmaxf(u - 1.f, 0.f)) * s2[r];
-              rampv[r] = u < 1.f;
-            } else {
-              v[r] = fmaxf(pre, 0.f);
-            }
-            const bool live = col + r < nact;
-            on[r] = live && (act == 1 ? pre > 0.f : v[r] > 0.f);
-            rampv[r] = rampv[r] && on[r];
-            v[r] = live ? v[r] : 0.f;
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            l1 += fabsf(v[r]);
-            const float onf = on[r] ? 1.f : 0.f;
-            l0 += onf;
-            cnt[r] += onf;
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[i][j][r] + bj[r], 0.f);
-          // branch-free (a block-uniform `if (masked)` made hipcc version the whole
-          // epilogue and spill at 128x64 per wave)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (col + r < nact) ? v[r] : 0.f;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            l1 += v[r];
-            on[r] = v[r] > 0.f;
-            const float onf = on[r] ? 1.f : 0.f;
-            l0 += onf;
-            cnt[r] += onf;
-          }
-        }
-        *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + col) =
-            make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
-        if (p.cmask) {  // block-uniform
-          const uint64_t b0 = __ballot(on[0]), b1 = __ballot(on[1]);
-          const uint64_t b2 = __ballot(on[2]), b3 = __ballot(on[3]);
-          const long frag = ((long)g * (p.M >> 4) + ((rowb + i * 16) >> 4)) * (p.N >> 4) + ((colb + j * 16) >> 4);
-          if (lane == 0) {
-            u32x4_t* dst = reinterpret_cast<u32x4_t*>(p.cmask + frag * 4);
-            dst[0] = u32x4_t{(uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32)};
-            dst[1] = u32x4_t{(uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32)};
-          }
-          if (ACTV && act == 2 && p.cmask2) {  // ramp bits of the threshold activation
-            const uint64_t q0 = __ballot(rampv[0]), q1 = __ballot(rampv[1]);
-            const uint64_t q2 = __ballot(rampv[2]), q3 = __ballot(rampv[3]);
-            if (lane == 0) {
-              u32x4_t* dst = reinterpret_cast<u32x4_t*>(p.cmask2 + frag * 4);
-              dst[0] = u32x4_t{(uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32)};
-              dst[1] = u32x4_t{(uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)q3, (uint32_t)(q3 >> 32)};
-            }
-          }
-        }
-      }
-      if (counting) colred_lane(cnt, j, 0);
-    }
-    l1 = block_sum<NW>(l1, red + 4096);  // its barriers also publish the colred_lane writes
-    l0 = block_sum<NW>(l0, red + 4096);
-    if (counting) colred_store(p.colpart, 0);
-    scalar_partial(p.part, 2, 0, l1);
-    scalar_partial(p.part, 2, 1, l0);
-    return;
-  }
-  if constexpr (EPI == EPI_DEC) {
-    uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-    float se = 0.f;
-    const bool rcol = p.rcol != nullptr;  // fp32 column sums of R (learned-centering gradient)
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) {
-      f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < WI; ++i) {
-        const long row = rowb + i * 16;
-        const int col = colb + j * 16;
-        const uint2 xv = AUX_EARLY ? auxv[i][j]
-                                   : *reinterpret_cast<const uint2*>(p.aux + (long)g * p.saux + row * p.ldaux + col);
-        const float r0 = acc[i][j][0] - bf2f(xv.x & 0xFFFF), r1 = acc[i][j][1] - bf2f(xv.x >> 16);
-        const float r2 = acc[i][j][2] - bf2f(xv.y & 0xFFFF), r3 = acc[i][j][3] - bf2f(xv.y >> 16);
-        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) = make_ushort4(f2bf(r0), f2bf(r1), f2bf(r2), f2bf(r3));
-        se += r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
-        cs[0] += r0; cs[1] += r1; cs[2] += r2; cs[3] += r3;
-      }
-      if (rcol) colred_lane(cs, j, 0);
-    }
-    se = block_sum<NW>(se, red + 8192);  // its barriers also publish the colred_lane writes
-    if (rcol) colred_store(p.rcol, 0);
-    scalar_partial(p.part, 1, 0, se);
-    return;
-  }
-  if constexpr (EPI == EPI_DC) {
-    uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-    const float add = p.l1[g] * p.l1_add_scale;
-    const bool want_dot = p.dotpart != nullptr;
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) {
-      f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f}, ds = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const int col = colb + j * 16;
-      f32x4_t bj = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      if (p.dc_tied) bj = *reinterpret_cast<const f32x4_t*>(p.bias + (long)g * p.sbias + col);
-#pragma unroll
-      for (int i = 0; i < WI; ++i) {
-        const long row = rowb + i * 16;
-        const uint2 cv = AUX_EARLY ? auxv[i][j]
-                                   : *reinterpret_cast<const uint2*>(p.aux + (long)g * p.saux + row * p.ldaux + col);
-        const uint16_t cvs[4] = {(uint16_t)(cv.x & 0xFFFF), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xFFFF),
-                                 (uint16_t)(cv.y >> 16)};
-        f32x4_t dv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float c = bf2f(cvs[r]);
-          dv[r] = c > 0.f ? acc[i][j][r] + add : 0.f;  // c is a ReLU output
-          cs[r] += dv[r];
-          if (want_dot) {
-            // <w_hat_j, dL/dw_hat_j> (in units of 2/(B d)): decoder path c * (R w_hat^T),
-            // tied encoder path dpre * (x w_hat^T) = dpre * (pre - b) = dpre * (c - b)
-            ds[r] += c * acc[i][j][r] + (p.dc_tied ? dv[r] * (c - bj[r]) : 0.f);
-          }
-        }
-        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
-            make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
-      }
-      colred_lane(cs, j, 0);
-      if (want_dot) colred_lane(ds, j, 1);
-    }
-    __syncthreads();
-    colred_store(p.colpart, 0);
-    if (want_dot) colred_store(p.dotpart, 1);
-    return;
-  }
-  if constexpr (EPI == EPI_DC_MASK) {
-    // EPI_DC with the code activity read from the encoder's bitmask (no norm-Jacobian dots)
-    uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-    const float add = p.l1[g] * p.l1_add_scale;
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) {
-      f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const int col = colb + j * 16;
-#pragma unroll
-      for (int i = 0; i < WI; ++i) {
-        const long row = rowb + i * 16;
-        const long frag = ((long)g * (p.M >> 4) + ((rowb + i * 16) >> 4)) * (p.N >> 4) + (col >> 4);
-        const uint64_t* mk = p.cmask + frag * 4;  // wave-uniform address
-        f32x4_t dv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool on = (mk[r] >> lane) & 1ull;
-          dv[r] = on ? acc[i][j][r] + add : 0.f;
-          cs[r] += dv[r];
-        }
-        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
-            make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
-      }
-      colred_lane(cs, j, 0);
-    }
-    __syncthreads();
-    colred_store(p.colpart, 0);
-    return;
-  }
-  if constexpr (EPI == EPI_DC_ACT) {
-    // Code gradient of the reverse / threshold activations: activity from the encoder's
-    // bitmask, the codes themselves (aux) for the L1 sign (reverse codes can be negative)
-    // and the threshold's slope.  Threshold: thr' = 10 on the ramp (c / s^2 < 1), 1 above;
-    // region 1 collects sum_b dL/dc * (thr - u thr') = -9 dL/dc on the ramp (the s^2
-    // gradient: dL/ds = 2 s * that); reverse SAEs get no bias gradient (column sums 0).
-    uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-    const float add = p.l1[g] * p.l1_add_scale;
-    const int act = p.act;
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) {
-      f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f}, ds = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const int col = colb + j * 16;
-      f32x4_t is2 = f32x4_t{1.f, 1.f, 1.f, 1.f};
-      if (act == 2) {
-        const f32x4_t s2 = *reinterpret_cast<const f32x4_t*>(p.ascale + (long)g * p.sbias + col);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) is2[r] = 1.f / fmaxf(s2[r], 1e-8f);
-      }
-#pragma unroll
-      for (int i = 0; i < WI; ++i) {
-        const long row = rowb + i * 16;
-        const long frag = ((long)g * (p.M >> 4) + (row >> 4)) * (p.N >> 4) + (col >> 4);
-        const uint64_t* mk = p.cmask + frag * 4;  // wave-uniform address
-        const uint2 cv = AUX_EARLY ? auxv[i][j]
-                                   : *reinterpret_cast<const uint2*>(p.aux + (long)g * p.saux + row * p.ldaux + col);
-        const uint16_t cvs[4] = {(uint16_t)(cv.x & 0xFFFF), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xFFFF),
-                                 (uint16_t)(cv.y >> 16)};
-        f32x4_t dv;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool on = (mk[r] >> lane) & 1ull;
-          const float c = bf2f(cvs[r]);
-          if (act == 1) {
-            const float sgn = c > 0.f ? 1.f : (c < 0.f ? -1.f : 0.f);
-            dv[r] = on ? acc[i][j][r] + add * sgn : 0.f;
-          } else if (act == 2) {
-            const float dc = acc[i][j][r] + add;
-            // ramp bit from the encoder's fp32 decision; without it, from the bf16 code
-            const bool ramp = p.cmask2 ? (bool)((p.cmask2[frag * 4 + r] >> lane) & 1ull) : c * is2[r] < 1.f;
-            dv[r] = on ? dc * (ramp ? 10.f : 1.f) : 0.f;
-            cs[r] += dv[r];
-            ds[r] += (on && ramp) ? -9.f * dc : 0.f;
-          } else {
-            dv[r] = on ? acc[i][j][r] + add : 0.f;
-            cs[r] += dv[r];
-          }
-        }
-        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
-            make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
-      }
-      colred_lane(cs, j, 0);
-      colred_lane(ds, j, 1);
-    }
-    __syncthreads();
-    colred_store(p.colpart, 0);
-    if (p.dotpart) colred_store(p.dotpart, 1);
-    return;
-  }
-  if constexpr (EPI == EPI_ROWMAX) {
-    // max over this wave's columns of each output row, then over the four 16-lane groups
-    // holding the same row; one partial per (row, wave column) -> C[g][row][tn * WGN + wc]
-    float* C = reinterpret_cast<float*>(cptr) + (long)g * p.sc;
-    const long ldp = (long)tiles_n * WGN;
-#pragma unroll
-    for (int i = 0; i < WI; ++i) {
-      float mx = -3.0e38f;
-#pragma unroll
-      for (int j = 0; j < WJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, alpha * acc[i][j][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      if (lane < 16) C[(long)(rowb + i * 16) * ldp + tn * WGN + wc] = mx;
-    }
-    return;
-  }
-  if constexpr (EPI == EPI_ADAM) {
-    // Weight gradient -> Adam in registers; the fp32 gradient never touches HBM.
-    const AdamEpi E = p1 ? p.adam[1] : p.adam[0];
-    const long gb = (long)g * p.sc;
-    const float bc1 = 1.f - __powf(p.b1, (float)(*p.step + 1));
-    const float bc2 = 1.f - __powf(p.b2, (float)(*p.step + 1));
-    const float stp = p.lr[g] / bc1, rbc2 = 1.f / bc2, b1 = p.b1, b2 = p.b2, eps = p.eps;
-    float ca[WI], cp[WI];
-    if (E.mode) {
-      for (int r = tid; r < BM; r += NT) {
-        const int row = m0 + r;
-        float dsum = 0.f;
-        for (int t = 0; t < p.dot_tm; ++t) dsum += E.dotpart[((long)g * p.dot_tm + t) * p.M + row];
-        red[r] = dsum * p.dot_scale;
-        red[BM + r] = E.norms[(long)g * p.M + row];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < WI; ++i) {
-        const int lr_ = wr * (WI * 16) + i * 16 + (lane & 15);
-        const float dot = red[lr_], nrm = red[BM + lr_];
-        if (nrm > 1e-8f) {
-          const float inv = 1.f / nrm;
-          ca[i] = alpha * inv;      // dW = dW_hat / |w| - w <w_hat, dW_hat> / |w|^2
-          cp[i] = dot * inv * inv;
-        } else {
-          ca[i] = alpha * 1e8f;     // below the clamp floor the norm has zero derivative
-          cp[i] = 0.f;
-        }
-      }
-      __syncthreads();
-    } else {
-#pragma unroll
-      for (int i = 0; i < WI; ++i) { ca[i] = alpha; cp[i] = 0.f; }
-    }
-    float ss[WI];
-#pragma unroll
-    for (int i = 0; i < WI; ++i) ss[i] = 0.f;
-#pragma unroll
-    for (int i = 0; i < WI; ++i)
-#pragma unroll
-      for (int j = 0; j < WJ; ++j) {
-        const long off = gb + (long)(rowb + i * 16) * p.ldc + colb + j * 16;
-        f32x4_t pv = *reinterpret_cast<const f32x4_t*>(E.p + off);
-        f32x4_t mv = *reinterpret_cast<const f32x4_t*>(E.m + off);
-        f32x4_t vv = *reinterpret_cast<const f32x4_t*>(E.v + off);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float gr = acc[i][j][r] * ca[i] - pv[r] * cp[i];
-          mv[r] = b1 * mv[r] + (1.f - b1) * gr;
-          vv[r] = b2 * vv[r] + (1.f - b2) * gr * gr;
-          pv[r] -= stp * mv[r] / (sqrtf(vv[r] * rbc2) + eps);
-          ss[i] += pv[r] * pv[r];
-        }
-        *reinterpret_cast<f32x4_t*>(E.p + off) = pv;
-        *reinterpret_cast<f32x4_t*>(E.m + off) = mv;
-        *reinterpret_cast<f32x4_t*>(E.v + off) = vv;
-        *reinterpret_cast<ushort4*>(E.sh + off) = make_ushort4(f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3]));
-      }
-    if (E.mode) {
-      // partial |w_j|^2 over each 128-column slot -> sqpart[g][row][slot]
-      constexpr int WPC = PT / (WJ * 16);  // wave columns per 128-column slot
-#pragma unroll
-      for (int i = 0; i < WI; ++i) {
-        ss[i] += __shfl_xor(ss[i], 16, 64);
-        ss[i] += __shfl_xor(ss[i], 32, 64);
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int i = 0; i < WI; ++i) red[wc * BM + wr * (WI * 16) + i * 16 + lane] = ss[i];
-      }
-      __syncthreads();
-      for (int idx = tid; idx < (BN / PT) * BM; idx += NT) {
-        const int s = idx / BM, row = idx - s * BM;
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < WPC; ++w) v += red[(s * WPC + w) * BM + row];
-        E.sqpart[((long)g * p.M + m0 + row) * ptn + n0 / PT + s] = v;
-      }
-    }
-    return;
-  }
-}
-
-}  // namespace scamd
+#include <stdlib.h>
 
 using namespace scamd;
 
 namespace {
 
-template <class S>
-bool fits(int M, int N) { return M % S::BM == 0 && N % S::BN == 0; }
-
-template <class S>
-long n_blocks(int M, int N, int G, int nprob) { return (long)(M / S::BM) * (N / S::BN) * G * nprob; }
-
-// FULL = every (layout, epilogue) pair; the alternative K pipelines (deeper LDS rings,
-// selected with cfg bits 2-3) instantiate only the step's epilogues and the weight-gradient
-// layout, to keep the build small.
-template <class S, int BKT, int NST, bool FULL = true>
-int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
-  const dim3 grid((unsigned)(n_blocks<S>(p.M, p.N, p.G, nprob) * p.ksplit)), block(S::NT);
-  if constexpr (!FULL) {
-    if (epi == EPI_ADAM || epi == EPI_BF16 || epi >= EPI_ENC_ACT || (epi == EPI_F32 && (ak || bk))) return 8;
-  }
-#define SC_L(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_kernel<S, AKV, BKV, E, BKT, NST>), grid, block, 0, stream, p)
-  // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
-  // epilogues; the plain F32 / BF16 epilogues exist for every layout.
+// Persistent 128x128 launch (sae_gemm_pt_kernel): grid = workgroups resident at once (2 per
+// CU at NST 2, 1 at NST 3), each looping over tiles with a continuous LDS-DMA stream.
+template <int NST>
+int launch_pt(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
+  const long total = n_blocks<S128>(p.M, p.N, p.G, nprob);
+  const long slots = (NST == 2 ? 2 : 1) * 256;
+  const dim3 grid((unsigned)(total < slots ? total : slots)), block(S128::NT);
+#define SC_LP(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_pt_kernel<S128, AKV, BKV, E, NST>), grid, block, 0, stream, p)
   switch (epi) {
-    case EPI_ENC: if (!(ak && bk)) return 5; SC_L(true, true, EPI_ENC); break;
-    case EPI_ENC_CNT: if (!(ak && bk)) return 5; SC_L(true, true, EPI_ENC_CNT); break;
-    case EPI_DEC: if (!(ak && !bk)) return 5; SC_L(true, false, EPI_DEC); break;
-    case EPI_DC: if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC); break;
-    case EPI_DC_MASK: if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC_MASK); break;
-    case EPI_ENC_ACT:
-      if constexpr (FULL) { if (!(ak && bk)) return 5; SC_L(true, true, EPI_ENC_ACT); }
-      break;
-    case EPI_DC_ACT:
-      if constexpr (FULL) { if (!(ak && bk)) return 5; SC_L(true, true, EPI_DC_ACT); }
-      break;
-    case EPI_ROWMAX:
-      if constexpr (FULL) { if (!(ak && bk)) return 5; SC_L(true, true, EPI_ROWMAX); }
-      break;
-    case EPI_ADAM:
-      if constexpr (FULL) { if (ak || bk) return 5; SC_L(false, false, EPI_ADAM); }
-      break;
+    case EPI_ENC: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_ENC); break;
+    case EPI_ENC_CNT: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_ENC_CNT); break;
+    case EPI_ENC_ACT: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_ENC_ACT); break;
+    case EPI_DEC: if (!(ak && !bk)) return 5; SC_LP(true, false, EPI_DEC); break;
+    case EPI_DC_MASK: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_DC_MASK); break;
+    case EPI_DC_ACT: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_DC_ACT); break;
     case EPI_F32:
-      if constexpr (FULL) {
-        if (ak && bk) SC_L(true, true, EPI_F32);
-        else if (ak) SC_L(true, false, EPI_F32);
-        else if (bk) SC_L(false, true, EPI_F32);
-        else SC_L(false, false, EPI_F32);
-      } else {
-        SC_L(false, false, EPI_F32);
-      }
+      if (ak && bk) SC_LP(true, true, EPI_F32);
+      else if (ak) SC_LP(true, false, EPI_F32);
+      else if (bk) SC_LP(false, true, EPI_F32);
+      else SC_LP(false, false, EPI_F32);
       break;
     case EPI_BF16:
-      if constexpr (FULL) {
-        if (ak && bk) SC_L(true, true, EPI_BF16);
-        else if (ak) SC_L(true, false, EPI_BF16);
-        else if (bk) SC_L(false, true, EPI_BF16);
-        else SC_L(false, false, EPI_BF16);
-      }
+      if (ak && bk) SC_LP(true, true, EPI_BF16);
+      else if (ak) SC_LP(true, false, EPI_BF16);
+      else if (bk) SC_LP(false, true, EPI_BF16);
+      else SC_LP(false, false, EPI_BF16);
       break;
-    default: return 2;
+    default: return 9;
   }
-#undef SC_L
+#undef SC_LP
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -699,8 +73,10 @@ int sc_gemm_shape(int M, int N, int G, int nprob) {
 }
 
 // layout: bit0 = A is K-major, bit1 = B is K-major.
-// cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256;
-// bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4, 2: BK32 x 2, 3: BK32 x 3).
+// cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256; bit 4 (128x128
+// only): persistent tile loop with a continuous LDS-DMA stream (sae_gemm_pt_kernel);
+// bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4 (128x128 blocks: BK64 x 3),
+// 2: BK32 x 2, 3: BK32 x 3).
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             const ScOperand* a /* [nprob][2] */, const ScOperand* b /* [nprob][2] */,
             void* const* c /* [nprob] */, const float* alpha /* [nprob] */, long ldc, long sc,
@@ -742,6 +118,8 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   if (epi == EPI_ADAM && (!adam || !lr || !step)) return 4;
   p.lr = lr; p.step = step; p.b1 = b1; p.b2 = b2; p.eps = eps; p.dot_tm = dot_tm; p.dot_scale = dot_scale;
   p.ksplit = ksplit; p.split_stride = split_stride;
+  static const int dbg = getenv("SC_GEMM_DBG") ? atoi(getenv("SC_GEMM_DBG")) : 0;
+  p.dbg = dbg;
   p.act = act; p.ascale = ascale;
   p.cmask2 = reinterpret_cast<uint64_t*>(cmask2); p.rcol = rcol;
   const bool ak = layout & 1, bk = layout & 2;
@@ -751,16 +129,16 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   switch (shape) {
     case 3:
       if (!fits<S256>(M, N)) return 6;
-      if (pipe == 1) return launch<S256, 32, 4, false>(epi, ak, bk, p, nprob, stream);
-      if (pipe == 3) return launch<S256, 32, 3, false>(epi, ak, bk, p, nprob, stream);
-      if (pipe == 2) return launch<S256, 32, 2, false>(epi, ak, bk, p, nprob, stream);
-      return launch<S256, 64, 2>(epi, ak, bk, p, nprob, stream);
+      return launch_big(3, pipe, epi, ak, bk, p, nprob, stream);
     case 2:
       if (!fits<S256x128>(M, N)) return 6;
-      if (pipe) return 8;
-      return launch<S256x128, 64, 2>(epi, ak, bk, p, nprob, stream);
+      return launch_big(2, pipe, epi, ak, bk, p, nprob, stream);
     default:
-      if (pipe == 1) return launch<S128, 32, 4, false>(epi, ak, bk, p, nprob, stream);
+      if (cfg & 16) {  // persistent tile loop (BK64 rings only, no split-K)
+        if (ksplit != 1 || (pipe != 0 && pipe != 1)) return 9;
+        return pipe == 1 ? launch_pt<3>(epi, ak, bk, p, nprob, stream) : launch_pt<2>(epi, ak, bk, p, nprob, stream);
+      }
+      if (pipe == 1) return launch<S128, 64, 3, false>(epi, ak, bk, p, nprob, stream);  // 96 KB: 1 block/CU
       if (pipe == 2) return launch<S128, 32, 2, false>(epi, ak, bk, p, nprob, stream);  // 32 KB: 4-5 blocks/CU
       if (pipe == 3) return launch<S128, 32, 3, false>(epi, ak, bk, p, nprob, stream);
       return launch<S128, 64, 2>(epi, ak, bk, p, nprob, stream);

@@ -31,10 +31,10 @@ from .dist import DistInfo
 
 
 def _check_kind(engine):
-    # the threshold SAE's scale / centering gradients are reduced inside the engine's own
-    # update, not through the flat gradient buffer these wrappers all-reduce
-    if getattr(engine, "kind", None) == "threshold" or getattr(engine, "learned_center", False):
-        raise NotImplementedError("data-parallel threshold SAEs: use ensemble sharding (parallel='es')")
+    # threshold / learned-centering SAEs carry their scale / centering gradient sources in the
+    # same flat buffer (engine._g_flat), so every fused kind reduces with the same collectives
+    if getattr(engine, "kind", None) not in ("untied", "tied", "reverse", "threshold"):
+        raise NotImplementedError(f"data-parallel fused training of kind {getattr(engine, 'kind', None)}")
 
 
 class DataParallelFused:

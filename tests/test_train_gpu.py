@@ -124,7 +124,14 @@ def test_huge_batch_fused_reinit(tmp_path):
     assert sd["encoder"].shape == (256, 512) and sd["decoder"].shape == (512, 256)
 
 
-def _dp_gpu_worker(rank, world, port, x, init, q):
+def _sig(kind):
+    from sparse_coding__amd.models import signatures as S
+
+    return {"untied": S.FunctionalSAE, "threshold": S.FunctionalThresholdingSAE,
+            "tied_centered": S.FunctionalTiedCenteredSAE, "tied": S.FunctionalTiedSAE}[kind]
+
+
+def _dp_gpu_worker(rank, world, port, x, init, kind, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     from sparse_coding__amd.engine.fused import FusedSAEEnsemble
@@ -134,22 +141,25 @@ def _dp_gpu_worker(rank, world, port, x, init, q):
     info = init_distributed("gloo", device="cuda:0")  # two ranks share the box's one GPU; gloo moves CUDA tensors
     torch.manual_seed(300 + rank)
     models = [({k: v.cuda() for k, v in p.items()}, {k: v.cuda() for k, v in b.items()}) for p, b in init]
-    if rank:
+    if rank:  # rank 0's parameters must win the initial broadcast
         models = [(dict((k, torch.randn_like(v)) for k, v in p.items()), b) for p, b in models]
-    engines = [FusedSAEEnsemble(m, FunctionalSAE, lr=1e-3, batch_size=x.shape[0] // world, device="cuda:0")
+    engines = [FusedSAEEnsemble(m, _sig(kind), lr=1e-3, batch_size=x.shape[0] // world, device="cuda:0")
                for m in split_models(models, 2)]
     dp = ChunkedDataParallel([FusedChunk(e) for e in engines], info)
     xs = x.cuda().chunk(world)[rank].contiguous()
     for _ in range(3):
         dp.step_batch(xs)
     torch.cuda.synchronize()
-    q.put((rank, torch.cat([e.params["decoder"] for e in engines]).cpu().numpy()))
+    q.put((rank, {k: torch.cat([e.params[k] for e in engines]).cpu().numpy() for k in engines[0].params}))
     shutdown(info)
 
 
-def test_chunked_dp_fused_two_ranks_one_gpu():
-    """Two gloo ranks sharing cuda:0 run the chunk-pipelined fused DP step; replicas stay
-    identical and match single-process training on the global batch."""
+@pytest.mark.parametrize("kind", ["untied", "threshold", "tied_centered"])
+def test_chunked_dp_fused_two_ranks_one_gpu(kind):
+    """Two gloo ranks sharing cuda:0 run the chunk-pipelined fused DP step (every fused kind,
+    including the threshold SAE's scale / centering and the learned center, whose gradient
+    sources ride in the same flat all-reduce buffer); replicas stay identical and match
+    single-process training on the global batch."""
     import socket
 
     import torch.multiprocessing as mp
@@ -158,11 +168,12 @@ def test_chunked_dp_fused_two_ranks_one_gpu():
 
     torch.manual_seed(0)
     d, n, B = 256, 512, 512
-    init = [FunctionalSAE.init(d, n, l1) for l1 in (1e-4, 3e-4, 1e-3, 2e-3)]
+    sig = _sig(kind)
+    init = [sig.init(d, n, l1) for l1 in (1e-4, 3e-4, 1e-3, 2e-3)]
     feats = torch.nn.functional.normalize(torch.randn(1024, d), dim=-1)
-    x = (torch.relu(torch.randn(B, 1024) - 2.0) @ feats).to(torch.bfloat16)
+    x = (torch.relu(torch.randn(B, 1024) - 2.0) @ feats + 0.1).to(torch.bfloat16)
     ref = FusedSAEEnsemble([({k: v.cuda() for k, v in p.items()}, {k: v.cuda() for k, v in b.items()})
-                            for p, b in init], FunctionalSAE, lr=1e-3, batch_size=B, device="cuda:0")
+                            for p, b in init], sig, lr=1e-3, batch_size=B, device="cuda:0")
     for _ in range(3):
         ref.step_batch(x.cuda())
     torch.cuda.synchronize()
@@ -172,20 +183,21 @@ def test_chunked_dp_fused_two_ranks_one_gpu():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dp_gpu_worker, args=(r, 2, port, x, init, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_gpu_worker, args=(r, 2, port, x, init, kind, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    np.testing.assert_array_equal(res[0], res[1])
-    want = ref.params["decoder"].cpu().numpy()
-    # bf16 GEMM partial sums differ between the half batches and the full batch: compare updates
-    init_dec = np.stack([p["decoder"].numpy() for p, _ in init])
-    du, dr = (res[0] - init_dec).ravel(), (want - init_dec).ravel()
-    cos = float(du @ dr / (np.linalg.norm(du) * np.linalg.norm(dr)))
-    assert cos > 0.99, cos
+    for k in res[0]:
+        np.testing.assert_array_equal(res[0][k], res[1][k])
+        want = ref.params[k].cpu().numpy()
+        # bf16 GEMM partial sums differ between the half batches and the full batch: compare updates
+        init_k = np.stack([p[k].numpy() for p, _ in init])
+        du, dr = (res[0][k] - init_k).ravel(), (want - init_k).ravel()
+        cos = float(du @ dr / (np.linalg.norm(du) * np.linalg.norm(dr) + 1e-30))
+        assert cos > 0.99, (k, cos)
 
 
 def test_sweep_cli_ensemble_sharded_rccl(tmp_path):
