@@ -90,6 +90,9 @@ def parse(argv=None):
                     help="N>1: after the headline run, also time the other strategy (es <-> dp) and report it "
                          "under alt_parallelism")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of a HIP graph")
+    ap.add_argument("--fuse-adam", type=int, default=-1,
+                    help="1: Adam inside the weight-gradient GEMM epilogue (single GPU); 0: separate streaming "
+                         "Adam kernel; -1: the engine default")
     return ap.parse_args(argv)
 
 
@@ -157,7 +160,8 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
     if args.engine == "fused":
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
 
-        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
+        kw = {} if args.fuse_adam < 0 else {"fuse_adam": bool(args.fuse_adam)}
+        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device, **kw)
         if not args.no_graph:
             eng.enable_graph()  # whole step = one HIP graph replay
 

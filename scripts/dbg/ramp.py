@@ -1,6 +1,6 @@
 """Debug: threshold-activation ramp bits (cmask2) of the persistent vs the tile kernel."""
 import sys, os
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from sparse_coding__amd.ops import gemm
 

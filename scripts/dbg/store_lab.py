@@ -1,7 +1,7 @@
 """Where does the plain bf16 grouped GEMM spend its time: output stores vs main loop?
 Run twice: SC_GEMM_DBG=0 (normal) and SC_GEMM_DBG=1 (EPI_BF16 skips its stores)."""
 import json, os, statistics, sys
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from sparse_coding__amd.ops import gemm
 

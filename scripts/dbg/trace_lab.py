@@ -1,7 +1,7 @@
 """Kernel-trace lab: run each case N times (one sc_gemm dispatch per call); the case order
 goes to stdout so rocprofv3's kernel trace can be split per case (scripts/dbg/trace_split.py)."""
 import os, sys, json
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from sparse_coding__amd.ops import gemm
 

@@ -107,8 +107,8 @@ def main():
     }
     gemm.encode_relu(x, we, bias, c, part, None, None, mask_out=cmask)
     modes = [("tile", lambda: gemm.force_persistent(False)),
-             ("p3", lambda: gemm.force_persistent(True, nst=3)),
-             ("p4", lambda: gemm.force_persistent(True, nst=4))]
+             ("p2", lambda: gemm.force_persistent(True, nst=2)),
+             ("p3", lambda: gemm.force_persistent(True, nst=3))]
     if a.cfgs:  # explicit tile-kernel configurations (block shape | pipeline << 2) instead
         modes = [(f"cfg{c}", lambda c=int(c): gemm.force_shape(c)) for c in a.cfgs.split(",")]
     cases["step_torch_enc"] = (lambda: torch.matmul(x, we.transpose(1, 2), out=c), fl)

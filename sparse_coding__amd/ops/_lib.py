@@ -33,18 +33,6 @@ class ScAdamEpi(C.Structure):
                 ("dotpart", c_void_p), ("norms", c_void_p), ("sqpart", c_void_p), ("mode", c_int)]
 
 
-class ScGemmArgs(C.Structure):
-    """Arguments of the persistent GEMM (``sc_gemm_p``, csrc/sae_gemm_p.hip)."""
-    _fields_ = [("epi", c_int), ("layout", c_int), ("nprob", c_int), ("M", c_int), ("N", c_int),
-                ("K1", c_int), ("K2", c_int), ("G", c_int),
-                ("a", ScOperand * 4), ("b", ScOperand * 4), ("c", c_void_p * 2), ("alpha", c_float * 2),
-                ("ldc", c_long), ("sc", c_long), ("bias", c_void_p), ("sbias", c_long), ("nactive", c_void_p),
-                ("aux", c_void_p), ("ldaux", c_long), ("saux", c_long), ("part", c_void_p),
-                ("colpart", c_void_p), ("l1", c_void_p), ("l1_add_scale", c_float), ("dotpart", c_void_p),
-                ("cmask", c_void_p), ("cmask2", c_void_p), ("rcol", c_void_p), ("act", c_int),
-                ("ascale", c_void_p), ("nst", c_int), ("max_blocks", c_int)]
-
-
 class KernelError(RuntimeError):
     pass
 
@@ -80,7 +68,6 @@ def _declare(lib):
         "sc_fista_gram": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_void_p],
         "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_void_p],
-        "sc_gemm_p": [C.POINTER(ScGemmArgs), c_void_p],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)

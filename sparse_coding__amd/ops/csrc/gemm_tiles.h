@@ -1,5 +1,5 @@
 // Grouped-GEMM building blocks shared by the tile kernels (sae_gemm.hip) and the
-// persistent kernel (sae_gemm_p.hip): kernel parameters, LDS image layouts, the LDS-DMA
+// persistent tile loop (sae_gemm_kernel.h): kernel parameters, LDS image layouts, the LDS-DMA
 // staging primitives and the MFMA fragment reads.  gfx950 only.
 #pragma once
 #include "common.h"
@@ -23,12 +23,26 @@ constexpr int PT = 128;
 enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5, EPI_ENC_CNT = 6,
        EPI_DC_MASK = 7, EPI_ENC_ACT = 8, EPI_DC_ACT = 9, EPI_ROWMAX = 10 };
 
-// Activity bitmask of the codes, in MFMA-fragment order: for the 16x16 output fragment at
-// (row/16, col/16) the encoder epilogue stores its four wave ballots (bit l of word r: lane
-// l's value r, i.e. output row 16 i + (l & 15), column 16 j + 4 (l >> 4) + r, is > 0).  The
-// code-gradient epilogue only needs 1[c > 0]: reading these 32 bytes per fragment instead
-// of the bf16 codes (512 bytes) removes B n G x 2 bytes of HBM reads per step.
-// Layout [G][B/16][n/16][4] uint64; every GEMM block shape uses the same fragment map.
+// Activity bitmask of the codes: see mask_bit() in sae_gemm_kernel.h (one 64-bit word per lane
+// per 64x64 block, written by the encoder epilogue, read by the code-gradient epilogue instead
+// of the bf16 codes -- 1/16 of the bytes).
+
+// Division by a launch-constant divisor without the ~30-instruction integer-division
+// sequence: q = (umulhi(n, m) + n) >> s with m, s computed on the host (round-up method,
+// exact for n < 2^31).  The tile decomposition of every block is on its critical path
+// (nothing is loaded until it is done), so it must be a handful of SALU ops.
+struct FDiv {
+  uint32_t m, s;
+};
+__host__ __device__ inline FDiv make_fdiv(uint32_t d) {
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  const uint64_t m = ((((1ull << s) - d) << 32) / d) + 1;
+  return FDiv{(uint32_t)m, s};
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FDiv f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
 
 struct Operand {
   const uint16_t* ptr;
@@ -92,6 +106,8 @@ struct GemmParams {
   int ksplit;
   long split_stride;
   int dbg;  // diagnostics (SC_GEMM_DBG): bit 0 = EPI_BF16 skips its output stores
+  // host-precomputed divisors of the block -> tile decomposition (set by the launcher)
+  FDiv f_prob, f_split, f_plane, f_tn, f_ksplit;
   // --- EPI_ENC_ACT / EPI_DC_ACT: activation mode and the threshold SAE's per-feature s^2
   int act;
   const float* ascale;  // [G][N] (group stride sbias)
@@ -143,13 +159,14 @@ __device__ __forceinline__ void piece_offsets(uint32_t (&voff)[PPW], long ld, in
       const int row = piece * RPP + lane / LPR;
       const int slot = lane % LPR;
       const int ch = (BKT == 64) ? (slot ^ ((row >> 1) & 7)) : (slot ^ (((row >> 2) & 1) << 1));
-      voff[i] = (uint32_t)(((long)(r0 + row) * ld + ch * 8) * 2);
+      // 32-bit: the buffer offset is 32-bit anyway (one group operand < 4 GiB)
+      voff[i] = ((uint32_t)(r0 + row) * (uint32_t)ld + (uint32_t)(ch * 8)) * 2u;
     } else {
       constexpr int PPH = BKT / 4;  // pieces per 128-column half
       const int half = piece / PPH;
       const int row = (piece % PPH) * 4 + (lane >> 4);
       const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-      voff[i] = (uint32_t)(((long)row * ld + r0 + half * 128 + ch * 8) * 2);
+      voff[i] = ((uint32_t)row * (uint32_t)ld + (uint32_t)(r0 + half * 128 + ch * 8)) * 2u;
     }
   }
 }

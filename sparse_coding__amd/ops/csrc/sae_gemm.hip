@@ -12,10 +12,12 @@ namespace {
 // Persistent 128x128 launch (sae_gemm_pt_kernel): grid = workgroups resident at once (2 per
 // CU at NST 2, 1 at NST 3), each looping over tiles with a continuous LDS-DMA stream.
 template <int NST>
-int launch_pt(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
+int launch_pt(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t stream, int max_blocks) {
+  set_divisors<S128>(p);
   const long total = n_blocks<S128>(p.M, p.N, p.G, nprob);
-  const long slots = (NST == 2 ? 2 : 1) * 256;
-  const dim3 grid((unsigned)(total < slots ? total : slots)), block(S128::NT);
+  long nb = (NST == 2 ? 2 : 1) * 256;
+  if (max_blocks > 0 && max_blocks < nb) nb = max_blocks;
+  const dim3 grid((unsigned)(total < nb ? total : nb)), block(S128::NT);
 #define SC_LP(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_pt_kernel<S128, AKV, BKV, E, NST>), grid, block, 0, stream, p)
   switch (epi) {
     case EPI_ENC: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_ENC); break;
@@ -74,7 +76,8 @@ int sc_gemm_shape(int M, int N, int G, int nprob) {
 
 // layout: bit0 = A is K-major, bit1 = B is K-major.
 // cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256; bit 4 (128x128
-// only): persistent tile loop with a continuous LDS-DMA stream (sae_gemm_pt_kernel);
+// only): persistent tile loop with a continuous LDS-DMA stream (sae_gemm_pt_kernel), bits 8-23
+// then cap its grid (0 = one workgroup per CU slot);
 // bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4 (128x128 blocks: BK64 x 3),
 // 2: BK32 x 2, 3: BK32 x 3).
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
@@ -136,7 +139,8 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
     default:
       if (cfg & 16) {  // persistent tile loop (BK64 rings only, no split-K)
         if (ksplit != 1 || (pipe != 0 && pipe != 1)) return 9;
-        return pipe == 1 ? launch_pt<3>(epi, ak, bk, p, nprob, stream) : launch_pt<2>(epi, ak, bk, p, nprob, stream);
+        const int mb = (cfg >> 8) & 0xFFFF;
+        return pipe == 1 ? launch_pt<3>(epi, ak, bk, p, nprob, stream, mb) : launch_pt<2>(epi, ak, bk, p, nprob, stream, mb);
       }
       if (pipe == 1) return launch<S128, 64, 3, false>(epi, ak, bk, p, nprob, stream);  // 96 KB: 1 block/CU
       if (pipe == 2) return launch<S128, 32, 2, false>(epi, ak, bk, p, nprob, stream);  // 32 KB: 4-5 blocks/CU

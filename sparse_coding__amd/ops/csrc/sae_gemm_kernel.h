@@ -63,6 +63,19 @@ __device__ __forceinline__ void sched_interleave() {
   }
 }
 
+// ------------------------------------------------------------------ code activity bitmask
+// Layout [G][B/64][n/64][64 lanes] uint64: within each 64x64 block of the codes, lane l owns
+// the 64 elements it holds in the MFMA output layout -- rows 16 ii + (l & 15), columns
+// 16 jj + 4 (l >> 4) + r for ii, jj, r in 0..3 -- as bit (4 ii + jj) * 4 + r.  Any wave
+// sub-tile made of 64x64 blocks (64x64 at 128x128 blocks, 128x64 at 256-row blocks) writes
+// and reads it with one 8-byte access per lane per block: no ballots, no lane-0 scatter.
+__device__ __forceinline__ constexpr int mask_bit(int i, int j, int r) { return (((i & 3) * 4 + j) * 4 + r); }
+__device__ __forceinline__ bool mask_get(uint64_t w, int i, int j, int r) { return (w >> mask_bit(i, j, r)) & 1ull; }
+// word index of the 64x64 block at (row0, col0) (multiples of 64) for this lane
+__device__ __forceinline__ long mask_word(const GemmParams& p, int g, int row0, int col0, int lane) {
+  return (((long)g * (p.M >> 6) + (row0 >> 6)) * (p.N >> 6) + (col0 >> 6)) * 64 + lane;
+}
+
 // ------------------------------------------------------------------ epilogues
 // The fused epilogue of one output tile (shared by the tile kernel and the persistent
 // kernel).  `red` is LDS scratch of at least epi_scratch_floats<S>() floats; every
@@ -71,7 +84,16 @@ __device__ __forceinline__ void sched_interleave() {
 template <class S>
 constexpr int epi_scratch_floats() { return 2 * S::WGM * S::BN + S::NW; }
 
-template <class S, int EPI, bool AUX_EARLY>
+// LDS-staged bf16 output stores (STAGE, 128x128 tile kernel: the ring is free after the K
+// loop): each wave parks its 64x64 bf16 sub-tile in LDS in the MFMA layout (144-byte rows:
+// conflict-free 8-byte writes), then streams it out row-contiguous -- 8 global_store_dwordx4
+// per wave, each covering 8 whole 128-byte row segments, instead of 16 dwordx2 stores that
+// each touch 16 half-filled 32-byte segments (the store tail is issue-bound otherwise).
+constexpr int STAGE_OFF = 4096, STAGE_ROW = 144, STAGE_WAVE = 64 * STAGE_ROW;
+template <class S>
+constexpr int stage_bytes() { return STAGE_OFF + S::NW * STAGE_WAVE; }
+
+template <class S, int EPI, bool AUX_EARLY, bool STAGE = false>
 __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)[S::WI][S::WJ],
                                              const uint2 (&auxv)[S::WI][S::WJ], float* red, int pi, int g, int m0,
                                              int n0, int tn, int tiles_n, void* cptr, float alpha) {
@@ -85,6 +107,28 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   const bool p1 = pi != 0;
   const int rowb = m0 + wr * (WI * 16) + (lane & 15);
   const int colb = n0 + wc * (WJ * 16) + 4 * (lane >> 4);
+  static_assert(!STAGE || (WI == 4 && WJ == 4 && 2 * S::WGM * BN + NW <= STAGE_OFF / 4), "stage layout");
+  char* stage = reinterpret_cast<char*>(red) + STAGE_OFF + wid * STAGE_WAVE;
+  // one 4-wide bf16 output fragment (rows rowb + 16 i, columns colb + 16 j .. +3)
+  auto put = [&](uint16_t* C, int i, int j, ushort4 h) {
+    if constexpr (STAGE) {
+      *reinterpret_cast<ushort4*>(stage + (i * 16 + (lane & 15)) * STAGE_ROW + (j * 16 + 4 * (lane >> 4)) * 2) = h;
+    } else {
+      *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + colb + j * 16) = h;
+    }
+  };
+  auto flush = [&](uint16_t* C) {
+    if constexpr (STAGE) {  // (one wave's LDS ops complete in order: no barrier needed)
+      uint16_t* Cw = C + (long)(m0 + wr * (WI * 16)) * p.ldc + n0 + wc * (WJ * 16);
+      const int ch = lane & 7;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int row = 8 * k + (lane >> 3);
+        const uint4 v = *reinterpret_cast<const uint4*>(stage + row * STAGE_ROW + ch * 16);
+        *reinterpret_cast<uint4*>(Cw + (long)row * p.ldc + ch * 8) = v;
+      }
+    }
+  };
 
   if constexpr (EPI == EPI_F32) {
     float* C = reinterpret_cast<float*>(cptr) + (long)g * p.sc;
@@ -115,8 +159,9 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
         ushort4 h;
         h.x = f2bf(alpha * acc[i][j][0]); h.y = f2bf(alpha * acc[i][j][1]);
         h.z = f2bf(alpha * acc[i][j][2]); h.w = f2bf(alpha * acc[i][j][3]);
-        *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + colb + j * 16) = h;
+        put(C, i, j, h);
       }
+    flush(C);
     return;
   }
   // Column partial sums (ENC: on-counts, DC: bias gradient) per 128-row slot, in
@@ -161,7 +206,15 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
     constexpr bool ACTV = EPI == EPI_ENC_ACT;
     const int act = ACTV ? p.act : 0;  // compile-time 0 for the plain ReLU instantiations
     const bool counting = EPI == EPI_ENC_CNT || (ACTV && p.colpart != nullptr);
+    // 128x128 blocks: column masking only where the block reaches past nactive (uniform
+    // branch); L0 from the activity ballots' popcounts (scalar) whenever they are taken
+    const bool full = WI * WJ <= 16 && nact >= n0 + BN;
+    const bool l0_from_mask = !ACTV && EPI != EPI_ENC_CNT && p.cmask != nullptr;
     float l1 = 0.f, l0 = 0.f;
+    // activity / ramp bitmask words of this lane, one 64-bit word per 64x64 block (mask_bit)
+    uint32_t mw[WI / 4][2], qw[WI / 4][2];
+#pragma unroll
+    for (int k = 0; k < WI / 4; ++k) mw[k][0] = mw[k][1] = qw[k][0] = qw[k][1] = 0u;
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
       const int col = colb + j * 16;
@@ -205,42 +258,47 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[i][j][r] + bj[r], 0.f);
-          // branch-free (a block-uniform `if (masked)` made hipcc version the whole
-          // epilogue and spill at 128x64 per wave)
+          // (128x64-per-wave blocks stay branch-free: a block-uniform `if (masked)` made hipcc
+          // version the whole epilogue and spill there)
+          if (!full) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (col + r < nact) ? v[r] : 0.f;
+            for (int r = 0; r < 4; ++r) v[r] = (col + r < nact) ? v[r] : 0.f;
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             l1 += v[r];
             on[r] = v[r] > 0.f;
-            const float onf = on[r] ? 1.f : 0.f;
-            l0 += onf;
-            cnt[r] += onf;
+          }
+          if (!l0_from_mask) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float onf = on[r] ? 1.f : 0.f;
+              l0 += onf;
+              cnt[r] += onf;
+            }
           }
         }
-        *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + col) =
-            make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
-        if (p.cmask) {  // block-uniform
-          const uint64_t b0 = __ballot(on[0]), b1 = __ballot(on[1]);
-          const uint64_t b2 = __ballot(on[2]), b3 = __ballot(on[3]);
-          const long frag = ((long)g * (p.M >> 4) + ((rowb + i * 16) >> 4)) * (p.N >> 4) + ((colb + j * 16) >> 4);
-          if (lane == 0) {
-            u32x4_t* dst = reinterpret_cast<u32x4_t*>(p.cmask + frag * 4);
-            dst[0] = u32x4_t{(uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32)};
-            dst[1] = u32x4_t{(uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32)};
-          }
-          if (ACTV && act == 2 && p.cmask2) {  // ramp bits of the threshold activation
-            const uint64_t q0 = __ballot(rampv[0]), q1 = __ballot(rampv[1]);
-            const uint64_t q2 = __ballot(rampv[2]), q3 = __ballot(rampv[3]);
-            if (lane == 0) {
-              u32x4_t* dst = reinterpret_cast<u32x4_t*>(p.cmask2 + frag * 4);
-              dst[0] = u32x4_t{(uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32)};
-              dst[1] = u32x4_t{(uint32_t)q2, (uint32_t)(q2 >> 32), (uint32_t)q3, (uint32_t)(q3 >> 32)};
-            }
+        put(C, i, j, make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])));
+        if (p.cmask) {  // block-uniform: set this lane's bits (compile-time positions)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int bit = mask_bit(i, j, r);
+            mw[i / 4][bit >> 5] |= on[r] ? (1u << (bit & 31)) : 0u;
+            if (ACTV) qw[i / 4][bit >> 5] |= rampv[r] ? (1u << (bit & 31)) : 0u;
           }
         }
       }
       if (counting) colred_lane(cnt, j, 0);
+    }
+    flush(C);
+    if (p.cmask) {
+#pragma unroll
+      for (int k = 0; k < WI / 4; ++k) {
+        const long w = mask_word(p, g, rowb - (lane & 15) + 64 * k, colb - 4 * (lane >> 4), lane);
+        p.cmask[w] = ((uint64_t)mw[k][1] << 32) | mw[k][0];
+        if (ACTV && act == 2 && p.cmask2) p.cmask2[w] = ((uint64_t)qw[k][1] << 32) | qw[k][0];
+        if (l0_from_mask) l0 += (float)(__popc(mw[k][0]) + __popc(mw[k][1]));
+      }
     }
     l1 = block_sum_lds<NW>(l1, red + RED_SUM);  // its barriers also publish the colred_lane writes
     l0 = block_sum_lds<NW>(l0, red + RED_SUM);
@@ -264,12 +322,13 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
                                    : *reinterpret_cast<const uint2*>(p.aux + (long)g * p.saux + row * p.ldaux + col);
         const float r0 = acc[i][j][0] - bf2f(xv.x & 0xFFFF), r1 = acc[i][j][1] - bf2f(xv.x >> 16);
         const float r2 = acc[i][j][2] - bf2f(xv.y & 0xFFFF), r3 = acc[i][j][3] - bf2f(xv.y >> 16);
-        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) = make_ushort4(f2bf(r0), f2bf(r1), f2bf(r2), f2bf(r3));
+        put(C, i, j, make_ushort4(f2bf(r0), f2bf(r1), f2bf(r2), f2bf(r3)));
         se += r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
         cs[0] += r0; cs[1] += r1; cs[2] += r2; cs[3] += r3;
       }
       if (rcol) colred_lane(cs, j, 0);
     }
+    flush(C);
     se = block_sum_lds<NW>(se, red + RED_SUM);  // its barriers also publish the colred_lane writes
     if (rcol) colred_store(p.rcol, 0);
     scalar_partial(p.part, 1, 0, se);
@@ -304,12 +363,12 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
             ds[r] += c * acc[i][j][r] + (p.dc_tied ? dv[r] * (c - bj[r]) : 0.f);
           }
         }
-        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
-            make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
+        put(C, i, j, make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3])));
       }
       colred_lane(cs, j, 0);
       if (want_dot) colred_lane(ds, j, 1);
     }
+    flush(C);
     lds_barrier();
     colred_store(p.colpart, 0);
     if (want_dot) colred_store(p.dotpart, 1);
@@ -319,6 +378,9 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
     // EPI_DC with the code activity read from the encoder's bitmask (no norm-Jacobian dots)
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     const float add = p.l1[g] * p.l1_add_scale;
+    uint64_t mk[WI / 4];  // this lane's activity words (one 8-byte load per 64x64 block)
+#pragma unroll
+    for (int k = 0; k < WI / 4; ++k) mk[k] = p.cmask[mask_word(p, g, rowb - (lane & 15) + 64 * k, colb - 4 * (lane >> 4), lane)];
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
       f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -326,20 +388,18 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
 #pragma unroll
       for (int i = 0; i < WI; ++i) {
         const long row = rowb + i * 16;
-        const long frag = ((long)g * (p.M >> 4) + ((rowb + i * 16) >> 4)) * (p.N >> 4) + (col >> 4);
-        const uint64_t* mk = p.cmask + frag * 4;  // wave-uniform address
         f32x4_t dv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool on = (mk[r] >> lane) & 1ull;
+          const bool on = mask_get(mk[i / 4], i, j, r);
           dv[r] = on ? acc[i][j][r] + add : 0.f;
           cs[r] += dv[r];
         }
-        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
-            make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
+        put(C, i, j, make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3])));
       }
       colred_lane(cs, j, 0);
     }
+    flush(C);
     lds_barrier();
     colred_store(p.colpart, 0);
     return;
@@ -353,6 +413,13 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     const float add = p.l1[g] * p.l1_add_scale;
     const int act = p.act;
+    uint64_t mk[WI / 4], rk[WI / 4];  // activity / ramp words of this lane
+#pragma unroll
+    for (int k = 0; k < WI / 4; ++k) {
+      const long w = mask_word(p, g, rowb - (lane & 15) + 64 * k, colb - 4 * (lane >> 4), lane);
+      mk[k] = p.cmask[w];
+      rk[k] = p.cmask2 ? p.cmask2[w] : 0ull;
+    }
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
       f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f}, ds = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -366,8 +433,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
 #pragma unroll
       for (int i = 0; i < WI; ++i) {
         const long row = rowb + i * 16;
-        const long frag = ((long)g * (p.M >> 4) + (row >> 4)) * (p.N >> 4) + (col >> 4);
-        const uint64_t* mk = p.cmask + frag * 4;  // wave-uniform address
+
         const uint2 cv = AUX_EARLY ? auxv[i][j]
                                    : *reinterpret_cast<const uint2*>(p.aux + (long)g * p.saux + row * p.ldaux + col);
         const uint16_t cvs[4] = {(uint16_t)(cv.x & 0xFFFF), (uint16_t)(cv.x >> 16), (uint16_t)(cv.y & 0xFFFF),
@@ -375,7 +441,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
         f32x4_t dv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool on = (mk[r] >> lane) & 1ull;
+          const bool on = mask_get(mk[i / 4], i, j, r);
           const float c = bf2f(cvs[r]);
           if (act == 1) {
             const float sgn = c > 0.f ? 1.f : (c < 0.f ? -1.f : 0.f);
@@ -383,7 +449,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
           } else if (act == 2) {
             const float dc = acc[i][j][r] + add;
             // ramp bit from the encoder's fp32 decision; without it, from the bf16 code
-            const bool ramp = p.cmask2 ? (bool)((p.cmask2[frag * 4 + r] >> lane) & 1ull) : c * is2[r] < 1.f;
+            const bool ramp = p.cmask2 ? mask_get(rk[i / 4], i, j, r) : c * is2[r] < 1.f;
             dv[r] = on ? dc * (ramp ? 10.f : 1.f) : 0.f;
             cs[r] += dv[r];
             ds[r] += (on && ramp) ? -9.f * dc : 0.f;
@@ -392,12 +458,12 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
             cs[r] += dv[r];
           }
         }
-        *reinterpret_cast<ushort4*>(C + row * p.ldc + col) =
-            make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3]));
+        put(C, i, j, make_ushort4(f2bf(dv[0]), f2bf(dv[1]), f2bf(dv[2]), f2bf(dv[3])));
       }
       colred_lane(cs, j, 0);
       colred_lane(ds, j, 1);
     }
+    flush(C);
     lds_barrier();
     colred_store(p.colpart, 0);
     if (p.dotpart) colred_store(p.dotpart, 1);
@@ -459,14 +525,32 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
     float ss[WI];
 #pragma unroll
     for (int i = 0; i < WI; ++i) ss[i] = 0.f;
+    // Software-prefetched streaming update: the p / m / v fragments of fragment f + D are
+    // loaded before fragment f is updated (D = 8 fragments = 24 x 1 KiB loads in flight per
+    // wave), so the epilogue runs at the HBM rate instead of one load round trip per fragment.
+    constexpr int NF = WI * WJ;
+    constexpr int D = NF < 8 ? NF : 8;
+    auto foff = [&](int f) { return gb + (long)(rowb + (f / WJ) * 16) * p.ldc + colb + (f % WJ) * 16; };
+    f32x4_t pb[D], mb[D], vb[D];
 #pragma unroll
-    for (int i = 0; i < WI; ++i)
+    for (int f = 0; f < D; ++f) {
+      const long o = foff(f);
+      pb[f] = *reinterpret_cast<const f32x4_t*>(E.p + o);
+      mb[f] = *reinterpret_cast<const f32x4_t*>(E.m + o);
+      vb[f] = *reinterpret_cast<const f32x4_t*>(E.v + o);
+    }
 #pragma unroll
-      for (int j = 0; j < WJ; ++j) {
-        const long off = gb + (long)(rowb + i * 16) * p.ldc + colb + j * 16;
-        f32x4_t pv = *reinterpret_cast<const f32x4_t*>(E.p + off);
-        f32x4_t mv = *reinterpret_cast<const f32x4_t*>(E.m + off);
-        f32x4_t vv = *reinterpret_cast<const f32x4_t*>(E.v + off);
+    for (int f = 0; f < NF; ++f) {
+      const int i = f / WJ, j = f % WJ, sl = f % D;
+      const long off = foff(f);
+      f32x4_t pv = pb[sl], mv = mb[sl], vv = vb[sl];
+      if (f + D < NF) {
+        const long o = foff(f + D);
+        pb[sl] = *reinterpret_cast<const f32x4_t*>(E.p + o);
+        mb[sl] = *reinterpret_cast<const f32x4_t*>(E.m + o);
+        vb[sl] = *reinterpret_cast<const f32x4_t*>(E.v + o);
+      }
+      {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float gr = acc[i][j][r] * ca[i] - pv[r] * cp[i];
@@ -480,6 +564,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
         *reinterpret_cast<f32x4_t*>(E.v + off) = vv;
         *reinterpret_cast<ushort4*>(E.sh + off) = make_ushort4(f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3]));
       }
+    }
     if (E.mode) {
       // partial |w_j|^2 over each 128-column slot -> sqpart[g][row][slot]
       constexpr int WPC = PT / (WJ * 16);  // wave columns per 128-column slot
@@ -523,13 +608,13 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   const int per_split = tiles_m * tiles_n * p.G;
   const int per_prob = per_split * p.ksplit;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int pi = bid / per_prob;
+  const int pi = (int)fdiv(bid, p.f_prob);
   int rem = bid - pi * per_prob;
-  const int ksi = rem / per_split;
+  const int ksi = (int)fdiv(rem, p.f_split);
   rem -= ksi * per_split;
-  const int g = rem / (tiles_m * tiles_n);
+  const int g = (int)fdiv(rem, p.f_plane);
   rem -= g * tiles_m * tiles_n;
-  const int tm = rem / tiles_n, tn = rem - tm * tiles_n;
+  const int tm = (int)fdiv(rem, p.f_tn), tn = rem - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
   // Resolve the problem's operands with selects (a dynamically indexed kernarg
@@ -550,8 +635,8 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   constexpr bool ENC = (EPI == EPI_ENC || EPI == EPI_ENC_CNT || EPI == EPI_ENC_ACT);
   const int nk1 = p.K1 / BKT, nk_all = nk1 + (SEG2 ? p.K2 / BKT : 0);
   // this block's K-tile range [kbeg, nk) (the whole range unless split-K)
-  const int kbeg = (int)(((long)ksi * nk_all) / p.ksplit);
-  const int nk = (int)(((long)(ksi + 1) * nk_all) / p.ksplit);
+  const int kbeg = p.ksplit == 1 ? 0 : (int)fdiv(ksi * nk_all, p.f_ksplit);
+  const int nk = p.ksplit == 1 ? nk_all : (int)fdiv((ksi + 1) * nk_all, p.f_ksplit);
   // per-lane DMA source offsets for both K segments
   uint32_t va0[PPWA], vb0[PPWB], va1[SEG2 ? PPWA : 1], vb1[SEG2 ? PPWB : 1];
   piece_offsets<AK, BKT, PPWA>(va0, oa0.ld, m0, wid, lane);
@@ -734,7 +819,9 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   }
 #undef SC_ISSUE
   lds_barrier();  // all reads of the ring done before smem is reused below
-  sae_epilogue<S, EPI, AUX_EARLY>(p, acc, auxv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn, tiles_n, cptr, alpha);
+  constexpr bool STAGE = S::WI == 4 && S::WJ == 4 && NST * STG >= stage_bytes<S>();
+  sae_epilogue<S, EPI, AUX_EARLY, STAGE>(p, acc, auxv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn, tiles_n,
+                                         cptr, alpha);
 }
 
 
@@ -788,11 +875,11 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_pt_kernel(GemmParams p) {
   auto tile_of = [&](int i) {
     const int lin = xcd_remap((int)blockIdx.x + i * (int)gridDim.x, total);
     Tile t;
-    t.pi = lin / per_prob;
+    t.pi = (int)fdiv(lin, p.f_prob);
     int rem = lin - t.pi * per_prob;
-    t.g = rem / (tiles_m * tiles_n);
+    t.g = (int)fdiv(rem, p.f_plane);
     rem -= t.g * tiles_m * tiles_n;
-    const int tm = rem / tiles_n;
+    const int tm = (int)fdiv(rem, p.f_tn);
     t.tn = rem - tm * tiles_n;
     t.m0 = tm * BM;
     t.n0 = t.tn * BN;
@@ -935,8 +1022,20 @@ long n_blocks(int M, int N, int G, int nprob) { return (long)(M / S::BM) * (N / 
 // FULL = every (layout, epilogue) pair; the alternative K pipelines (deeper LDS rings,
 // selected with cfg bits 2-3) instantiate only the step's epilogues and the weight-gradient
 // layout, to keep the build small.
+// Host: the decomposition divisors for block shape S (ksplit-aware).
+template <class S>
+void set_divisors(GemmParams& p) {
+  const uint32_t tn = p.N / S::BN, plane = (uint32_t)(p.M / S::BM) * tn, split = plane * p.G;
+  p.f_tn = make_fdiv(tn);
+  p.f_plane = make_fdiv(plane);
+  p.f_split = make_fdiv(split);
+  p.f_prob = make_fdiv(split * p.ksplit);
+  p.f_ksplit = make_fdiv(p.ksplit);
+}
+
 template <class S, int BKT, int NST, bool FULL = true>
-int launch(int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
+int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t stream) {
+  set_divisors<S>(p);
   const dim3 grid((unsigned)(n_blocks<S>(p.M, p.N, p.G, nprob) * p.ksplit)), block(S::NT);
   if constexpr (!FULL) {
     if (epi == EPI_ADAM || epi == EPI_BF16 || epi >= EPI_ENC_ACT || (epi == EPI_F32 && (ak || bk))) return 8;

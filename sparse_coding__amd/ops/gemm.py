@@ -47,22 +47,23 @@ def set_config(epi: int, cfg: int):
     _CFG_DEFAULT[epi] = int(cfg)
 
 
-# Persistent, wave-specialised kernel (csrc/sae_gemm_p.hip): 4 MFMA waves + 4 epilogue waves per
-# CU, the previous tile's fused epilogue overlapped with the current tile's MFMAs.  Opt-in
-# (SC_GEMM_PERSIST=1 / force_persistent): on MI355X its single MFMA wave per SIMD issues the
-# LDS-DMA and the fragment reads itself and loses to two tile-kernel workgroups per CU on every
-# step GEMM (enc 80 vs 59 us, wgrad 114 vs 64 us; profiles/gemm_lab_r2_v1.jsonl), although its
-# outputs are bit-identical (tests/test_gemm_persistent_gpu.py).
+# Persistent 128x128 tile loop (cfg bit 4, csrc/sae_gemm_kernel.h sae_gemm_pt_kernel): one
+# workgroup per (CU, slot) walks several output tiles with a continuous LDS-DMA stream across
+# tile boundaries.  Bit-identical to the tile kernel (tests/test_gemm_persistent_gpu.py,
+# tests/test_gemm_pt_gpu.py); opt-in (SC_GEMM_PERSIST=1 / force_persistent) because on MI355X
+# two co-resident tile-kernel workgroups per CU already hide the same latencies (enc 64 vs
+# 60 us, profiles/gemm_lab_r2_v2.jsonl).  cfg bits 8-23 carry a grid cap (tests: many tiles
+# per workgroup).
 _PERSIST = os.environ.get("SC_GEMM_PERSIST", "0") not in ("", "0")
 _P_EPIS = {EPI_F32, EPI_BF16, EPI_ENC, EPI_ENC_CNT, EPI_ENC_ACT, EPI_DEC, EPI_DC_MASK, EPI_DC_ACT}
-_P_NST = int(os.environ.get("SC_GEMM_NST", "3"))
+_P_NST = int(os.environ.get("SC_GEMM_NST", "2"))
 _P_MAX_BLOCKS = 0
 
 
 class force_persistent:
-    """Context manager: route eligible GEMMs to the persistent kernel (``on``) or to the tile
-    kernel; ``max_blocks`` caps the grid (tests: several tiles per workgroup); ``nst`` sets
-    the LDS ring depth (3 or 4)."""
+    """Context manager: route eligible GEMMs to the persistent tile loop (``on``) or to the tile
+    kernel; ``max_blocks`` caps the grid (tests: several tiles per workgroup); ``nst`` sets the
+    LDS ring depth (2: two workgroups per CU, 3: one)."""
 
     def __init__(self, on: bool = True, max_blocks: int = 0, nst: int | None = None):
         self.on, self.max_blocks, self.nst = bool(on), int(max_blocks), nst
@@ -80,20 +81,13 @@ class force_persistent:
         _PERSIST, _P_MAX_BLOCKS, _P_NST = self._old
 
 
-def _persistent_ok(epi, layout, K1, K2, nprob, cfg, ksplit, cmask, act=0, cmask2=None):
-    if not _PERSIST or epi not in _P_EPIS or ksplit != 1 or cfg is not None or _CFG_OVERRIDE is not None:
-        return False
-    if K1 + K2 < 512:
-        return False
-    if K2 and (epi != EPI_F32 or layout != 0):
-        return False
-    if epi in (EPI_ENC, EPI_ENC_CNT, EPI_ENC_ACT, EPI_DC_MASK, EPI_DC_ACT) and (cmask is None or layout != 3):
-        return False
-    if epi == EPI_DEC and layout != 1:
-        return False
-    if act == ACT_THRESHOLD and epi in (EPI_ENC_ACT, EPI_DC_ACT) and cmask2 is None:
-        return False  # the persistent kernel takes the ramp bits from the encoder's fp32 decision
-    return _lib.lib() is not None and hasattr(_lib.lib(), "sc_gemm_p")
+def _persistent_cfg(epi, M, N, ksplit, cfg_explicit):
+    """cfg word of the persistent loop for this GEMM, or None when it does not apply."""
+    if not _PERSIST or epi not in _P_EPIS or ksplit != 1 or cfg_explicit is not None or _CFG_OVERRIDE is not None:
+        return None
+    if M % 128 or N % 128 or _P_NST not in (2, 3):
+        return None
+    return 1 | 16 | (4 if _P_NST == 3 else 0) | (min(_P_MAX_BLOCKS, 0xFFFF) << 8)
 
 
 class force_shape:
@@ -143,28 +137,9 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
     cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
     _need((cfg & 3) == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg & 3)} does not tile M={M}, N={N}")
     nprob = len(outs)
-    if _persistent_ok(epi, layout, K1, K2, nprob, cfg_explicit, ksplit, cmask, act, cmask2):
-        args = _lib.ScGemmArgs()
-        args.epi, args.layout, args.nprob = epi, layout, nprob
-        args.M, args.N, args.K1, args.K2, args.G = M, N, K1, K2, G
-        for i, op in enumerate(a_ops):
-            args.a[i] = op
-        for i, op in enumerate(b_ops):
-            args.b[i] = op
-        for i, o in enumerate(outs):
-            args.c[i] = _lib.ptr(o)
-            args.alpha[i] = float(alphas[i])
-        args.ldc, args.sc = ldc, sc
-        args.bias, args.sbias, args.nactive = _lib.ptr(bias), sbias, _lib.ptr(nactive)
-        args.aux, args.ldaux, args.saux = _lib.ptr(aux), ldaux, saux
-        args.part, args.colpart, args.l1 = _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1)
-        args.l1_add_scale, args.dotpart = float(l1_add_scale), _lib.ptr(dotpart)
-        args.cmask, args.cmask2, args.rcol = _lib.ptr(cmask), _lib.ptr(cmask2), _lib.ptr(rcol)
-        args.act, args.ascale = int(act), _lib.ptr(ascale)
-        args.nst, args.max_blocks = _P_NST, _P_MAX_BLOCKS
-        rc = _lib.lib().sc_gemm_p(C.byref(args), _lib.stream_handle())
-        _lib.check(rc, f"sc_gemm_p(epi={epi})")
-        return
+    pcfg = _persistent_cfg(epi, M, N, ksplit, cfg_explicit)
+    if pcfg is not None:
+        cfg = pcfg
     A = (_lib.ScOperand * (2 * nprob))(*a_ops)
     Bo = (_lib.ScOperand * (2 * nprob))(*b_ops)
     Cp = (C.c_void_p * nprob)(*[_lib.ptr(o) for o in outs])
@@ -191,8 +166,9 @@ def _x_stride(x, B, d, G):
 
 
 def code_mask_shape(G, B, n):
-    """Shape of the encoder's activity bitmask (fragment-ordered ballots, see sae_gemm.hip)."""
-    return (G, B // 16, n // 16, 4)
+    """Shape of the encoder's activity bitmask: one 64-bit word per lane per 64x64 block of the
+    codes (csrc/sae_gemm_kernel.h, mask_bit)."""
+    return (G, B // 64, n // 64, 64)
 
 
 def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=None, act=ACT_RELU, ascale=None,

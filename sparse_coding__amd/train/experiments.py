@@ -252,8 +252,183 @@ def run_synthetic(argv=None):
     sweep(synthetic_linear_range, cfg)
 
 
+def _synthetic_base(argv, **overrides):
+    """The reference's synthetic-shape defaults for its real-data runs (activation width 512,
+    1024 ground-truth features, 10 nonzero, decay 0.99, noise 1e-3)."""
+    base = dict(model_name="pythia-70m-deduped", layer=2, layer_loc="residual", n_chunks=10, batch_size=1024,
+                gen_batch_size=4096, n_ground_truth_components=1024, activation_width=512,
+                noise_magnitude_scale=0.001, feature_prob_decay=0.99, feature_num_nonzero=10, lr=1e-3)
+    base.update(overrides)
+    return _cfg(argv, cls=SyntheticEnsembleArgs, **base)
+
+
+def run_thresholding(argv=None):
+    """Thresholding SAEs on Pythia-70m layer-2 residual chunks (reference :437-464)."""
+    from .sweep import sweep
+
+    sweep(thresholding_experiment, _synthetic_base(argv, dataset_folder="activation_data",
+                                                   output_folder="output_thresholding"))
+
+
+def run_resid_denoise(argv=None):
+    """LISTA residual-denoising SAEs at dict ratio 4 (reference :467-496)."""
+    from .sweep import sweep
+
+    for ratio in (4,):
+        sweep(residual_denoising_experiment, _synthetic_base(argv, dataset_folder="activation_data",
+                                                             learned_dict_ratio=float(ratio),
+                                                             output_folder=f"output_{ratio}_lista_neg"))
+
+
+def run_dict_ratio(argv=None):
+    """Masked tied SAEs of 8 dictionary sizes stacked in one ensemble, synthetic data
+    (reference :583-620)."""
+    from .sweep import sweep
+
+    cfg = _cfg(argv, cls=SyntheticEnsembleArgs, model_name="pythia-70m-deduped", layer=4, layer_loc="residual",
+               use_synthetic_dataset=True, lr=1e-3, n_chunks=10, correlated_components=False, chunk_size_gb=2.0,
+               batch_size=1024, n_epochs=1, dataset_folder="activation_data", output_folder="output_dict_ratio")
+    sweep(dict_ratio_experiment, cfg)
+
+
+def run_dense_l1_range(argv=None):
+    """Dense L1 range on Pythia-70m layer-3 MLP, tied (reference :623-643)."""
+    from .sweep import sweep
+
+    cfg = _cfg(argv, model_name="pythia-70m-deduped", batch_size=2048, layer_loc="mlp", layer=3, bias_decay=0.0,
+               tied_ae=True, use_synthetic_dataset=False, lr=1e-3, n_chunks=20, n_epochs=15)
+    if not cfg.output_folder or cfg.output_folder == "outputs":
+        cfg.output_folder = f"normal_{'_tied' if cfg.tied_ae else ''}_{cfg.layer_loc}_l{cfg.layer}_r{int(cfg.learned_dict_ratio)}"
+    if not cfg.dataset_folder:
+        cfg.dataset_folder = f"pilechunks_l{cfg.layer}_{cfg.layer_loc}"
+    sweep(dense_l1_range_experiment, cfg)
+
+
+def _across_layers(argv, init, layers, locs, ratios, tied, lr, base_out, **extra):
+    from .sweep import sweep
+
+    for layer in layers:
+        for loc in locs:
+            for ratio in ratios:
+                cfg = _cfg(argv, model_name="pythia-70m-deduped", tied_ae=tied, layer=layer, layer_loc=loc,
+                           learned_dict_ratio=float(ratio), use_synthetic_dataset=False, lr=lr,
+                           dataset_folder=f"pilechunks_l{layer}_{loc}",
+                           output_folder=f"{base_out}{'_tied' if tied else ''}_{loc}_l{layer}_r{int(ratio)}", **extra)
+                sweep(init, cfg)
+
+
+def run_across_layers(argv=None):
+    """Tied residual dictionaries (ratio 4) for layers 0-5 (reference :646-679)."""
+    _across_layers(argv, simple_setoff, range(6), ["residual"], [4], True, 1e-3, "longrun",
+                   batch_size=1024, save_every=5, n_chunks=20, n_epochs=20)
+
+
+def run_across_layers_attn(argv=None):
+    """Attention-output dictionaries, ratios 1-8, layers 0-5 (reference :682-710)."""
+    _across_layers(argv, dense_l1_range_experiment, range(6), ["attn"], [1, 2, 4, 8], True, 3e-4,
+                   "output_attn_sweep", batch_size=2048, save_every=2, n_chunks=10)
+
+
+def run_across_layers_mlp_out(argv=None):
+    """MLP-out (hook_mlp_out, d_model wide) dictionaries, ratios 1-8 (reference :713-741)."""
+    _across_layers(argv, dense_l1_range_experiment, [0, 1, 3, 4, 5], ["mlpout"], [1, 2, 4, 8], True, 3e-4,
+                   "output_sweep", batch_size=2048, save_every=2, n_chunks=10)
+
+
+def run_across_layers_mlp_untied(argv=None):
+    """Untied MLP (hook_post, d_mlp wide) dictionaries, ratios 1-8 (reference :744-772)."""
+    _across_layers(argv, dense_l1_range_experiment, range(6), ["mlp"], [1, 2, 4, 8], False, 3e-4, "output_sweep",
+                   batch_size=2048, save_every=2, n_chunks=10)
+
+
+def run_zero_l1_baseline(argv=None):
+    """L1 = 0 tied baseline on layer-3 residual, ratio 4 (reference :775-796)."""
+    from .sweep import sweep
+
+    cfg = _cfg(argv, model_name="pythia-70m-deduped", layer=3, layer_loc="residual", tied_ae=True,
+               learned_dict_ratio=4.0, batch_size=2048, output_folder="output_zero_b_4",
+               dataset_folder="activation_data/layer_3", use_synthetic_dataset=False, lr=3e-4, n_chunks=38)
+    sweep(zero_l1_baseline, cfg)
+
+
+def run_topk(argv=None):
+    """Top-k encoder sweep (reference ``topk`` :799-814)."""
+    from .sweep import sweep
+
+    cfg = _cfg(argv, model_name="pythia-70m-deduped", batch_size=1024, output_folder="output_topk",
+               dataset_folder="activation_data", use_synthetic_dataset=False, lr=1e-3, n_chunks=10, n_epochs=5)
+    sweep(topk_experiment, cfg)
+
+
+def run_synthetic_test(argv=None):
+    """Synthetic ground-truth grid: n_ground_truth in {1024, 2048} x nonzero in {10, 50, 100},
+    noise 0.1 (reference ``synthetic_test`` :817-851)."""
+    import shutil
+
+    from .sweep import sweep
+
+    for noise, nz, ngt in product([0.1], [10, 50, 100], [1024, 2048]):
+        cfg = _cfg(argv, cls=SyntheticEnsembleArgs, use_synthetic_dataset=True,
+                   dataset_folder="activation_data_synthetic", batch_size=1024, gen_batch_size=4096,
+                   activation_width=512, feature_prob_decay=1.0, lr=1e-3, n_chunks=10, correlated_components=False,
+                   noise_magnitude_scale=noise, n_ground_truth_components=ngt, feature_num_nonzero=nz,
+                   output_folder=f"output_synthetic_{noise:.2E}_{ngt}_{nz}")
+        shutil.rmtree(cfg.dataset_folder, ignore_errors=True)  # regenerate per ground-truth setting
+        sweep(synthetic_linear_range, cfg)
+
+
+def run_setup_positives(argv=None):
+    """Positive tied SAEs on the MLP (bias decay 0.01, ratio 1; reference ``setup_positives``
+    :1071-1096)."""
+    from .sweep import sweep
+
+    for bias_decay in (0.01,):
+        for ratio in (1.0,):
+            cfg = _cfg(argv, model_name="pythia-70m-deduped", batch_size=2048, save_every=10, tied_ae=True,
+                       use_synthetic_dataset=False, lr=1e-3, n_chunks=20, n_epochs=15, activation_width=2048,
+                       layer_loc="mlp", bias_decay=bias_decay, learned_dict_ratio=ratio)
+            cfg.output_folder = f"positive_{cfg.layer_loc}_l{cfg.layer}_r{cfg.learned_dict_ratio}_bd{cfg.bias_decay}"
+            cfg.dataset_folder = f"pilechunks_l{cfg.layer}_{cfg.layer_loc}"
+            sweep(run_positive_init, cfg)
+
+
+def run_all_zeros(argv=None):
+    """L1 = 0 dictionaries over tied/untied x {residual, mlpout} x ratios 0.5-32 for one layer
+    (reference :1146-1177; ``--layer`` / ``--device`` from the command line)."""
+    from .sweep import sweep
+
+    for tied in (True, False):
+        for loc in ("residual", "mlpout"):
+            for ratio in (0.5, 1, 2, 4, 8, 16, 32):
+                cfg = _cfg(argv, model_name="pythia-70m-deduped", batch_size=2048, save_every=10,
+                           use_synthetic_dataset=False, lr=1e-3, activation_width=2048, tied_ae=tied, layer_loc=loc,
+                           learned_dict_ratio=float(ratio), n_chunks=20 if loc == "mlp" else 10,
+                           n_epochs=3 if loc == "mlp" else 1)
+                cfg.output_folder = f"zeros_{loc}_l{cfg.layer}_r{cfg.learned_dict_ratio}_{'tied' if tied else 'untied'}"
+                cfg.dataset_folder = f"pilechunks_l{cfg.layer}_{loc}"
+                sweep(run_zeros_only_init, cfg)
+
+
+def run_simple(argv=None):
+    """GPT-2-small layer-6 MLP, untied, ratio 4 (reference ``simple_run`` :1180-1208)."""
+    from datetime import datetime
+
+    from .sweep import sweep
+
+    cfg = _cfg(argv, model_name="gpt2", batch_size=2048, save_every=10, use_synthetic_dataset=False, lr=1e-3,
+               n_chunks=40, n_epochs=10, activation_width=2048, layer=6, layer_loc="mlp", tied_ae=False,
+               learned_dict_ratio=4.0)
+    stamp = datetime.now().strftime("%Y-%m-%d_%H-%M-%S")
+    cfg.output_folder = f"gpt2small_{'tied' if cfg.tied_ae else 'untied'}_{cfg.layer_loc}_l{cfg.layer}_r{cfg.learned_dict_ratio}_{stamp}"
+    cfg.dataset_folder = f"pilechunks_l{cfg.layer}_{cfg.layer_loc}_gpt2"
+    sweep(simple_setoff, cfg)
+
+
 RUNS = {f.__name__: f for f in [run_single_layer, run_single_layer_gpt2, run_across_layers_mlp_long,
-                                run_pythia_1_4_b_sweep, run_synthetic]}
+                                run_pythia_1_4_b_sweep, run_synthetic, run_thresholding, run_resid_denoise,
+                                run_dict_ratio, run_dense_l1_range, run_across_layers, run_across_layers_attn,
+                                run_across_layers_mlp_out, run_across_layers_mlp_untied, run_zero_l1_baseline,
+                                run_topk, run_synthetic_test, run_setup_positives, run_all_zeros, run_simple]}
 
 
 def main(argv=None):

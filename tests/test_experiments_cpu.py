@@ -106,3 +106,22 @@ def test_layer_baselines(tmp_path):
     assert hp["kind"] == "ica" and hp["sparsity"] > 0
     (topk, _), = load_learned_dicts(str(tmp_path / "out" / "l0_residual" / "pca_topk.pt"))
     assert int((topk.encode(x) != 0).sum(-1).max()) <= hp["sparsity"]
+
+
+def test_every_run_entry_point_builds_its_sweeps(monkeypatch):
+    """Every ``run_*`` runner (reference big_sweep_experiments.py:437-1286) builds configs whose
+    init function returns well-formed ensembles (sweep itself stubbed out)."""
+    from sparse_coding__amd.train import experiments as E
+    from sparse_coding__amd.train import sweep as S
+
+    calls = []
+    monkeypatch.setattr(S, "sweep", lambda init, cfg: calls.append((init, cfg)))
+    for name, fn in E.RUNS.items():
+        calls.clear()
+        fn(["--device", "cpu", "--activation_width", "32"])
+        assert calls, name
+        for init, cfg in calls[:2]:
+            assert cfg.output_folder and cfg.device == "cpu", name
+            ens, ens_h, buf_h, ranges = init(cfg)
+            assert ens and all(len(e) == 4 and len(e[0]) >= 1 for e in ens), name
+            assert isinstance(ranges, dict), name

@@ -1,10 +1,10 @@
-"""The persistent wave-specialised GEMM (csrc/sae_gemm_p.hip) against fp32 PyTorch and the
-tile kernel (csrc/sae_gemm.hip).
+"""The persistent 128x128 tile loop (sae_gemm_pt_kernel, cfg bit 4) against fp32 PyTorch and
+the tile kernel; the reverse / threshold epilogues against fp32 formulas.
 
 Every case runs with the grid capped to a few workgroups too (``max_blocks``), so each
-workgroup walks several tiles and the cross-tile paths are exercised: the LDS-DMA ring running
-into the next tile, the staged hand-off of the previous tile's fragments, the epilogue waves'
-deferred partial-sum flush.  Outputs (codes, residuals, code gradients, activity bitmasks)
+workgroup walks several tiles and the cross-tile paths are exercised: the LDS-DMA stream
+running into the next tile's K-tiles during the current tile's last steps, the epilogue's
+stores still in flight under the next tile's first DMA waits.  Outputs (codes, residuals, code gradients, activity bitmasks)
 must be bit-identical to the tile kernel's -- both accumulate the same MFMA fragments in the
 same K order; partial sums are compared with a tolerance (different summation order).
 """
@@ -23,7 +23,6 @@ def _lib():
     from sparse_coding__amd.ops import _lib as L
 
     L.lib()
-    assert hasattr(L.lib(), "sc_gemm_p"), "persistent GEMM missing from the kernel library"
     yield
 
 
@@ -192,10 +191,11 @@ def test_activation_epilogues(act, grid):
     else:
         ramp = on & (u < 1)
         dref = gdc * on * torch.where(ramp, 10.0, 1.0)
-        # the ramp bit is decided on the kernel's own fp32 pre-activation: within a few ulps of
-        # u = 1 it may fall either way (bf16 MFMA vs torch accumulation order), so those
-        # elements may contribute -9 dL/dc or not
-        amb = on & ((u - 1).abs() < 2e-3)
+        # the on / ramp bits are decided on the kernel's own fp32 pre-activation: within a few
+        # ulps of either knee (u = 0.9: on/off, u = 1: ramp/linear) they may fall either way
+        # (bf16 MFMA vs torch accumulation order), so those elements may contribute -9 dL/dc
+        # or not (seed 7 puts one element at u = 0.90000004)
+        amb = ((u - 1).abs() < 2e-3) | ((u - 0.9).abs() < 2e-3)
         certain = (-9.0 * gdc * (ramp & ~amb)).sum(1)
         slack = (9.0 * gdc.abs() * amb).sum(1)
         assert bool(((dotpart.sum(1) - certain).abs() <= slack + 2e-2 + 2e-2 * certain.abs()).all())

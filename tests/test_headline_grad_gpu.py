@@ -4,7 +4,14 @@ configurations the bench selects (128x128 pipelined encoder / decoder / code-gra
 epilogues, the automatic weight-gradient shape and split): the pre-Adam gradients of the
 decoder (through the row-norm Jacobian), encoder and bias against fp32 autograd of
 ``FunctionalSAE.loss`` (reference autoencoders/sae_ensemble.py:53-77), per model, at a
-relative Frobenius error <= 1e-2."""
+relative Frobenius error <= 1e-2.
+
+The autograd oracle is evaluated at the encoder weights the kernels actually multiply by:
+the bf16-rounded encoder master (BASELINE specifies bf16 GEMM operands).  Rounding W_e alone
+moves the fp32 encoder gradient by 1.7% at init for l1 = 1e-4 (ReLU mask flips of
+near-zero pre-activations; CPU emulation of each bf16 stage: W_e 1.7e-2, W_hat 1.8e-3,
+c 6.8e-4, R 8.3e-4, dpre 9.4e-4) -- that is operand precision, not kernel error, and the
+fused gradients match autograd at the rounded operands to ~2e-3."""
 
 import numpy as np
 import pytest
@@ -56,8 +63,9 @@ def test_headline_pre_adam_gradients(trained_steps):
     w_hat = W / nrm
     g_dec = (g_dec_hat - w_hat * (w_hat * g_dec_hat).sum(-1, keepdim=True)) / nrm
     for g in range(G):
-        p = {k: eng.params[k][g].detach().clone().requires_grad_(True)
-             for k in ("encoder", "encoder_bias", "decoder")}
+        p = {k: eng.params[k][g].detach().clone() for k in ("encoder", "encoder_bias", "decoder")}
+        p["encoder"] = p["encoder"].to(torch.bfloat16).float()  # the operand the encoder GEMM reads
+        p = {k: v.requires_grad_(True) for k, v in p.items()}
         b = {"l1_alpha": eng.l1[g].detach().clone(), "bias_decay": torch.zeros((), device=DEV)}
         loss, _ = FunctionalSAE.loss(p, b, x.float())
         ge, gb, gd = torch.autograd.grad(loss, [p["encoder"], p["encoder_bias"], p["decoder"]])
