@@ -41,9 +41,9 @@ import torch
 # is published, BASELINE.json "published": {}).
 BASELINE_ACT_PER_S = 1.86e3
 # This repo's PyTorch-eager engine (FunctionalEnsemble: torch.func vmap(grad(loss)) + vmapped
-# Adam, fp32, the reference's algorithm) on ONE MI355X at the same config
-# (profiles/bench_eager_r2.json); None until measured.
-EAGER_SAME_BOX_ACT_PER_S = None
+# Adam, fp32, the reference's algorithm) on ONE MI355X at the same config, measured with
+# ``bench.py --engine eager`` (profiles/bench_eager_r2.json: 2.63 ms/step).
+EAGER_SAME_BOX_ACT_PER_S = 779054.6
 METRIC = "activations/sec (ensemble train) + FVU@L0, Pythia-70m resid SAE at 1/2/4/8 GPU"
 
 

@@ -3,7 +3,8 @@
   python scripts/bench_configs.py cpu      # config 1: tied SAE d=128 ratio 2 l1=1e-3, CPU eager
   python scripts/bench_configs.py topk     # config 4: GPT-2-small residual (d=768), ratio 8, top-k
   python scripts/bench_configs.py fista    # config 5: FISTA 300-step dictionary learning, d=1024
-  python scripts/bench_configs.py mlp      # config 3 shapes on one GPU: Pythia-70m MLP (d=2048)
+  python scripts/bench_configs.py mlpout   # config 3: Pythia-70m MLP-out (hook_mlp_out, d=512), DP path
+  python scripts/bench_configs.py mlp      # Pythia-70m MLP hidden (hook_post, d_mlp=2048) shapes
 
 Every line is one JSON record: activations/s over the timed steps (full steps: gather,
 forward, backward, optimiser, and for FISTA the solve + basis update), synthetic data,
@@ -124,8 +125,41 @@ def cfg_fista(a):
             "ring_gb": round(ring.capacity * d * 2 / 1e9, 1), "ring_fill_s": round(fill_s, 1)}
 
 
+def cfg_mlpout(a):
+    """Config 3: Pythia-70m MLP-out -- the reference's ``mlpout`` hook is ``hook_mlp_out``, d_model
+    = 512 wide (reference activation_dataset.py:66-67, 104-105) -- 8-model L1 sweep, ratio 4, on
+    the data-parallel path (BASELINE config 3's mechanism): ``bench.py --parallelism dp``, i.e.
+    ChunkedDataParallel over the fused engine with the chunk-pipelined RCCL gradient all-reduce.
+    On one GPU it runs under a 1-rank RCCL process group (the collectives are issued but move
+    nothing); the N-GPU numbers come from the driver's ``bench.py --parallelism dp`` runs."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--parallelism", "dp", "--force-dist", "--no-eval",
+           "--compare-parallelism", "0", "--steps", str(a.steps), "--warmup", str(a.warmup)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr[-2000:])
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    G, n, d = 8, 2048, 512
+    grad_bytes = (2 * G * n * d + G * n) * 4
+    return {"config": "3: Pythia-70m MLP-out (hook_mlp_out, d=512), ratio 4, 8 models, data-parallel fused step "
+                      "(ChunkedDataParallel, 1-rank RCCL group on one GPU)", "unit": "activations/s",
+            "value": rec["value"], "ms_per_step": rec["ms_per_step"], "dtype": "bf16", "data": "synthetic",
+            "parallelism": rec["config"]["parallelism"], "dp_chunks": rec["config"]["dp_chunks"],
+            "allreduce_bytes_per_step": grad_bytes,
+            "allreduce_ring_bytes_sent_per_gpu_at_8": round(2 * 7 / 8 * grad_bytes),
+            "note": "per-GPU compute of the DP step; the all-reduce is measured by the driver's multi-GPU runs"}
+
+
 def cfg_mlp(a):
-    """Config 3 shapes on one GPU: Pythia-70m MLP-out width d_mlp = 2048, ratio 4 (n = 8192),
+    """Pythia-70m MLP hidden activations (``mlp`` = hook_post, d_mlp = 2048), ratio 4 (n = 8192),
     8-model L1 sweep, fused engine in one HIP graph; plus the per-GPU step of the
     ensemble-sharded layout at N = 2, 4, 8 (G/N models on N*B gathered rows) that the
     8-GPU run uses."""
@@ -139,7 +173,7 @@ def cfg_mlp(a):
     l1s = np.logspace(-4, -2, a.models)
     models = [FunctionalSAE.init(d, n, float(l), device=dev) for l in l1s]
     ring = _ring(d, dev, rows=1 << 18)
-    out = {"config": f"3: Pythia-70m MLP-out shapes d={d}, ratio {ratio} (n={n}), {a.models} models, fused, "
+    out = {"config": f"Pythia-70m MLP hidden (hook_post) shapes d={d}, ratio {ratio} (n={n}), {a.models} models, fused, "
                      "per-GPU work of the 8-GPU ensemble-sharded run", "unit": "activations/s", "batch": B,
            "dtype": "bf16", "data": "synthetic", "per_n": []}
     for N in (1, 2, 4, 8):
@@ -212,7 +246,7 @@ def cfg_harvest(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["cpu", "topk", "fista", "mlp", "harvest"])
+    ap.add_argument("which", choices=["cpu", "topk", "fista", "mlp", "mlpout", "harvest"])
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=2048)
@@ -221,7 +255,8 @@ def main():
     ap.add_argument("--ratio", type=float, default=1.0)
     ap.add_argument("--ring-gb", type=float, default=0.0, help="fista: ring size in GB of HBM (0: 512k rows)")
     a = ap.parse_args()
-    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp, "harvest": cfg_harvest}[a.which](a)
+    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp, "mlpout": cfg_mlpout,
+           "harvest": cfg_harvest}[a.which](a)
     print(json.dumps(rec), flush=True)
 
 

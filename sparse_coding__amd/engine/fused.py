@@ -275,16 +275,16 @@ class FusedSAEEnsemble:
                              self.cnt_part if count else None, self.nactive, mask_out=self.cmask,
                              act=self.act, ascale=ascale, mask2_out=self.cmask2)
         gemm_ops.decode_residual(self.c, self.dec_shadow, x if target is None else target, self.r, self.dec_part,
-                                 rcol=self.rcol)
+                                 rcol=self.rcol, nactive=self.nactive)
         if self.act:
             gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                                dotpart=self.dotpart if self.kind == "threshold" else None, mask=self.cmask,
-                               act=self.act, ascale=ascale, mask2=self.cmask2)
+                               act=self.act, ascale=ascale, mask2=self.cmask2, nactive=self.nactive)
             return
         gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                            dotpart=self.dotpart if self.fuse_adam else None,
                            tied_bias=self.params["encoder_bias"] if (self.fuse_adam and self.kind == "tied") else None,
-                           mask=self.cmask)
+                           mask=self.cmask, nactive=self.nactive)
 
     def wgrad_adam(self, x):
         """Weight gradients with Adam in the GEMM epilogue, then the decoder-row normalisation."""
@@ -312,15 +312,16 @@ class FusedSAEEnsemble:
         """Untied: dW_hat = c^T R (decoder).  Tied: the whole dictionary gradient + bias grad."""
         self._g_from_parts = False
         if self.kind == "untied":
-            gemm_ops.weight_grads([[(self.c, self.r)]], [self.g_dec], self._alpha)
+            gemm_ops.weight_grads([[(self.c, self.r)]], [self.g_dec], self._alpha, nactive=self.nactive)
         else:
-            gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], [self.g_dec], self._alpha)
+            gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], [self.g_dec], self._alpha,
+                                  nactive=self.nactive)
             self._reduce_bias_grad()
 
     def wgrad_second(self, x, reduce_bias=True):
         """Untied: dW_e = dpre^T x (encoder) + bias grad.  Tied: nothing."""
         if self.kind == "untied":
-            gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha)
+            gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha, nactive=self.nactive)
             if reduce_bias:
                 self._reduce_bias_grad()
 
@@ -348,10 +349,12 @@ class FusedSAEEnsemble:
         self._g_from_parts = split
         if self.kind == "untied":
             outs = [self.g_parts[0], self.g_parts[1]] if split else [self.g_dec, self.g_enc]
-            gemm_ops.weight_grads([[(self.c, self.r)], [(self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit)
+            gemm_ops.weight_grads([[(self.c, self.r)], [(self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit,
+                                  nactive=self.nactive)
         else:
             outs = [self.g_parts[0]] if split else [self.g_dec]
-            gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit)
+            gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit,
+                                  nactive=self.nactive)
 
     def _adam_sets(self):
         parts = self._g_from_parts
@@ -372,13 +375,13 @@ class FusedSAEEnsemble:
 
     def adam_first(self):
         adam_ops.adam_rows(self._adam_sets()[:1], self.lr, self.step_count + 1, *self.betas, self.eps,
-                           step_dev=self.step_dev)
+                           step_dev=self.step_dev, live=self.nactive)
 
     def adam_second(self, reduced_bias=True):
         """Encoder Adam (untied) and bias Adam + loss reduction (advances the step counter)."""
         if self.kind == "untied":
             adam_ops.adam_rows(self._adam_sets()[1:], self.lr, self.step_count + 1, *self.betas, self.eps,
-                               step_dev=self.step_dev)
+                               step_dev=self.step_dev, live=self.nactive)
         if self.kind == "threshold" or self.learned_center:
             self._threshold_extra_adam(reduced=reduced_bias)
         self._bias_loss(update=True, reduced=reduced_bias)
@@ -392,7 +395,7 @@ class FusedSAEEnsemble:
     def _apply_update_kernels(self):
         if not self.fuse_adam:  # with fuse_adam the weights were already updated in wgrad_adam
             adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
-                               step_dev=self.step_dev, **self._adam_split_kw())
+                               step_dev=self.step_dev, live=self.nactive, **self._adam_split_kw())
         if self.kind == "threshold" or self.learned_center:
             self._threshold_extra_adam()
         self._bias_loss(update=True, reduced=False)
@@ -498,10 +501,10 @@ class FusedSAEEnsemble:
             self._side.wait_stream(main)
             with torch.cuda.stream(self._side):
                 adam_ops.adam_rows(sets[:1], self.lr, self.step_count + 1, *self.betas, self.eps,
-                                   step_dev=self.step_dev)
+                                   step_dev=self.step_dev, live=self.nactive)
             self.wgrad_second(x, reduce_bias=False)
             adam_ops.adam_rows(sets[1:], self.lr, self.step_count + 1, *self.betas, self.eps,
-                               step_dev=self.step_dev)
+                               step_dev=self.step_dev, live=self.nactive)
             main.wait_stream(self._side)  # join before the step counter advances
             self._bias_loss(update=True, reduced=False)
         else:

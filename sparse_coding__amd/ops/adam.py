@@ -14,7 +14,7 @@ def _vp(seq):
 
 
 def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, step_dev=None, nsplit=1,
-              gstride=0, row0=0):
+              gstride=0, row0=0, live=None):
     """Fused row-wise Adam over one or two parameter sets.
 
     sets: list of dicts with keys p, g, m, v (fp32 [G, n, d]), shadow (bf16 [G, n, d] or None),
@@ -24,7 +24,9 @@ def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, s
     graph-capturable).  ``nsplit`` > 1: each ``g`` is the first of ``nsplit`` split-K partial
     slabs ``gstride`` elements apart, summed in the kernel.  ``row0``: global index of the
     sets' first row (row-sharded updates; the per-model lr is ``lr[(row0 + row) // n]``).
-    Tensors may be [G, n, d] or [rows, d] (then pass ``rows_per_model``).
+    Tensors may be [G, n, d] or [rows, d] (then pass ``rows_per_model``).  ``live``: optional
+    int32 [G] live row count per model (masked ensembles; rows past it have zero gradient and
+    are skipped -- their Adam update is exactly zero).
     """
     if not 1 <= len(sets) <= 2:
         raise ValueError("1 or 2 parameter sets")
@@ -56,7 +58,7 @@ def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, s
         _vp([s["m"] for s in sets]), _vp([s["v"] for s in sets]),
         _vp([s.get("shadow") for s in sets]), _vp([s.get("norms") for s in sets]),
         rows, norm, d, rpm, _lib.ptr(lr), b1, b2, eps, bc1, bc2,
-        _lib.ptr(step_dev), int(nsplit), int(gstride), int(row0), _lib.stream_handle(),
+        _lib.ptr(step_dev), int(nsplit), int(gstride), int(row0), _lib.stream_handle(), _lib.ptr(live),
     )
     _lib.check(rc, "sc_adam_rows")
 

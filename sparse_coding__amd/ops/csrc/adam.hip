@@ -37,6 +37,7 @@ struct AdamArgs {
   const float* lr;  // per model
   float b1, b2, eps, bc1, bc2;
   const int* step;  // optional device step counter (graph-capturable); t = *step + 1
+  const int* live;  // optional per-model live row count (masked ensembles): rows past it are skipped
 };
 
 // Adam bias corrections for 1-based step t, computed on the device so a captured
@@ -60,7 +61,9 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   const AdamRows& R = a.set[s];
   const int d = NV * 256;
   const long base = row * d;
-  const float lr = a.lr[(row + a.row0) / a.rows_per_model];
+  const long grow = row + a.row0;
+  if (a.live && (int)(grow % a.rows_per_model) >= a.live[grow / a.rows_per_model]) return;  // dead row: zero grad
+  const float lr = a.lr[grow / a.rows_per_model];
   // NV float4 chunks per lane (d == 256 * NV); compile-time so pv/gv stay in VGPRs.
   const float* P4 = R.p + base;
   const float* G4 = R.g + base;
@@ -323,7 +326,8 @@ extern "C" {
 int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const* m, float* const* v,
                  void* const* shadow, float* const* norms, const int* rows, const int* norm, int d,
                  int rows_per_model, const float* lr, float b1, float b2, float eps, float bc1,
-                 float bc2, const int* step, int nsplit, long gstride, long row0, hipStream_t stream) {
+                 float bc2, const int* step, int nsplit, long gstride, long row0, hipStream_t stream,
+                 const int* live) {
   if (d % 256 || d > 4096 || nset < 1 || nset > 2 || nsplit < 1) return 1;
   AdamArgs a;
   long total = 0;
@@ -334,7 +338,7 @@ int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const*
   if (nset == 1) a.set[1] = a.set[0], a.set[1].rows = 0;
   a.nset = nset; a.d = d; a.rows_per_model = rows_per_model; a.lr = lr;
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.step = step;
-  a.nsplit = nsplit; a.gstride = gstride; a.row0 = row0;
+  a.nsplit = nsplit; a.gstride = gstride; a.row0 = row0; a.live = live;
   const long blocks = (total + 3) / 4;
   switch (d / 256) {
     case 1: hipLaunchKernelGGL(adam_rows_kernel<1>, dim3(blocks), dim3(256), 0, stream, a); break;

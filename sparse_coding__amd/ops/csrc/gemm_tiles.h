@@ -106,6 +106,9 @@ struct GemmParams {
   int ksplit;
   long split_stride;
   int dbg;  // diagnostics (SC_GEMM_DBG): bit 0 = EPI_BF16 skips its output stores
+  // masked ensembles: per-group live extent of the n dimension when it is M / K (may be null)
+  const int* nact_m;
+  const int* nact_k;
   // host-precomputed divisors of the block -> tile decomposition (set by the launcher)
   FDiv f_prob, f_split, f_plane, f_tn, f_ksplit;
   // --- EPI_ENC_ACT / EPI_DC_ACT: activation mode and the threshold SAE's per-feature s^2

@@ -88,7 +88,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             float* dotpart, int dc_tied, const ScAdamEpi* adam /* [nprob] or null */, const float* lr,
             const int* step, float b1, float b2, float eps, int dot_tm, float dot_scale,
             int cfg, int ksplit, long split_stride, void* cmask, int act, const float* ascale,
-            void* cmask2, float* rcol, hipStream_t stream) {
+            void* cmask2, float* rcol, const int* nact_m, const int* nact_k, hipStream_t stream) {
   if (M % PT || N % PT || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
   if ((epi == EPI_DC_MASK || epi == EPI_DC_ACT) && !cmask) return 4;
   if (epi == EPI_DC_ACT && (!aux || !colpart || !l1)) return 4;
@@ -125,6 +125,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.dbg = dbg;
   p.act = act; p.ascale = ascale;
   p.cmask2 = reinterpret_cast<uint64_t*>(cmask2); p.rcol = rcol;
+  p.nact_m = nact_m; p.nact_k = nact_k;
   const bool ak = layout & 1, bk = layout & 2;
   int shape = cfg & 3;
   const int pipe = (cfg >> 2) & 3;  // 0: BK64 x 2 stages, 1: BK32 x 4, 2: BK32 x 2, 3: BK32 x 3

@@ -636,7 +636,17 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   const int nk1 = p.K1 / BKT, nk_all = nk1 + (SEG2 ? p.K2 / BKT : 0);
   // this block's K-tile range [kbeg, nk) (the whole range unless split-K)
   const int kbeg = p.ksplit == 1 ? 0 : (int)fdiv(ksi * nk_all, p.f_ksplit);
-  const int nk = p.ksplit == 1 ? nk_all : (int)fdiv((ksi + 1) * nk_all, p.f_ksplit);
+  int nk = p.ksplit == 1 ? nk_all : (int)fdiv((ksi + 1) * nk_all, p.f_ksplit);
+  // Masked ensembles (models with different live dictionary sizes stacked to one width,
+  // reference sae_ensemble.py:306-442): output tiles wholly past a model's live columns
+  // (nactive: the n dimension is N) or rows (nact_m: n is M), and K-tiles past its live
+  // K range (nact_k: n is K), do no MFMA work -- the tile's epilogue still writes its zeros
+  // and partial sums.  Block-uniform.
+  bool dead = false;
+  if (p.nactive && (ENC || EPI == EPI_DC || EPI == EPI_DC_MASK || EPI == EPI_DC_ACT)) dead = n0 >= p.nactive[g];
+  if (p.nact_m) dead = dead || m0 >= p.nact_m[g];
+  if (p.nact_k) nk = min(nk, (p.nact_k[g] + BKT - 1) / BKT);
+  dead = dead || nk <= kbeg;
   // per-lane DMA source offsets for both K segments
   uint32_t va0[PPWA], vb0[PPWB], va1[SEG2 ? PPWA : 1], vb1[SEG2 ? PPWB : 1];
   piece_offsets<AK, BKT, PPWA>(va0, oa0.ld, m0, wid, lane);
@@ -689,6 +699,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
         auxv[i][j] = *reinterpret_cast<const uint2*>(X + (long)(rowb + i * 16) * p.ldaux + colb + j * 16);
   }
 
+  if (!dead) {  // ---------------------------------------------------------------- K loop
 #pragma unroll
   for (int t = 0; t < NST - 1; ++t)
     if (kbeg + t < nk) SC_ISSUE(kbeg + t);
@@ -817,6 +828,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
       __builtin_amdgcn_s_setprio(0);
     }
   }
+  }  // !dead
 #undef SC_ISSUE
   lds_barrier();  // all reads of the ring done before smem is reused below
   constexpr bool STAGE = S::WI == 4 && S::WJ == 4 && NST * STG >= stage_bytes<S>();

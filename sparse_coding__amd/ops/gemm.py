@@ -130,7 +130,8 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
             bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
             colpart=None, l1=None, l1_add_scale=0.0, dotpart=None, dc_tied=False, adam=None,
             lr=None, step=None, betas=(0.9, 0.999), eps=1e-8, dot_tm=0, dot_scale=0.0, cfg=None,
-            ksplit=1, split_stride=0, cmask=None, act=0, ascale=None, cmask2=None, rcol=None):
+            ksplit=1, split_stride=0, cmask=None, act=0, ascale=None, cmask2=None, rcol=None, nact_m=None,
+            nact_k=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     cfg_explicit = cfg
@@ -151,7 +152,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
         _lib.ptr(dotpart), int(bool(dc_tied)), adam, _lib.ptr(lr), _lib.ptr(step),
         float(betas[0]), float(betas[1]), float(eps), int(dot_tm), float(dot_scale),
         cfg, int(ksplit), int(split_stride), _lib.ptr(cmask), int(act), _lib.ptr(ascale),
-        _lib.ptr(cmask2), _lib.ptr(rcol), _lib.stream_handle(),
+        _lib.ptr(cmask2), _lib.ptr(rcol), _lib.ptr(nact_m), _lib.ptr(nact_k), _lib.stream_handle(),
     )
     _lib.check(rc, f"sc_gemm(epi={epi})")
 
@@ -217,7 +218,7 @@ def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=No
             ascale=ascale, cmask2=mask2_out)
 
 
-def decode_residual(c, w_hat, x, r_out, part, rcol=None):
+def decode_residual(c, w_hat, x, r_out, part, rcol=None, nactive=None):
     """r[g] = c[g] @ w_hat[g] - x[g]  (bf16 out) with sum(r^2) partials.
 
     c: [G, B, n] bf16; w_hat: [G, n, d] bf16 (row-normalised dictionary);
@@ -236,12 +237,13 @@ def decode_residual(c, w_hat, x, r_out, part, rcol=None):
               "rcol must be fp32 [G, B/128, d]")
     a = [_op(c, n, B * n)] * 2
     b = [_op(w_hat, d, n * d)] * 2  # stored [K=n][N=d] -> N-major
-    _launch(EPI_DEC, 1, B, d, n, 0, G, a, b, [r_out], [1.0], d, B * d,
+    # nactive (masked ensembles): codes past a model's live size are zero -- skip those K-tiles
+    _launch(EPI_DEC, 1, B, d, n, 0, G, a, b, [r_out], [1.0], d, B * d, nact_k=nactive,
             aux=x, ldaux=d, saux=sx, part=part, rcol=rcol)
 
 
 def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, mask=None, act=ACT_RELU,
-              ascale=None, mask2=None):
+              ascale=None, mask2=None, nactive=None):
     """dpre_s[g] = 1[c>0] * (r[g] @ w_hat[g]^T + l1[g] * d / 2).
 
     dpre_s is the code gradient in units of the residual: dL/dpre = 2/(B d) * dpre_s.
@@ -278,12 +280,12 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, 
                   and tuple(mask2.shape) == code_mask_shape(G, B, n), "mask2 must match the encoder's mask2_out")
         _launch(EPI_DC_ACT, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
                 aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0,
-                dotpart=dotpart, cmask=mask, act=act, ascale=ascale, sbias=n, cmask2=mask2)
+                dotpart=dotpart, cmask=mask, act=act, ascale=ascale, sbias=n, cmask2=mask2, nactive=nactive)
         return
     if mask is not None and dotpart is None:
         _need(mask.dtype == torch.int64 and tuple(mask.shape) == code_mask_shape(G, B, n), "mask shape")
         _launch(EPI_DC_MASK, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
-                colpart=colpart, l1=l1, l1_add_scale=d / 2.0, cmask=mask)
+                colpart=colpart, l1=l1, l1_add_scale=d / 2.0, cmask=mask, nactive=nactive)
         return
     _launch(EPI_DC, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
             aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0,
@@ -302,7 +304,7 @@ def wgrad_split(G, n, d, K, nprob):
     return s
 
 
-def weight_grads(pairs, outs, alpha, ksplit=1):
+def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None):
     """out_i[g] = alpha * sum_segments A_s[g]^T @ B_s[g]   (reduction over batch rows).
 
     pairs: list (one per problem, 1 or 2 problems) of lists of (A, B) segments
@@ -339,8 +341,10 @@ def weight_grads(pairs, outs, alpha, ksplit=1):
     cfg = None
     if ksplit > 1:
         cfg = 3 if shape_fits(3, n, d) else 1
+    # nactive (masked ensembles): gradient rows past a model's live size are zero -- those tiles
+    # skip their MFMAs and only write the zeros
     _launch(EPI_F32, 0, n, d, K1, K2, G, a_ops, b_ops, list(outs), [alpha] * len(outs), d, n * d,
-            cfg=cfg, ksplit=ksplit, split_stride=G * n * d)
+            cfg=cfg, ksplit=ksplit, split_stride=G * n * d, nact_m=nactive)
 
 
 def weight_grads_adam(pairs, states, alpha, lr, step_dev, betas=(0.9, 0.999), eps=1e-8, dot_tm=0):
