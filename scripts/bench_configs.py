@@ -158,6 +158,38 @@ def cfg_mlpout(a):
             "note": "per-GPU compute of the DP step; the all-reduce is measured by the driver's multi-GPU runs"}
 
 
+def cfg_masked(a):
+    """Masked ensemble (reference dict_ratio_experiment, big_sweep_experiments.py:546-580): tied
+    SAEs of 8 dictionary sizes 512 * linspace(1, 5, 8) stacked to width 2560 on d = 512; the
+    fused step skips every tile past a model's live size, so its time should track the sum of
+    live sizes (3/5 of the stacked width) -- compared with the same 8 models unmasked."""
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalMaskedTiedSAE, FunctionalTiedSAE
+
+    dev = "cuda:0"
+    torch.manual_seed(0)
+    d, B = 512, a.batch
+    sizes = [int(512 * x) for x in np.linspace(1, 5, 8)]
+    stack = ((max(sizes) + 127) // 128) * 128
+    ring = _ring(d, dev, rows=1 << 18)
+    out = {"config": f"masked: {len(sizes)} tied SAEs of sizes {sizes} stacked to {stack}, d={d}, batch {B}",
+           "unit": "activations/s", "dtype": "bf16", "data": "synthetic",
+           "live_fraction": round(sum(sizes) / (stack * len(sizes)), 4)}
+    for name, sig, models in (
+            ("masked", FunctionalMaskedTiedSAE, [FunctionalMaskedTiedSAE.init(d, s, stack, 1e-3, device=dev) for s in sizes]),
+            ("unmasked", FunctionalTiedSAE, [FunctionalTiedSAE.init(d, stack, 1e-3, device=dev) for _ in sizes])):
+        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=dev)
+        eng.enable_graph()
+        el = _timed(lambda: (ring.sample(B, out=eng.x_static), eng.step_static()), a.steps, a.warmup,
+                    torch.cuda.synchronize)
+        out[f"{name}_ms_per_step"] = round(1e3 * el / a.steps, 4)
+        del eng
+        torch.cuda.empty_cache()
+    out["time_ratio"] = round(out["masked_ms_per_step"] / out["unmasked_ms_per_step"], 4)
+    out["value"] = round(B / out["masked_ms_per_step"] * 1e3, 1)
+    return out
+
+
 def cfg_mlp(a):
     """Pythia-70m MLP hidden activations (``mlp`` = hook_post, d_mlp = 2048), ratio 4 (n = 8192),
     8-model L1 sweep, fused engine in one HIP graph; plus the per-GPU step of the
@@ -246,7 +278,7 @@ def cfg_harvest(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["cpu", "topk", "fista", "mlp", "mlpout", "harvest"])
+    ap.add_argument("which", choices=["cpu", "topk", "fista", "mlp", "mlpout", "masked", "harvest"])
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=2048)
@@ -255,7 +287,7 @@ def main():
     ap.add_argument("--ratio", type=float, default=1.0)
     ap.add_argument("--ring-gb", type=float, default=0.0, help="fista: ring size in GB of HBM (0: 512k rows)")
     a = ap.parse_args()
-    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp, "mlpout": cfg_mlpout,
+    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp, "mlpout": cfg_mlpout, "masked": cfg_masked,
            "harvest": cfg_harvest}[a.which](a)
     print(json.dumps(rec), flush=True)
 

@@ -69,6 +69,11 @@ def _declare(lib):
         "sc_fista_gram": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_void_p],
         "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_void_p],
+        "sc_stream_create_cumask": [c_void_p, c_int, C.POINTER(c_void_p)],
+        "sc_stream_destroy": [c_void_p],
+        "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
+        "sc_basis_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int,
+                           c_void_p],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -133,6 +138,18 @@ def check(rc: int, what: str):
 
 def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+def cu_mask_stream(cus, n_cus: int = 256, device=None):
+    """A torch stream whose kernels run only on compute units ``cus`` (iterable of CU ids),
+    created with hipExtStreamCreateWithCUMask (csrc/streams.hip)."""
+    words = (C.c_uint32 * ((n_cus + 31) // 32))()
+    for c in cus:
+        words[c // 32] |= 1 << (c % 32)
+    out = c_void_p()
+    rc = lib().sc_stream_create_cumask(C.cast(words, c_void_p), len(words), C.byref(out))
+    check(rc, "sc_stream_create_cumask")
+    return torch.cuda.ExternalStream(out.value, device=device)
 
 
 def stream_handle(device=None) -> int:

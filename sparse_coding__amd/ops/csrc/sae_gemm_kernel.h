@@ -96,7 +96,7 @@ constexpr int stage_bytes() { return STAGE_OFF + S::NW * STAGE_WAVE; }
 template <class S, int EPI, bool AUX_EARLY, bool STAGE = false>
 __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)[S::WI][S::WJ],
                                              const uint2 (&auxv)[S::WI][S::WJ], float* red, int pi, int g, int m0,
-                                             int n0, int tn, int tiles_n, void* cptr, float alpha) {
+                                             int n0, int tn, int tiles_n, void* cptr, float alpha, bool dead = false) {
   constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
   constexpr bool ENC = (EPI == EPI_ENC || EPI == EPI_ENC_CNT || EPI == EPI_ENC_ACT);
   constexpr int RED_SUM = 2 * S::WGM * BN;  // block_sum scratch after the two column-sum regions
@@ -129,6 +129,60 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
       }
     }
   };
+
+  constexpr bool CAN_DIE = ENC || EPI == EPI_DC || EPI == EPI_DC_MASK || EPI == EPI_DC_ACT || EPI == EPI_F32 ||
+                           EPI == EPI_ADAM;
+  if (CAN_DIE && dead) {
+    // A tile wholly past a model's live dictionary (masked ensembles): no MFMA work ran.  The
+    // encoder still writes its zero codes and activity words and the weight gradient its
+    // zero rows (API outputs); the code gradient's dead columns are left unwritten (only the
+    // engine passes nactive there, and nothing downstream reads them: the weight gradient
+    // skips those rows); the partial sums consumers add over every tile are zeroed.
+    if constexpr (ENC) {
+      uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
+#pragma unroll
+      for (int i = 0; i < WI; ++i)
+#pragma unroll
+        for (int j = 0; j < WJ; ++j)
+          *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + colb + j * 16) = make_ushort4(0, 0, 0, 0);
+      if (p.cmask) {
+#pragma unroll
+        for (int k = 0; k < WI / 4; ++k) {
+          const long w = mask_word(p, g, rowb - (lane & 15) + 64 * k, colb - 4 * (lane >> 4), lane);
+          p.cmask[w] = 0ull;
+          if (p.cmask2) p.cmask2[w] = 0ull;
+        }
+      }
+    }
+    if constexpr (EPI == EPI_F32) {
+      float* C = reinterpret_cast<float*>(cptr) + (long)g * p.sc;
+#pragma unroll
+      for (int i = 0; i < WI; ++i)
+#pragma unroll
+        for (int j = 0; j < WJ; ++j)
+          *reinterpret_cast<f32x4_t*>(C + (long)(rowb + i * 16) * p.ldc + colb + j * 16) = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (ENC) {
+      for (int idx = tid; idx < (BM / PT) * (BN / PT); idx += NT) {
+        const int sm = idx / (BN / PT), sn = idx - sm * (BN / PT);
+        float* dst = p.part + ((long)g * ptm * ptn + (m0 / PT + sm) * ptn + n0 / PT + sn) * 2;
+        dst[0] = 0.f;
+        dst[1] = 0.f;
+      }
+    }
+    if constexpr (ENC || EPI == EPI_DC || EPI == EPI_DC_MASK || EPI == EPI_DC_ACT) {
+      float* outs[2] = {p.colpart, (EPI == EPI_DC || EPI == EPI_DC_ACT) ? p.dotpart : nullptr};
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+        if (!outs[o]) continue;
+        for (int idx = tid; idx < (BM / PT) * BN; idx += NT) {
+          const int sl = idx / BN, col = idx - sl * BN;
+          outs[o][((long)g * ptm + m0 / PT + sl) * p.N + n0 + col] = 0.f;
+        }
+      }
+    }
+    return;
+  }
 
   if constexpr (EPI == EPI_F32) {
     float* C = reinterpret_cast<float*>(cptr) + (long)g * p.sc;
@@ -833,7 +887,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   lds_barrier();  // all reads of the ring done before smem is reused below
   constexpr bool STAGE = S::WI == 4 && S::WJ == 4 && NST * STG >= stage_bytes<S>();
   sae_epilogue<S, EPI, AUX_EARLY, STAGE>(p, acc, auxv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn, tiles_n,
-                                         cptr, alpha);
+                                         cptr, alpha, dead);
 }
 
 

@@ -170,25 +170,58 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
     return A, Xf - torch.bmm(A, D.float())
 
 
-def hessian_ema(H, A, history: int = 300):
-    """H <- H (history-1)/history + mean_b(A^2)/history (reference fista.py:91-92)."""
-    return H * ((history - 1.0) / history) + A.pow(2).mean(dim=-2) / history
+def _hip_ok(*ts) -> bool:
+    return all(t.is_cuda for t in ts) and _lib.available()
+
+
+def hessian_ema(H, A, history: int = 300, backend: str = "auto"):
+    """H <- H (history-1)/history + mean_b(A^2)/history (reference fista.py:91-92).
+
+    HIP path (``backend`` "hip" / "auto" on the GPU): one column-reduction kernel for every
+    model (csrc/fista_update.hip); returns a new tensor either way."""
+    G, B, n = A.shape
+    if backend == "torch" or not (_hip_ok(A, H) and n % 64 == 0):
+        return H * ((history - 1.0) / history) + A.pow(2).mean(dim=-2) / history
+    out = H.float().contiguous().clone()
+    rc = _lib.lib().sc_hessian_ema(_lib.ptr(A.float().contiguous()), _lib.ptr(out), G, B, n, float(history),
+                                   _lib.stream_handle())
+    _lib.check(rc, "sc_hessian_ema")
+    return out
 
 
 def quadratic_basis_update(D, Res, A, H, lowest_activation=0.001, step=0.001, nonneg=False,
-                           normalize: str = "column"):
+                           normalize: str = "column", backend: str = "auto", shadow_out=None):
     """D' = D + (step Res^T A / B / (H + lowest))^T, then renormalise (reference :131-138).
 
     normalize="column" reproduces the reference (``D.norm(2, 0)``: per activation
     dimension, SURVEY B#4); "row" normalises each atom (the intended unit-norm dictionary).
     Batched over models: D [G, n, d], Res [G, B, d], A [G, B, n], H [G, n].
+
+    HIP path: A^T Res by the grouped MFMA GEMM (bf16 operands, fp32 accumulation, the
+    step/B scale in its epilogue), then one kernel adds the H-scaled update, clamps and
+    renormalises (csrc/fista_update.hip); ``shadow_out`` (bf16 [G, n, d]) optionally receives
+    the bf16 copy the next solve multiplies by.
     """
-    B = A.shape[-2]
-    dB = step * torch.bmm(Res.transpose(1, 2).float(), A.float()) / B  # [G, d, n]
-    dB = dB / (H.unsqueeze(1) + lowest_activation)
-    D = D.float() + dB.transpose(1, 2)
-    if nonneg:
-        D = D.clamp(min=0.0)
-    if normalize == "column":
-        return D / D.norm(dim=1, keepdim=True)
-    return D / D.norm(dim=2, keepdim=True).clamp(min=1e-8)
+    G, B, n = A.shape
+    d = D.shape[-1]
+    hip = backend != "torch" and _hip_ok(D, Res, A, H) and n % 128 == 0 and d % 128 == 0 and B % 64 == 0
+    if not hip:
+        dB = step * torch.bmm(Res.transpose(1, 2).float(), A.float()) / B  # [G, d, n]
+        dB = dB / (H.unsqueeze(1) + lowest_activation)
+        D = D.float() + dB.transpose(1, 2)
+        if nonneg:
+            D = D.clamp(min=0.0)
+        out = D / D.norm(dim=1, keepdim=True) if normalize == "column" else D / D.norm(dim=2, keepdim=True).clamp(min=1e-8)
+        if shadow_out is not None:
+            shadow_out.copy_(out)
+        return out
+    from . import gemm
+
+    dBt = torch.empty(G, n, d, device=D.device)
+    gemm.weight_grads([[(A.to(torch.bfloat16).contiguous(), Res.to(torch.bfloat16).contiguous())]], [dBt], step / B)
+    out = D.float().contiguous().clone()
+    rc = _lib.lib().sc_basis_apply(_lib.ptr(out), _lib.ptr(dBt), _lib.ptr(H.float().contiguous()),
+                                   _lib.ptr(shadow_out), G, n, d, float(lowest_activation), int(bool(nonneg)),
+                                   1 if normalize == "row" else 0, _lib.stream_handle())
+    _lib.check(rc, "sc_basis_apply")
+    return out

@@ -258,6 +258,9 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, 
     (the bias gets no gradient through the codes).  Threshold (``ascale`` = s2): dpre_s =
     active * (r w^T + l1 d/2) thr', column sums = gain gradient, and ``dotpart`` receives
     the partials of sum_b dL/dc (thr - u thr') (x 2 s: the scale gradient).
+    ``nactive`` (masked ensembles, the engine): column tiles wholly past a model's live size
+    skip their MFMA work and leave ``dpre_out`` there unwritten (the weight gradient skips
+    those rows); their bias-gradient partials are zeroed.
     """
     G, B, d = r.shape
     n = w_hat.shape[1]

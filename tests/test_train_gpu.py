@@ -219,3 +219,34 @@ def test_sweep_cli_ensemble_sharded_rccl(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     lds = ckpt.load_learned_dicts(str(tmp_path / "o" / "learned_dicts_epoch_0.pt"))
     assert len(lds) == 2 and all(torch.isfinite(ld.get_learned_dict()).all() for ld, _ in lds)
+
+
+def test_masked_ensemble_fused_skips_dead_tiles():
+    """Masked tied SAEs of several sizes stacked to one width (reference sae_ensemble.py:306-371,
+    dict_ratio_experiment): the fused engine (which skips the MFMA work of tiles past each model's
+    live size) tracks the eager masked signature, and parameters past dict_size never change."""
+    from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.engine.optim import adam
+    from sparse_coding__amd.models.signatures import FunctionalMaskedTiedSAE
+
+    torch.manual_seed(5)
+    d, stack, B = 256, 640, 256
+    sizes = [128, 256, 384, 640]
+    models = [FunctionalMaskedTiedSAE.init(d, s, stack, 1e-3, device="cuda") for s in sizes]
+    ref = FunctionalEnsemble([({k: v.clone() for k, v in p.items()}, b) for p, b in models], FunctionalMaskedTiedSAE,
+                             adam, {"lr": 1e-3}, device="cuda")
+    fused = FusedSAEEnsemble(models, FunctionalMaskedTiedSAE, lr=1e-3, batch_size=B, device="cuda")
+    feats = torch.nn.functional.normalize(torch.randn(1024, d, device="cuda"), dim=-1)
+    for _ in range(4):
+        x = (torch.relu(torch.randn(B, 1024, device="cuda") - 2.0) @ feats).to(torch.bfloat16)
+        loss_ref, _ = ref.step_batch(x.float())
+        out = fused.step_batch(x)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(out[:, 0], loss_ref["loss"], rtol=3e-2, atol=1e-4)
+    init = torch.stack([p["encoder"] for p, _ in models])
+    for g, s in enumerate(sizes):
+        assert torch.equal(fused.params["encoder"][g, s:], init[g, s:]), g
+        mv_f = (fused.params["encoder"][g, :s] - init[g, :s]).flatten()
+        mv_r = (ref.params["encoder"][g, :s] - init[g, :s]).flatten()
+        assert torch.nn.functional.cosine_similarity(mv_f, mv_r, dim=0).item() > 0.97, g
