@@ -75,11 +75,11 @@ def cfg_topk(a):
     n = d * ratio
     ks = [8, 16, 24, 32, 48, 64, 96, 128][: a.models]
     models = [TopKEncoder.init(d, n, k, device=dev) for k in ks]
-    eng = FusedTopKEnsemble(models, lr=1e-3, batch_size=B, device=dev)
+    eng = FusedTopKEnsemble(models, lr=1e-3, batch_size=B, device=dev, decode=a.decode)
     ring = _ring(d, dev)
     xbuf = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
     el = _timed(lambda: eng.step_batch(ring.sample(B, out=xbuf)), a.steps, a.warmup, torch.cuda.synchronize)
-    return {"config": f"4: GPT-2-small residual d={d}, ratio {ratio} (n={n}), fused top-k, k={ks}",
+    return {"config": f"4: GPT-2-small residual d={d}, ratio {ratio} (n={n}), fused top-k, k={ks}, {a.decode} decode",
             "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
             "batch": B, "models": len(ks), "dtype": "bf16", "data": "synthetic"}
 
@@ -285,6 +285,7 @@ def main():
     ap.add_argument("--models", type=int, default=8)
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--ratio", type=float, default=1.0)
+    ap.add_argument("--decode", choices=["gather", "gemm"], default="gather", help="topk: decode path")
     ap.add_argument("--ring-gb", type=float, default=0.0, help="fista: ring size in GB of HBM (0: 512k rows)")
     a = ap.parse_args()
     rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp, "mlpout": cfg_mlpout, "masked": cfg_masked,

@@ -22,7 +22,8 @@ from ..ops import topk as topk_ops
 
 
 class FusedTopKEnsemble:
-    def __init__(self, models, sig=None, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999), eps=1e-8):
+    def __init__(self, models, sig=None, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999), eps=1e-8,
+                 decode: str = "gather"):
         from ..models.topk import TopKEncoder
 
         self.sig = sig or TopKEncoder
@@ -55,14 +56,31 @@ class FusedTopKEnsemble:
         self.dscbuf = torch.zeros(G, B, n, device=dev, dtype=bf)
         self.g = torch.empty(G, n, d, device=dev)
         self.idx = self.val = None
+        # decode: "gather" (sparse, one wave per row) or "gemm" (dense codes through the decoder and
+        # code-gradient epilogue GEMMs); chosen from measurement (profiles/config4_topk_r2.json)
+        self.decode = decode
+        self.dec_part = torch.zeros(G, (B // 128) * (d // 128), device=dev)
+        self._colpart = torch.zeros(G, B // 128, n, device=dev)
+        self._zero_l1 = torch.zeros(G, device=dev)
+        self._se = torch.zeros(G, device=dev)
 
     def step_batch(self, batch):
         x = batch.to(self.device, torch.bfloat16).contiguous()
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
         gemm_ops.matmul_nt(x, self.shadow, self.scores)
         self.idx, self.val = topk_ops.topk_select(self.scores, self.k, self.kmax)
-        topk_ops.decode_grad(self.idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
-                             self.dscbuf)
+        if self.decode == "gemm":
+            # dense-GEMM decode: scatter the codes, R = codes D_hat - x (decoder-epilogue GEMM,
+            # sum R^2 partials), code gradients 1[c > 0] (R D_hat^T) (code-gradient epilogue GEMM)
+            topk_ops.scatter(self.idx, self.val, self.k, self.codebuf)
+            gemm_ops.decode_residual(self.codebuf, self.shadow, x, self.r, self.dec_part)
+            gemm_ops.code_grad(self.r, self.shadow, self.codebuf, self._zero_l1, self.dscbuf, self._colpart)
+            torch.sum(self.dec_part, dim=1, out=self._se)
+        else:
+            # gather decode: one wave per row, k dictionary rows gathered twice from L2 / MALL
+            topk_ops.decode_grad(self.idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
+                                 self.dscbuf)
+            torch.sum(self.row_se, dim=1, out=self._se)
         gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g], 2.0 / (B * d))
         topk_ops.clear(self.idx, self.codebuf, self.dscbuf)
         adam_ops.adam_rows([dict(p=self.params["dict"], g=self.g, m=self.m["dict"], v=self.v["dict"],
@@ -70,7 +88,7 @@ class FusedTopKEnsemble:
                            self.lr, self.step_count + 1, *self.betas, self.eps, step_dev=self.step_dev)
         self.step_dev += 1
         self.step_count += 1
-        return self.row_se.sum(dim=1) / (B * d)  # per-model MSE (the reference's loss), on device
+        return self._se / (B * d)  # per-model MSE (the reference's loss), on device
 
     def encode(self, x):
         """Dense top-k codes [G, B, n] for ``x`` [B, d] with the current dictionaries."""

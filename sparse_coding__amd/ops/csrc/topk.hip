@@ -633,6 +633,20 @@ __global__ __launch_bounds__(256) void topk_clear_kernel(const int* __restrict__
   b[row * n + c] = 0;
 }
 
+// Dense bf16 codes from the select's (idx, val) pairs: codebuf[row, idx] = val for the first
+// k[g] slots of each row (the padded slots >= k[g] carry (0, 0.0) and are skipped, so a real
+// pick of feature 0 is never overwritten).  For the dense-GEMM decode path.
+__global__ __launch_bounds__(256) void topk_scatter_kernel(const int* __restrict__ idx, const float* __restrict__ val,
+                                                           const int* __restrict__ kv, uint16_t* __restrict__ code,
+                                                           long rows, int rows_per_model, int n, int kmax) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= rows * kmax) return;
+  const long row = t / kmax;
+  const int s = (int)(t - row * kmax);
+  if (s >= kv[row / rows_per_model]) return;
+  code[row * n + idx[t]] = f2bf(val[t]);
+}
+
 }  // namespace scamd
 
 using namespace scamd;
@@ -685,6 +699,14 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
   SC_D(1) SC_D(2) SC_D(3) SC_D(4) SC_D(8) SC_D(16)
 #undef SC_D
   return 1;
+}
+
+int sc_topk_scatter(const int* idx, const float* val, const int* k, void* code, long rows, int rows_per_model, int n,
+                    int kmax, hipStream_t stream) {
+  const long total = rows * kmax;
+  hipLaunchKernelGGL(topk_scatter_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, idx, val, k,
+                     reinterpret_cast<uint16_t*>(code), rows, rows_per_model, n, kmax);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 int sc_topk_clear(const int* idx, void* a, void* b, long rows, int n, int kmax, hipStream_t stream) {

@@ -43,3 +43,13 @@ def clear(idx, a, b):
     n = a.shape[-1]
     rc = _lib.lib().sc_topk_clear(_lib.ptr(idx), _lib.ptr(a), _lib.ptr(b), G * B, n, kmax, _lib.stream_handle())
     _lib.check(rc, "sc_topk_clear")
+
+
+def scatter(idx, val, k, code):
+    """Dense bf16 codes: code[g, b, idx] = val for the first k[g] slots of every row (the rest of
+    ``code`` must already be zero -- ``clear`` restores that after use)."""
+    G, B, kmax = idx.shape
+    n = code.shape[-1]
+    rc = _lib.lib().sc_topk_scatter(_lib.ptr(idx), _lib.ptr(val), _lib.ptr(k), _lib.ptr(code), G * B, B, n, kmax,
+                                    _lib.stream_handle())
+    _lib.check(rc, "sc_topk_scatter")

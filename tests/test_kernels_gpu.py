@@ -301,14 +301,32 @@ def test_topk_select_exact(radix, n, monkeypatch):
     torch.testing.assert_close(va[2].abs().sort(-1).values, ref)
 
 
-def test_fused_topk_matches_autograd():
+def test_topk_scatter_and_clear_roundtrip():
+    from sparse_coding__amd.ops import topk as T
+
+    torch.manual_seed(4)
+    G, B, n = 3, 128, 512
+    scores = torch.randn(G, B, n, device=DEV)
+    k = torch.tensor([1, 7, 40], dtype=torch.int32, device=DEV)
+    idx, val = T.topk_select(scores, k, 40)
+    code = torch.zeros(G, B, n, device=DEV, dtype=torch.bfloat16)
+    T.scatter(idx, val, k, code)
+    ref = torch.zeros(G, B, n, device=DEV).scatter_add_(-1, idx.long(), val)
+    torch.testing.assert_close(code.float(), ref.to(torch.bfloat16).float(), rtol=0, atol=0)
+    other = torch.zeros_like(code)
+    T.clear(idx, code, other)
+    assert int(code.ne(0).sum()) == 0
+
+
+@pytest.mark.parametrize("decode", ["gather", "gemm"])
+def test_fused_topk_matches_autograd(decode):
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
     from sparse_coding__amd.models.topk import TopKEncoder
 
     torch.manual_seed(7)
     d, n, B = 256, 1024, 256
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
-    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3)
+    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, decode=decode)
     x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
     mse = eng.step_batch(x)
     torch.cuda.synchronize()
