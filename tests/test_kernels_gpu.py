@@ -270,17 +270,22 @@ def test_fused_adam_epilogue_matches_separate_adam():
         _close(a.dec_shadow, b.dec_shadow, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("radix", [False, True])
+@pytest.mark.parametrize("mode", ["default", "radix", "nobracket"])
 @pytest.mark.parametrize("n", [6144, 1000, 12288])  # block-per-row, wave-per-row, block (PL=48)
-def test_topk_select_exact(radix, n, monkeypatch):
+def test_topk_select_exact(mode, n, monkeypatch):
     from sparse_coding__amd.ops import topk as T
 
-    if radix:
+    if mode == "radix":
         monkeypatch.setenv("SC_TOPK_RADIX", "1")  # the block-radix kernel instead of wave bisection
+    if mode == "nobracket":
+        if n <= 4096:
+            pytest.skip("the bracket only exists in the block-per-row kernel")
+        monkeypatch.setenv("SC_TOPK_NOBRACKET", "1")  # read once per process: only effective first
     torch.manual_seed(6)
     G, B = 3, 64
     scores = torch.randn(G, B, n, device=DEV)
     scores[0, 0, :10] = 5.0  # ties at the threshold
+    scores[1, 2, :] = 0.0  # every key tied: the bracket overflows and the full bisection runs
     scores[2, 1, 100:400] = 0.75  # a crowded bucket: 300 equal keys straddle the threshold
     scores[2, 1, 400:] = -1.0
     k = torch.tensor([1, 32, 150], device=DEV, dtype=torch.int32)
