@@ -24,8 +24,8 @@ constexpr int FNT = 512;  // 8 waves
 
 struct FistaArgs {
   const uint16_t* X;   // [G][B][d] bf16
-  const uint16_t* D;   // [G][n][d] bf16 (row-normalised dictionary)
-  const uint16_t* Dt;  // [G][d][n] bf16 (transpose)
+  const uint16_t* D;   // [G][n/16][d/32][64][8] bf16 row-normalised dictionary, MFMA-fragment order
+  const uint16_t* Dt;  // [G][d/16][n/32][64][8] bf16 its transpose, fragment order
   const float* A0;     // [G][B][n] warm start (may be null -> zeros)
   const float* eta;    // [G]
   const float* lam;    // [G]
@@ -53,7 +53,7 @@ __device__ __forceinline__ void lds_put4(char* base, int row, int col, int rowby
 
 // DW: 16-column output tiles per wave in phase 1 (d = 8 * 16 * DW)
 // NW: 16-column output tiles per wave in phase 2 (n = 8 * 16 * NW)
-template <int DW, int NW>
+template <int DW, int NW, int PH = (NW >= 16 ? (DW >= 4 ? 4 : 2) : 1)>
 __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int n = a.n, d = a.d;
@@ -101,12 +101,15 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
     f32x4_t P[DW];
 #pragma unroll
     for (int t = 0; t < DW; ++t) P[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    constexpr int UNR1 = NW >= 16 ? 1 : 2;  // two k-steps of loads in flight where registers allow
+#pragma unroll UNR1
     for (int k0 = 0; k0 < n; k0 += 32) {
       const bf16x8_t fy = lds_frag(Ybf, row, k0 + 8 * q, nrb);
 #pragma unroll
       for (int t = 0; t < DW; ++t) {
         // B side (output columns = d): lane reads D^T[dcol = dbase + 16t + row][k0 + 8q .. +7]
-        const bf16x8_t fd = *reinterpret_cast<const bf16x8_t*>(Dt + (long)(dbase + t * 16 + row) * n + k0 + 8 * q);
+        const bf16x8_t fd =
+            *reinterpret_cast<const bf16x8_t*>(Dt + ((long)((dbase >> 4) + t) * (n >> 5) + (k0 >> 5)) * 512 + lane * 8);
         P[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd, fy, P[t], 0, 0, 0);
       }
     }
@@ -126,35 +129,43 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
     }
     if (last) break;
     __syncthreads();
-    // ---- phase 2: Z[16, n_w] = Res[16, d] x D^T[d, n_w]; lane gets Z[row][ncol 4q..4q+3]
-    f32x4_t Z[NW];
-#pragma unroll
-    for (int t = 0; t < NW; ++t) Z[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < d; k0 += 32) {
-      const bf16x8_t fr = lds_frag(Rs, row, k0 + 8 * q, drb);
-#pragma unroll
-      for (int t = 0; t < NW; ++t) {
-        const bf16x8_t fd = *reinterpret_cast<const bf16x8_t*>(D + (long)(nbase + t * 16 + row) * d + k0 + 8 * q);
-        Z[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd, fr, Z[t], 0, 0, 0);
-      }
-    }
-    // ---- FISTA update (fp32): Y += eta Z; A = relu(Y - eta lambda); Y = A + mom (A - A_prev)
+    // ---- phase 2: Z[16, n_w] = Res[16, d] x D^T[d, n_w]; lane gets Z[row][ncol 4q..4q+3],
+    // in PH column passes (n_w / PH tiles each) so the accumulators of wide n fit beside the
+    // fp32 iterates
     const float mo = a.mom[it];
     const bool final_iter = it + 1 == a.T;
 #pragma unroll
-    for (int t = 0; t < NW; ++t) {
-      f32x4_t an;
+    for (int h = 0; h < PH; ++h) {
+      f32x4_t Z[NW / PH];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float y = Y[t][r] + eta * Z[t][r];
-        an[r] = fmaxf(y - thr, 0.f);
-        Y[t][r] = an[r] + (an[r] - Ap[t][r]) * mo;
+      for (int t = 0; t < NW / PH; ++t) Z[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < d; k0 += 32) {
+        const bf16x8_t fr = lds_frag(Rs, row, k0 + 8 * q, drb);
+#pragma unroll
+        for (int t = 0; t < NW / PH; ++t) {
+          const int tile = (nbase >> 4) + h * (NW / PH) + t;
+          const bf16x8_t fd =
+              *reinterpret_cast<const bf16x8_t*>(D + ((long)tile * (d >> 5) + (k0 >> 5)) * 512 + lane * 8);
+          Z[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd, fr, Z[t], 0, 0, 0);
+        }
       }
-      Ap[t] = an;
-      const int col = nbase + t * 16 + 4 * q;
-      // the next phase 1 multiplies Y -- or, after the last iteration, A
-      const f32x4_t& nxt = final_iter ? an : Y[t];
-      lds_put4(Ybf, row, col, nrb, nxt[0], nxt[1], nxt[2], nxt[3]);
+      // ---- FISTA update (fp32): Y += eta Z; A = relu(Y - eta lambda); Y = A + mom (A - A_prev)
+#pragma unroll
+      for (int t = 0; t < NW / PH; ++t) {
+        const int tt = h * (NW / PH) + t;
+        f32x4_t an;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float y = Y[tt][r] + eta * Z[t][r];
+          an[r] = fmaxf(y - thr, 0.f);
+          Y[tt][r] = an[r] + (an[r] - Ap[tt][r]) * mo;
+        }
+        Ap[tt] = an;
+        const int col = nbase + tt * 16 + 4 * q;
+        // the next phase 1 multiplies Y -- or, after the last iteration, A
+        const f32x4_t& nxt = final_iter ? an : Y[tt];
+        lds_put4(Ybf, row, col, nrb, nxt[0], nxt[1], nxt[2], nxt[3]);
+      }
     }
     __syncthreads();
   }
@@ -183,7 +194,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
 // columns, then their FISTA update) so only half the accumulators are live, and the bf16
 // copy of Y is double-buffered in LDS (read the current iterate, write the next): one
 // barrier per iteration.
-template <int NW, int RT, int HALVES>
+template <int NW, int RT, int HALVES, int PF>
 __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restrict__ C, const uint16_t* __restrict__ Gm,
                                                         const float* __restrict__ A0, const float* __restrict__ eta_,
                                                         const float* __restrict__ lam_, const float* __restrict__ mom,
@@ -216,6 +227,20 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
       lds_put4(Ybuf, u * FR + row, col, nrb, v[0], v[1], v[2], v[3]);
     }
   __syncthreads();
+  // Gm fragment stream: PF k-steps in flight per wave, one ring running continuously across
+  // the column halves and the iterations (Gm is constant), so the L2 latency is paid once per
+  // solve instead of once per k-step (the unpipelined loop waited on every load: 3.3x slower)
+  constexpr int KS = n / 32;
+  static_assert(KS % PF == 0, "k-steps per half must be a multiple of the ring depth");
+  // Gm arrives in fragment order: [col tile][k-step][lane][8] -> one contiguous 1 KB per load
+  auto gfrag = [&](int hh, int t, int k) {
+    return *reinterpret_cast<const bf16x8_t*>(Gg + ((long)((nbase >> 4) + hh * NH + t) * KS + (k >> 5)) * 512 + lane * 8);
+  };
+  bf16x8_t gq[PF][NH];
+#pragma unroll
+  for (int s = 0; s < PF; ++s)
+#pragma unroll
+    for (int t = 0; t < NH; ++t) gq[s][t] = gfrag(0, t, s * 32);
   for (int it = 0; it < T; ++it) {
     const char* Ycur = Ybuf + (it & 1) * (R * nrb);
     char* Ynxt = Ybuf + ((it + 1) & 1) * (R * nrb);
@@ -223,26 +248,37 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
     const bool final_iter = it + 1 == T;
 #pragma unroll
     for (int h = 0; h < HALVES; ++h) {
+      // C for this half's update, issued ahead of the half's GEMM
+      f32x4_t cv[RT][NH];
+#pragma unroll
+      for (int u = 0; u < RT; ++u)
+#pragma unroll
+        for (int t = 0; t < NH; ++t)
+          cv[u][t] = *reinterpret_cast<const f32x4_t*>(Cg + (long)(u * FR + row) * n + nbase + (h * NH + t) * 16 + 4 * q);
       // Z[R, this half of n_w] = Ycur[R, n] x Gm[n, half]
       f32x4_t Z[RT][NH];
 #pragma unroll
       for (int u = 0; u < RT; ++u)
 #pragma unroll
         for (int t = 0; t < NH; ++t) Z[u][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      // n is a compile-time constant here: cap the unroll, a full one hoists every Gm
-      // load (NH x n / 32 fragments) and spills; the largest state keeps one step
-      constexpr int UNR = RT * NW >= 16 ? 1 : 2;
-#pragma unroll UNR
-      for (int k0 = 0; k0 < n; k0 += 32) {
-        bf16x8_t fy[RT];
+      const int hn = (h + 1) % HALVES;
+#pragma unroll 1
+      for (int k0 = 0; k0 < n; k0 += 32 * PF) {
 #pragma unroll
-        for (int u = 0; u < RT; ++u) fy[u] = lds_frag(Ycur, u * FR + row, k0 + 8 * q, nrb);
+        for (int s = 0; s < PF; ++s) {
+          const int kk = k0 + s * 32;
+          bf16x8_t fy[RT];
 #pragma unroll
-        for (int t = 0; t < NH; ++t) {
-          const int c16 = nbase + (h * NH + t) * 16;
-          const bf16x8_t fg = *reinterpret_cast<const bf16x8_t*>(Gg + (long)(c16 + row) * n + k0 + 8 * q);
+          for (int u = 0; u < RT; ++u) fy[u] = lds_frag(Ycur, u * FR + row, kk + 8 * q, nrb);
 #pragma unroll
-          for (int u = 0; u < RT; ++u) Z[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fg, fy[u], Z[u][t], 0, 0, 0);
+          for (int t = 0; t < NH; ++t)
+#pragma unroll
+            for (int u = 0; u < RT; ++u) Z[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gq[s][t], fy[u], Z[u][t], 0, 0, 0);
+          // refill the slot with the fragment PF steps ahead (next half / next iteration past n)
+          const int kn = kk + PF * 32;
+          const bool wrap = kn >= n;
+#pragma unroll
+          for (int t = 0; t < NH; ++t) gq[s][t] = wrap ? gfrag(hn, t, kn - n) : gfrag(h, t, kn);
         }
       }
       // FISTA update of this half: Y += eta (C - Z); A = relu(Y - eta lambda); Y = A + mom (A - A_prev)
@@ -252,11 +288,10 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
         for (int t = 0; t < NH; ++t) {
           const int tt = h * NH + t;
           const int col = nbase + tt * 16 + 4 * q;
-          const f32x4_t cv = *reinterpret_cast<const f32x4_t*>(Cg + (long)(u * FR + row) * n + col);
           f32x4_t an;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float y = Y[u][tt][r] + eta * (cv[r] - Z[u][t][r]);
+            const float y = Y[u][tt][r] + eta * (cv[u][t][r] - Z[u][t][r]);
             an[r] = fmaxf(y - thr, 0.f);
             Y[u][tt][r] = an[r] + (an[r] - Ap[u][tt][r]) * mo;
           }
@@ -264,7 +299,9 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
           if (!final_iter) lds_put4(Ynxt, u * FR + row, col, nrb, Y[u][tt][0], Y[u][tt][1], Y[u][tt][2], Y[u][tt][3]);
         }
     }
-    __syncthreads();  // the next iterate is complete in Ynxt; nobody reads Ycur any more
+    // the next iterate is complete in Ynxt; nobody reads Ycur any more.  LDS-only barrier: the
+    // Gm prefetches stay in flight across it
+    lds_barrier();
   }
 #pragma unroll
   for (int u = 0; u < RT; ++u)
@@ -305,7 +342,8 @@ int sc_fista(const void* X, const void* D, const void* Dt, const float* A0, cons
   return 2;  // shape not instantiated: caller falls back to the torch path
 }
 
-// Gram-form solver: C = X D^T [G][B][n] fp32, Gm = D D^T [G][n][n] bf16.
+// Gram-form solver: C = X D^T [G][B][n] fp32, Gm = D D^T bf16 in MFMA-fragment order
+// [G][n/16][n/32][64 lanes][8] (lane = 16 q + r holds Gm[16 tile + r][32 step + 8 q .. + 7]).
 int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* eta, const float* lam,
                   const float* mom, float* A, int G, int B, int n, int T, hipStream_t stream) {
   if (B % FR || n % 128 || T < 0) return 1;
@@ -313,14 +351,15 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
   // 32-row workgroups when they still give >= 2 per CU (256 CUs); else 16 rows
   const bool two = (B % (2 * FR) == 0) && (long)G * (B / (2 * FR)) >= 512 && !getenv("SC_FISTA_RT1");
   const dim3 g2(G * (B / (2 * FR))), g1(G * (B / FR));
-  // (NW, halves): 32 rows x n fp32 iterates need the column passes split in two past n = 512
-#define SC_G(NWV, H2)                                                                                      \
+  // (NW, halves, ring depth) for 32-row, then 16-row workgroups: past n = 512 the fp32 iterates
+  // need the column passes split, and the Gm ring shrinks to stay spill-free in 256 VGPRs
+#define SC_G(NWV, H2, PF2, H1, PF1)                                                                                    \
   if (n == NWV * 128) {                                                                                    \
-    if (two) hipLaunchKernelGGL((fista_gram_kernel<NWV, 2, H2>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
-    else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, 1>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
+    if (two) hipLaunchKernelGGL((fista_gram_kernel<NWV, 2, H2, PF2>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
+    else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                        \
   }
-  SC_G(2, 1) SC_G(4, 1) SC_G(6, 2) SC_G(8, 4)
+  SC_G(2, 1, 4, 1, 4) SC_G(4, 1, 4, 1, 8) SC_G(6, 2, 2, 2, 4) SC_G(8, 4, 2, 2, 4)
 #undef SC_G
   return 2;
 }

@@ -153,11 +153,17 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
             torch.bmm(Xb.float(), Db.float().transpose(1, 2), out=C)
         Gm = torch.empty(G, n, n, device=dev, dtype=torch.bfloat16)
         gemm.matmul_nt(Db, Db, Gm)                      # Gm = D D^T (bf16 out)
+        # MFMA-fragment order (constant over the solve): [G][n/16 col tiles][n/32 k-steps][q][row][8]
+        # so every wave fragment load is 1 KB contiguous (8 full lines instead of 16 half lines)
+        Gm = Gm.view(G, n // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
         rc = _lib.lib().sc_fista_gram(_lib.ptr(C), _lib.ptr(Gm), _lib.ptr(a0), _lib.ptr(eta), _lib.ptr(lam),
                                       _lib.ptr(mom), _lib.ptr(A), G, B, n, iters, _lib.stream_handle())
     else:
-        Dtb = Db.transpose(1, 2).contiguous()
-        rc = _lib.lib().sc_fista(_lib.ptr(Xb), _lib.ptr(Db), _lib.ptr(Dtb), _lib.ptr(a0), _lib.ptr(eta),
+        # both operands in MFMA-fragment order (see the Gram form): D [G][n/16][d/32][64][8] for the
+        # (Res D^T) product, D^T [G][d/16][n/32][64][8] for the (Y D) product
+        Dtb = Db.transpose(1, 2).reshape(G, d // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
+        Dfb = Db.view(G, n // 16, 16, d // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
+        rc = _lib.lib().sc_fista(_lib.ptr(Xb), _lib.ptr(Dfb), _lib.ptr(Dtb), _lib.ptr(a0), _lib.ptr(eta),
                                  _lib.ptr(lam), _lib.ptr(mom), _lib.ptr(A), 0, G, B, n, d, iters,
                                  _lib.stream_handle())
     if rc == 2 and backend == "auto":
