@@ -125,6 +125,30 @@ def cfg_fista(a):
             "ring_gb": round(ring.capacity * d * 2 / 1e9, 1), "ring_fill_s": round(fill_s, 1)}
 
 
+def cfg_fistaloss(a):
+    """FISTA in the loss (reference autoencoders/fista.py:141-172, the fork's fista_13_10 runs):
+    8-model L1 sweep, d = n = 512 (dict_size 512), 50 unrolled iterations inside the loss."""
+    from sparse_coding__amd.engine.fista_loss import FistaLossEnsemble
+    from sparse_coding__amd.models.fista import FunctionalFista
+
+    dev = "cuda:0"
+    torch.manual_seed(0)
+    d, n, B = 512, int(512 * a.ratio), a.batch
+    models = [FunctionalFista.init(d, n, float(l1), device=dev) for l1 in np.logspace(-4, -2, a.models)]
+    eng = FistaLossEnsemble(models, lr=1e-3, batch_size=B, device=dev, num_iter=a.iters, backend="hip")
+    ring = _ring(d, dev)
+    xbuf = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
+    losses = []
+    el = _timed(lambda: losses.append(eng.step_batch(ring.sample(B, out=xbuf))), a.steps, a.warmup,
+                torch.cuda.synchronize)
+    return {"config": f"FISTA-in-loss ensemble: d={d}, n={n}, {a.models} models, {a.iters} unrolled iterations, "
+                      "HIP solver + adjoint sweep",
+            "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
+            "batch": B, "loss_first": [round(float(v), 5) for v in losses[0]],
+            "loss_last": [round(float(v), 5) for v in losses[-1]], "dtype": "bf16 GEMM operands, fp32 iterates",
+            "data": "synthetic"}
+
+
 def cfg_mlpout(a):
     """Config 3: Pythia-70m MLP-out -- the reference's ``mlpout`` hook is ``hook_mlp_out``, d_model
     = 512 wide (reference activation_dataset.py:66-67, 104-105) -- 8-model L1 sweep, ratio 4, on
@@ -278,7 +302,7 @@ def cfg_harvest(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["cpu", "topk", "fista", "mlp", "mlpout", "masked", "harvest"])
+    ap.add_argument("which", choices=["cpu", "topk", "fista", "fistaloss", "mlp", "mlpout", "masked", "harvest"])
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=2048)
@@ -288,7 +312,7 @@ def main():
     ap.add_argument("--decode", choices=["gather", "gemm"], default="gather", help="topk: decode path")
     ap.add_argument("--ring-gb", type=float, default=0.0, help="fista: ring size in GB of HBM (0: 512k rows)")
     a = ap.parse_args()
-    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "mlp": cfg_mlp, "mlpout": cfg_mlpout, "masked": cfg_masked,
+    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "fistaloss": cfg_fistaloss, "mlp": cfg_mlp, "mlpout": cfg_mlpout, "masked": cfg_masked,
            "harvest": cfg_harvest}[a.which](a)
     print(json.dumps(rec), flush=True)
 

@@ -100,18 +100,14 @@ class FunctionalFista(DictSignature):
         return l, ({"loss": l}, {"c_fista": c})
 
 
-def _unrolled_fista_residual(X, D, lam, A0, iters):
-    """Differentiable FISTA (autograd through every iteration); eta via eigvalsh as upstream."""
-    eta = 1.0 / torch.linalg.eigvalsh(D @ D.T).max().detach()
-    mom = fista_ops.momentum_schedule(iters).tolist()
-    A = A0
-    Y = A0
-    for t in range(iters):
-        A_prev = A
-        Y = Y + eta * (X - Y @ D) @ D.T
-        A = torch.clamp(Y - eta * lam, min=0.0)
-        Y = A + (A - A_prev) * mom[t]
-    return X - A @ D
+def _unrolled_fista_residual(X, D, lam, A0, iters, eta=None):
+    """Differentiable FISTA residual X - A_T D (eta via eigvalsh, detached, as upstream) through
+    ``ops.fista.unrolled_fista_residual``: an explicit adjoint sweep (HIP slabs + MFMA GEMMs on
+    the GPU, fp32 torch otherwise) instead of autograd through every iteration."""
+    if eta is None:
+        eta = 1.0 / torch.linalg.eigvalsh(D @ D.T).max().detach()
+    R = fista_ops.unrolled_fista_residual(X, D[None], lam, A0[None], iters, eta)
+    return R[0]
 
 
 class Fista(_CenteredTied):

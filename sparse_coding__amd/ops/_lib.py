@@ -66,7 +66,11 @@ def _declare(lib):
         "sc_topk_clear": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p],
         "sc_topk_scatter": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_void_p],
         "sc_fista": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                     c_void_p],
+        "sc_fista_adjoint": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_float, c_float, c_int, c_int, c_int, c_int, c_int, c_void_p],
+        "sc_fista_adjoint_init": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
         "sc_fista_gram": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_void_p],
         "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_void_p],

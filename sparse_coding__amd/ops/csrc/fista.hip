@@ -33,6 +33,10 @@ struct FistaArgs {
   float* A;            // [G][B][n] out
   float* Res;          // [G][B][d] out (may be null)
   int B, n, d, T;
+  // iterate slabs for the unrolled-FISTA adjoint (all null unless differentiating), bf16:
+  uint16_t* Ysave;     // [G][T][B][n] slot t = Y_t, the iterate phase 1 multiplies (Y_0 = A0)
+  uint16_t* Rsave;     // [G][T][B][d] slot t = Res_t = X - Y_t D
+  uint16_t* Asave;     // [G][T][B][n] slot t = A_{t+1} (its support masks the adjoint)
 };
 
 // LDS image of a [16][K] bf16 tile: 16-byte chunk index XORed with the row, so
@@ -91,6 +95,9 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
     Y[t] = v;
     Ap[t] = v;
     lds_put4(Ybf, row, col, nrb, v[0], v[1], v[2], v[3]);
+    if (a.Ysave)
+      *reinterpret_cast<ushort4*>(a.Ysave + ((long)g * a.T * a.B + r0 + row) * n + col) =
+          make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
   }
   __syncthreads();
 
@@ -125,6 +132,9 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
           *reinterpret_cast<f32x4_t*>(a.Res + ((long)g * a.B + r0 + row) * d + col) = f32x4_t{r_0, r_1, r_2, r_3};
       } else {
         lds_put4(Rs, row, col, drb, r_0, r_1, r_2, r_3);
+        if (a.Rsave)
+          *reinterpret_cast<ushort4*>(a.Rsave + (((long)g * a.T + it) * a.B + r0 + row) * d + col) =
+              make_ushort4(f2bf(r_0), f2bf(r_1), f2bf(r_2), f2bf(r_3));
       }
     }
     if (last) break;
@@ -165,6 +175,13 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
         // the next phase 1 multiplies Y -- or, after the last iteration, A
         const f32x4_t& nxt = final_iter ? an : Y[tt];
         lds_put4(Ybf, row, col, nrb, nxt[0], nxt[1], nxt[2], nxt[3]);
+        if (a.Asave) {
+          const long o = (((long)g * a.T + it) * a.B + r0 + row) * n + col;
+          *reinterpret_cast<ushort4*>(a.Asave + o) = make_ushort4(f2bf(an[0]), f2bf(an[1]), f2bf(an[2]), f2bf(an[3]));
+          if (!final_iter)  // Y_{it+1} -> slot it + 1
+            *reinterpret_cast<ushort4*>(a.Ysave + o + (long)a.B * n) =
+                make_ushort4(f2bf(Y[tt][0]), f2bf(Y[tt][1]), f2bf(Y[tt][2]), f2bf(Y[tt][3]));
+        }
       }
     }
     __syncthreads();
@@ -318,14 +335,18 @@ using namespace scamd;
 
 extern "C" {
 
+// Ysave / Rsave / Asave: the iterate slabs of FistaArgs, all three or none (then plain solve).
 int sc_fista(const void* X, const void* D, const void* Dt, const float* A0, const float* eta, const float* lam,
-             const float* mom, float* A, float* Res, int G, int B, int n, int d, int T, hipStream_t stream) {
+             const float* mom, float* A, float* Res, int G, int B, int n, int d, int T, void* Ysave, void* Rsave,
+             void* Asave, hipStream_t stream) {
   if (B % FR || n % 128 || d % 128 || T < 0) return 1;
+  if ((Ysave != nullptr) != (Asave != nullptr) || (Ysave != nullptr) != (Rsave != nullptr)) return 1;
   const int DW = d / 128, NW = n / 128;
   const size_t lds = (size_t)FR * (2 * n + 4 * d);
   if (lds > 160 * 1024) return 1;
   FistaArgs a{reinterpret_cast<const uint16_t*>(X), reinterpret_cast<const uint16_t*>(D),
-              reinterpret_cast<const uint16_t*>(Dt), A0, eta, lam, mom, A, Res, B, n, d, T};
+              reinterpret_cast<const uint16_t*>(Dt), A0, eta, lam, mom, A, Res, B, n, d, T,
+              reinterpret_cast<uint16_t*>(Ysave), reinterpret_cast<uint16_t*>(Rsave), reinterpret_cast<uint16_t*>(Asave)};
   dim3 grid(G * (B / FR));
 #define SC_F(DWV, NWV)                                                                                    \
   if (DW == DWV && NW == NWV) {                                                                           \

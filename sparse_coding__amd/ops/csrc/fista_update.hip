@@ -90,6 +90,56 @@ __global__ __launch_bounds__(256) void basis_apply_cols_kernel(float* __restrict
   }
 }
 
+// Adjoint of the unrolled FISTA loop (the "FISTA in the loss" objective, reference
+// autoencoders/fista.py:141-172), one elementwise pass per iteration t = T-1 .. 0 over
+// [G][B][n].  Forward: V_t = Y_t + eta (X - Y_t D) D^T, A_{t+1} = relu(V_t - eta lam),
+// Y_{t+1} = A_{t+1} + m_t (A_{t+1} - A_t), Y_0 = A_0 = c.  With nS = -(Vbar_t D) (GEMM) and
+// T2 = nS D^T (GEMM):
+//   Ybar_t = Vbar_t + eta T2
+//   t >= 1: Abar_t = (1 + m_{t-1}) Ybar_t - m_t Ybar_{t+1};  Vbar_{t-1} = Abar_t 1[A_t > 0]
+//   t == 0: cbar = Ybar_0 - m_0 Ybar_1
+// Slab slot s of Asave holds A_{s+1}; Vbar_{t-1} also goes to slab slot t-1 (bf16) for the
+// dictionary-gradient GEMM.
+__global__ __launch_bounds__(256) void fista_adjoint_kernel(const float* __restrict__ T2, float* __restrict__ Vbar,
+                                                            const float* __restrict__ Ynext, float* __restrict__ Ycur,
+                                                            const uint16_t* __restrict__ Aslab,
+                                                            uint16_t* __restrict__ Vslab, float* __restrict__ cbar,
+                                                            const float* __restrict__ eta, float m_prev, float m_t,
+                                                            int B, int n, int T, int t, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const long per = (long)B * n;
+  const int g = (int)(i / per);
+  const long e = i - (long)g * per;
+  const float yb = Vbar[i] + eta[g] * T2[i];
+  const float yn = Ynext[i];
+  Ycur[i] = yb;
+  if (t == 0) {
+    cbar[i] = yb - m_t * yn;
+    return;
+  }
+  const long slot = ((long)g * T + (t - 1)) * per + e;  // A_t lives in slot t - 1
+  const float ab = (1.f + m_prev) * yb - m_t * yn;
+  const float v = bf2f(Aslab[slot]) > 0.f ? ab : 0.f;
+  Vbar[i] = v;
+  Vslab[slot] = f2bf(v);
+}
+
+// Start of the sweep: Vbar_{T-1} = -(Rbar D^T) 1[A_T > 0] (T2 = Rbar D^T from the GEMM).
+__global__ __launch_bounds__(256) void fista_adjoint_init_kernel(const float* __restrict__ T2, float* __restrict__ Vbar,
+                                                                 const uint16_t* __restrict__ Aslab,
+                                                                 uint16_t* __restrict__ Vslab, int B, int n, int T,
+                                                                 long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const long per = (long)B * n;
+  const int g = (int)(i / per);
+  const long slot = ((long)g * T + (T - 1)) * per + (i - (long)g * per);
+  const float v = bf2f(Aslab[slot]) > 0.f ? -T2[i] : 0.f;
+  Vbar[i] = v;
+  Vslab[slot] = f2bf(v);
+}
+
 }  // namespace scamd
 
 using namespace scamd;
@@ -119,6 +169,27 @@ int sc_basis_apply(float* D, const float* dBt, const float* H, void* Db, int G, 
     hipLaunchKernelGGL(basis_apply_cols_kernel, dim3(d / 64, G), dim3(256), 0, stream, D, dBt, H, db, n, d, lowest,
                        nonneg);
   }
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_fista_adjoint(const float* T2, float* Vbar, const float* Ynext, float* Ycur, const void* Aslab, void* Vslab,
+                     float* cbar, const float* eta, float m_prev, float m_t, int G, int B, int n, int T, int t,
+                     hipStream_t stream) {
+  if (t < 0 || t >= T || (t == 0 && !cbar)) return 1;
+  const long total = (long)G * B * n;
+  hipLaunchKernelGGL(fista_adjoint_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, T2, Vbar,
+                     Ynext, Ycur, reinterpret_cast<const uint16_t*>(Aslab), reinterpret_cast<uint16_t*>(Vslab), cbar,
+                     eta, m_prev, m_t, B, n, T, t, total);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_fista_adjoint_init(const float* T2, float* Vbar, const void* Aslab, void* Vslab, int G, int B, int n, int T,
+                          hipStream_t stream) {
+  if (T < 1) return 1;
+  const long total = (long)G * B * n;
+  hipLaunchKernelGGL(fista_adjoint_init_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, T2,
+                     Vbar, reinterpret_cast<const uint16_t*>(Aslab), reinterpret_cast<uint16_t*>(Vslab), B, n, T,
+                     total);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

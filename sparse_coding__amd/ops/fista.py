@@ -110,6 +110,8 @@ def fista_torch(X, D, lam, A0=None, iters=500, eta=None) -> Tuple[torch.Tensor, 
 
 
 GRAM_N = (256, 512, 768, 1024)
+# (d / 128, n / 128) instantiated for the direct-form solver (csrc/fista.hip sc_fista)
+DIRECT_TILES = {(2, 2), (2, 4), (2, 8), (2, 16), (4, 4), (4, 8), (4, 16), (6, 6), (6, 12), (8, 4), (8, 8), (8, 16)}
 
 
 def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_res: bool = True,
@@ -164,7 +166,7 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
         Dtb = Db.transpose(1, 2).reshape(G, d // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
         Dfb = Db.view(G, n // 16, 16, d // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
         rc = _lib.lib().sc_fista(_lib.ptr(Xb), _lib.ptr(Dfb), _lib.ptr(Dtb), _lib.ptr(a0), _lib.ptr(eta),
-                                 _lib.ptr(lam), _lib.ptr(mom), _lib.ptr(A), 0, G, B, n, d, iters,
+                                 _lib.ptr(lam), _lib.ptr(mom), _lib.ptr(A), 0, G, B, n, d, iters, None, None, None,
                                  _lib.stream_handle())
     if rc == 2 and backend == "auto":
         return fista_torch(X, D, lam, A0, iters, eta)
@@ -231,3 +233,190 @@ def quadratic_basis_update(D, Res, A, H, lowest_activation=0.001, step=0.001, no
                                    1 if normalize == "row" else 0, _lib.stream_handle())
     _lib.check(rc, "sc_basis_apply")
     return out
+
+
+# --------------------------------------------------------------------- FISTA in the loss
+def unrolled_fista_residual(X, D, lam, A0, iters: int = 50, eta=None, backend: str = "auto"):
+    """R = X - A_T D after ``iters`` unrolled FISTA iterations warm-started at A0, differentiable
+    in D and A0 -- the "FISTA in the loss" term of reference autoencoders/fista.py:141-172 for
+    every model at once (D [G, n, d], X [B, d] or [G, B, d], A0 [G, B, n], lam / eta [G]; eta is
+    a constant, as the reference's detached eigvalsh).
+
+    Forward: the direct-form HIP solver saving the bf16 iterate slabs Y_t, Res_t, A_{t+1}
+    ([G][T][B][*], 288 GB of HBM makes storing every iterate the cheap option).  Backward: the
+    adjoint sweep t = T-1 .. 0, per iteration two grouped MFMA GEMMs (nS = -(Vbar D),
+    nS D^T) and one elementwise kernel; the dictionary gradient of all T iterations is ONE
+    K-concatenated GEMM over the slabs:  Dbar = eta sum_t (Vbar_t^T Res_t - Y_t^T S_t)
+    - A_T^T Rbar.  ``backend="torch"`` runs the same adjoint in fp32 torch (the CPU path)."""
+    D = D if D.dim() == 3 else D[None]
+    G = D.shape[0]
+    lam = torch.as_tensor(lam, dtype=torch.float32, device=D.device).reshape(-1).expand(G).contiguous()
+    if eta is None:
+        eta = step_size(D.detach())
+    eta = torch.as_tensor(eta, dtype=torch.float32, device=D.device).reshape(-1).expand(G).contiguous()
+    return _UnrolledFista.apply(X, D, A0, lam, eta, int(iters), backend)
+
+
+def _unrolled_hip_ok(X, D, A0, backend):
+    if backend == "torch":
+        return False
+    G, n, d = D.shape
+    B = A0.shape[-2]
+    ok = (_hip_ok(D) and B % 128 == 0 and n % 128 == 0 and d % 128 == 0
+          and (d // 128, n // 128) in DIRECT_TILES)
+    if backend == "hip" and not ok:
+        raise ValueError(f"unrolled FISTA HIP path needs B % 128 == 0 and (d/128, n/128) in {sorted(DIRECT_TILES)} "
+                         f"(B={B}, n={n}, d={d})")
+    return ok
+
+
+class _UnrolledFista(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, D, A0, lam, eta, iters, backend):
+        G, n, d = D.shape
+        B = A0.shape[-2]
+        mom = momentum_schedule(max(iters, 1))
+        ctx.iters, ctx.mom = iters, mom.tolist()
+        ctx.x_shape = X.shape
+        if _unrolled_hip_ok(X, D, A0, backend):
+            R, Db, Ys, Rs, As = unrolled_forward_hip(X, D.detach(), A0.detach(), lam, eta, iters, mom)
+            ctx.hip = True
+            ctx.save_for_backward(Db, Ys, Rs, As, eta)
+            return R
+        ctx.hip = False
+        Df = D.detach().float()
+        Xf = X.detach().float()
+        e = eta[:, None, None]
+        thr = (eta * lam)[:, None, None]
+        A = A0.detach().float()
+        Y = A
+        Ys, Rs, As = [], [], []
+        for t in range(iters):
+            Res = Xf - Y @ Df
+            Ys.append(Y)
+            Rs.append(Res)
+            A_prev = A
+            A = torch.clamp(Y + e * (Res @ Df.transpose(1, 2)) - thr, min=0.0)
+            As.append(A)
+            Y = A + (A - A_prev) * ctx.mom[t]
+        R = Xf - A @ Df
+        ctx.save_for_backward(Df, torch.stack(Ys, 1) if Ys else None, torch.stack(Rs, 1) if Rs else None,
+                              torch.stack(As, 1) if As else None, eta, A)
+        return R
+
+    @staticmethod
+    def backward(ctx, Rbar):
+        if ctx.hip:
+            Db, Ys, Rs, As, eta = ctx.saved_tensors
+            Dbar, cbar = unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, ctx.mom, ctx.iters)
+            return None, Dbar, cbar, None, None, None, None
+        Df, Ys, Rs, As, eta, A_T = ctx.saved_tensors
+        Dbar, cbar = unrolled_backward_torch(Rbar, Df, Ys, Rs, As, eta, ctx.mom, ctx.iters, A_T)
+        return None, Dbar, cbar, None, None, None, None
+
+
+def unrolled_backward_torch(Rbar, Df, Ys, Rs, As, eta, mom, T, A_T=None):
+    """fp32 adjoint sweep over saved iterate slabs ([G][T][B][*], any float dtype): the
+    reference arithmetic for ``_unrolled_backward_hip`` (given the same slabs, the two differ
+    only by the bf16 rounding of Vbar / S and of the GEMM operands)."""
+    Df = Df.float()
+    e = eta[:, None, None]
+    Rbar = Rbar.float()
+    Dt = Df.transpose(1, 2)
+    if A_T is None:
+        A_T = As[:, T - 1]
+    Dbar = -A_T.float().transpose(1, 2) @ Rbar
+    if T == 0:
+        return Dbar, -Rbar @ Dt
+    Vbar = -(Rbar @ Dt) * (As[:, T - 1] > 0)
+    Ynext = torch.zeros_like(Vbar)
+    cbar = None
+    for t in range(T - 1, -1, -1):
+        S = Vbar @ Df
+        Dbar = Dbar + e * (Vbar.transpose(1, 2) @ Rs[:, t].float() - Ys[:, t].float().transpose(1, 2) @ S)
+        Yb = Vbar - e * (S @ Dt)
+        if t >= 1:
+            Vbar = ((1 + mom[t - 1]) * Yb - mom[t] * Ynext) * (As[:, t - 1] > 0)
+        else:
+            cbar = Yb - mom[0] * Ynext
+        Ynext = Yb
+    return Dbar, cbar
+
+
+def unrolled_forward_hip(X, D, A0, lam, eta, iters, mom=None):
+    """Direct-form HIP solve of ``iters`` iterations saving the bf16 slabs; returns
+    (R fp32 [G, B, d], D bf16, Y slab, Res slab, A slab)."""
+    G, n, d = D.shape
+    B = A0.shape[-2]
+    dev = D.device
+    mom = momentum_schedule(max(iters, 1)) if mom is None else mom
+    # the solver reads X per model ([G][B][d])
+    Xb = (X if X.dim() == 3 else X.expand(G, B, X.shape[-1])).to(torch.bfloat16).contiguous()
+    if tuple(Xb.shape) != (G, B, d):
+        raise ValueError(f"X shape {tuple(X.shape)} does not match {(B, d)} or {(G, B, d)}")
+    Db = D.to(torch.bfloat16).contiguous()
+    Dtb = Db.transpose(1, 2).reshape(G, d // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
+    Dfb = Db.view(G, n // 16, 16, d // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
+    T = max(iters, 1)
+    Ys = torch.empty(G, T, B, n, device=dev, dtype=torch.bfloat16)
+    Rs = torch.empty(G, T, B, d, device=dev, dtype=torch.bfloat16)
+    As = torch.empty(G, T, B, n, device=dev, dtype=torch.bfloat16)
+    A = torch.empty(G, B, n, device=dev)
+    R = torch.empty(G, B, d, device=dev)
+    a0 = A0.float().contiguous()
+    if tuple(a0.shape) != (G, B, n):
+        raise ValueError(f"A0 shape {tuple(A0.shape)} != {(G, B, n)}")
+    mom_d = mom.to(dev)
+    rc = _lib.lib().sc_fista(_lib.ptr(Xb), _lib.ptr(Dfb), _lib.ptr(Dtb), _lib.ptr(a0), _lib.ptr(eta),
+                             _lib.ptr(lam), _lib.ptr(mom_d), _lib.ptr(A), _lib.ptr(R), G, B, n, d, iters,
+                             _lib.ptr(Ys), _lib.ptr(Rs), _lib.ptr(As), _lib.stream_handle())
+    _lib.check(rc, "sc_fista (saving iterates)")
+    return R, Db, Ys, Rs, As
+
+
+def _strided_mm(epi, layout, M, N, K, a, lda, sa, b, ldb, sb, out, ldc, sc, alpha):
+    from . import gemm
+
+    G = b.shape[0]
+    gemm._launch(epi, layout, M, N, K, 0, G, [gemm._op(a, lda, sa)] * 2, [gemm._op(b, ldb, sb)] * 2, [out],
+                 [alpha], ldc, sc)
+
+
+def unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, mom, T):
+    from . import gemm
+
+    G, n, d = Db.shape
+    B = Ys.shape[2]
+    dev = Db.device
+    Rb = Rbar.to(torch.bfloat16)
+    Rb = (Rb if Rb.dim() == 3 else Rb.expand(G, B, d)).contiguous()
+    if tuple(Rb.shape) != (G, B, d) or tuple(Ys.shape) != (G, T, B, n) or tuple(Rs.shape) != (G, T, B, d):
+        raise ValueError("unrolled FISTA backward: slab / gradient shapes disagree")
+    T2 = torch.empty(G, B, n, device=dev)
+    gemm.matmul_nt(Rb, Db, T2)                                   # Rbar D^T
+    Vs = torch.empty(G, T, B, n, device=dev, dtype=torch.bfloat16)
+    Ss = torch.empty(G, T, B, d, device=dev, dtype=torch.bfloat16)
+    Vbar = torch.empty(G, B, n, device=dev)
+    Ya, Yb_ = torch.zeros(G, B, n, device=dev), torch.empty(G, B, n, device=dev)
+    cbar = torch.empty(G, B, n, device=dev)
+    stream = _lib.stream_handle()
+    _lib.check(_lib.lib().sc_fista_adjoint_init(_lib.ptr(T2), _lib.ptr(Vbar), _lib.ptr(As), _lib.ptr(Vs), G, B, n,
+                                                T, stream), "sc_fista_adjoint_init")
+    EPI_F32, EPI_BF16 = gemm.EPI_F32, gemm.EPI_BF16
+    for t in range(T - 1, -1, -1):
+        # nS_t = -(Vbar_t D) into slab slot t, then T2 = nS_t D^T
+        _strided_mm(EPI_BF16, 1, B, d, n, Vs[:, t], n, T * B * n, Db, d, n * d, Ss[:, t], d, T * B * d, -1.0)
+        _strided_mm(EPI_F32, 3, B, n, d, Ss[:, t], d, T * B * d, Db, d, n * d, T2, n, B * n, 1.0)
+        _lib.check(_lib.lib().sc_fista_adjoint(_lib.ptr(T2), _lib.ptr(Vbar), _lib.ptr(Ya), _lib.ptr(Yb_),
+                                               _lib.ptr(As), _lib.ptr(Vs), _lib.ptr(cbar), _lib.ptr(eta),
+                                               float(mom[t - 1]) if t >= 1 else 0.0, float(mom[t]), G, B, n, T,
+                                               t, stream), "sc_fista_adjoint")
+        Ya, Yb_ = Yb_, Ya
+    # Dbar = eta sum_t (Vbar_t^T Res_t + Y_t^T nS_t) - A_T^T Rbar: one K = T B GEMM + one K = B GEMM
+    Dbar = torch.empty(G, n, d, device=dev)
+    gemm.weight_grads([[(Vs.view(G, T * B, n), Rs.view(G, T * B, d)), (Ys.view(G, T * B, n), Ss.view(G, T * B, d))]],
+                      [Dbar], 1.0)
+    Dfin = torch.empty(G, n, d, device=dev)
+    gemm.weight_grads([[(As[:, T - 1].contiguous(), Rb)]], [Dfin], -1.0)
+    Dbar.mul_(eta[:, None, None]).add_(Dfin)
+    return Dbar, cbar
