@@ -68,3 +68,21 @@ class FistaLossEnsemble:
         return [({k: v[i].detach().to(device).clone() for k, v in self.params.items()},
                  {k: (v.detach().to(device).clone() if torch.is_tensor(v) else v) for k, v in self.meta[i].items()})
                 for i in range(self.n_models)]
+
+    def to_learned_dicts(self, device="cpu"):
+        """The trained objective is a tied SAE with row-normalised dictionary (reference
+        FunctionalFista.loss2 normalises the encoder rows)."""
+        from ..models.learned_dict import TiedSAE
+
+        return [TiedSAE(p["encoder"], p["encoder_bias"], norm_encoder=True) for p, _ in self.unstack(device)]
+
+    def state_dict(self):
+        return {"params": {k: v.detach().clone() for k, v in self.params.items()}, "optim": self.opt.state_dict(),
+                "step": self.step_count}
+
+    def load_state_dict(self, st):
+        with torch.no_grad():
+            for k, v in st["params"].items():
+                self.params[k].copy_(v)
+        self.opt.load_state_dict(st["optim"])
+        self.step_count = int(st["step"])

@@ -52,7 +52,10 @@ class EnsembleTrainer:
                  device="cuda", engine: str = "auto", name: str = "ensemble", args: Optional[dict] = None,
                  fista_iters: int = 500, fista_backend: str = "auto", persist_hessian: bool = False,
                  basis_normalize: str = "column", use_graph: bool = False, fista_eta: str = "tracked",
-                 dist=None, parallel: str = "none"):
+                 dist=None, parallel: str = "none", objective: str = "loss", fista_loss_iters: int = 50):
+        """``objective="fista_loss"`` (FunctionalFista only): the "FISTA in the loss" variant
+        (reference autoencoders/fista.py:141-172) on ``FistaLossEnsemble`` -- tied normalised
+        SAE loss plus the residual of ``fista_loss_iters`` unrolled FISTA iterations."""
         self.sig = sig
         self.name = name
         self.args = dict(args or {})
@@ -69,7 +72,13 @@ class EnsembleTrainer:
             models = list(models[self.local])
         elif parallel != "none":
             raise ValueError(f"parallel must be 'none' or 'es', got {parallel!r}")
+        if objective not in ("loss", "fista_loss"):
+            raise ValueError(f"objective must be 'loss' or 'fista_loss', got {objective!r}")
+        if objective == "fista_loss" and (sig is not FunctionalFista or parallel != "none"):
+            raise ValueError("objective='fista_loss' needs the FunctionalFista signature and parallel='none'")
         ok, why = _fused_ok(models, sig, batch_size, device) if engine in ("auto", "fused") else (False, "eager")
+        if objective == "fista_loss":
+            ok, why = False, "fista-in-loss engine"
         if engine == "fused" and not ok:
             raise ValueError(f"fused engine requested but unavailable: {why}")
         self.engine_reason = why
@@ -77,6 +86,12 @@ class EnsembleTrainer:
         if self.es is not None:
             self.impl = self.es.engine
             self.kind = self._es_kind
+        elif objective == "fista_loss":
+            from .fista_loss import FistaLossEnsemble
+
+            self.impl = FistaLossEnsemble(models, lr=lr, batch_size=batch_size, device=device,
+                                          num_iter=fista_loss_iters, backend=fista_backend)
+            self.kind = "fista-loss"
         elif ok and sig is TopKEncoder:
             from .topk import FusedTopKEnsemble
 
@@ -97,7 +112,7 @@ class EnsembleTrainer:
             self.impl = FunctionalEnsemble(models, sig, adam, {"lr": lr}, device=device,
                                            no_stacking=sig is TopKEncoder)
         self.fista = None
-        if sig is FunctionalFista:
+        if sig is FunctionalFista and objective == "loss":
             self.fista = FistaDictUpdater(num_iter=fista_iters, persist_hessian=persist_hessian,
                                           normalize=basis_normalize, backend=fista_backend, eta_method=fista_eta)
         self.last_loss = None
@@ -160,6 +175,10 @@ class EnsembleTrainer:
         elif self.kind == "fused-topk":
             mse = self.impl.step_batch(batch)
             self.last_losses = {"loss": mse}
+            codes = None
+        elif self.kind == "fista-loss":
+            total = self.impl.step_batch(batch)
+            self.last_losses = {"loss": total, **self.impl.last}
             codes = None
         else:
             loss, aux = self.impl.step_batch(batch.to(self.device, torch.float32))
@@ -225,7 +244,7 @@ class EnsembleTrainer:
         elif self.kind == "fused-topk":
             st["impl"] = {"params": self.impl.params, "m": self.impl.m, "v": self.impl.v,
                           "step": self.impl.step_count}
-        elif self.kind == "analytic":
+        elif self.kind in ("analytic", "fista-loss"):
             st["impl"] = self.impl.state_dict()
         else:
             st["impl"] = {"params": self.impl.params, "optim": self.impl.optim_states}
@@ -238,7 +257,7 @@ class EnsembleTrainer:
             raise ValueError(f"checkpoint engine {st['kind']} != {self.kind}")
         self.steps = int(st["steps"])
         imp = st["impl"]
-        if self.kind in ("fused-sae", "analytic"):
+        if self.kind in ("fused-sae", "analytic", "fista-loss"):
             self.impl.load_state_dict(imp)
         elif self.kind == "fused-topk":
             for d_ in ("params", "m", "v"):

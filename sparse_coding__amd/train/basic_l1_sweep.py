@@ -33,7 +33,7 @@ from ..utils import checkpoint as ckpt
 from ..utils.config import SweepArgs
 from .sweep import ensemble_train_loop
 
-_SIGS = {"fista": FunctionalFista, "sae": FunctionalSAE, "tied": FunctionalTiedSAE}
+_SIGS = {"fista": FunctionalFista, "fista_loss": FunctionalFista, "sae": FunctionalSAE, "tied": FunctionalTiedSAE}
 
 
 class ProgressBar:
@@ -103,7 +103,8 @@ def basic_l1_sweep(dataset_dir: str, output_dir: str, ratio: float, l1_values=np
                                                      "dict_size": latent},
                               fista_iters=fista_iters, fista_backend=fista_backend,
                               persist_hessian=persist_hessian, basis_normalize=basis_normalize, fista_eta=fista_eta,
-                              dist=info, parallel=parallel)
+                              dist=info, parallel=parallel,
+                              objective="fista_loss" if signature == "fista_loss" else "loss")
     rows_max = max(folder.meta(i)[0][0] for i in folder.indices)
     fused = trainer.kind.startswith("fused")
     ring = DeviceRing(rows_max, d, device=device, dtype=torch.bfloat16 if fused else torch.float32, seed=seed)

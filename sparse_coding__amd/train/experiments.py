@@ -186,8 +186,21 @@ def fista_sweep(cfg):
         {"dict_size": [n], "l1_alpha": l1_values}
 
 
+def fista_in_loss_sweep(cfg):
+    """The fork's "FISTA in the loss" runs (fista_13_10, output_basic_test/filename_explanations.txt:7-8;
+    reference autoencoders/fista.py:141-172): tied normalised SAE + the residual of 50 unrolled
+    FISTA iterations warm-started from the codes, over an L1 sweep."""
+    l1_values = np.logspace(getattr(cfg, "l1_value_min", -4), getattr(cfg, "l1_value_max", -2),
+                            getattr(cfg, "l1_value_n", 4))
+    n = int(cfg.activation_width * getattr(cfg, "ratio", cfg.learned_dict_ratio))
+    models = [FunctionalFista.init(cfg.activation_width, n, float(l1)) for l1 in l1_values]
+    args = dict(_args(cfg, n), objective="fista_loss", fista_loss_iters=int(getattr(cfg, "fista_loss_iters", 50)))
+    return [(models, FunctionalFista, args, "fista_loss")], ["dict_size"], ["l1_alpha"], \
+        {"dict_size": [n], "l1_alpha": l1_values}
+
+
 INIT_FUNCS: Dict[str, Callable] = {f.__name__: f for f in [
-    tied_vs_not_experiment, topk_experiment, synthetic_linear_range, dense_l1_range_experiment,
+    fista_in_loss_sweep, tied_vs_not_experiment, topk_experiment, synthetic_linear_range, dense_l1_range_experiment,
     residual_denoising_experiment, residual_denoising_comparison, thresholding_experiment, zero_l1_baseline,
     dict_ratio_experiment, pythia_1_4_b_dict, run_zeros_only_init, long_mlp_sweep, run_positive_init,
     simple_setoff, fista_sweep]}
@@ -360,6 +373,16 @@ def run_topk(argv=None):
     sweep(topk_experiment, cfg)
 
 
+def run_fista_in_loss(argv=None):
+    """FISTA-in-the-loss L1 sweep, dict_size = d (the fork's fista_13_10 runs; d = 512 on Pythia-70m)."""
+    from .sweep import sweep
+
+    cfg = _cfg(argv, model_name="pythia-70m-deduped", batch_size=1024, output_folder="output_fista_loss",
+               dataset_folder="activation_data", use_synthetic_dataset=False, lr=1e-3, n_chunks=10,
+               learned_dict_ratio=1.0)
+    sweep(fista_in_loss_sweep, cfg)
+
+
 def run_synthetic_test(argv=None):
     """Synthetic ground-truth grid: n_ground_truth in {1024, 2048} x nonzero in {10, 50, 100},
     noise 0.1 (reference ``synthetic_test`` :817-851)."""
@@ -428,7 +451,7 @@ RUNS = {f.__name__: f for f in [run_single_layer, run_single_layer_gpt2, run_acr
                                 run_pythia_1_4_b_sweep, run_synthetic, run_thresholding, run_resid_denoise,
                                 run_dict_ratio, run_dense_l1_range, run_across_layers, run_across_layers_attn,
                                 run_across_layers_mlp_out, run_across_layers_mlp_untied, run_zero_l1_baseline,
-                                run_topk, run_synthetic_test, run_setup_positives, run_all_zeros, run_simple]}
+                                run_topk, run_fista_in_loss, run_synthetic_test, run_setup_positives, run_all_zeros, run_simple]}
 
 
 def main(argv=None):

@@ -176,7 +176,9 @@ def sweep(ensemble_init_func, cfg, info: Optional[DistInfo] = None) -> List[Tupl
                                         persist_hessian=getattr(cfg, "persist_hessian", False),
                                         basis_normalize=getattr(cfg, "basis_normalize", "column"),
                                         fista_eta=getattr(cfg, "fista_eta", "tracked"),
-                                        use_graph=cfg.use_graph))
+                                        use_graph=cfg.use_graph,
+                                        objective=args.get("objective", "loss"),
+                                        fista_loss_iters=int(args.get("fista_loss_iters", 50))))
 
     n_chunks = len(folder)
     chunk_order = np.random.permutation(folder.indices)

@@ -284,7 +284,7 @@ class SweepArgs(EnsembleArgs):
     fista_eta: str = "tracked"        # "eigh" reproduces the reference's exact eigvalsh per call
     persist_hessian: bool = False     # reference quirk B#3 (throwaway EMA) by default
     basis_normalize: str = "column"   # reference quirk B#4 by default
-    signature: str = "fista"          # fista | sae | tied
+    signature: str = "fista"          # fista | fista_loss | sae | tied
     parallel: str = "none"            # "es": ensemble-axis sharding over torchrun ranks
 
 

@@ -87,3 +87,29 @@ def test_fista_loss_ensemble_gradients_cpu():
     before = eng.params["encoder"].detach().clone()
     eng.opt.step()
     assert not torch.equal(before, eng.params["encoder"].detach())
+
+
+def test_trainer_fista_loss_objective_cpu(tmp_path):
+    from sparse_coding__amd.engine.trainer import EnsembleTrainer
+    from sparse_coding__amd.models.fista import FunctionalFista
+
+    torch.manual_seed(3)
+    d, n, B = 16, 32, 24
+    models = [FunctionalFista.init(d, n, l1) for l1 in (1e-4, 1e-2)]
+    tr = EnsembleTrainer(models, FunctionalFista, lr=1e-2, batch_size=B, device="cpu", objective="fista_loss",
+                         fista_loss_iters=5)
+    assert tr.kind == "fista-loss" and tr.fista is None
+    x = torch.randn(B, d)
+    first = tr.step(x).clone()
+    for _ in range(30):
+        last = tr.step(x)
+    assert (last < first).all()
+    hosts = tr.losses_host()
+    assert set(hosts[0]) >= {"loss", "l_reconstruction", "l_fista", "l_l1"}
+    lds = tr.to_learned_dicts(ensemble_hyperparams=())
+    assert len(lds) == 2 and lds[0][0].get_learned_dict().shape == (n, d)
+    st = tr.state_dict()
+    tr2 = EnsembleTrainer(models, FunctionalFista, lr=1e-2, batch_size=B, device="cpu", objective="fista_loss",
+                          fista_loss_iters=5)
+    tr2.load_state_dict(st)
+    torch.testing.assert_close(tr2.impl.params["encoder"], tr.impl.params["encoder"])
