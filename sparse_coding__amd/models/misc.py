@@ -205,9 +205,20 @@ class DirectCoefOptimizer(DictSignature):
 
     @staticmethod
     def basis_pursuit(params, buffers, batch, normed_dict=None, n_iters=N_ITERS_OPT, momentum=0.9):
-        """Projected SGD with momentum on the codes (closed-form gradient of the objective)."""
+        """Projected SGD with momentum on the codes (closed-form gradient of the objective).
+        On the GPU (outside autograd / vmap, supported shapes) this is the persistent HIP
+        solver's coefficient-search mode (``ops.fista.coef_search``)."""
         D = unit_rows(params["decoder"]) if normed_dict is None else normed_dict
         B, d = batch.shape
+        if batch.is_cuda and not torch._C._functorch.is_functorch_wrapped_tensor(batch) \
+                and not torch.is_grad_enabled():
+            from ..ops import fista as fista_ops
+
+            try:
+                return fista_ops.coef_search(batch, D.detach()[None], buffers["l1_alpha"], buffers["lr"], n_iters,
+                                             momentum, backend="auto")[0].to(batch.dtype)
+            except ValueError:
+                pass
         c = torch.zeros(B, D.shape[0], device=batch.device, dtype=batch.dtype)
         buf = torch.zeros_like(c)
         lr, lam = buffers["lr"], buffers["l1_alpha"]

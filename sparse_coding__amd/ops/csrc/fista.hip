@@ -37,6 +37,12 @@ struct FistaArgs {
   uint16_t* Ysave;     // [G][T][B][n] slot t = Y_t, the iterate phase 1 multiplies (Y_0 = A0)
   uint16_t* Rsave;     // [G][T][B][d] slot t = Res_t = X - Y_t D
   uint16_t* Asave;     // [G][T][B][n] slot t = A_{t+1} (its support masks the adjoint)
+  // mode 1: projected gradient descent with momentum on the codes instead of FISTA (the
+  // direct coefficient search, reference autoencoders/direct_coef_search.py:52-56):
+  //   g = lam lscale sign(c) - gscale (X - c D) D^T;  buf = mom buf + g;  c = relu(c - eta buf)
+  // (eta = the learning rate; Y holds c, Ap the momentum buffer)
+  int mode;
+  float gscale, lscale;
 };
 
 // LDS image of a [16][K] bf16 tile: 16-byte chunk index XORed with the row, so
@@ -76,7 +82,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
   const uint16_t* X = a.X + ((long)g * a.B + r0) * d;
   const uint16_t* D = a.D + (long)g * n * d;
   const uint16_t* Dt = a.Dt + (long)g * d * n;
-  const float eta = a.eta[g], thr = a.eta[g] * a.lam[g];
+  const float eta = a.eta[g], thr = a.eta[g] * a.lam[g], lsc = a.lam[g] * a.lscale;
   const int row = lane & 15, q = lane >> 4;
 
   // stage X rows into LDS
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
     f32x4_t v = f32x4_t{0.f, 0.f, 0.f, 0.f};
     if (a.A0) v = *reinterpret_cast<const f32x4_t*>(a.A0 + ((long)g * a.B + r0 + row) * n + col);
     Y[t] = v;
-    Ap[t] = v;
+    Ap[t] = a.mode ? f32x4_t{0.f, 0.f, 0.f, 0.f} : v;  // mode 1: zero momentum buffer
     lds_put4(Ybf, row, col, nrb, v[0], v[1], v[2], v[3]);
     if (a.Ysave)
       *reinterpret_cast<ushort4*>(a.Ysave + ((long)g * a.T * a.B + r0 + row) * n + col) =
@@ -164,13 +170,25 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
       for (int t = 0; t < NW / PH; ++t) {
         const int tt = h * (NW / PH) + t;
         f32x4_t an;
+        if (a.mode == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float y = Y[tt][r] + eta * Z[t][r];
-          an[r] = fmaxf(y - thr, 0.f);
-          Y[tt][r] = an[r] + (an[r] - Ap[tt][r]) * mo;
+          for (int r = 0; r < 4; ++r) {
+            const float y = Y[tt][r] + eta * Z[t][r];
+            an[r] = fmaxf(y - thr, 0.f);
+            Y[tt][r] = an[r] + (an[r] - Ap[tt][r]) * mo;
+          }
+          Ap[tt] = an;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float c = Y[tt][r];
+            const float gr = (c > 0.f ? lsc : 0.f) - a.gscale * Z[t][r];
+            const float bu = mo * Ap[tt][r] + gr;
+            Ap[tt][r] = bu;
+            an[r] = fmaxf(c - eta * bu, 0.f);
+            Y[tt][r] = an[r];
+          }
         }
-        Ap[tt] = an;
         const int col = nbase + tt * 16 + 4 * q;
         // the next phase 1 multiplies Y -- or, after the last iteration, A
         const f32x4_t& nxt = final_iter ? an : Y[tt];
@@ -190,7 +208,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
 #pragma unroll
   for (int t = 0; t < NW; ++t) {
     const int col = nbase + t * 16 + 4 * q;
-    *reinterpret_cast<f32x4_t*>(a.A + ((long)g * a.B + r0 + row) * n + col) = Ap[t];
+    *reinterpret_cast<f32x4_t*>(a.A + ((long)g * a.B + r0 + row) * n + col) = a.mode ? Y[t] : Ap[t];
   }
 }
 
@@ -336,17 +354,38 @@ using namespace scamd;
 extern "C" {
 
 // Ysave / Rsave / Asave: the iterate slabs of FistaArgs, all three or none (then plain solve).
+static int launch_direct(const FistaArgs& a, int G, hipStream_t stream);
+
 int sc_fista(const void* X, const void* D, const void* Dt, const float* A0, const float* eta, const float* lam,
              const float* mom, float* A, float* Res, int G, int B, int n, int d, int T, void* Ysave, void* Rsave,
              void* Asave, hipStream_t stream) {
   if (B % FR || n % 128 || d % 128 || T < 0) return 1;
   if ((Ysave != nullptr) != (Asave != nullptr) || (Ysave != nullptr) != (Rsave != nullptr)) return 1;
+  FistaArgs a{reinterpret_cast<const uint16_t*>(X), reinterpret_cast<const uint16_t*>(D),
+              reinterpret_cast<const uint16_t*>(Dt), A0, eta, lam, mom, A, Res, B, n, d, T,
+              reinterpret_cast<uint16_t*>(Ysave), reinterpret_cast<uint16_t*>(Rsave), reinterpret_cast<uint16_t*>(Asave),
+              0, 0.f, 0.f};
+  return launch_direct(a, G, stream);
+}
+
+// Direct coefficient search (mode 1 of the direct solver): T projected-SGD-with-momentum steps
+// on the codes of every model; lr [G], lam [G], mom [T]; gscale = 2 / (B d), lscale = 1 / B
+// for the reference's mean-reduced objective.
+int sc_coef_search(const void* X, const void* D, const void* Dt, const float* A0, const float* lr, const float* lam,
+                   const float* mom, float* A, float* Res, int G, int B, int n, int d, int T, float gscale,
+                   float lscale, hipStream_t stream) {
+  if (B % FR || n % 128 || d % 128 || T < 0) return 1;
+  FistaArgs a{reinterpret_cast<const uint16_t*>(X), reinterpret_cast<const uint16_t*>(D),
+              reinterpret_cast<const uint16_t*>(Dt), A0, lr, lam, mom, A, Res, B, n, d, T,
+              nullptr, nullptr, nullptr, 1, gscale, lscale};
+  return launch_direct(a, G, stream);
+}
+
+static int launch_direct(const FistaArgs& a, int G, hipStream_t stream) {
+  const int B = a.B, n = a.n, d = a.d;
   const int DW = d / 128, NW = n / 128;
   const size_t lds = (size_t)FR * (2 * n + 4 * d);
   if (lds > 160 * 1024) return 1;
-  FistaArgs a{reinterpret_cast<const uint16_t*>(X), reinterpret_cast<const uint16_t*>(D),
-              reinterpret_cast<const uint16_t*>(Dt), A0, eta, lam, mom, A, Res, B, n, d, T,
-              reinterpret_cast<uint16_t*>(Ysave), reinterpret_cast<uint16_t*>(Rsave), reinterpret_cast<uint16_t*>(Asave)};
   dim3 grid(G * (B / FR));
 #define SC_F(DWV, NWV)                                                                                    \
   if (DW == DWV && NW == NWV) {                                                                           \

@@ -614,7 +614,7 @@ __global__ __launch_bounds__(256) void topk_block_kernel(const float* __restrict
 // every lane accumulates 16 partial dots, four exchange steps (8, 4, 2, 1) leave lane
 // L with dot j = L & 15 summed over its 16-lane group, two more finish the wave --
 // 17 shuffles per 16 dots instead of 6 per dot.
-template <int NV>  // d <= 256 * NV
+template <int NV, int RU = (NV <= 3 ? 8 : 4)>  // d <= 256 * NV; RU gathered rows per iteration
 __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
     const int* __restrict__ idx, const float* __restrict__ val, const int* __restrict__ kv,
     const uint16_t* __restrict__ D, const uint16_t* __restrict__ X, long sx, uint16_t* __restrict__ R,
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
   float acc[NV * 4];
 #pragma unroll
   for (int e = 0; e < NV * 4; ++e) acc[e] = 0.f;
-  constexpr int RU = NV <= 2 ? 8 : 4;  // gathered rows per iteration (loads in flight: NV * RU; more costs occupancy)
+  // loads in flight per lane: NV * RU (more costs occupancy)
   for (int j0 = 0; j0 < k; j0 += RU) {
     int ij[RU];
     float wj[RU];
@@ -805,6 +805,21 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx, reinterpret_cast<uint16_t*>(R), \
       row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
+  static const int ru = getenv("SC_TOPK_RU") ? atoi(getenv("SC_TOPK_RU")) : 0;
+  if (nv == 3 && ru == 16) {  // A/B knob (SC_TOPK_RU): 8 rows per iteration is the default for d <= 768
+    hipLaunchKernelGGL((topk_decode_grad_kernel<3, 16>), grid, dim3(256), 0, stream, idx, val, k,
+                       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,
+                       reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),
+                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
+  if (nv == 3 && ru == 4) {
+    hipLaunchKernelGGL((topk_decode_grad_kernel<3, 4>), grid, dim3(256), 0, stream, idx, val, k,
+                       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,
+                       reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),
+                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
   SC_D(1) SC_D(2) SC_D(3) SC_D(4) SC_D(8) SC_D(16)
 #undef SC_D
   return 1;

@@ -420,3 +420,58 @@ def unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, mom, T):
     gemm.weight_grads([[(As[:, T - 1].contiguous(), Rb)]], [Dfin], -1.0)
     Dbar.mul_(eta[:, None, None]).add_(Dfin)
     return Dbar, cbar
+
+
+# --------------------------------------------------------------------- direct coefficient search
+def coef_search_torch(X, D, lam, lr, iters=100, momentum=0.9, A0=None):
+    """Projected SGD with momentum on the codes (reference autoencoders/direct_coef_search.py:
+    52-56): grad = 2/(B d) (c D - x) D^T + lam/B sign(c); buf = m buf + grad; c = relu(c - lr buf).
+    Batched over models: D [G, n, d], X [B, d] or [G, B, d], lam / lr [G]."""
+    D = D.float()
+    G, n, d = D.shape
+    B = X.shape[-2]
+    Xf = X.float()
+    lam = torch.as_tensor(lam, dtype=torch.float32, device=D.device).reshape(-1, 1, 1)
+    lr = torch.as_tensor(lr, dtype=torch.float32, device=D.device).reshape(-1, 1, 1)
+    c = torch.zeros(G, B, n, device=D.device) if A0 is None else A0.float().clone()
+    buf = torch.zeros_like(c)
+    Dt = D.transpose(1, 2)
+    for _ in range(iters):
+        grad = 2.0 / (B * d) * (c @ D - Xf) @ Dt + lam / B * torch.sign(c)
+        buf = momentum * buf + grad
+        c = torch.relu(c - lr * buf)
+    return c
+
+
+def coef_search(X, D, lam, lr, iters: int = 100, momentum: float = 0.9, A0=None, backend: str = "auto"):
+    """Direct coefficient search for every model at once; the GPU path is the persistent
+    direct-form solver in its projected-momentum mode (one launch for all models and steps,
+    bf16 MFMA products, fp32 codes and momentum)."""
+    D = D if D.dim() == 3 else D[None]
+    G, n, d = D.shape
+    B = X.shape[-2]
+    ok = (backend != "torch" and _hip_ok(D) and B % 16 == 0 and n % 128 == 0 and d % 128 == 0
+          and (d // 128, n // 128) in DIRECT_TILES)
+    if backend == "hip" and not ok:
+        raise ValueError(f"coef_search HIP path needs B % 16 == 0 and (d/128, n/128) in {sorted(DIRECT_TILES)}")
+    if not ok:
+        return coef_search_torch(X, D, lam, lr, iters, momentum, A0)
+    dev = D.device
+    Xb = (X if X.dim() == 3 else X.expand(G, B, d)).to(torch.bfloat16).contiguous()
+    if tuple(Xb.shape) != (G, B, d):
+        raise ValueError(f"X shape {tuple(X.shape)} does not match {(B, d)} or {(G, B, d)}")
+    Db = D.to(torch.bfloat16).contiguous()
+    Dtb = Db.transpose(1, 2).reshape(G, d // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
+    Dfb = Db.view(G, n // 16, 16, d // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
+    lam_t = torch.as_tensor(lam, dtype=torch.float32, device=dev).reshape(-1).expand(G).contiguous()
+    lr_t = torch.as_tensor(lr, dtype=torch.float32, device=dev).reshape(-1).expand(G).contiguous()
+    mom = torch.full((max(iters, 1),), float(momentum), device=dev)
+    a0 = None if A0 is None else A0.float().contiguous()
+    if a0 is not None and tuple(a0.shape) != (G, B, n):
+        raise ValueError(f"A0 shape {tuple(A0.shape)} != {(G, B, n)}")
+    A = torch.empty(G, B, n, device=dev)
+    rc = _lib.lib().sc_coef_search(_lib.ptr(Xb), _lib.ptr(Dfb), _lib.ptr(Dtb), _lib.ptr(a0), _lib.ptr(lr_t),
+                                   _lib.ptr(lam_t), _lib.ptr(mom), _lib.ptr(A), None, G, B, n, d, iters,
+                                   2.0 / (B * d), 1.0 / B, _lib.stream_handle())
+    _lib.check(rc, "sc_coef_search")
+    return A

@@ -113,3 +113,16 @@ def test_trainer_fista_loss_objective_cpu(tmp_path):
                           fista_loss_iters=5)
     tr2.load_state_dict(st)
     torch.testing.assert_close(tr2.impl.params["encoder"], tr.impl.params["encoder"])
+
+
+def test_coef_search_torch_matches_basis_pursuit():
+    from sparse_coding__amd.models.misc import DirectCoefOptimizer
+    from sparse_coding__amd.models.signatures import unit_rows
+
+    torch.manual_seed(4)
+    p, b = DirectCoefOptimizer.init(16, 32, 1e-2, lr=1e-1)
+    x = torch.randn(20, 16)
+    with torch.no_grad():
+        ref = DirectCoefOptimizer.basis_pursuit(p, b, x, n_iters=30)
+        got = F.coef_search_torch(x, unit_rows(p["decoder"])[None], b["l1_alpha"], b["lr"], 30)[0]
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)

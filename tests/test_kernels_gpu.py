@@ -731,3 +731,30 @@ def test_fista_loss_ensemble_trains_on_gpu():
         last = eng.step_batch(x)
     torch.cuda.synchronize()
     assert torch.isfinite(last).all() and (last < first).all(), (first, last)
+
+
+def test_coef_search_hip_matches_torch():
+    """Direct coefficient search (reference direct_coef_search.py:52-56) on the persistent
+    solver's projected-momentum mode vs the fp32 loop, 3 models at once."""
+    from sparse_coding__amd.ops import fista as F
+
+    torch.manual_seed(14)
+    G, B, n, d = 3, 64, 512, 256
+    D = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1)
+    X = torch.randn(B, d, device=DEV)
+    lam = torch.tensor([1e-3, 1e-2, 5e-2], device=DEV)
+    lr = torch.tensor([50.0, 50.0, 20.0], device=DEV)
+    A = F.coef_search(X, D, lam, lr, 60, backend="hip")
+    R = F.coef_search_torch(X, D.to(torch.bfloat16).float(), lam, lr, 60)
+    torch.cuda.synchronize()
+
+    def obj(C):
+        return ((X - C @ D) ** 2).mean(dim=(1, 2)) + lam * C.abs().sum(-1).mean(-1)
+
+    torch.testing.assert_close(obj(A), obj(R), rtol=1e-2, atol=1e-4)
+    # codes: the two lightly regularised models; at lam = 5e-2 (3 % density) the projected
+    # momentum iteration is degenerate -- a CPU emulation with bf16 operands lands on codes 64 %
+    # away with the same objective to 4 digits
+    for g in range(2):
+        rel = ((A[g] - R[g]).norm() / R[g].norm()).item()
+        assert rel < 3e-2, (g, rel)
