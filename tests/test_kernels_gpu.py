@@ -758,3 +758,56 @@ def test_coef_search_hip_matches_torch():
     for g in range(2):
         rel = ((A[g] - R[g]).norm() / R[g].norm()).item()
         assert rel < 3e-2, (g, rel)
+
+
+def test_fused_topk_encode_matches_reference_encode():
+    """FusedTopKEnsemble.encode (padded slots of small-k models must not clobber feature 0)
+    against TopKEncoder.encode per model, mixed k."""
+    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
+    from sparse_coding__amd.models.topk import TopKEncoder
+
+    torch.manual_seed(15)
+    d, n, B = 256, 1024, 256
+    models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16)]
+    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV)
+    x = torch.randn(B, d, device=DEV)
+    x[:, :] += 10.0 * (eng.shadow[0, 0] + eng.shadow[1, 0]).float()  # feature 0: a real pick of every row
+    got = eng.encode(x)
+    torch.cuda.synchronize()
+    for g, (p, b) in enumerate(models):
+        D = eng.shadow[g].float()
+        ref = TopKEncoder.encode(x.to(torch.bfloat16).float(), b["sparsity"], D)
+        assert bool((got[g, :, 0] > 0).all())
+        torch.testing.assert_close(got[g], ref, rtol=1e-3, atol=1e-3)
+
+
+def test_tied_centered_center_update_direction_at_dense_codes():
+    """Learned-centre tied SAE with dense codes (bias 0, about half the atoms on): the two
+    terms of the centre gradient largely cancel, so they come from fp32 data (the decoder
+    epilogue's fp32 residual column sums, fp32 masters).  One Adam step from zero moments moves
+    the centre by ~lr sign(g): the signs must agree with the eager fp32 ensemble's."""
+    from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.engine.optim import adam
+    from sparse_coding__amd.models.signatures import FunctionalTiedCenteredSAE as sig
+
+    torch.manual_seed(16)
+    d, n, B = 256, 512, 512
+    models = [sig.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3)]
+    for p, _ in models:
+        p["encoder_bias"].zero_()
+        p["center"].normal_(0.0, 0.5)
+    ref = FunctionalEnsemble([({k: v.clone() for k, v in p.items()}, b) for p, b in models], sig, adam,
+                             {"lr": 1e-3}, device=DEV)
+    fused = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=DEV)
+    feats = torch.nn.functional.normalize(torch.randn(1024, d, device=DEV), dim=-1)
+    x = ((torch.relu(torch.randn(B, 1024, device=DEV) - 1.0) * 2.0) @ feats + 0.3).to(torch.bfloat16)
+    ref.step_batch(x.float())
+    out = fused.step_batch(x)
+    torch.cuda.synchronize()
+    assert float(out[:, 4].min()) > 0.3 * n, "codes must be dense for this test"
+    init = torch.stack([m[0]["center"] for m in models]).to(DEV)
+    mf, mr = fused.params["center"] - init, ref.params["center"] - init
+    big = mr.abs() > 0.5e-3  # Adam's first step: ~lr where the gradient is not tiny
+    agree = (torch.sign(mf) == torch.sign(mr))[big].float().mean().item()
+    assert agree > 0.9, agree
