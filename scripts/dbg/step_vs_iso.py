@@ -43,4 +43,10 @@ c2 = torch.rand_like(e.c.float()).to(torch.bfloat16)
 for _ in range(30):
     gemm.decode_residual(c2, e.dec_shadow, x, e.r, e.dec_part)
 torch.cuda.synchronize()
+# phase D: ENC -> DEC -> DEC (is the first DEC after ENC slow because c was just written?)
+for _ in range(20):
+    gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c, e.enc_part, None, None, mask_out=e.cmask)
+    gemm.decode_residual(e.c, e.dec_shadow, x, e.r, e.dec_part)
+    gemm.decode_residual(e.c, e.dec_shadow, x, e.r, e.dec_part)
+torch.cuda.synchronize()
 print("done")

@@ -106,6 +106,9 @@ class RandomDatasetGenerator(_GenBase):
     correlated: bool
     device: Device
     seed: int = 0
+    # "hip": codes from the Philox kernel (ops/synth.py) and an MFMA GEMM, bf16 throughout (the
+    # same distribution; a different random stream than the torch path)
+    backend: str = "torch"
 
     frac_nonzero: float = field(init=False)
     decay: torch.Tensor = field(init=False)
@@ -126,6 +129,8 @@ class RandomDatasetGenerator(_GenBase):
         self.t_type = torch.float32
 
     def send(self, ignored: Any = None) -> torch.Tensor:
+        if self.backend == "hip":
+            return self._send_hip()
         if self.correlated:
             _, _, data = generate_correlated_dataset(self.n_ground_truth_components, self.batch_size,
                                                      self.corr_matrix, self.feats, self.frac_nonzero, self.decay,
@@ -134,6 +139,31 @@ class RandomDatasetGenerator(_GenBase):
             _, _, data = generate_rand_dataset(self.n_ground_truth_components, self.batch_size,
                                                self.component_probs, self.feats, self.device, self.generator)
         return data.to(self.t_type)
+
+    def _send_hip(self) -> torch.Tensor:
+        from ..ops import synth
+
+        if not hasattr(self, "_rows"):
+            self._rows = 0
+            self._feats_bf16 = self.feats.to(torch.bfloat16).contiguous()
+        if self.correlated:  # one MVN draw per batch sets the per-feature probabilities
+            chol = torch.linalg.cholesky(self.corr_matrix.double()).float()
+            z = chol @ torch.randn(self.n_ground_truth_components, device=self.device, generator=self.generator)
+            probs = torch.special.ndtr(z) * self.decay
+            probs = probs * (self.frac_nonzero / probs.mean())
+        else:
+            probs = self.component_probs
+        codes = synth.sparse_codes(probs, self.batch_size, self.seed, self._rows)
+        self._rows += self.batch_size
+        if self.correlated:  # every row gets at least one active feature (reference :236-240)
+            empty = (codes != 0).sum(1) == 0
+            if bool(empty.any()):
+                rows = empty.nonzero()[:, 0]
+                cols = torch.randint(0, self.n_ground_truth_components, (rows.numel(),), device=self.device,
+                                     generator=self.generator)
+                codes[rows, cols] = torch.rand(rows.numel(), device=self.device,
+                                               generator=self.generator).to(codes.dtype)  # 1 x strength
+        return synth.mix(codes, self._feats_bf16).to(self.t_type)
 
 
 @dataclass

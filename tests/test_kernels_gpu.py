@@ -811,3 +811,38 @@ def test_tied_centered_center_update_direction_at_dense_codes():
     big = mr.abs() > 0.5e-3  # Adam's first step: ~lr where the gradient is not tiny
     agree = (torch.sign(mf) == torch.sign(mr))[big].float().mean().item()
     assert agree > 0.9, agree
+
+
+def test_synth_codes_kernel_statistics_and_reproducibility():
+    """K17: Philox sparse codes -- per-feature firing rates match the probabilities, nonzero
+    codes have mean E[U U] = 1/4, any row slice regenerates exactly, and the MFMA mixing GEMM
+    matches fp32 matmul; the generator's hip backend produces data of the right shape/scale."""
+    from sparse_coding__amd.data.synthetic import RandomDatasetGenerator
+    from sparse_coding__amd.ops import synth
+
+    n, B = 512, 65536
+    probs = (0.999 ** torch.arange(n, device=DEV, dtype=torch.float32)) * (32.0 / n)
+    c = synth.sparse_codes(probs, B, seed=1234)
+    c2 = synth.sparse_codes(probs, B, seed=1234)
+    assert torch.equal(c, c2)
+    part = synth.sparse_codes(probs, 1000, seed=1234, row0=5000)
+    assert torch.equal(part, c[5000:6000])
+    assert not torch.equal(synth.sparse_codes(probs, 1000, seed=99), c[:1000])
+    rate = (c != 0).float().mean(0)
+    sd = (probs * (1 - probs) / B).sqrt()
+    assert bool(((rate - probs).abs() <= 5 * sd + 1e-4).all())
+    nz = c[c != 0].float()
+    assert abs(nz.mean().item() - 0.25) < 0.01
+    feats = torch.nn.functional.normalize(torch.randn(n, 256, device=DEV), dim=-1).to(torch.bfloat16)
+    x = synth.mix(c[:4096], feats)
+    ref = c[:4096].float() @ feats.float()
+    torch.testing.assert_close(x.float(), ref, rtol=2e-2, atol=2e-2)
+    gen = RandomDatasetGenerator(activation_dim=256, n_ground_truth_components=512, batch_size=2048,
+                                 feature_num_nonzero=16, feature_prob_decay=0.99, correlated=False, device=DEV,
+                                 seed=5, backend="hip")
+    a, b = gen.send(None), gen.send(None)
+    assert a.shape == (2048, 256) and not torch.equal(a, b) and torch.isfinite(a).all()
+    genc = RandomDatasetGenerator(activation_dim=256, n_ground_truth_components=512, batch_size=2048,
+                                  feature_num_nonzero=16, feature_prob_decay=0.99, correlated=True, device=DEV,
+                                  seed=5, backend="hip")
+    assert torch.isfinite(genc.send(None)).all()
