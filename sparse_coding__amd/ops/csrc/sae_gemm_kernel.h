@@ -85,11 +85,19 @@ template <class S>
 constexpr int epi_scratch_floats() { return 2 * S::WGM * S::BN + S::NW; }
 
 // LDS-staged bf16 output stores (STAGE, 128x128 tile kernel: the ring is free after the K
-// loop): each wave parks its 64x64 bf16 sub-tile in LDS in the MFMA layout (144-byte rows:
-// conflict-free 8-byte writes), then streams it out row-contiguous -- 8 global_store_dwordx4
-// per wave, each covering 8 whole 128-byte row segments, instead of 16 dwordx2 stores that
-// each touch 16 half-filled 32-byte segments (the store tail is issue-bound otherwise).
-constexpr int STAGE_OFF = 4096, STAGE_ROW = 144, STAGE_WAVE = 64 * STAGE_ROW;
+// loop): each wave parks its 64x64 bf16 sub-tile in LDS in the MFMA layout, then streams it
+// out row-contiguous -- 8 global_store_dwordx4 per wave, each covering 8 whole 128-byte row
+// segments, instead of 16 dwordx2 stores that each touch 16 half-filled 32-byte segments (the
+// store tail is issue-bound otherwise).  Rows are 128 bytes; the 16-byte chunk index is XORed
+// with (row >> 1) & 7 and the two 8-byte halves of a chunk swap on odd rows.  Banking per
+// instruction (MI355X_MICROARCH.md, LDS): ds_write_b64 serves 16 contiguous lanes at a time on
+// 32 banks -- a group is 16 rows at one column, and the chunk XOR alone gives only 8 distinct
+// bank pairs (2-way, measured: 64 extra cycles per wave); the half swap makes them 16.
+// ds_read_b128 serves 16-lane groups on 64 banks: 2 rows x 8 chunks, distinct with the XOR.
+constexpr int STAGE_OFF = 4096, STAGE_ROW = 128, STAGE_WAVE = 64 * STAGE_ROW;
+__device__ __forceinline__ int stage_at(int row, int byte) {  // 8-byte granule of (row, byte)
+  return row * STAGE_ROW + ((((byte >> 4) ^ (row >> 1)) & 7) << 4) + ((((byte >> 3) ^ row) & 1) << 3);
+}
 template <class S>
 constexpr int stage_bytes() { return STAGE_OFF + S::NW * STAGE_WAVE; }
 
@@ -112,7 +120,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   // one 4-wide bf16 output fragment (rows rowb + 16 i, columns colb + 16 j .. +3)
   auto put = [&](uint16_t* C, int i, int j, ushort4 h) {
     if constexpr (STAGE) {
-      *reinterpret_cast<ushort4*>(stage + (i * 16 + (lane & 15)) * STAGE_ROW + (j * 16 + 4 * (lane >> 4)) * 2) = h;
+      *reinterpret_cast<ushort4*>(stage + stage_at(i * 16 + (lane & 15), (j * 16 + 4 * (lane >> 4)) * 2)) = h;
     } else {
       *reinterpret_cast<ushort4*>(C + (long)(rowb + i * 16) * p.ldc + colb + j * 16) = h;
     }
@@ -124,7 +132,8 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int row = 8 * k + (lane >> 3);
-        const uint4 v = *reinterpret_cast<const uint4*>(stage + row * STAGE_ROW + ch * 16);
+        uint4 v = *reinterpret_cast<const uint4*>(stage + row * STAGE_ROW + (((ch ^ (row >> 1)) & 7) << 4));
+        if (row & 1) v = make_uint4(v.z, v.w, v.x, v.y);  // halves stored swapped on odd rows
         *reinterpret_cast<uint4*>(Cw + (long)row * p.ldc + ch * 8) = v;
       }
     }
