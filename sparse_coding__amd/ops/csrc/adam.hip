@@ -12,6 +12,7 @@
 // also reduces the deterministic per-tile partials written by the GEMM
 // epilogues (no float atomics anywhere in the step).
 #include "common.h"
+#include <stdlib.h>
 
 namespace scamd {
 
@@ -47,7 +48,10 @@ __device__ __forceinline__ void bias_corrections(float b1, float b2, int t, floa
   bc2 = 1.f - __powf(b2, (float)t);
 }
 
-template <int NV>
+// NT: the fp32 state (p, m, v) is written with non-temporal stores and the gradient read with
+// non-temporal loads -- none of it is touched again this step, so it should not displace the
+// next GEMMs' operands from L2 / MALL or leave dirty lines for them to write back.
+template <int NV, bool NT = false>
 __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   const int lane = threadIdx.x & 63;
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -75,7 +79,13 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   for (int i = 0; i < NV; ++i) {
     const int e = (i * 64 + lane) * 4;
     pv[i] = *reinterpret_cast<const float4*>(P4 + e);
-    gv[i] = *reinterpret_cast<const float4*>(G4 + e);
+    if constexpr (NT)
+    {
+      const f32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(G4 + e));
+      gv[i] = make_float4(t[0], t[1], t[2], t[3]);
+    }
+    else
+      gv[i] = *reinterpret_cast<const float4*>(G4 + e);
     mv_[i] = *reinterpret_cast<const float4*>(R.m + base + e);
     vv_[i] = *reinterpret_cast<const float4*>(R.v + base + e);
   }
@@ -130,9 +140,16 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
       pp[k] -= step * mm[k] / (sqrtf(vvv[k] * rbc2) + a.eps);
       ss2 += pp[k] * pp[k];
     }
-    *reinterpret_cast<float4*>(R.m + base + e) = mv;
-    *reinterpret_cast<float4*>(R.v + base + e) = vv;
-    *reinterpret_cast<float4*>(R.p + base + e) = pv[i];
+    if constexpr (NT) {
+      __builtin_nontemporal_store(f32x4_t{mv.x, mv.y, mv.z, mv.w}, reinterpret_cast<f32x4_t*>(R.m + base + e));
+      __builtin_nontemporal_store(f32x4_t{vv.x, vv.y, vv.z, vv.w}, reinterpret_cast<f32x4_t*>(R.v + base + e));
+      __builtin_nontemporal_store(f32x4_t{pv[i].x, pv[i].y, pv[i].z, pv[i].w},
+                                  reinterpret_cast<f32x4_t*>(R.p + base + e));
+    } else {
+      *reinterpret_cast<float4*>(R.m + base + e) = mv;
+      *reinterpret_cast<float4*>(R.v + base + e) = vv;
+      *reinterpret_cast<float4*>(R.p + base + e) = pv[i];
+    }
   }
   float sc = 1.f;
   if (R.norm) {
@@ -329,6 +346,7 @@ int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const*
                  float bc2, const int* step, int nsplit, long gstride, long row0, hipStream_t stream,
                  const int* live) {
   if (d % 256 || d > 4096 || nset < 1 || nset > 2 || nsplit < 1) return 1;
+  static const int nt = getenv("SC_ADAM_NT") ? atoi(getenv("SC_ADAM_NT")) : 0;
   AdamArgs a;
   long total = 0;
   for (int i = 0; i < nset; ++i) {
@@ -341,13 +359,20 @@ int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const*
   a.nsplit = nsplit; a.gstride = gstride; a.row0 = row0; a.live = live;
   const long blocks = (total + 3) / 4;
   switch (d / 256) {
-    case 1: hipLaunchKernelGGL(adam_rows_kernel<1>, dim3(blocks), dim3(256), 0, stream, a); break;
-    case 2: hipLaunchKernelGGL(adam_rows_kernel<2>, dim3(blocks), dim3(256), 0, stream, a); break;
-    case 3: hipLaunchKernelGGL(adam_rows_kernel<3>, dim3(blocks), dim3(256), 0, stream, a); break;
-    case 4: hipLaunchKernelGGL(adam_rows_kernel<4>, dim3(blocks), dim3(256), 0, stream, a); break;
-    case 6: hipLaunchKernelGGL(adam_rows_kernel<6>, dim3(blocks), dim3(256), 0, stream, a); break;
-    case 8: hipLaunchKernelGGL(adam_rows_kernel<8>, dim3(blocks), dim3(256), 0, stream, a); break;
-    case 16: hipLaunchKernelGGL(adam_rows_kernel<16>, dim3(blocks), dim3(256), 0, stream, a); break;
+    case 1: if (nt) hipLaunchKernelGGL((adam_rows_kernel<1, true>), dim3(blocks), dim3(256), 0, stream, a);
+             else hipLaunchKernelGGL((adam_rows_kernel<1, false>), dim3(blocks), dim3(256), 0, stream, a); break;
+    case 2: if (nt) hipLaunchKernelGGL((adam_rows_kernel<2, true>), dim3(blocks), dim3(256), 0, stream, a);
+             else hipLaunchKernelGGL((adam_rows_kernel<2, false>), dim3(blocks), dim3(256), 0, stream, a); break;
+    case 3: if (nt) hipLaunchKernelGGL((adam_rows_kernel<3, true>), dim3(blocks), dim3(256), 0, stream, a);
+             else hipLaunchKernelGGL((adam_rows_kernel<3, false>), dim3(blocks), dim3(256), 0, stream, a); break;
+    case 4: if (nt) hipLaunchKernelGGL((adam_rows_kernel<4, true>), dim3(blocks), dim3(256), 0, stream, a);
+             else hipLaunchKernelGGL((adam_rows_kernel<4, false>), dim3(blocks), dim3(256), 0, stream, a); break;
+    case 6: if (nt) hipLaunchKernelGGL((adam_rows_kernel<6, true>), dim3(blocks), dim3(256), 0, stream, a);
+             else hipLaunchKernelGGL((adam_rows_kernel<6, false>), dim3(blocks), dim3(256), 0, stream, a); break;
+    case 8: if (nt) hipLaunchKernelGGL((adam_rows_kernel<8, true>), dim3(blocks), dim3(256), 0, stream, a);
+             else hipLaunchKernelGGL((adam_rows_kernel<8, false>), dim3(blocks), dim3(256), 0, stream, a); break;
+    case 16: if (nt) hipLaunchKernelGGL((adam_rows_kernel<16, true>), dim3(blocks), dim3(256), 0, stream, a);
+             else hipLaunchKernelGGL((adam_rows_kernel<16, false>), dim3(blocks), dim3(256), 0, stream, a); break;
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
