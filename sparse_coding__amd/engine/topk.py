@@ -54,7 +54,15 @@ class FusedTopKEnsemble:
         self.row_se = torch.empty(G, B, device=dev)
         self.codebuf = torch.zeros(G, B, n, device=dev, dtype=bf)
         self.dscbuf = torch.zeros(G, B, n, device=dev, dtype=bf)
-        self.g = torch.empty(G, n, d, device=dev)
+        # optional split-K weight gradient (SC_TOPK_WSPLIT): 256x256 tiles give only
+        # G * (n/256) * (d/256) workgroups (576 for config 4: 2.25 waves over 256 CUs); K halves
+        # fill the machine and Adam sums the slabs -- A/B'd slower (1.344 / 1.406 ms for 2 / 3
+        # slabs vs 1.318 ms): the extra fp32 slab traffic through Adam costs more than the tail
+        import os
+
+        self.wg_split = int(os.environ.get("SC_TOPK_WSPLIT", "1"))
+        self.g_all = torch.empty(self.wg_split, G, n, d, device=dev)
+        self.g = self.g_all[0]
         self.idx = self.val = None
         # decode: "gather" (sparse, one wave per row) or "gemm" (dense codes through the decoder and
         # code-gradient epilogue GEMMs); chosen from measurement (profiles/config4_topk_r2.json)
@@ -81,11 +89,16 @@ class FusedTopKEnsemble:
             topk_ops.decode_grad(self.idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
                                  self.dscbuf)
             torch.sum(self.row_se, dim=1, out=self._se)
-        gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g], 2.0 / (B * d))
+        if self.wg_split > 1:
+            gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g_all], 2.0 / (B * d),
+                                  ksplit=self.wg_split)
+        else:
+            gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g], 2.0 / (B * d))
         topk_ops.clear(self.idx, self.codebuf, self.dscbuf)
         adam_ops.adam_rows([dict(p=self.params["dict"], g=self.g, m=self.m["dict"], v=self.v["dict"],
                                  shadow=self.shadow, norms=self.norms, norm=True)],
-                           self.lr, self.step_count + 1, *self.betas, self.eps, step_dev=self.step_dev)
+                           self.lr, self.step_count + 1, *self.betas, self.eps, step_dev=self.step_dev,
+                           nsplit=self.wg_split, gstride=G * n * d)
         self.step_dev += 1
         self.step_count += 1
         return self._se / (B * d)  # per-model MSE (the reference's loss), on device
