@@ -414,8 +414,19 @@ def unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, mom, T):
         Ya, Yb_ = Yb_, Ya
     # Dbar = eta sum_t (Vbar_t^T Res_t + Y_t^T nS_t) - A_T^T Rbar: one K = T B GEMM + one K = B GEMM
     Dbar = torch.empty(G, n, d, device=dev)
-    gemm.weight_grads([[(Vs.view(G, T * B, n), Rs.view(G, T * B, d)), (Ys.view(G, T * B, n), Ss.view(G, T * B, d))]],
-                      [Dbar], 1.0)
+    # G (n/256)(d/256) output tiles over a K = T B reduction: few tiles (32 for 8 models at
+    # d = n = 512), so split K until the machine is full; the slabs are summed after
+    tiles = G * ((n + 255) // 256) * ((d + 255) // 256)
+    ks = 1
+    while ks < 16 and tiles * ks * 2 <= 512 and (T * B) % (64 * ks * 2) == 0:
+        ks *= 2
+    segs = [[(Vs.view(G, T * B, n), Rs.view(G, T * B, d)), (Ys.view(G, T * B, n), Ss.view(G, T * B, d))]]
+    if ks > 1:
+        slabs = torch.empty(ks, G, n, d, device=dev)
+        gemm.weight_grads(segs, [slabs], 1.0, ksplit=ks)
+        torch.sum(slabs, dim=0, out=Dbar)
+    else:
+        gemm.weight_grads(segs, [Dbar], 1.0)
     Dfin = torch.empty(G, n, d, device=dev)
     gemm.weight_grads([[(As[:, T - 1].contiguous(), Rb)]], [Dfin], -1.0)
     Dbar.mul_(eta[:, None, None]).add_(Dfin)
