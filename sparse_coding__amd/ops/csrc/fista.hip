@@ -63,22 +63,28 @@ __device__ __forceinline__ void lds_put4(char* base, int row, int col, int rowby
 
 // DW: 16-column output tiles per wave in phase 1 (d = 8 * 16 * DW)
 // NW: 16-column output tiles per wave in phase 2 (n = 8 * 16 * NW)
-template <int DW, int NW, int PH = (NW >= 16 ? (DW >= 4 ? 4 : 2) : 1)>
+// RT: 16-row tiles per workgroup.  Every dictionary fragment a wave streams from L2 feeds RT
+// MFMAs, so RT = 2 halves the L2 traffic per FLOP (the solver streams D and D^T once per
+// iteration per workgroup); used where the doubled fp32 state still fits the registers.
+// MODE: 0 FISTA, 1 coefficient search (a.mode), 2 FISTA saving the iterate slabs -- compile-time
+// so each variant carries only its own registers (the slab stores alone cost ~40 VGPRs)
+template <int DW, int NW, int RT = 1, int MODE = 0, int PH = (NW >= 16 ? (DW >= 4 ? 4 : 2) : 1)>
 __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int R = FR * RT;           // rows per workgroup
   const int n = a.n, d = a.d;
   const int nrb = n * 2, drb = d * 2;  // LDS row bytes
-  char* Ybf = lds;                     // [16][n]
-  char* Xs = lds + FR * nrb;           // [16][d]
-  char* Rs = Xs + FR * drb;            // [16][d]
+  char* Ybf = lds;                     // [R][n]
+  char* Xs = lds + R * nrb;            // [R][d]
+  char* Rs = Xs + R * drb;             // [R][d]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int rb = a.B / FR;
+  const int rb = a.B / R;
   // XCD-aware order: each XCD works on a contiguous run of row blocks, i.e. on one or two
   // models, so its L2 holds those dictionaries (D and D^T, 4 n d bytes) instead of a slice
   // of every model's.
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int g = bid / rb, r0 = (bid % rb) * FR;
+  const int g = bid / rb, r0 = (bid % rb) * R;
   const uint16_t* X = a.X + ((long)g * a.B + r0) * d;
   const uint16_t* D = a.D + (long)g * n * d;
   const uint16_t* Dt = a.Dt + (long)g * d * n;
@@ -86,130 +92,151 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
   const int row = lane & 15, q = lane >> 4;
 
   // stage X rows into LDS
-  for (int e = tid * 8; e < FR * d; e += FNT * 8) {
+  for (int e = tid * 8; e < R * d; e += FNT * 8) {
     const int rr = e / d, cc = e % d;
     *reinterpret_cast<u32x4_t*>(Xs + fo(rr, cc, drb)) = *reinterpret_cast<const u32x4_t*>(X + (long)rr * d + cc);
   }
-  // state: this lane owns rows `row`, columns n0 + 16 t + 4 q + r (t < NW, r < 4)
+  // state: this lane owns rows 16 u + `row`, columns n0 + 16 t + 4 q + r (u < RT, t < NW, r < 4)
   const int nbase = w * NW * 16;
-  f32x4_t Y[NW], Ap[NW];
+  f32x4_t Y[RT][NW], Ap[RT][NW];
 #pragma unroll
-  for (int t = 0; t < NW; ++t) {
-    const int col = nbase + t * 16 + 4 * q;
-    f32x4_t v = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    if (a.A0) v = *reinterpret_cast<const f32x4_t*>(a.A0 + ((long)g * a.B + r0 + row) * n + col);
-    Y[t] = v;
-    Ap[t] = a.mode ? f32x4_t{0.f, 0.f, 0.f, 0.f} : v;  // mode 1: zero momentum buffer
-    lds_put4(Ybf, row, col, nrb, v[0], v[1], v[2], v[3]);
-    if (a.Ysave)
-      *reinterpret_cast<ushort4*>(a.Ysave + ((long)g * a.T * a.B + r0 + row) * n + col) =
-          make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
-  }
+  for (int u = 0; u < RT; ++u)
+#pragma unroll
+    for (int t = 0; t < NW; ++t) {
+      const int col = nbase + t * 16 + 4 * q;
+      const int rr = u * FR + row;
+      f32x4_t v = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if (a.A0) v = *reinterpret_cast<const f32x4_t*>(a.A0 + ((long)g * a.B + r0 + rr) * n + col);
+      Y[u][t] = v;
+      Ap[u][t] = MODE == 1 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : v;  // mode 1: zero momentum buffer
+      lds_put4(Ybf, rr, col, nrb, v[0], v[1], v[2], v[3]);
+      if (MODE == 2)
+        *reinterpret_cast<ushort4*>(a.Ysave + ((long)g * a.T * a.B + r0 + rr) * n + col) =
+            make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
+    }
   __syncthreads();
 
   const int dbase = w * DW * 16;
   for (int it = 0; it <= a.T; ++it) {
     const bool last = it == a.T;  // final pass: Res = X - A D with the solution A
-    // ---- phase 1: P[16, d_w] = Ybf[16, n] x D[n, d_w]; lane gets P[row][dcol 4q..4q+3]
-    f32x4_t P[DW];
+    // ---- phase 1: P[R, d_w] = Ybf[R, n] x D[n, d_w]; lane gets P[16 u + row][dcol 4q..4q+3]
+    f32x4_t P[RT][DW];
 #pragma unroll
-    for (int t = 0; t < DW; ++t) P[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    constexpr int UNR1 = NW >= 16 ? 1 : 2;  // two k-steps of loads in flight where registers allow
+    for (int u = 0; u < RT; ++u)
+#pragma unroll
+      for (int t = 0; t < DW; ++t) P[u][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    constexpr int UNR1 = (NW >= 16 || RT > 1) ? 1 : 2;  // two k-steps of loads in flight where registers allow
 #pragma unroll UNR1
     for (int k0 = 0; k0 < n; k0 += 32) {
-      const bf16x8_t fy = lds_frag(Ybf, row, k0 + 8 * q, nrb);
+      bf16x8_t fy[RT];
+#pragma unroll
+      for (int u = 0; u < RT; ++u) fy[u] = lds_frag(Ybf, u * FR + row, k0 + 8 * q, nrb);
 #pragma unroll
       for (int t = 0; t < DW; ++t) {
         // B side (output columns = d): lane reads D^T[dcol = dbase + 16t + row][k0 + 8q .. +7]
         const bf16x8_t fd =
             *reinterpret_cast<const bf16x8_t*>(Dt + ((long)((dbase >> 4) + t) * (n >> 5) + (k0 >> 5)) * 512 + lane * 8);
-        P[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd, fy, P[t], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < RT; ++u) P[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd, fy[u], P[u][t], 0, 0, 0);
       }
     }
     // Res = X - P  -> LDS (bf16) for phase 2, or global fp32 on the final pass
 #pragma unroll
-    for (int t = 0; t < DW; ++t) {
-      const int col = dbase + t * 16 + 4 * q;
-      const ushort4 xv = *reinterpret_cast<const ushort4*>(Xs + fo(row, col, drb));
-      const float r_0 = bf2f(xv.x) - P[t][0], r_1 = bf2f(xv.y) - P[t][1];
-      const float r_2 = bf2f(xv.z) - P[t][2], r_3 = bf2f(xv.w) - P[t][3];
-      if (last) {
-        if (a.Res)
-          *reinterpret_cast<f32x4_t*>(a.Res + ((long)g * a.B + r0 + row) * d + col) = f32x4_t{r_0, r_1, r_2, r_3};
-      } else {
-        lds_put4(Rs, row, col, drb, r_0, r_1, r_2, r_3);
-        if (a.Rsave)
-          *reinterpret_cast<ushort4*>(a.Rsave + (((long)g * a.T + it) * a.B + r0 + row) * d + col) =
-              make_ushort4(f2bf(r_0), f2bf(r_1), f2bf(r_2), f2bf(r_3));
+    for (int u = 0; u < RT; ++u)
+#pragma unroll
+      for (int t = 0; t < DW; ++t) {
+        const int col = dbase + t * 16 + 4 * q;
+        const int rr = u * FR + row;
+        const ushort4 xv = *reinterpret_cast<const ushort4*>(Xs + fo(rr, col, drb));
+        const float r_0 = bf2f(xv.x) - P[u][t][0], r_1 = bf2f(xv.y) - P[u][t][1];
+        const float r_2 = bf2f(xv.z) - P[u][t][2], r_3 = bf2f(xv.w) - P[u][t][3];
+        if (last) {
+          if (a.Res)
+            *reinterpret_cast<f32x4_t*>(a.Res + ((long)g * a.B + r0 + rr) * d + col) = f32x4_t{r_0, r_1, r_2, r_3};
+        } else {
+          lds_put4(Rs, rr, col, drb, r_0, r_1, r_2, r_3);
+          if (MODE == 2)
+            *reinterpret_cast<ushort4*>(a.Rsave + (((long)g * a.T + it) * a.B + r0 + rr) * d + col) =
+                make_ushort4(f2bf(r_0), f2bf(r_1), f2bf(r_2), f2bf(r_3));
+        }
       }
-    }
     if (last) break;
     __syncthreads();
-    // ---- phase 2: Z[16, n_w] = Res[16, d] x D^T[d, n_w]; lane gets Z[row][ncol 4q..4q+3],
+    // ---- phase 2: Z[R, n_w] = Res[R, d] x D^T[d, n_w]; lane gets Z[16 u + row][ncol 4q..4q+3],
     // in PH column passes (n_w / PH tiles each) so the accumulators of wide n fit beside the
     // fp32 iterates
     const float mo = a.mom[it];
     const bool final_iter = it + 1 == a.T;
 #pragma unroll
     for (int h = 0; h < PH; ++h) {
-      f32x4_t Z[NW / PH];
+      f32x4_t Z[RT][NW / PH];
 #pragma unroll
-      for (int t = 0; t < NW / PH; ++t) Z[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < RT; ++u)
+#pragma unroll
+        for (int t = 0; t < NW / PH; ++t) Z[u][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
       for (int k0 = 0; k0 < d; k0 += 32) {
-        const bf16x8_t fr = lds_frag(Rs, row, k0 + 8 * q, drb);
+        bf16x8_t fr[RT];
+#pragma unroll
+        for (int u = 0; u < RT; ++u) fr[u] = lds_frag(Rs, u * FR + row, k0 + 8 * q, drb);
 #pragma unroll
         for (int t = 0; t < NW / PH; ++t) {
           const int tile = (nbase >> 4) + h * (NW / PH) + t;
           const bf16x8_t fd =
               *reinterpret_cast<const bf16x8_t*>(D + ((long)tile * (d >> 5) + (k0 >> 5)) * 512 + lane * 8);
-          Z[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd, fr, Z[t], 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < RT; ++u) Z[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fd, fr[u], Z[u][t], 0, 0, 0);
         }
       }
       // ---- FISTA update (fp32): Y += eta Z; A = relu(Y - eta lambda); Y = A + mom (A - A_prev)
 #pragma unroll
-      for (int t = 0; t < NW / PH; ++t) {
-        const int tt = h * (NW / PH) + t;
-        f32x4_t an;
-        if (a.mode == 0) {
+      for (int u = 0; u < RT; ++u)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float y = Y[tt][r] + eta * Z[t][r];
-            an[r] = fmaxf(y - thr, 0.f);
-            Y[tt][r] = an[r] + (an[r] - Ap[tt][r]) * mo;
+        for (int t = 0; t < NW / PH; ++t) {
+          const int tt = h * (NW / PH) + t;
+          const int rr = u * FR + row;
+          f32x4_t an;
+          if constexpr (MODE != 1) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float y = Y[u][tt][r] + eta * Z[u][t][r];
+              an[r] = fmaxf(y - thr, 0.f);
+              Y[u][tt][r] = an[r] + (an[r] - Ap[u][tt][r]) * mo;
+            }
+            Ap[u][tt] = an;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float c = Y[u][tt][r];
+              const float gr = (c > 0.f ? lsc : 0.f) - a.gscale * Z[u][t][r];
+              const float bu = mo * Ap[u][tt][r] + gr;
+              Ap[u][tt][r] = bu;
+              an[r] = fmaxf(c - eta * bu, 0.f);
+              Y[u][tt][r] = an[r];
+            }
           }
-          Ap[tt] = an;
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float c = Y[tt][r];
-            const float gr = (c > 0.f ? lsc : 0.f) - a.gscale * Z[t][r];
-            const float bu = mo * Ap[tt][r] + gr;
-            Ap[tt][r] = bu;
-            an[r] = fmaxf(c - eta * bu, 0.f);
-            Y[tt][r] = an[r];
+          const int col = nbase + tt * 16 + 4 * q;
+          // the next phase 1 multiplies Y -- or, after the last iteration, A
+          const f32x4_t& nxt = final_iter ? an : Y[u][tt];
+          lds_put4(Ybf, rr, col, nrb, nxt[0], nxt[1], nxt[2], nxt[3]);
+          if constexpr (MODE == 2) {
+            const long o = (((long)g * a.T + it) * a.B + r0 + rr) * n + col;
+            *reinterpret_cast<ushort4*>(a.Asave + o) = make_ushort4(f2bf(an[0]), f2bf(an[1]), f2bf(an[2]), f2bf(an[3]));
+            if (!final_iter)  // Y_{it+1} -> slot it + 1
+              *reinterpret_cast<ushort4*>(a.Ysave + o + (long)a.B * n) =
+                  make_ushort4(f2bf(Y[u][tt][0]), f2bf(Y[u][tt][1]), f2bf(Y[u][tt][2]), f2bf(Y[u][tt][3]));
           }
         }
-        const int col = nbase + tt * 16 + 4 * q;
-        // the next phase 1 multiplies Y -- or, after the last iteration, A
-        const f32x4_t& nxt = final_iter ? an : Y[tt];
-        lds_put4(Ybf, row, col, nrb, nxt[0], nxt[1], nxt[2], nxt[3]);
-        if (a.Asave) {
-          const long o = (((long)g * a.T + it) * a.B + r0 + row) * n + col;
-          *reinterpret_cast<ushort4*>(a.Asave + o) = make_ushort4(f2bf(an[0]), f2bf(an[1]), f2bf(an[2]), f2bf(an[3]));
-          if (!final_iter)  // Y_{it+1} -> slot it + 1
-            *reinterpret_cast<ushort4*>(a.Ysave + o + (long)a.B * n) =
-                make_ushort4(f2bf(Y[tt][0]), f2bf(Y[tt][1]), f2bf(Y[tt][2]), f2bf(Y[tt][3]));
-        }
-      }
     }
     __syncthreads();
   }
   // write the solution A
 #pragma unroll
-  for (int t = 0; t < NW; ++t) {
-    const int col = nbase + t * 16 + 4 * q;
-    *reinterpret_cast<f32x4_t*>(a.A + ((long)g * a.B + r0 + row) * n + col) = a.mode ? Y[t] : Ap[t];
-  }
+  for (int u = 0; u < RT; ++u)
+#pragma unroll
+    for (int t = 0; t < NW; ++t) {
+      const int col = nbase + t * 16 + 4 * q;
+      *reinterpret_cast<f32x4_t*>(a.A + ((long)g * a.B + r0 + u * FR + row) * n + col) = MODE == 1 ? Y[u][t] : Ap[u][t];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -384,21 +411,41 @@ int sc_coef_search(const void* X, const void* D, const void* Dt, const float* A0
 static int launch_direct(const FistaArgs& a, int G, hipStream_t stream) {
   const int B = a.B, n = a.n, d = a.d;
   const int DW = d / 128, NW = n / 128;
-  const size_t lds = (size_t)FR * (2 * n + 4 * d);
-  if (lds > 160 * 1024) return 1;
-  dim3 grid(G * (B / FR));
-#define SC_F(DWV, NWV)                                                                                    \
-  if (DW == DWV && NW == NWV) {                                                                           \
-    hipFuncSetAttribute((const void*)fista_kernel<DWV, NWV>, hipFuncAttributeMaxDynamicSharedMemorySize,  \
-                        (int)lds);                                                                        \
-    hipLaunchKernelGGL((fista_kernel<DWV, NWV>), grid, dim3(FNT), lds, stream, a);                        \
+  // 32-row workgroups where the doubled fp32 state fits (NW * DW small) and the LDS does
+  // (SC_FISTA_RT1 / SC_FISTA_RT2: force the 16- / 32-row form where it is legal -- tests, A/B)
+  const bool no_rt2 = getenv("SC_FISTA_RT1") != nullptr, force_rt2 = getenv("SC_FISTA_RT2") != nullptr;
+  const size_t lds1 = (size_t)FR * (2 * n + 4 * d), lds2 = 2 * lds1;
+  const bool rt2 = !no_rt2 && B % (2 * FR) == 0 && lds2 <= 160 * 1024 &&
+                   (force_rt2 || (long)G * (B / (2 * FR)) >= 256);
+  if (lds1 > 160 * 1024) return 1;
+  const int mode = a.mode == 1 ? 1 : (a.Ysave ? 2 : 0);
+#define SC_FK(DWV, NWV, RTV, MV, LDS)                                                                     \
+  {                                                                                                       \
+    hipFuncSetAttribute((const void*)fista_kernel<DWV, NWV, RTV, MV>,                                     \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);                            \
+    hipLaunchKernelGGL((fista_kernel<DWV, NWV, RTV, MV>), dim3(G * (B / (RTV * FR))), dim3(FNT), LDS, stream, a); \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                       \
   }
+#define SC_F(DWV, NWV)                                                                                    \
+  if (DW == DWV && NW == NWV) {                                                                           \
+    if (mode == 1) SC_FK(DWV, NWV, 1, 1, lds1)                                                            \
+    if (mode == 2) SC_FK(DWV, NWV, 1, 2, lds1)                                                            \
+    SC_FK(DWV, NWV, 1, 0, lds1)                                                                           \
+  }
+#define SC_F2(DWV, NWV)                                                                                   \
+  if (DW == DWV && NW == NWV && rt2) {                                                                    \
+    if (mode == 1) SC_FK(DWV, NWV, 2, 1, lds2)                                                            \
+    if (mode == 2) SC_FK(DWV, NWV, 2, 2, lds2)                                                            \
+    SC_FK(DWV, NWV, 2, 0, lds2)                                                                           \
+  }
+  SC_F2(2, 2) SC_F2(2, 4) SC_F2(4, 4) SC_F2(8, 4)
   SC_F(2, 2) SC_F(2, 4) SC_F(2, 8) SC_F(2, 16)
   SC_F(4, 4) SC_F(4, 8) SC_F(4, 16)
   SC_F(6, 6) SC_F(6, 12)
   SC_F(8, 4) SC_F(8, 8) SC_F(8, 16)
 #undef SC_F
+#undef SC_F2
+#undef SC_FK
   return 2;  // shape not instantiated: caller falls back to the torch path
 }
 

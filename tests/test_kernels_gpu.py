@@ -347,13 +347,19 @@ def test_fused_topk_matches_autograd(decode):
         assert agree.float().mean() > 0.97, agree.float().mean()
 
 
-@pytest.mark.parametrize("form", ["direct", "gram"])
-@pytest.mark.parametrize("G,B,n,d", [(2, 64, 512, 512), (3, 32, 2048, 512), (1, 48, 1024, 1024), (2, 256, 512, 1024)])
-def test_fista_kernel_matches_oracle(G, B, n, d, form):
+@pytest.mark.parametrize("form", ["direct", "gram", "direct_rt2"])
+@pytest.mark.parametrize("G,B,n,d", [(2, 64, 512, 512), (3, 32, 2048, 512), (1, 48, 1024, 1024), (2, 256, 512, 1024),
+                                     (2, 64, 256, 256), (2, 64, 512, 256)])
+def test_fista_kernel_matches_oracle(G, B, n, d, form, monkeypatch):
     from sparse_coding__amd.ops import fista as F
 
     if form == "gram" and n not in F.GRAM_N:
         pytest.skip("gram form instantiated for n <= 1024")
+    if form == "direct_rt2":  # the 32-row workgroups (instantiated for n/128 <= 4, d/128 in 2, 4, 8)
+        if B % 32 or (d // 128, n // 128) not in {(2, 2), (2, 4), (4, 4), (8, 4)}:
+            pytest.skip("no 32-row variant for this shape")
+        monkeypatch.setenv("SC_FISTA_RT2", "1")
+        form = "direct"
 
     torch.manual_seed(8)
     D = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1)
