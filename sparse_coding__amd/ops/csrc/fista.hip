@@ -466,6 +466,17 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
     else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                        \
   }
+  static const int alt = getenv("SC_FISTA_GRAM_ALT") ? atoi(getenv("SC_FISTA_GRAM_ALT")) : 0;
+  // A/B knob: eight column passes with a 4- / 8-deep Gm ring (fewer accumulators live, more LDS
+  // re-reads of Y): 14.2 / 15.3 ms vs 12.9 ms for the default (4 passes, ring 2) -- kept off
+  if (n == 1024 && two && alt == 1) {
+    hipLaunchKernelGGL((fista_gram_kernel<8, 2, 8, 4>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
+  if (n == 1024 && two && alt == 2) {
+    hipLaunchKernelGGL((fista_gram_kernel<8, 2, 8, 8>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T);
+    return hipGetLastError() == hipSuccess ? 0 : 3;
+  }
   SC_G(2, 1, 4, 1, 4) SC_G(4, 1, 4, 1, 8) SC_G(6, 2, 2, 2, 4) SC_G(8, 4, 2, 2, 4)
 #undef SC_G
   return 2;
