@@ -234,13 +234,11 @@ class FusedSAEEnsemble:
         """The kernels' input: ``x`` itself, or its per-model centred copy for tied SAEs
         with non-identity centering (threshold SAEs: x - centering, learned)."""
         if self.kind == "threshold":
-            torch.sub(x.unsqueeze(0), self.params["centering"].unsqueeze(1), out=self._xr)
-            self.x_c.copy_(self._xr)
+            self._center_rows(x, self.params["centering"])
             torch.mul(self.params["activation_scale"], self.params["activation_scale"], out=self.s2)
             return self.x_c
         if self.learned_center:
-            torch.sub(x.unsqueeze(0), self.params["center"].unsqueeze(1), out=self._xr)
-            self.x_c.copy_(self._xr)
+            self._center_rows(x, self.params["center"])
             return self.x_c
         if self.centering is None:
             return x
@@ -250,6 +248,17 @@ class FusedSAEEnsemble:
         self._xr.mul_(c["scale"])
         self.x_c.copy_(self._xr)
         return self.x_c
+
+    def _center_rows(self, x, c):
+        """x_c[g] = bf16(x - c[g]) in one elementwise kernel (csrc/elementwise.hip)."""
+        from ..ops import _lib
+
+        G, B, d = self.x_c.shape
+        if x.dtype != torch.bfloat16 or tuple(x.shape) != (B, d) or not x.is_contiguous():
+            raise ValueError("centred input needs the contiguous bf16 [B, d] batch")
+        rc = _lib.lib().sc_center_rows(_lib.ptr(x), _lib.ptr(c.contiguous()), _lib.ptr(self.x_c), G, B, d,
+                                       _lib.stream_handle())
+        _lib.check(rc, "sc_center_rows")
 
     def _x_bf16(self, batch):
         if batch.dtype != torch.bfloat16:
@@ -431,16 +440,25 @@ class FusedSAEEnsemble:
                 torch.sum(self.dotpart, dim=1, out=self._gsum)
             g_s = self._gsum * s * (2.0 * a)
             upd = (("activation_scale", g_s), ("centering", g_c))
-        t = self.step_dev.float() + 1.0
         b1, b2 = self.betas
-        bc1 = 1.0 - torch.pow(b1, t)
-        bc2 = 1.0 - torch.pow(b2, t)
-        lr = self.lr.unsqueeze(1)
+        t = bc1 = bc2 = None
         for k, g in upd:
             p, m, v = self.params[k], self.m[k], self.v[k]
+            X = p.shape[-1]
+            if p.dim() == 2 and X % 256 == 0 and X <= 4096:
+                # one row-Adam launch per vector set (rows = models, device step counter): the
+                # torch form below is ~10 launches of tiny elementwise kernels per vector
+                adam_ops.adam_rows([dict(p=p, g=g.contiguous(), m=m, v=v, shadow=None, norms=None, norm=False)],
+                                   self.lr, self.step_count + 1, *self.betas, self.eps, rows_per_model=1,
+                                   step_dev=self.step_dev)
+                continue
+            if t is None:
+                t = self.step_dev.float() + 1.0
+                bc1 = 1.0 - torch.pow(b1, t)
+                bc2 = 1.0 - torch.pow(b2, t)
             m.mul_(b1).add_(g, alpha=1.0 - b1)
             v.mul_(b2).addcmul_(g, g, value=1.0 - b2)
-            p.sub_(lr * (m / bc1) / ((v / bc2).sqrt() + self.eps))
+            p.sub_(self.lr.unsqueeze(1) * (m / bc1) / ((v / bc2).sqrt() + self.eps))
 
     def _host_step(self):
         if self._counted:

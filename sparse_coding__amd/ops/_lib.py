@@ -68,6 +68,7 @@ def _declare(lib):
         "sc_fista": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                      c_void_p],
+        "sc_center_rows": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
         "sc_synth_codes": [c_void_p, c_void_p, c_long, c_int, C.c_ulonglong, C.c_ulonglong, c_void_p],
         "sc_coef_search": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p],
