@@ -14,6 +14,12 @@
 #   pmc        three rocprofv3 --pmc passes over scripts/prof_step_kernels.py
 #   lab        scripts/gemm_lab.py (LAB_ARGS env passes flags)
 #   py:FILE    python -u FILE (PY_ARGS env passes flags), e.g. py:scripts/kernel_bench.py
+#   ab         alternating A/B of one env knob: AB_CMD (a python command line printing one JSON
+#              line), AB_VAR (env variable), AB_VALUES (space-separated), AB_ROUNDS (default 2);
+#              every run appends to gpurun_out/ab/<value>.jsonl, then a ms_per_step summary.
+#              e.g. AB_CMD="scripts/bench_configs.py topk --steps 40" AB_VAR=SC_TOPK_RU AB_VALUES="4 8"
+#   ktest:K    pytest tests/test_kernels_gpu.py tests/test_train_gpu.py -k K
+#   profile:CMD  rocprofv3 --kernel-trace --stats of "python3 CMD" (top-20 summary)
 # Extra bench flags: BENCH_ARGS env.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -61,6 +67,27 @@ PY
       python3 scripts/pmc_summary.py gpurun_out/pmc > "$O/pmc_summary.md" && cat "$O/pmc_summary.md" ;;
     lab)
       timeout -k 10 400 python -u scripts/gemm_lab.py ${LAB_ARGS} > "$O/gemm_lab.log" 2>&1; local rc=$?; cat "$O/gemm_lab.log"; return $rc ;;
+    ab)
+      mkdir -p "$O/ab"
+      for r in $(seq 1 "${AB_ROUNDS:-2}"); do
+        for v in ${AB_VALUES}; do
+          env "${AB_VAR}=$v" timeout -k 10 300 python ${AB_CMD} >> "$O/ab/$v.jsonl" 2>> "$O/ab/err.log" || { tail -20 "$O/ab/err.log"; return 1; }
+        done
+      done
+      grep -o '"ms_per_step": [0-9.]*\|"solve_ms_all_models": [0-9.]*' "$O"/ab/*.jsonl ;;
+    ktest:*)
+      timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_train_gpu.py -x -q --timeout 300 --timeout-method thread -k "${s#ktest:}" > "$O/ktest.log" 2>&1
+      local rc=$?; tail -15 "$O/ktest.log"; return $rc ;;
+    profile:*)
+      rm -rf "$O/profile"
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/profile" -o run --output-format csv -- python3 $R/${s#profile:} > "$O/profile.log" 2>&1) || { tail -20 "$O/profile.log"; return 1; }
+      python3 - > "$O/profile_summary.txt" <<'PY' || return 1
+import csv, glob
+f = glob.glob("gpurun_out/profile/**/*kernel_stats.csv", recursive=True)[0]
+for r in list(csv.DictReader(open(f)))[:20]:
+    print(f"{r['Name'][:90]:90s} {r['Calls']:>5} {float(r['AverageNs'])/1e3:9.2f}us {float(r['Percentage']):6.2f}%")
+PY
+      cat "$O/profile_summary.txt" ;;
     py:*)
       local f="${s#py:}"
       timeout -k 10 600 python -u "$f" ${PY_ARGS} > "$O/$(basename "$f" .py).log" 2>&1; local rc=$?
