@@ -614,8 +614,12 @@ __global__ __launch_bounds__(256) void topk_block_kernel(const float* __restrict
 // every lane accumulates 16 partial dots, four exchange steps (8, 4, 2, 1) leave lane
 // L with dot j = L & 15 summed over its 16-lane group, two more finish the wave --
 // 17 shuffles per 16 dots instead of 6 per dot.
-template <int NV, int RU = (NV <= 3 ? 8 : 4)>  // d <= 256 * NV; RU gathered rows per iteration
-__global__ __launch_bounds__(256) void topk_decode_grad_kernel(
+// OCC: minimum waves per SIMD requested from the register allocator (0: compiler's choice);
+// DOTS: code gradients reduced per butterfly round (16 rows in flight, or 8 for fewer registers)
+// (A/B on config 4, d = 768: 4 waves/SIMD with 16 dots 1.19 ms/step vs 1.32 at the compiler's
+// 2 waves; 5-6 waves need 8 dots or spill, and both lose: 1.20-1.23 ms)
+template <int NV, int RU = (NV <= 3 ? 8 : 4), int OCC = (NV == 3 ? 4 : 0), int DOTS = 16>
+__global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
     const int* __restrict__ idx, const float* __restrict__ val, const int* __restrict__ kv,
     const uint16_t* __restrict__ D, const uint16_t* __restrict__ X, long sx, uint16_t* __restrict__ R,
     float* __restrict__ row_se, uint16_t* __restrict__ codebuf, uint16_t* __restrict__ dscbuf, int G, int B,
@@ -688,10 +692,10 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
   // code gradients (units of R): dscore_j = 1[v_j > 0] <R, D[idx_j]>; scatter code and dscore
   uint16_t* Cb = codebuf + row * (long)n;
   uint16_t* Sb = dscbuf + row * (long)n;
-  for (int j0 = 0; j0 < k; j0 += 16) {
-    float p[16];
+  for (int j0 = 0; j0 < k; j0 += DOTS) {
+    float p[DOTS];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < DOTS; ++u) {
       const int j = j0 + u;
       const int ij = j < k ? I[j] : 0;
       const uint16_t* Dr = Dg + (long)ij * d;
@@ -705,9 +709,9 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
       }
       p[u] = dot;
     }
-    // butterfly reduce-scatter over lane bits 3..0: lane L keeps index L & 15
+    // butterfly reduce-scatter over lane bits log2(DOTS)-1 .. 0: lane L keeps index L % DOTS
 #pragma unroll
-    for (int sft = 8; sft >= 1; sft >>= 1) {
+    for (int sft = DOTS / 2; sft >= 1; sft >>= 1) {
       const bool upper = (lane & sft) != 0;
 #pragma unroll
       for (int t = 0; t < sft; ++t) {
@@ -717,10 +721,10 @@ __global__ __launch_bounds__(256) void topk_decode_grad_kernel(
       }
     }
     float dot = p[0];
-    dot += __shfl_xor(dot, 16, 64);
-    dot += __shfl_xor(dot, 32, 64);
-    const int j = j0 + (lane & 15);
-    if (lane < 16 && j < k) {
+#pragma unroll
+    for (int b = DOTS; b < 64; b <<= 1) dot += __shfl_xor(dot, b, 64);
+    const int j = j0 + (lane & (DOTS - 1));
+    if (lane < DOTS && j < k) {
       const float w = V[j];
       if (w > 0.f) {
         const int c = I[j];
@@ -806,6 +810,24 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
       row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   static const int ru = getenv("SC_TOPK_RU") ? atoi(getenv("SC_TOPK_RU")) : 0;
+  static const int occ = getenv("SC_TOPK_OCC") ? atoi(getenv("SC_TOPK_OCC")) : 0;
+#define SC_DO(RUV, OCCV, DV)                                                                              \
+  {                                                                                                       \
+    hipLaunchKernelGGL((topk_decode_grad_kernel<3, RUV, OCCV, DV>), grid, dim3(256), 0, stream, idx, val, k,  \
+                       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,    \
+                       reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),      \
+                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax);                            \
+    return hipGetLastError() == hipSuccess ? 0 : 3;                                                       \
+  }
+  if (nv == 3 && occ) {  // A/B knob: cap registers for more resident waves (SC_TOPK_OCC = waves / SIMD)
+    if (occ == 3) SC_DO(8, 3, 16)
+    if (occ == 4) SC_DO(8, 4, 16)
+    if (occ == 5) SC_DO(8, 5, 8)
+    if (occ == 6) SC_DO(4, 6, 8)
+    if (occ == 48) SC_DO(8, 4, 8)
+    if (occ == 44) SC_DO(4, 4, 8)
+  }
+#undef SC_DO
   if (nv == 3 && ru == 16) {  // A/B knob (SC_TOPK_RU): 8 rows per iteration is the default for d <= 768
     hipLaunchKernelGGL((topk_decode_grad_kernel<3, 16>), grid, dim3(256), 0, stream, idx, val, k,
                        reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,
