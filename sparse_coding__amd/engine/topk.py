@@ -61,6 +61,7 @@ class FusedTopKEnsemble:
         import os
 
         self.wg_split = int(os.environ.get("SC_TOPK_WSPLIT", "1"))
+        self.wg_cfg = int(os.environ["SC_TOPK_WCFG"]) if os.environ.get("SC_TOPK_WCFG") else None
         self.g_all = torch.empty(self.wg_split, G, n, d, device=dev)
         self.g = self.g_all[0]
         self.idx = self.val = None
@@ -92,6 +93,9 @@ class FusedTopKEnsemble:
         if self.wg_split > 1:
             gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g_all], 2.0 / (B * d),
                                   ksplit=self.wg_split)
+        elif self.wg_cfg is not None:  # A/B knob SC_TOPK_WCFG: block shape of the weight gradient
+            with gemm_ops.force_shape(self.wg_cfg):
+                gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g], 2.0 / (B * d))
         else:
             gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g], 2.0 / (B * d))
         topk_ops.clear(self.idx, self.codebuf, self.dscbuf)

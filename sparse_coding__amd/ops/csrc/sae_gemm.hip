@@ -66,10 +66,17 @@ struct ScAdamEpi {
 };
 
 
-// Block shape chosen by sc_gemm when cfg == 0: the largest tile that divides the
-// problem and still gives at least one block per CU (256 CUs on MI355X).
+// Block shape chosen by sc_gemm when cfg == 0: the largest tile that divides the problem,
+// gives at least one block per CU (256 CUs on MI355X) and does not end on a mostly idle last
+// wave of blocks -- 256x256 runs one block per CU, 128x128 two: the larger tile must fill
+// its waves at least as well (within 10 %) as 128x128 would.  (Top-k weight gradient,
+// 576 blocks of 256x256 = 2.25 waves: 128x128 measured 1.165 vs 1.201 ms/step.)
+static double wave_fill(long blocks, long slots) { return (double)blocks / (double)(slots * ((blocks + slots - 1) / slots)); }
 int sc_gemm_shape(int M, int N, int G, int nprob) {
-  if (fits<S256>(M, N) && n_blocks<S256>(M, N, G, nprob) >= 256) return 3;
+  if (fits<S256>(M, N) && n_blocks<S256>(M, N, G, nprob) >= 256) {
+    const double f128 = wave_fill(n_blocks<S128>(M, N, G, nprob), 512);
+    return wave_fill(n_blocks<S256>(M, N, G, nprob), 256) >= f128 - 0.1 ? 3 : 1;  // (256x128 measured slower)
+  }
   if (fits<S256x128>(M, N) && n_blocks<S256x128>(M, N, G, nprob) >= 256) return 2;
   return 1;
 }
