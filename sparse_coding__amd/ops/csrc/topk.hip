@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
     const int* __restrict__ idx, const float* __restrict__ val, const int* __restrict__ kv,
     const uint16_t* __restrict__ D, const uint16_t* __restrict__ X, long sx, uint16_t* __restrict__ R,
     float* __restrict__ row_se, uint16_t* __restrict__ codebuf, uint16_t* __restrict__ dscbuf, int G, int B,
-    int n, int d, int kmax) {
+    int n, int d, int kmax, float* __restrict__ dscv) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)G * B) return;
@@ -731,8 +731,71 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
         Cb[c] = f2bf(w);
         Sb[c] = f2bf(dot);
       }
+      // per-slot fp32 code gradient for the sparse weight gradient (0 where the code is off)
+      if (dscv) dscv[row * kmax + j] = w > 0.f ? dot : 0.f;
     }
   }
+}
+
+// Sparse weight gradient for top-k dictionaries with small k / n (the dense GEMM would multiply
+// mostly zeros): for dictionary row j of model g,
+//   G[g, j, :] = alpha * sum over the slots (b, s) that picked j of  val * R[g, b, :] + dscv * X[b, :]
+// Slot lists come from a stable sort of the picked indices (deterministic summation order).
+// One wave per dictionary row; rows nobody picked get zeros (Adam reads every row).
+template <int NV>  // d == 256 * NV
+__global__ __launch_bounds__(256) void topk_sparse_wgrad_kernel(const long* __restrict__ perm, const int* __restrict__ offs,
+                                                                const float* __restrict__ val,
+                                                                const float* __restrict__ dscv,
+                                                                const uint16_t* __restrict__ R,
+                                                                const uint16_t* __restrict__ X, long sx,
+                                                                float* __restrict__ Gout, int Gs, int B, int n, int kmax,
+                                                                float alpha) {
+  constexpr int d = NV * 256;
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)Gs * n) return;
+  const int g = (int)(row / n);
+  const int beg = offs[row], end = offs[row + 1];
+  float acc[NV * 4];
+#pragma unroll
+  for (int e = 0; e < NV * 4; ++e) acc[e] = 0.f;
+  for (int e0 = beg; e0 < end; e0 += 2) {  // two slots in flight
+    long slot[2];
+    float cv[2], sv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool ok = e0 + u < end;
+      slot[u] = ok ? perm[e0 + u] : perm[beg];
+      cv[u] = ok ? val[slot[u]] : 0.f;
+      sv[u] = ok ? dscv[slot[u]] : 0.f;
+    }
+    ushort4 hr[2][NV], hx[2][NV];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int b = (int)((slot[u] / kmax) % B);
+      const uint16_t* Rr = R + ((long)g * B + b) * d;
+      const uint16_t* Xr = X + (long)g * sx + (long)b * d;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        hr[u][v] = *reinterpret_cast<const ushort4*>(Rr + (v * 64 + lane) * 4);
+        hx[u][v] = *reinterpret_cast<const ushort4*>(Xr + (v * 64 + lane) * 4);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        acc[v * 4 + 0] += cv[u] * bf2f(hr[u][v].x) + sv[u] * bf2f(hx[u][v].x);
+        acc[v * 4 + 1] += cv[u] * bf2f(hr[u][v].y) + sv[u] * bf2f(hx[u][v].y);
+        acc[v * 4 + 2] += cv[u] * bf2f(hr[u][v].z) + sv[u] * bf2f(hx[u][v].z);
+        acc[v * 4 + 3] += cv[u] * bf2f(hr[u][v].w) + sv[u] * bf2f(hx[u][v].w);
+      }
+  }
+  float* Gr = Gout + row * d;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    *reinterpret_cast<float4*>(Gr + (v * 64 + lane) * 4) =
+        make_float4(alpha * acc[v * 4 + 0], alpha * acc[v * 4 + 1], alpha * acc[v * 4 + 2], alpha * acc[v * 4 + 3]);
 }
 
 __global__ __launch_bounds__(256) void topk_clear_kernel(const int* __restrict__ idx, uint16_t* __restrict__ a,
@@ -800,14 +863,14 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
 
 int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const void* D, const void* X, long sx,
                         void* R, float* row_se, void* codebuf, void* dscbuf, int G, int B, int n, int d, int kmax,
-                        hipStream_t stream) {
+                        hipStream_t stream, float* dscv) {
   if (d % 4) return 1;
   const int nv = (d + 255) / 256;
   dim3 grid(((long)G * B + 3) / 4);
 #define SC_D(V) \
   if (nv <= V) { hipLaunchKernelGGL((topk_decode_grad_kernel<V>), grid, dim3(256), 0, stream, idx, val, k, \
       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx, reinterpret_cast<uint16_t*>(R), \
-      row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax); \
+      row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   static const int ru = getenv("SC_TOPK_RU") ? atoi(getenv("SC_TOPK_RU")) : 0;
   static const int occ = getenv("SC_TOPK_OCC") ? atoi(getenv("SC_TOPK_OCC")) : 0;
@@ -816,7 +879,7 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
     hipLaunchKernelGGL((topk_decode_grad_kernel<3, RUV, OCCV, DV>), grid, dim3(256), 0, stream, idx, val, k,  \
                        reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,    \
                        reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),      \
-                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax);                            \
+                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv);                            \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                       \
   }
   if (nv == 3 && occ) {  // A/B knob: cap registers for more resident waves (SC_TOPK_OCC = waves / SIMD)
@@ -832,18 +895,32 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
     hipLaunchKernelGGL((topk_decode_grad_kernel<3, 16>), grid, dim3(256), 0, stream, idx, val, k,
                        reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,
                        reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),
-                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax);
+                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   if (nv == 3 && ru == 4) {
     hipLaunchKernelGGL((topk_decode_grad_kernel<3, 4>), grid, dim3(256), 0, stream, idx, val, k,
                        reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,
                        reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),
-                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax);
+                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   SC_D(1) SC_D(2) SC_D(3) SC_D(4) SC_D(8) SC_D(16)
 #undef SC_D
+  return 1;
+}
+
+// G[0 .. Gs) rows of the weight gradient from the sorted slot lists (see the kernel).
+int sc_topk_sparse_wgrad(const long* perm, const int* offs, const float* val, const float* dscv, const void* R,
+                         const void* X, long sx, float* Gout, int Gs, int B, int n, int d, int kmax, float alpha,
+                         hipStream_t stream) {
+  dim3 grid((unsigned)(((long)Gs * n + 3) / 4));
+#define SC_SW(V) \
+  if (d == 256 * V) { hipLaunchKernelGGL((topk_sparse_wgrad_kernel<V>), grid, dim3(256), 0, stream, perm, offs, val, dscv, \
+      reinterpret_cast<const uint16_t*>(R), reinterpret_cast<const uint16_t*>(X), sx, Gout, Gs, B, n, kmax, alpha); \
+    return hipGetLastError() == hipSuccess ? 0 : 3; }
+  SC_SW(1) SC_SW(2) SC_SW(3) SC_SW(4)
+#undef SC_SW
   return 1;
 }
 

@@ -26,16 +26,40 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
     return idx, val
 
 
-def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None):
+def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dscv=None):
     """Sparse decode + residual (bf16 r_out [G, B, d]) + per-row squared error; with the dense
-    buffers, also scatter codes and code gradients <R, D[idx]> (units of R) for the wgrad GEMM."""
+    buffers, also scatter codes and code gradients <R, D[idx]> (units of R) for the wgrad GEMM;
+    with ``dscv`` ([G, B, kmax] fp32) also the per-slot code gradients for ``sparse_wgrad``."""
     G, B, kmax = idx.shape
     n, d = D.shape[1], D.shape[2]
     sx = 0 if x.dim() == 2 else B * d
     rc = _lib.lib().sc_topk_decode_grad(_lib.ptr(idx), _lib.ptr(val), _lib.ptr(k), _lib.ptr(D), _lib.ptr(x), sx,
                                         _lib.ptr(r_out), _lib.ptr(row_se), _lib.ptr(codebuf), _lib.ptr(dscbuf),
-                                        G, B, n, d, kmax, _lib.stream_handle())
+                                        G, B, n, d, kmax, _lib.stream_handle(), _lib.ptr(dscv))
     _lib.check(rc, "sc_topk_decode_grad")
+
+
+def sparse_wgrad(idx, val, dscv, k, r, x, g_out, alpha):
+    """Weight gradient of the first Gs = g_out.shape[0] models from their picked slots only:
+    g[g, j] = alpha * sum_{(b, s): idx[g, b, s] = j, s < k[g]} val R[g, b] + dscv x[b]
+    (= codes^T R + dscores^T x of the dense path).  The slots are ordered by a stable sort of
+    (model, feature), so every row's sum has a fixed order."""
+    Gs, n, d = g_out.shape
+    _, B, kmax = idx.shape
+    dev = idx.device
+    slot = torch.arange(kmax, device=dev, dtype=torch.int32)
+    valid = slot.view(1, 1, kmax) < k[:Gs].view(Gs, 1, 1)
+    key = (torch.arange(Gs, device=dev, dtype=torch.int32).view(Gs, 1, 1) * n + idx[:Gs]).masked_fill(~valid, Gs * n)
+    key = key.reshape(-1)
+    perm = torch.argsort(key, stable=True)
+    counts = torch.bincount(key, minlength=Gs * n + 1)[: Gs * n]
+    offs = torch.zeros(Gs * n + 1, device=dev, dtype=torch.int32)
+    torch.cumsum(counts, 0, dtype=torch.int32, out=offs[1:])
+    sx = 0 if x.dim() == 2 else B * d
+    rc = _lib.lib().sc_topk_sparse_wgrad(_lib.ptr(perm), _lib.ptr(offs), _lib.ptr(val), _lib.ptr(dscv), _lib.ptr(r),
+                                         _lib.ptr(x), sx, _lib.ptr(g_out), Gs, B, n, d, kmax, float(alpha),
+                                         _lib.stream_handle())
+    _lib.check(rc, "sc_topk_sparse_wgrad")
 
 
 def clear(idx, a, b):
