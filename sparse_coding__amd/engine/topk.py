@@ -65,14 +65,14 @@ class FusedTopKEnsemble:
         # optional sparse weight gradient for the leading models whose k / n is small
         # (SC_TOPK_SPARSE_K = the largest k routed there): the dense GEMM costs the same for every
         # model, the slot-list form is proportional to k -- but one wave per dictionary row
-        # serialises the popular features (rows picked by most of the batch): A/B on config 4
-        # 12.0-16.3 ms/step vs 1.17 dense, so it stays off until rows are split across waves
+        # (A/B: profiles/README.md)
         sparse_k = int(os.environ.get("SC_TOPK_SPARSE_K", "0"))
         ks = [int(m[1]["sparsity"]) for m in models]
         gs = 0
         while gs < G and ks[gs] <= sparse_k:
             gs += 1
         self.sparse_g = gs if d % 256 == 0 and d <= 1024 else 0
+        self._ks, self._sp_cache = ks, {}
         self.dscv = torch.zeros(G, B, self.kmax, device=dev) if self.sparse_g else None
         self.g_all = torch.empty(self.wg_split, G, n, d, device=dev)
         self.g = self.g_all[0]
@@ -104,7 +104,8 @@ class FusedTopKEnsemble:
             torch.sum(self.row_se, dim=1, out=self._se)
         gs = self.sparse_g if self.decode == "gather" else 0
         if gs:
-            topk_ops.sparse_wgrad(self.idx, self.val, self.dscv, self.k, self.r, x, self.g[:gs], 2.0 / (B * d))
+            topk_ops.sparse_wgrad(self.idx, self.val, self.dscv, self._ks, self.r, x, self.g[:gs], 2.0 / (B * d),
+                                  cache=self._sp_cache)
         if gs == G:
             pass
         elif gs:

@@ -39,22 +39,33 @@ def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dsc
     _lib.check(rc, "sc_topk_decode_grad")
 
 
-def sparse_wgrad(idx, val, dscv, k, r, x, g_out, alpha):
+def sparse_wgrad(idx, val, dscv, ks, r, x, g_out, alpha, cache=None):
     """Weight gradient of the first Gs = g_out.shape[0] models from their picked slots only:
-    g[g, j] = alpha * sum_{(b, s): idx[g, b, s] = j, s < k[g]} val R[g, b] + dscv x[b]
-    (= codes^T R + dscores^T x of the dense path).  The slots are ordered by a stable sort of
-    (model, feature), so every row's sum has a fixed order."""
+    g[g, j] = alpha * sum_{(b, s): idx[g, b, s] = j, s < ks[g]} val R[g, b] + dscv x[b]
+    (= codes^T R + dscores^T x of the dense path).  ``ks``: the models' k (host ints).  The
+    slots are ordered by sorting the unique keys ((g n + j) B + b) -- a fixed summation order per
+    row without a stable sort -- and the row offsets come from a binary search over the sorted
+    keys (no histogram atomics: padding and popular features made one hot bin).  ``cache``: a
+    dict reused across calls for the step-invariant index tensors."""
     Gs, n, d = g_out.shape
     _, B, kmax = idx.shape
     dev = idx.device
-    slot = torch.arange(kmax, device=dev, dtype=torch.int32)
-    valid = slot.view(1, 1, kmax) < k[:Gs].view(Gs, 1, 1)
-    key = (torch.arange(Gs, device=dev, dtype=torch.int32).view(Gs, 1, 1) * n + idx[:Gs]).masked_fill(~valid, Gs * n)
-    key = key.reshape(-1)
-    perm = torch.argsort(key, stable=True)
-    counts = torch.bincount(key, minlength=Gs * n + 1)[: Gs * n]
-    offs = torch.zeros(Gs * n + 1, device=dev, dtype=torch.int32)
-    torch.cumsum(counts, 0, dtype=torch.int32, out=offs[1:])
+    cache = {} if cache is None else cache
+    sig = (tuple(ks[:Gs]), B, kmax, n)
+    if cache.get("sig") != sig:
+        bcol = torch.arange(B, device=dev, dtype=torch.int64).view(B, 1)
+        base, slot = [], []
+        for g in range(Gs):
+            kg = int(ks[g])
+            base.append((torch.full((B, kg), g * n, device=dev, dtype=torch.int64) * B + bcol).reshape(-1))
+            slot.append(((g * B + bcol) * kmax + torch.arange(kg, device=dev, dtype=torch.int64).view(1, kg)).reshape(-1))
+        cache.update(sig=sig, base=torch.cat(base), slot=torch.cat(slot),
+                     rows=torch.arange(Gs * n + 1, device=dev, dtype=torch.int64))
+    picks = torch.cat([idx[g, :, : int(ks[g])].reshape(-1) for g in range(Gs)]).to(torch.int64)
+    key = picks * B + cache["base"]
+    skey, order = torch.sort(key)
+    perm = cache["slot"][order]
+    offs = torch.searchsorted(skey // B, cache["rows"]).to(torch.int32)
     sx = 0 if x.dim() == 2 else B * d
     rc = _lib.lib().sc_topk_sparse_wgrad(_lib.ptr(perm), _lib.ptr(offs), _lib.ptr(val), _lib.ptr(dscv), _lib.ptr(r),
                                          _lib.ptr(x), sx, _lib.ptr(g_out), Gs, B, n, d, kmax, float(alpha),

@@ -877,9 +877,9 @@ def test_topk_sparse_wgrad_matches_dense():
     dense = torch.empty(G, n, d, device=DEV)
     GM.weight_grads([[(cb, r), (db, x)]], [dense], 1e-2)
     sparse = torch.empty(G, n, d, device=DEV)
-    T.sparse_wgrad(idx, val, dscv, k, r, x, sparse, 1e-2)
+    T.sparse_wgrad(idx, val, dscv, [3, 8, 20], r, x, sparse, 1e-2)
     sparse2 = torch.empty(G, n, d, device=DEV)
-    T.sparse_wgrad(idx, val, dscv, k, r, x, sparse2, 1e-2)
+    T.sparse_wgrad(idx, val, dscv, [3, 8, 20], r, x, sparse2, 1e-2)
     torch.cuda.synchronize()
     assert torch.equal(sparse, sparse2)  # deterministic
     for g in range(G):
