@@ -62,6 +62,7 @@ class FusedTopKEnsemble:
 
         self.wg_split = int(os.environ.get("SC_TOPK_WSPLIT", "1"))
         self.wg_cfg = int(os.environ["SC_TOPK_WCFG"]) if os.environ.get("SC_TOPK_WCFG") else None
+        self.sc_cfg = int(os.environ["SC_TOPK_SCFG"]) if os.environ.get("SC_TOPK_SCFG") else None
         # optional sparse weight gradient for the leading models whose k / n is small
         # (SC_TOPK_SPARSE_K = the largest k routed there): the dense GEMM costs the same for every
         # model, the slot-list form is proportional to k -- but one wave per dictionary row
@@ -88,7 +89,11 @@ class FusedTopKEnsemble:
     def step_batch(self, batch):
         x = batch.to(self.device, torch.bfloat16).contiguous()
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
-        gemm_ops.matmul_nt(x, self.shadow, self.scores)
+        if self.sc_cfg is not None:  # A/B knob SC_TOPK_SCFG: block shape of the scores GEMM
+            with gemm_ops.force_shape(self.sc_cfg):
+                gemm_ops.matmul_nt(x, self.shadow, self.scores)
+        else:
+            gemm_ops.matmul_nt(x, self.shadow, self.scores)
         self.idx, self.val = topk_ops.topk_select(self.scores, self.k, self.kmax)
         if self.decode == "gemm":
             # dense-GEMM decode: scatter the codes, R = codes D_hat - x (decoder-epilogue GEMM,
