@@ -51,7 +51,7 @@ class FusedSAEEnsemble:
 
     def __init__(self, models, sig, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999),
                  eps=1e-8, track_feature_counts=True, kind: Optional[str] = None, fuse_adam: bool = False,
-                 count_every: int = 8, wgrad_split="auto"):
+                 count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
         # FunctionalTiedCenteredSAE (sae_ensemble.py:162-228): the tied kernels on x - center
@@ -186,6 +186,16 @@ class FusedSAEEnsemble:
         self.g_parts = (torch.empty(nprob, self.wsplit, G, n, d, device=dev, dtype=torch.float32)
                         if self.wsplit > 1 else None)
         self._g_from_parts = False
+        # bf16 weight gradients for the single-device step (``grad_dtype='bf16'``, or env
+        # SC_GRAD_DTYPE): the weight-gradient GEMM's bf16 epilogue and Adam's bf16-gradient loads
+        # halve the gradient's HBM round trip; masters, moments and the update stay fp32.
+        # Data-parallel paths keep the fp32 flat buffers (their all-reduce reads those).
+        gdt = grad_dtype or os.environ.get("SC_GRAD_DTYPE", "fp32")
+        if gdt not in ("fp32", "bf16"):
+            raise ValueError(f"grad_dtype must be 'fp32' or 'bf16', got {gdt!r}")
+        self.g_bf = (torch.empty(nprob, G, n, d, device=dev, dtype=bf)
+                     if gdt == "bf16" and self.wsplit == 1 else None)
+        self._g_from_bf = False
         self.grad_scale = 1.0  # data parallel: 1 / world_size (gradients are then summed)
         self.enc_part = torch.zeros(G, tm * (n // 128), 2, device=dev)
         self.dec_part = torch.zeros(G, tm * (d // 128), device=dev)
@@ -319,7 +329,7 @@ class FusedSAEEnsemble:
 
     def wgrad_first(self, x):
         """Untied: dW_hat = c^T R (decoder).  Tied: the whole dictionary gradient + bias grad."""
-        self._g_from_parts = False
+        self._g_from_parts = self._g_from_bf = False
         if self.kind == "untied":
             gemm_ops.weight_grads([[(self.c, self.r)]], [self.g_dec], self._alpha, nactive=self.nactive)
         else:
@@ -356,20 +366,23 @@ class FusedSAEEnsemble:
             return
         split = self.g_parts is not None
         self._g_from_parts = split
+        self._g_from_bf = gbf = self.g_bf is not None
         if self.kind == "untied":
-            outs = [self.g_parts[0], self.g_parts[1]] if split else [self.g_dec, self.g_enc]
+            outs = ([self.g_parts[0], self.g_parts[1]] if split else
+                    [self.g_bf[0], self.g_bf[1]] if gbf else [self.g_dec, self.g_enc])
             gemm_ops.weight_grads([[(self.c, self.r)], [(self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit,
                                   nactive=self.nactive)
         else:
-            outs = [self.g_parts[0]] if split else [self.g_dec]
+            outs = [self.g_parts[0]] if split else [self.g_bf[0]] if gbf else [self.g_dec]
             gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit,
                                   nactive=self.nactive)
 
     def _adam_sets(self):
         parts = self._g_from_parts
-        g_dec = self.g_parts[0, 0] if parts else self.g_dec
+        gbf = self._g_from_bf
+        g_dec = self.g_parts[0, 0] if parts else self.g_bf[0] if gbf else self.g_dec
         if self.kind == "untied":
-            g_enc = self.g_parts[1, 0] if parts else self.g_enc
+            g_enc = self.g_parts[1, 0] if parts else self.g_bf[1] if gbf else self.g_enc
             return [dict(p=self.params["decoder"], g=g_dec, m=self.m["decoder"], v=self.v["decoder"],
                          shadow=self.dec_shadow, norms=self.norms, norm=True),
                     dict(p=self.params["encoder"], g=g_enc, m=self.m["encoder"], v=self.v["encoder"],

@@ -23,7 +23,7 @@ from ..ops import topk as topk_ops
 
 class FusedTopKEnsemble:
     def __init__(self, models, sig=None, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999), eps=1e-8,
-                 decode: str = "gather"):
+                 decode: str = "gather", grad_dtype: str | None = None):
         from ..models.topk import TopKEncoder
 
         self.sig = sig or TopKEncoder
@@ -75,7 +75,14 @@ class FusedTopKEnsemble:
         self.sparse_g = gs if d % 256 == 0 and d <= 1024 else 0
         self._ks, self._sp_cache = ks, {}
         self.dscv = torch.zeros(G, B, self.kmax, device=dev) if self.sparse_g else None
-        self.g_all = torch.empty(self.wg_split, G, n, d, device=dev)
+        # bf16 dictionary gradient (default; ``grad_dtype`` / env SC_GRAD_DTYPE): the weight-gradient
+        # GEMM's bf16 epilogue + Adam's bf16-gradient loads (dense GEMM path, no split-K).  Config 4
+        # A/B: 1.178 -> 1.133 ms/step (profiles/grad_dtype_ab_r2.json); Adam math stays fp32
+        gdt = grad_dtype or os.environ.get("SC_GRAD_DTYPE", "bf16")
+        if gdt not in ("fp32", "bf16"):
+            raise ValueError(f"grad_dtype must be 'fp32' or 'bf16', got {gdt!r}")
+        gbf = gdt == "bf16" and self.wg_split == 1 and not self.sparse_g
+        self.g_all = torch.empty(self.wg_split, G, n, d, device=dev, dtype=bf if gbf else torch.float32)
         self.g = self.g_all[0]
         self.idx = self.val = None
         # decode: "gather" (sparse, one wave per row) or "gemm" (dense codes through the decoder and

@@ -51,7 +51,7 @@ def _declare(lib):
                          C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
                          C.POINTER(c_int), C.POINTER(c_int), c_int, c_int, c_void_p,
                          c_float, c_float, c_float, c_float, c_float, c_void_p, c_int, c_long, c_long, c_void_p,
-                         c_void_p],
+                         c_void_p, c_int],
         "sc_shadow_rows": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p],
         "sc_bias_loss": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                          c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

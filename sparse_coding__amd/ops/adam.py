@@ -17,7 +17,8 @@ def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, s
               gstride=0, row0=0, live=None):
     """Fused row-wise Adam over one or two parameter sets.
 
-    sets: list of dicts with keys p, g, m, v (fp32 [G, n, d]), shadow (bf16 [G, n, d] or None),
+    sets: list of dicts with keys p, g, m, v (fp32 [G, n, d]; ``g`` may instead be bf16 -- then
+    every set's must be), shadow (bf16 [G, n, d] or None),
     norms (fp32 [G, n] or None), norm (bool: parameter is row-normalised inside the loss).
     lr: fp32 tensor [G] (per-model learning rate); step: 1-based Adam step (host value), or
     ``step_dev``: int32 device counter of completed steps (the kernel uses ``*step_dev + 1``;
@@ -34,17 +35,20 @@ def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, s
     d = shp[-1]
     nrows = sets[0]["p"].numel() // d
     n = shp[1] if len(shp) == 3 else None
+    gbf16 = sets[0]["g"].dtype == torch.bfloat16
+    gsize = 2 if gbf16 else 4
     for s in sets:
         for k in ("p", "g", "m", "v"):
             t = s[k]
-            if t.dtype != torch.float32 or tuple(t.shape) != shp or not t.is_contiguous():
-                raise ValueError(f"adam set tensor {k} must be contiguous fp32 {shp}")
+            want = torch.bfloat16 if (k == "g" and gbf16) else torch.float32
+            if t.dtype != want or tuple(t.shape) != shp or not t.is_contiguous():
+                raise ValueError(f"adam set tensor {k} must be contiguous {want} {shp} (bf16 gradients: all sets)")
         if s.get("shadow") is not None and (s["shadow"].dtype != torch.bfloat16 or s["shadow"].numel() != nrows * d):
             raise ValueError("shadow must be bf16 of the parameter's size")
         if s.get("norms") is not None and s["norms"].numel() != nrows:
             raise ValueError("norms must have one entry per row")
         if nsplit > 1 and s["g"].untyped_storage().nbytes() < (s["g"].storage_offset() + (nsplit - 1) * gstride
-                                                               + nrows * d) * 4:
+                                                               + nrows * d) * gsize:
             raise ValueError("gradient storage too small for nsplit slabs")
     rpm = rows_per_model or n
     if not rpm:
@@ -59,6 +63,7 @@ def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, s
         _vp([s.get("shadow") for s in sets]), _vp([s.get("norms") for s in sets]),
         rows, norm, d, rpm, _lib.ptr(lr), b1, b2, eps, bc1, bc2,
         _lib.ptr(step_dev), int(nsplit), int(gstride), int(row0), _lib.stream_handle(), _lib.ptr(live),
+        int(gbf16),
     )
     _lib.check(rc, "sc_adam_rows")
 

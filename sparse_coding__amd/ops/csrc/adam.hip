@@ -18,7 +18,7 @@ namespace scamd {
 
 struct AdamRows {
   float* p;         // [rows][d] fp32 master
-  const float* g;   // [rows][d] gradient (w.r.t. the normalised row if norm)
+  const void* g;    // [rows][d] gradient (w.r.t. the normalised row if norm): fp32, or bf16 (GBF)
   float* m;
   float* v;
   uint16_t* shadow; // [rows][d] bf16 copy for the GEMMs (normalised if norm)
@@ -51,7 +51,10 @@ __device__ __forceinline__ void bias_corrections(float b1, float b2, int t, floa
 // NT: the fp32 state (p, m, v) is written with non-temporal stores and the gradient read with
 // non-temporal loads -- none of it is touched again this step, so it should not displace the
 // next GEMMs' operands from L2 / MALL or leave dirty lines for them to write back.
-template <int NV, bool NT = false>
+// GBF: the gradient arrives in bf16 (the weight-gradient GEMM's bf16 epilogue): 1/7 of the
+// kernel's HBM bytes less to read and half the GEMM's output stores; the moments, the master
+// and the update arithmetic stay fp32.
+template <int NV, bool NT = false, bool GBF = false>
 __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   const int lane = threadIdx.x & 63;
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -70,7 +73,8 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   const float lr = a.lr[grow / a.rows_per_model];
   // NV float4 chunks per lane (d == 256 * NV); compile-time so pv/gv stay in VGPRs.
   const float* P4 = R.p + base;
-  const float* G4 = R.g + base;
+  const float* G4 = reinterpret_cast<const float*>(R.g) + base;
+  const uint16_t* GH = reinterpret_cast<const uint16_t*>(R.g) + base;
 
   // every load of the row is issued up front (p, g, m, v: 4 NV float4 per lane in flight)
   // so one memory round trip covers the row; the moments do not wait for the norm reductions
@@ -79,8 +83,10 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   for (int i = 0; i < NV; ++i) {
     const int e = (i * 64 + lane) * 4;
     pv[i] = *reinterpret_cast<const float4*>(P4 + e);
-    if constexpr (NT)
-    {
+    if constexpr (GBF) {
+      const ushort4 h = *reinterpret_cast<const ushort4*>(GH + e);
+      gv[i] = make_float4(bf2f(h.x), bf2f(h.y), bf2f(h.z), bf2f(h.w));
+    } else if constexpr (NT) {
       const f32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(G4 + e));
       gv[i] = make_float4(t[0], t[1], t[2], t[3]);
     }
@@ -93,7 +99,14 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
     for (int sp = 1; sp < a.nsplit; ++sp) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        const float4 q = *reinterpret_cast<const float4*>(G4 + sp * a.gstride + (i * 64 + lane) * 4);
+        const long e = sp * a.gstride + (i * 64 + lane) * 4;
+        float4 q;
+        if constexpr (GBF) {
+          const ushort4 h = *reinterpret_cast<const ushort4*>(GH + e);
+          q = make_float4(bf2f(h.x), bf2f(h.y), bf2f(h.z), bf2f(h.w));
+        } else {
+          q = *reinterpret_cast<const float4*>(G4 + e);
+        }
         gv[i].x += q.x; gv[i].y += q.y; gv[i].z += q.z; gv[i].w += q.w;
       }
     }
@@ -340,11 +353,11 @@ using namespace scamd;
 
 extern "C" {
 
-int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const* m, float* const* v,
+int sc_adam_rows(int nset, float* const* p, const void* const* g, float* const* m, float* const* v,
                  void* const* shadow, float* const* norms, const int* rows, const int* norm, int d,
                  int rows_per_model, const float* lr, float b1, float b2, float eps, float bc1,
                  float bc2, const int* step, int nsplit, long gstride, long row0, hipStream_t stream,
-                 const int* live) {
+                 const int* live, int gbf16) {
   if (d % 256 || d > 4096 || nset < 1 || nset > 2 || nsplit < 1) return 1;
   static const int nt = getenv("SC_ADAM_NT") ? atoi(getenv("SC_ADAM_NT")) : 0;
   AdamArgs a;
@@ -358,23 +371,18 @@ int sc_adam_rows(int nset, float* const* p, const float* const* g, float* const*
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.step = step;
   a.nsplit = nsplit; a.gstride = gstride; a.row0 = row0; a.live = live;
   const long blocks = (total + 3) / 4;
+  // bf16 gradients: plain loads only (the NT knob A/B'd slower, profiles/)
+#define SC_ADAM(NVV)                                                                                  \
+  case NVV:                                                                                           \
+    if (gbf16) hipLaunchKernelGGL((adam_rows_kernel<NVV, false, true>), dim3(blocks), dim3(256), 0, stream, a); \
+    else if (nt) hipLaunchKernelGGL((adam_rows_kernel<NVV, true>), dim3(blocks), dim3(256), 0, stream, a);      \
+    else hipLaunchKernelGGL((adam_rows_kernel<NVV, false>), dim3(blocks), dim3(256), 0, stream, a);            \
+    break;
   switch (d / 256) {
-    case 1: if (nt) hipLaunchKernelGGL((adam_rows_kernel<1, true>), dim3(blocks), dim3(256), 0, stream, a);
-             else hipLaunchKernelGGL((adam_rows_kernel<1, false>), dim3(blocks), dim3(256), 0, stream, a); break;
-    case 2: if (nt) hipLaunchKernelGGL((adam_rows_kernel<2, true>), dim3(blocks), dim3(256), 0, stream, a);
-             else hipLaunchKernelGGL((adam_rows_kernel<2, false>), dim3(blocks), dim3(256), 0, stream, a); break;
-    case 3: if (nt) hipLaunchKernelGGL((adam_rows_kernel<3, true>), dim3(blocks), dim3(256), 0, stream, a);
-             else hipLaunchKernelGGL((adam_rows_kernel<3, false>), dim3(blocks), dim3(256), 0, stream, a); break;
-    case 4: if (nt) hipLaunchKernelGGL((adam_rows_kernel<4, true>), dim3(blocks), dim3(256), 0, stream, a);
-             else hipLaunchKernelGGL((adam_rows_kernel<4, false>), dim3(blocks), dim3(256), 0, stream, a); break;
-    case 6: if (nt) hipLaunchKernelGGL((adam_rows_kernel<6, true>), dim3(blocks), dim3(256), 0, stream, a);
-             else hipLaunchKernelGGL((adam_rows_kernel<6, false>), dim3(blocks), dim3(256), 0, stream, a); break;
-    case 8: if (nt) hipLaunchKernelGGL((adam_rows_kernel<8, true>), dim3(blocks), dim3(256), 0, stream, a);
-             else hipLaunchKernelGGL((adam_rows_kernel<8, false>), dim3(blocks), dim3(256), 0, stream, a); break;
-    case 16: if (nt) hipLaunchKernelGGL((adam_rows_kernel<16, true>), dim3(blocks), dim3(256), 0, stream, a);
-             else hipLaunchKernelGGL((adam_rows_kernel<16, false>), dim3(blocks), dim3(256), 0, stream, a); break;
+    SC_ADAM(1) SC_ADAM(2) SC_ADAM(3) SC_ADAM(4) SC_ADAM(6) SC_ADAM(8) SC_ADAM(16)
     default: return 1;
   }
+#undef SC_ADAM
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

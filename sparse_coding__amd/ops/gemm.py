@@ -312,7 +312,7 @@ def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None):
 
     pairs: list (one per problem, 1 or 2 problems) of lists of (A, B) segments
     (1 or 2 segments, summed along K).  A: [G, Bk, n] bf16 (or [Bk, n] shared),
-    B: [G, Bk, d] bf16 (or [Bk, d] shared).  outs: [G, n, d] fp32, or with ``ksplit`` > 1
+    B: [G, Bk, d] bf16 (or [Bk, d] shared).  outs: [G, n, d] fp32 (or all bf16), or with ``ksplit`` > 1
     [ksplit, G, n, d] partial slabs (their sum is the product; the Adam kernel sums them).
     """
     _need(1 <= len(pairs) == len(outs) <= 2, "1 or 2 problems")
@@ -339,15 +339,18 @@ def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None):
     K1 = ks[0][0]
     K2 = ks[0][1] if nseg == 2 else 0
     want = (G, n, d) if ksplit == 1 else (ksplit, G, n, d)
+    # bf16 outputs (every problem's): the plain bf16 epilogue -- Adam reads bf16 gradients
+    odt = outs[0].dtype
+    _need(odt in (torch.float32, torch.bfloat16), "out must be fp32 or bf16")
     for o in outs:
-        _need(o.dtype == torch.float32 and tuple(o.shape) == want and o.is_contiguous(), f"out must be {want}")
+        _need(o.dtype == odt and tuple(o.shape) == want and o.is_contiguous(), f"out must be {want} {odt}")
     cfg = None
     if ksplit > 1:
         cfg = 3 if shape_fits(3, n, d) else 1
     # nactive (masked ensembles): gradient rows past a model's live size are zero -- those tiles
     # skip their MFMAs and only write the zeros
-    _launch(EPI_F32, 0, n, d, K1, K2, G, a_ops, b_ops, list(outs), [alpha] * len(outs), d, n * d,
-            cfg=cfg, ksplit=ksplit, split_stride=G * n * d, nact_m=nactive)
+    _launch(EPI_F32 if odt == torch.float32 else EPI_BF16, 0, n, d, K1, K2, G, a_ops, b_ops, list(outs),
+            [alpha] * len(outs), d, n * d, cfg=cfg, ksplit=ksplit, split_stride=G * n * d, nact_m=nactive)
 
 
 def weight_grads_adam(pairs, states, alpha, lr, step_dev, betas=(0.9, 0.999), eps=1e-8, dot_tm=0):

@@ -181,6 +181,53 @@ def test_adam_rows_matches_autograd():
     _close(shadow, sh_ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("d", [512, 768])
+def test_adam_rows_bf16_gradient_matches_fp32_kernel(d):
+    """bf16-gradient Adam == the fp32-gradient kernel fed the same (bf16-rounded) gradient,
+    including the split-K slab sum; the update arithmetic is fp32 in both."""
+    from sparse_coding__amd.ops import adam as adam_ops
+
+    torch.manual_seed(4)
+    G, n = 3, 256
+    p = torch.randn(G, n, d, device=DEV)
+    gb = (torch.randn(2, G, n, d, device=DEV) * 1e-3).to(torch.bfloat16)
+    m = torch.randn(G, n, d, device=DEV).abs() * 1e-4
+    v = torch.randn(G, n, d, device=DEV).abs() * 1e-6
+    lr = torch.tensor([1e-3, 2e-3, 5e-4], device=DEV)
+    for nsplit in (1, 2):
+        outs = []
+        for g in (gb, gb.float()):
+            st = dict(p=p.clone(), g=g[0], m=m.clone(), v=v.clone(),
+                      shadow=torch.empty(G, n, d, device=DEV, dtype=torch.bfloat16),
+                      norms=torch.empty(G, n, device=DEV), norm=True)
+            adam_ops.adam_rows([st], lr, 7, nsplit=nsplit, gstride=G * n * d)
+            outs.append(st)
+        a, b = outs
+        for k in ("p", "m", "v", "norms"):
+            torch.testing.assert_close(a[k], b[k], rtol=1e-6, atol=1e-12)
+        assert torch.equal(a["shadow"], b["shadow"])
+
+
+def test_weight_grads_bf16_out_matches_fp32():
+    from sparse_coding__amd.ops import gemm
+
+    torch.manual_seed(5)
+    G, Bk, n, d = 3, 1024, 512, 512
+    A = (torch.randn(G, Bk, n, device=DEV) * 0.1).to(torch.bfloat16)
+    Bm = (torch.randn(G, Bk, d, device=DEV) * 0.1).to(torch.bfloat16)
+    A2 = (torch.randn(G, Bk, n, device=DEV) * 0.1).to(torch.bfloat16)
+    for cfg in (1, 3):
+        with gemm.force_shape(cfg):
+            o32 = torch.empty(G, n, d, device=DEV)
+            o16 = torch.empty(G, n, d, device=DEV, dtype=torch.bfloat16)
+            gemm.weight_grads([[(A, Bm), (A2, Bm)]], [o32], 0.5)
+            gemm.weight_grads([[(A, Bm), (A2, Bm)]], [o16], 0.5)
+        torch.cuda.synchronize()
+        ref = 0.5 * (A.float().transpose(1, 2) @ Bm.float() + A2.float().transpose(1, 2) @ Bm.float())
+        torch.testing.assert_close(o32, ref, rtol=1e-3, atol=1e-3)
+        assert torch.equal(o16, o32.to(torch.bfloat16)), cfg
+
+
 @pytest.mark.parametrize("cfg", SHAPE_CFGS)
 @pytest.mark.parametrize("fuse_adam", [True, False])
 @pytest.mark.parametrize("kind", ["untied", "tied"])
@@ -323,15 +370,16 @@ def test_topk_scatter_and_clear_roundtrip():
     assert int(code.ne(0).sum()) == 0
 
 
-@pytest.mark.parametrize("decode", ["gather", "gemm"])
-def test_fused_topk_matches_autograd(decode):
+@pytest.mark.parametrize("decode,grad_dtype", [("gather", "fp32"), ("gemm", "fp32"), ("gather", "bf16")])
+def test_fused_topk_matches_autograd(decode, grad_dtype):
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
     from sparse_coding__amd.models.topk import TopKEncoder
 
     torch.manual_seed(7)
     d, n, B = 256, 1024, 256
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
-    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, decode=decode)
+    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, decode=decode, grad_dtype=grad_dtype)
+    assert eng.g.dtype == (torch.bfloat16 if grad_dtype == "bf16" else torch.float32)
     x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
     mse = eng.step_batch(x)
     torch.cuda.synchronize()
