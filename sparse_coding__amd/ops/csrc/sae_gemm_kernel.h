@@ -95,6 +95,8 @@ constexpr int epi_scratch_floats() { return 2 * S::WGM * S::BN + S::NW; }
 // bank pairs (2-way, measured: 64 extra cycles per wave); the half swap makes them 16.
 // ds_read_b128 serves 16-lane groups on 64 banks: 2 rows x 8 chunks, distinct with the XOR.
 constexpr int STAGE_OFF = 4096, STAGE_ROW = 128, STAGE_WAVE = 64 * STAGE_ROW;
+// Adam-fused weight gradient: wave-private transpose pads past the epilogue's scratch floats
+constexpr int ADAM_PAD_OFF = 8192;
 __device__ __forceinline__ int stage_at(int row, int byte) {  // 8-byte granule of (row, byte)
   return row * STAGE_ROW + ((((byte >> 4) ^ (row >> 1)) & 7) << 4) + ((((byte >> 3) ^ row) & 1) << 3);
 }
@@ -557,8 +559,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
     const float bc1 = 1.f - __powf(p.b1, (float)(*p.step + 1));
     const float bc2 = 1.f - __powf(p.b2, (float)(*p.step + 1));
     const float stp = p.lr[g] / bc1, rbc2 = 1.f / bc2, b1 = p.b1, b2 = p.b2, eps = p.eps;
-    float ca[WI], cp[WI];
-    if (E.mode) {
+    if (E.mode) {  // per-row <w_hat, dW_hat> (code-gradient partials) and |w| into LDS
       for (int r = tid; r < BM; r += NT) {
         const int row = m0 + r;
         float dsum = 0.f;
@@ -567,33 +568,23 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
         red[BM + r] = E.norms[(long)g * p.M + row];
       }
       lds_barrier();
-#pragma unroll
-      for (int i = 0; i < WI; ++i) {
-        const int lr_ = wr * (WI * 16) + i * 16 + (lane & 15);
-        const float dot = red[lr_], nrm = red[BM + lr_];
-        if (nrm > 1e-8f) {
-          const float inv = 1.f / nrm;
-          ca[i] = alpha * inv;      // dW = dW_hat / |w| - w <w_hat, dW_hat> / |w|^2
-          cp[i] = dot * inv * inv;
-        } else {
-          ca[i] = alpha * 1e8f;     // below the clamp floor the norm has zero derivative
-          cp[i] = 0.f;
-        }
-      }
-      lds_barrier();
-    } else {
-#pragma unroll
-      for (int i = 0; i < WI; ++i) { ca[i] = alpha; cp[i] = 0.f; }
     }
-    float ss[WI];
-#pragma unroll
-    for (int i = 0; i < WI; ++i) ss[i] = 0.f;
-    // Software-prefetched streaming update: the p / m / v fragments of fragment f + D are
-    // loaded before fragment f is updated (D = 8 fragments = 24 x 1 KiB loads in flight per
-    // wave), so the epilogue runs at the HBM rate instead of one load round trip per fragment.
-    constexpr int NF = WI * WJ;
-    constexpr int D = NF < 8 ? NF : 8;
-    auto foff = [&](int f) { return gb + (long)(rowb + (f / WJ) * 16) * p.ldc + colb + (f % WJ) * 16; };
+    // Row-contiguous streaming update.  In the MFMA layout one dwordx4 touches 16 rows x 64 B
+    // (16 half-used 128-byte lines of p, m and v); instead each 16-row group of the wave tile is
+    // transposed through a wave-private LDS pad (the ring is free after the K loop) so one
+    // dwordx4 covers 4 whole 256-byte row segments, and the p / m / v fragments of fragment
+    // f + D are loaded before fragment f is updated (D = 8: 24 x 1 KiB loads in flight per wave).
+    static_assert(WJ == 4, "row-contiguous Adam epilogue: 64-column wave tiles");
+    constexpr int PADW = 68;                     // floats per padded LDS row (16-byte skew)
+    constexpr int NF = WI * 4, D = NF < 8 ? NF : 8;
+    static_assert(ADAM_PAD_OFF + NW * 16 * PADW * 4 <= (S::BM + S::BN) * 64 * 2, "pad inside one ring stage");
+    float* pad = reinterpret_cast<float*>(reinterpret_cast<char*>(red) + ADAM_PAD_OFF) + wid * 16 * PADW;
+    float* ssr = red + 2 * BM;                   // per-(column wave, row) |w|^2 partials
+    static_assert((2 * BM + WGN * BM) * 4 <= ADAM_PAD_OFF, "scratch floats below the pads");
+    const int rsub = lane >> 4, cl = (lane & 15) * 4;
+    const int lrow0 = wr * (WI * 16);            // first tile-local row of the wave
+    const long rbase = gb + (long)(m0 + lrow0 + rsub) * p.ldc + n0 + wc * 64 + cl;
+    auto foff = [&](int f) { return rbase + (long)((f >> 2) * 16 + (f & 3) * 4) * p.ldc; };
     f32x4_t pb[D], mb[D], vb[D];
 #pragma unroll
     for (int f = 0; f < D; ++f) {
@@ -602,9 +593,17 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
       mb[f] = *reinterpret_cast<const f32x4_t*>(E.m + o);
       vb[f] = *reinterpret_cast<const f32x4_t*>(E.v + o);
     }
+    f32x4_t gt[4];
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      const int i = f / WJ, j = f % WJ, sl = f % D;
+      const int i = f >> 2, k = f & 3, sl = f % D;
+      if (k == 0) {  // transpose the 16 x 64 accumulator group i (wave-local LDS ops stay in order)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4_t*>(pad + (lane & 15) * PADW + 16 * j + 4 * (lane >> 4)) = acc[i][j];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) gt[kk] = *reinterpret_cast<const f32x4_t*>(pad + (4 * kk + rsub) * PADW + cl);
+      }
       const long off = foff(f);
       f32x4_t pv = pb[sl], mv = mb[sl], vv = vb[sl];
       if (f + D < NF) {
@@ -613,39 +612,48 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
         mb[sl] = *reinterpret_cast<const f32x4_t*>(E.m + o);
         vb[sl] = *reinterpret_cast<const f32x4_t*>(E.v + o);
       }
-      {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float gr = acc[i][j][r] * ca[i] - pv[r] * cp[i];
-          mv[r] = b1 * mv[r] + (1.f - b1) * gr;
-          vv[r] = b2 * vv[r] + (1.f - b2) * gr * gr;
-          pv[r] -= stp * mv[r] / (sqrtf(vv[r] * rbc2) + eps);
-          ss[i] += pv[r] * pv[r];
+      const int lrow = lrow0 + i * 16 + 4 * k + rsub;
+      float a_ = alpha, c_ = 0.f;
+      if (E.mode) {  // norm Jacobian of this row: dW = dW_hat / |w| - w <w_hat, dW_hat> / |w|^2
+        const float dot = red[lrow], nrm = red[BM + lrow];
+        if (nrm > 1e-8f) {
+          const float inv = 1.f / nrm;
+          a_ = alpha * inv;
+          c_ = dot * inv * inv;
+        } else {
+          a_ = alpha * 1e8f;  // below the clamp floor the norm has zero derivative
         }
-        *reinterpret_cast<f32x4_t*>(E.p + off) = pv;
-        *reinterpret_cast<f32x4_t*>(E.m + off) = mv;
-        *reinterpret_cast<f32x4_t*>(E.v + off) = vv;
-        *reinterpret_cast<ushort4*>(E.sh + off) = make_ushort4(f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3]));
+      }
+      float ss = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gr = gt[k][r] * a_ - pv[r] * c_;
+        mv[r] = b1 * mv[r] + (1.f - b1) * gr;
+        vv[r] = b2 * vv[r] + (1.f - b2) * gr * gr;
+        pv[r] -= stp * mv[r] / (sqrtf(vv[r] * rbc2) + eps);
+        ss += pv[r] * pv[r];
+      }
+      *reinterpret_cast<f32x4_t*>(E.p + off) = pv;
+      *reinterpret_cast<f32x4_t*>(E.m + off) = mv;
+      *reinterpret_cast<f32x4_t*>(E.v + off) = vv;
+      *reinterpret_cast<ushort4*>(E.sh + off) = make_ushort4(f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3]));
+      if (E.mode) {  // the row's 64-column |w|^2 partial: sum over the 16 lanes of the row
+        ss += __shfl_xor(ss, 1, 64);
+        ss += __shfl_xor(ss, 2, 64);
+        ss += __shfl_xor(ss, 4, 64);
+        ss += __shfl_xor(ss, 8, 64);
+        if ((lane & 15) == 0) ssr[wc * BM + lrow] = ss;
       }
     }
     if (E.mode) {
       // partial |w_j|^2 over each 128-column slot -> sqpart[g][row][slot]
       constexpr int WPC = PT / (WJ * 16);  // wave columns per 128-column slot
-#pragma unroll
-      for (int i = 0; i < WI; ++i) {
-        ss[i] += __shfl_xor(ss[i], 16, 64);
-        ss[i] += __shfl_xor(ss[i], 32, 64);
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int i = 0; i < WI; ++i) red[wc * BM + wr * (WI * 16) + i * 16 + lane] = ss[i];
-      }
       lds_barrier();
       for (int idx = tid; idx < (BN / PT) * BM; idx += NT) {
         const int s = idx / BM, row = idx - s * BM;
         float v = 0.f;
 #pragma unroll
-        for (int w = 0; w < WPC; ++w) v += red[(s * WPC + w) * BM + row];
+        for (int w = 0; w < WPC; ++w) v += ssr[(s * WPC + w) * BM + row];
         E.sqpart[((long)g * p.M + m0 + row) * ptn + n0 / PT + s] = v;
       }
     }

@@ -33,9 +33,11 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 # epilogues are fastest on 128x128 blocks (two blocks per CU overlap one block's epilogue
 # with the other's MFMA loop: enc 61 vs 84 us on 256x256), the plain fp32 weight-gradient
 # GEMM (K = B = 2048) on 256x256 blocks (65 vs 74 us) -- "auto" picks that.
-_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 1, EPI_ENC_CNT: 1,
+_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 0, EPI_ENC_CNT: 1,
                 EPI_DC_MASK: 1, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
 _CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
+if os.environ.get("SC_ADAM_EPI_CFG"):  # A/B knob: block shape of the Adam-fused weight gradient
+    _CFG_DEFAULT[EPI_ADAM] = int(os.environ["SC_ADAM_EPI_CFG"])
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 # cfg bits 2-3 select the K pipeline: 0 BK64 x 2-stage LDS ring (default), 1 BK32 x 4,
 # 2 BK32 x 2 (smallest LDS footprint: most co-resident blocks), 3 BK32 x 3 (the
