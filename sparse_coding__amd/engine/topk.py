@@ -14,6 +14,8 @@ k differs, ``autoencoders/ensemble.py:100-116``):
 
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..ops import adam as adam_ops
@@ -23,7 +25,7 @@ from ..ops import topk as topk_ops
 
 class FusedTopKEnsemble:
     def __init__(self, models, sig=None, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999), eps=1e-8,
-                 decode: str = "gather", grad_dtype: str | None = None):
+                 decode: str = "gather", grad_dtype: str | None = None, score_chunk: int | None = None):
         from ..models.topk import TopKEncoder
 
         self.sig = sig or TopKEncoder
@@ -44,12 +46,22 @@ class FusedTopKEnsemble:
         self.lr = torch.tensor([float(x) for x in lrs], device=dev)
         self.betas, self.eps = betas, eps
         self.step_count = 0
+
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         bf = torch.bfloat16
         self.shadow = torch.empty(G, n, d, device=dev, dtype=bf)
         self.norms = torch.ones(G, n, device=dev)
         adam_ops.shadow_rows(self.params["dict"], self.shadow, self.norms, normalize=True)
-        self.scores = torch.empty(G, B, n, device=dev)
+        # Scores GEMM + select in model chunks (``score_chunk`` models at a time, env SC_TOPK_GCHUNK):
+        # one chunk's fp32 scores (2 models: 100 MB at config 4) stay resident in the 256 MB MALL
+        # between the GEMM that writes them and the select that reads them, instead of a 403 MB
+        # round trip through HBM.
+        gc = int(score_chunk if score_chunk is not None else os.environ.get("SC_TOPK_GCHUNK", "0") or 0)
+        self.g_chunk = G if gc <= 0 else min(G, gc)
+        self.scores = torch.empty(self.g_chunk, B, n, device=dev)
+        if self.g_chunk < G:
+            self._idx_buf = torch.empty(G, B, self.kmax, device=dev, dtype=torch.int32)
+            self._val_buf = torch.empty(G, B, self.kmax, device=dev)
         self.r = torch.empty(G, B, d, device=dev, dtype=bf)
         self.row_se = torch.empty(G, B, device=dev)
         self.codebuf = torch.zeros(G, B, n, device=dev, dtype=bf)
@@ -58,8 +70,6 @@ class FusedTopKEnsemble:
         # G * (n/256) * (d/256) workgroups (576 for config 4: 2.25 waves over 256 CUs); K halves
         # fill the machine and Adam sums the slabs -- A/B'd slower (1.344 / 1.406 ms for 2 / 3
         # slabs vs 1.318 ms): the extra fp32 slab traffic through Adam costs more than the tail
-        import os
-
         self.wg_split = int(os.environ.get("SC_TOPK_WSPLIT", "1"))
         self.wg_cfg = int(os.environ["SC_TOPK_WCFG"]) if os.environ.get("SC_TOPK_WCFG") else None
         self.sc_cfg = int(os.environ["SC_TOPK_SCFG"]) if os.environ.get("SC_TOPK_SCFG") else None
@@ -96,12 +106,20 @@ class FusedTopKEnsemble:
     def step_batch(self, batch):
         x = batch.to(self.device, torch.bfloat16).contiguous()
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
-        if self.sc_cfg is not None:  # A/B knob SC_TOPK_SCFG: block shape of the scores GEMM
-            with gemm_ops.force_shape(self.sc_cfg):
-                gemm_ops.matmul_nt(x, self.shadow, self.scores)
-        else:
-            gemm_ops.matmul_nt(x, self.shadow, self.scores)
-        self.idx, self.val = topk_ops.topk_select(self.scores, self.k, self.kmax)
+        gc = self.g_chunk
+        for g0 in range(0, G, gc):
+            g1 = min(G, g0 + gc)
+            sc = self.scores[: g1 - g0]
+            if self.sc_cfg is not None:  # A/B knob SC_TOPK_SCFG: block shape of the scores GEMM
+                with gemm_ops.force_shape(self.sc_cfg):
+                    gemm_ops.matmul_nt(x, self.shadow[g0:g1], sc)
+            else:
+                gemm_ops.matmul_nt(x, self.shadow[g0:g1], sc)
+            if gc >= G:
+                self.idx, self.val = topk_ops.topk_select(sc, self.k, self.kmax)
+            else:
+                topk_ops.topk_select(sc, self.k[g0:g1], self.kmax, out=(self._idx_buf[g0:g1], self._val_buf[g0:g1]))
+                self.idx, self.val = self._idx_buf, self._val_buf
         if self.decode == "gemm":
             # dense-GEMM decode: scatter the codes, R = codes D_hat - x (decoder-epilogue GEMM,
             # sum R^2 partials), code gradients 1[c > 0] (R D_hat^T) (code-gradient epilogue GEMM)

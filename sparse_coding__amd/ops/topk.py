@@ -7,19 +7,27 @@ import torch
 from . import _lib
 
 
-def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool = False, relu: bool = True):
+def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool = False, relu: bool = True,
+                out=None):
     """Per-row top-k of ``scores`` [G, B, n] fp32 with per-model ``k`` (int32 [G]).
 
     Returns (idx int32 [G, B, kmax], val fp32 [G, B, kmax]); slots >= k[g] are (0, 0.0).
     ``absolute`` selects by |score| (PCA-style) and keeps the signed value; ``relu``
-    clamps kept values at 0 (TopKEncoder semantics)."""
+    clamps kept values at 0 (TopKEncoder semantics).  ``out``: optional (idx, val) to fill
+    (contiguous, e.g. a model slice of larger buffers)."""
     G, B, n = scores.shape
     if scores.dtype != torch.float32 or not scores.is_contiguous():
         raise ValueError("scores must be contiguous fp32")
     if k.dtype != torch.int32 or k.numel() != G:
         raise ValueError("k must be int32[G]")
-    idx = torch.empty(G, B, kmax, device=scores.device, dtype=torch.int32)
-    val = torch.empty(G, B, kmax, device=scores.device, dtype=torch.float32)
+    if out is not None:
+        idx, val = out
+        if (tuple(idx.shape) != (G, B, kmax) or tuple(val.shape) != (G, B, kmax) or idx.dtype != torch.int32
+                or val.dtype != torch.float32 or not idx.is_contiguous() or not val.is_contiguous()):
+            raise ValueError("out must be contiguous (int32, fp32) [G, B, kmax]")
+    else:
+        idx = torch.empty(G, B, kmax, device=scores.device, dtype=torch.int32)
+        val = torch.empty(G, B, kmax, device=scores.device, dtype=torch.float32)
     rc = _lib.lib().sc_topk_select(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n, kmax,
                                    int(absolute), int(relu), _lib.stream_handle())
     _lib.check(rc, "sc_topk_select")

@@ -395,6 +395,25 @@ def test_fused_topk_matches_autograd(decode, grad_dtype):
         assert agree.float().mean() > 0.97, agree.float().mean()
 
 
+def test_fused_topk_model_chunked_scores_bit_identical():
+    """Scores GEMM + select in model chunks (MALL-resident scores) == the one-shot form."""
+    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
+    from sparse_coding__amd.models.topk import TopKEncoder
+
+    torch.manual_seed(8)
+    d, n, B = 256, 1024, 256
+    models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64, 8, 32)]
+    engs = [FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, score_chunk=c) for c in (None, 2)]
+    assert engs[1].g_chunk == 2 and engs[0].g_chunk == 5
+    for s in range(3):
+        x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
+        mse = [e.step_batch(x) for e in engs]
+        torch.cuda.synchronize()
+        assert torch.equal(engs[0].idx, engs[1].idx) and torch.equal(engs[0].val, engs[1].val), s
+        assert torch.equal(mse[0], mse[1])
+    assert torch.equal(engs[0].params["dict"], engs[1].params["dict"])
+
+
 @pytest.mark.parametrize("form", ["direct", "gram", "direct_rt2"])
 @pytest.mark.parametrize("G,B,n,d", [(2, 64, 512, 512), (3, 32, 2048, 512), (1, 48, 1024, 1024), (2, 256, 512, 1024),
                                      (2, 64, 256, 256), (2, 64, 512, 256)])
