@@ -97,7 +97,12 @@ class DeviceRing:
             self._new_epoch()
         idx = self._perm[self._cursor + rank * batch_size:self._cursor + (rank + 1) * batch_size]
         self._cursor += batch_size * world
-        rows = self.buf.index_select(0, idx) if out is None else torch.index_select(self.buf, 0, idx, out=out)
+        if self.buf.is_cuda and (self.buf[0].numel() * self.buf.element_size()) % 16 == 0 and idx.dtype == torch.int64:
+            from ..ops.rows import gather_rows  # one wave per row (HIP); torch index_select elsewhere
+
+            rows = gather_rows(self.buf, idx, out=out)
+        else:
+            rows = self.buf.index_select(0, idx) if out is None else torch.index_select(self.buf, 0, idx, out=out)
         return (rows, idx) if return_index else rows
 
     def batches_per_epoch(self, batch_size: int) -> int:

@@ -71,6 +71,7 @@ def _declare(lib):
                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                      c_void_p],
         "sc_center_rows": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
+        "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_void_p],
         "sc_synth_codes": [c_void_p, c_void_p, c_long, c_int, C.c_ulonglong, C.c_ulonglong, c_void_p],
         "sc_coef_search": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p],
@@ -79,7 +80,6 @@ def _declare(lib):
         "sc_fista_adjoint_init": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
         "sc_fista_gram": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_int, c_int, c_int, c_void_p],
-        "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_float, c_void_p],
         "sc_stream_create_cumask": [c_void_p, c_int, C.POINTER(c_void_p)],
         "sc_stream_destroy": [c_void_p],
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],

@@ -243,15 +243,31 @@ __global__ __launch_bounds__(256) void loss_reduce_kernel(BiasArgs a) {
   __shared__ float red[8];
   const int g = blockIdx.x, tid = threadIdx.x;
   const int n = a.n;
+  // Only G blocks run, so every loop is latency-bound: the loads are vectorised and the loops
+  // unrolled so one memory round trip serves several iterations (was ~8 us at G = 8).
   const float* b = a.b + (long)g * n;
   float bs = 0.f;
-  for (int j = tid; j < n; j += 256) bs += b[j] * b[j];
+  if ((n & 3) == 0) {
+    const float4* b4 = reinterpret_cast<const float4*>(b);
+#pragma unroll 4
+    for (int j = tid; j < n / 4; j += 256) {
+      const float4 v = b4[j];
+      bs += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+  } else {
+#pragma unroll 4
+    for (int j = tid; j < n; j += 256) bs += b[j] * b[j];
+  }
   bs = block_sum_256(bs, red);
   float l1 = 0.f, l0 = 0.f, se = 0.f;
+  const float2* ep = reinterpret_cast<const float2*>(a.enc_part) + (long)g * a.enc_tiles;
+#pragma unroll 4
   for (int t = tid; t < a.enc_tiles; t += 256) {
-    l1 += a.enc_part[((long)g * a.enc_tiles + t) * 2];
-    l0 += a.enc_part[((long)g * a.enc_tiles + t) * 2 + 1];
+    const float2 v = ep[t];
+    l1 += v.x;
+    l0 += v.y;
   }
+#pragma unroll 4
   for (int t = tid; t < a.dec_tiles; t += 256) se += a.dec_part[(long)g * a.dec_tiles + t];
   l1 = block_sum_256(l1, red);
   l0 = block_sum_256(l0, red);

@@ -1,0 +1,29 @@
+"""Row gather for the step's batch fetch from the HBM activation ring (``csrc/elementwise.hip``)."""
+
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def gather_rows(buf: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[i] = buf[idx[i]] for a contiguous GPU ``buf`` [N, ...] whose rows are a multiple of 16 bytes;
+    ``idx`` int64 on the same device.  The HIP kernel moves one row per wave."""
+    if not (buf.is_cuda and buf.is_contiguous()):
+        raise ValueError("gather_rows needs a contiguous GPU buffer")
+    row_bytes = buf[0].numel() * buf.element_size() if buf.shape[0] else 0
+    if row_bytes % 16:
+        raise ValueError(f"rows of {row_bytes} bytes are not a multiple of 16")
+    if idx.dtype != torch.int64 or idx.device != buf.device:
+        raise ValueError("idx must be int64 on the buffer's device")
+    idx = idx.contiguous()
+    shape = (idx.numel(),) + tuple(buf.shape[1:])
+    if out is None:
+        out = torch.empty(shape, device=buf.device, dtype=buf.dtype)
+    elif tuple(out.shape) != shape or out.dtype != buf.dtype or not out.is_contiguous():
+        raise ValueError(f"out must be contiguous {buf.dtype} {shape}")
+    rc = _lib.lib().sc_gather_rows(_lib.ptr(buf), _lib.ptr(idx), _lib.ptr(out), idx.numel(), row_bytes,
+                                   _lib.stream_handle())
+    _lib.check(rc, "sc_gather_rows")
+    return out

@@ -395,6 +395,23 @@ def test_fused_topk_matches_autograd(decode, grad_dtype):
         assert agree.float().mean() > 0.97, agree.float().mean()
 
 
+def test_gather_rows_matches_index_select():
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.ops.rows import gather_rows
+
+    torch.manual_seed(9)
+    buf = torch.randn(5000, 512, device=DEV).to(torch.bfloat16)
+    idx = torch.randint(0, 5000, (2048,), device=DEV)
+    out = torch.empty(2048, 512, device=DEV, dtype=torch.bfloat16)
+    gather_rows(buf, idx, out=out)
+    assert torch.equal(out, buf.index_select(0, idx))
+    assert torch.equal(gather_rows(buf[:, :8].contiguous(), idx[:3]), buf[idx[:3], :8])
+    ring = DeviceRing(4096, 512, device=DEV)
+    ring.push(buf[:4096])
+    rows, ridx = ring.sample_shard(1024, 1, 2, return_index=True)
+    assert torch.equal(rows, ring.view().index_select(0, ridx))
+
+
 def test_fused_topk_model_chunked_scores_bit_identical():
     """Scores GEMM + select in model chunks (MALL-resident scores) == the one-shot form."""
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
