@@ -3,6 +3,7 @@
 * ``FusedSAEEnsemble`` (gfx950 kernels) for untied / tied / masked SAEs and the SAE
   step of ``FunctionalFista``;
 * ``FusedTopKEnsemble`` (gfx950 kernels) for ``TopKEncoder`` with per-model k;
+* ``UnrolledEnsemble`` (grouped MFMA GEMMs + torch autograd) for LISTA / residual-denoising SAEs;
 * ``FunctionalEnsemble`` (eager torch.func, CPU or GPU) for everything else and as
   the CPU oracle.
 
@@ -21,7 +22,7 @@ import torch
 from ..models.fista import FistaDictUpdater, FunctionalFista
 from ..models.signatures import unit_rows
 from ..models.topk import TopKEncoder
-from . import analytic
+from . import analytic, unrolled
 from .ensemble import FunctionalEnsemble
 from .optim import adam
 
@@ -104,6 +105,10 @@ class EnsembleTrainer:
             if use_graph:
                 self.impl.enable_graph()
             self.kind = "fused-sae"
+        elif engine in ("auto", "unrolled") and unrolled.supports(sig):
+            # LISTA / residual-denoising SAEs: the stacked batched loss on the grouped MFMA GEMM
+            self.impl = unrolled.UnrolledEnsemble(models, sig, lr=lr, device=device)
+            self.kind = "unrolled"
         elif engine in ("auto", "analytic") and analytic.supports(sig):
             # closed-form gradients with batched GEMMs (no vmap/autograd): the CPU fast path
             self.impl = analytic.AnalyticSAEEnsemble(models, sig, lr=lr, device=device)
@@ -244,7 +249,7 @@ class EnsembleTrainer:
         elif self.kind == "fused-topk":
             st["impl"] = {"params": self.impl.params, "m": self.impl.m, "v": self.impl.v,
                           "step": self.impl.step_count}
-        elif self.kind in ("analytic", "fista-loss"):
+        elif self.kind in ("analytic", "fista-loss", "unrolled"):
             st["impl"] = self.impl.state_dict()
         else:
             st["impl"] = {"params": self.impl.params, "optim": self.impl.optim_states}
@@ -257,7 +262,7 @@ class EnsembleTrainer:
             raise ValueError(f"checkpoint engine {st['kind']} != {self.kind}")
         self.steps = int(st["steps"])
         imp = st["impl"]
-        if self.kind in ("fused-sae", "analytic", "fista-loss"):
+        if self.kind in ("fused-sae", "analytic", "fista-loss", "unrolled"):
             self.impl.load_state_dict(imp)
         elif self.kind == "fused-topk":
             for d_ in ("params", "m", "v"):
