@@ -1,9 +1,13 @@
 """LISTA ensemble step: UnrolledEnsemble (grouped MFMA GEMMs) vs the vmap(grad) FunctionalEnsemble
 on the same GPU (8 models, d=512, n=2048, 3 layers, B=2048)."""
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
 from sparse_coding__amd.engine.optim import adam

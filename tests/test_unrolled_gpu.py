@@ -14,7 +14,8 @@ DEV = "cuda"
 
 
 def _rel(a, b):
-    return float((a.float().cpu() - b.float().cpu()).norm() / b.float().cpu().norm().clamp_min(1e-30))
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
 
 
 @pytest.mark.parametrize("tb", [True, False])
