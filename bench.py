@@ -164,10 +164,33 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
         eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device, **kw)
         if not args.no_graph:
             eng.enable_graph()  # whole step = one HIP graph replay
+        if args.no_graph or os.environ.get("SC_BENCH_PREFETCH", "0") in ("", "0"):
+            def step():
+                ring.sample_shard(B, 0, 1, out=eng.x_static)
+                eng.step_static() if not args.no_graph else eng.step_batch(eng.x_static)
+
+            return Runner(step, lambda: eng.to_learned_dicts(device))
+        # double-buffered batch fetch (SC_BENCH_PREFETCH=1, opt-in): the gather of step t+1's rows
+        # runs on a side stream under step t's graph (two graphs, one per input buffer).  A/B'd
+        # slower on MI355X: 0.339 vs 0.325 ms/step (profiles/stream_overlap_ab_r2.json)
+        bufs = [eng.x_static, torch.empty_like(eng.x_static)]
+        eng.add_static_input(bufs[1])
+        fetch = torch.cuda.Stream(device=device)
+        st = {"cur": 0, "ev": None}
+        ring.sample_shard(B, 0, 1, out=bufs[0])
 
         def step():
-            ring.sample_shard(B, 0, 1, out=eng.x_static)
-            eng.step_static() if not args.no_graph else eng.step_batch(eng.x_static)
+            main = torch.cuda.current_stream(device)
+            cur = st["cur"]
+            if st["ev"] is not None:
+                main.wait_event(st["ev"])       # this step's rows have landed
+            fetch.wait_stream(main)             # buffer 1-cur was last read by the previous step
+            with torch.cuda.stream(fetch):
+                ring.sample_shard(B, 0, 1, out=bufs[1 - cur])
+                st["ev"] = torch.cuda.Event()
+                st["ev"].record(fetch)
+            eng.step_static(cur)
+            st["cur"] = 1 - cur
 
         return Runner(step, lambda: eng.to_learned_dicts(device))
     from sparse_coding__amd.engine.ensemble import FunctionalEnsemble

@@ -478,7 +478,7 @@ class FusedSAEEnsemble:
             self.rows_seen += self.batch_size
         self.step_count += 1
 
-    def _bias_loss(self, update, reduced):
+    def _bias_loss(self, update, reduced, defer_step=False):
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
         b1, b2 = self.betas
         if reduced:  # bias gradient already summed (and possibly all-reduced) into g_bias
@@ -492,7 +492,7 @@ class FusedSAEEnsemble:
                            cnt_part=self.cnt_part if self._counted else None,
                            feat_count=self.feature_counts if self._counted else None,
                            b1=b1, b2=b2, eps=self.eps, update=update,
-                           step_dev=self.step_dev)
+                           step_dev=self.step_dev, defer_step=defer_step)
 
     def step_batch(self, batch, expand_dims=True):
         """One Adam step of every model on ``batch [B, d]``; returns a device tensor [G, 6]:
@@ -538,10 +538,32 @@ class FusedSAEEnsemble:
                                step_dev=self.step_dev, live=self.nactive)
             main.wait_stream(self._side)  # join before the step counter advances
             self._bias_loss(update=True, reduced=False)
+        elif self._overlap_tail():
+            # the loss reduction + bias Adam (G and n/32 x G small blocks; they need only the
+            # forward's partials) run on a side stream under the weight-gradient GEMM and the
+            # row Adam; the device step counter advances after the join
+            self.forward(x, count, target)
+            main = torch.cuda.current_stream(self.device)
+            self._side.wait_stream(main)
+            with torch.cuda.stream(self._side):
+                self._bias_loss(update=True, reduced=False, defer_step=True)
+            self.backward_weights(x)
+            adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
+                               step_dev=self.step_dev, live=self.nactive, **self._adam_split_kw())
+            main.wait_stream(self._side)
+            self.step_dev += 1
         else:
             self.forward(x, count, target)
             self.backward_weights(x)
             self._apply_update_kernels()
+
+    def _overlap_tail(self) -> bool:
+        """Side-stream tail (SC_OVERLAP_TAIL=1, opt-in) for plain untied / tied steps.  A/B on
+        MI355X (profiles/stream_overlap_ab_r2.json): +7 us per step -- the cross-stream edges
+        of the captured graph cost more than the ~10 us of small kernels they hide."""
+        return (self._side is not None and not self.fuse_adam and self.kind in ("untied", "tied")
+                and not self.learned_center and os.environ.get("SC_OVERLAP_TAIL", "0") not in ("", "0")
+                and os.environ.get("SC_SERIALIZE_STREAMS", "0") in ("", "0"))
 
     def add_static_input(self, t: torch.Tensor) -> int:
         """Register another persistent input buffer [B, d] bf16: ``step_batch(t)`` then replays

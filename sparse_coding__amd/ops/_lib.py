@@ -56,7 +56,7 @@ def _declare(lib):
         "sc_bias_loss": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                          c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
-                         c_float, c_float, c_int, c_void_p, c_void_p],
+                         c_float, c_float, c_int, c_void_p, c_void_p, c_int],
     }
     optional = {
         "sc_topk_select": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,

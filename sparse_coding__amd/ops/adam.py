@@ -81,9 +81,11 @@ def shadow_rows(p, shadow, norms=None, normalize=True):
 
 def bias_loss(b, m, v, colpart, tm, enc_part, enc_tiles, dec_part, dec_tiles, l1, bias_decay, lr,
               out, B, d, step, gscale, cnt_part=None, feat_count=None, b1=0.9, b2=0.999, eps=1e-8,
-              update=True, step_dev=None):
+              update=True, step_dev=None, defer_step=False):
     """Loss bookkeeping + bias Adam.  ``colpart`` [G, tm, n] holds partial sums of the bias
-    gradient; ``gscale`` converts their sum to dL/db."""
+    gradient; ``gscale`` converts their sum to dL/db.  ``defer_step``: leave the device step
+    counter alone (bias Adam uses ``*step_dev + 1``; the caller advances it) -- for running
+    concurrently with a row-Adam that reads the same counter."""
     G, n = b.shape
     bc1 = 1.0 - b1 ** max(step, 1)
     bc2 = 1.0 - b2 ** max(step, 1)
@@ -91,7 +93,7 @@ def bias_loss(b, m, v, colpart, tm, enc_part, enc_tiles, dec_part, dec_tiles, l1
         G, _lib.ptr(b), _lib.ptr(m), _lib.ptr(v), _lib.ptr(colpart), tm, _lib.ptr(enc_part),
         enc_tiles, _lib.ptr(dec_part), dec_tiles, _lib.ptr(cnt_part), _lib.ptr(feat_count),
         _lib.ptr(l1), _lib.ptr(bias_decay), _lib.ptr(lr), _lib.ptr(out), n, B, d, float(gscale), b1, b2, eps,
-        bc1, bc2, int(update), _lib.ptr(step_dev), _lib.stream_handle(),
+        bc1, bc2, int(update), _lib.ptr(step_dev), _lib.stream_handle(), int(bool(defer_step)),
     )
     _lib.check(rc, "sc_bias_loss")
 

@@ -235,6 +235,8 @@ struct BiasArgs {
   float b1, b2, eps, bc1, bc2;
   int update;                      // 0: only losses (eval)
   int* step;                       // optional device step counter, advanced by loss_reduce
+  int defer_step;                  // 1: do not advance (the caller does, after a concurrent
+                                   //    row-Adam that reads the same counter); bias Adam uses *step + 1
 };
 
 // Phase 1 (one block per model): reduce the GEMM-epilogue partials to the
@@ -285,7 +287,7 @@ __global__ __launch_bounds__(256) void loss_reduce_kernel(BiasArgs a) {
     o[4] = l0 / a.B;
     o[5] = bnorm;
     // the step counter advances once per optimizer step; bias_adam (next launch) reads the new value
-    if (g == 0 && a.update && a.step) *a.step += 1;
+    if (g == 0 && a.update && a.step && !a.defer_step) *a.step += 1;
   }
 }
 
@@ -326,7 +328,7 @@ __global__ __launch_bounds__(256) void bias_adam_kernel(BiasArgs a) {
   const float beta = a.bias_decay[g];
   const float bd = (beta != 0.f && bnorm > 0.f) ? beta / bnorm : 0.f;
   float bc1 = a.bc1, bc2 = a.bc2;
-  if (a.step) bias_corrections(a.b1, a.b2, *a.step, bc1, bc2);
+  if (a.step) bias_corrections(a.b1, a.b2, *a.step + a.defer_step, bc1, bc2);
   const float bj = a.b[idx];
   const float gj = gsum * a.gscale + bd * bj;
   const float mj = a.b1 * a.m[idx] + (1.f - a.b1) * gj;
@@ -422,7 +424,7 @@ int sc_bias_loss(int G, float* b, float* m, float* v, const float* colpart, int 
                  const float* enc_part, int enc_tiles, const float* dec_part, int dec_tiles,
                  const float* cnt_part, float* feat_count, const float* l1, const float* bias_decay,
                  const float* lr, float* out, int n, int B, int d, float gscale, float b1, float b2, float eps,
-                 float bc1, float bc2, int update, int* step, hipStream_t stream) {
+                 float bc1, float bc2, int update, int* step, hipStream_t stream, int defer_step) {
   BiasArgs a;
   a.b = b; a.m = m; a.v = v; a.colpart = colpart; a.tm = tm;
   a.enc_part = enc_part; a.enc_tiles = enc_tiles; a.dec_part = dec_part; a.dec_tiles = dec_tiles;
@@ -430,6 +432,7 @@ int sc_bias_loss(int G, float* b, float* m, float* v, const float* colpart, int 
   a.l1 = l1; a.bias_decay = bias_decay; a.lr = lr; a.out = out;
   a.n = n; a.B = B; a.d = d; a.gscale = gscale;
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.update = update; a.step = step;
+  a.defer_step = defer_step ? 1 : 0;
   hipLaunchKernelGGL(loss_reduce_kernel, dim3(G), dim3(256), 0, stream, a);
   if (update || (cnt_part && feat_count))
     hipLaunchKernelGGL(bias_adam_kernel, dim3((n + 31) / 32, G), dim3(256), 0, stream, a);

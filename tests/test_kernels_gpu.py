@@ -395,6 +395,36 @@ def test_fused_topk_matches_autograd(decode, grad_dtype):
         assert agree.float().mean() > 0.97, agree.float().mean()
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_overlapped_tail_bit_identical(monkeypatch, graph):
+    """Loss reduction + bias Adam on a side stream (deferred step counter) == the serial tail."""
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+
+    torch.manual_seed(12)
+    d, n, B = 256, 512, 256
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3, 1e-2)]
+    engs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SC_OVERLAP_TAIL", flag)
+        e = FusedSAEEnsemble(models, FunctionalSAE, lr=1e-3, batch_size=B, device=DEV)
+        if graph:
+            e.enable_graph()
+            e._capture()  # captured under this flag
+        engs.append(e)
+    for s in range(4):
+        x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
+        outs = []
+        for e, flag in zip(engs, ("1", "0")):
+            monkeypatch.setenv("SC_OVERLAP_TAIL", flag)
+            outs.append(e.step_batch(x).clone())
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), s
+    for k in engs[0].params:
+        assert torch.equal(engs[0].params[k], engs[1].params[k]), k
+    assert int(engs[0].step_dev) == int(engs[1].step_dev) == 4
+
+
 def test_gather_rows_matches_index_select():
     from sparse_coding__amd.data.ring import DeviceRing
     from sparse_coding__amd.ops.rows import gather_rows
