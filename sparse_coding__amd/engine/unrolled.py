@@ -8,8 +8,9 @@ denoising layers), trained by ``FunctionalEnsemble`` = ``vmap(grad(loss))`` per 
 Here every model's parameters are stacked on a leading model axis and the loss of all models
 is written once in batched form.  Each layer's matrix products are grouped GEMMs over the
 model axis (``grouped_mm``: one ``csrc/sae_gemm`` launch per product -- bf16 MFMA operands,
-fp32 accumulation -- forward and both backward products), the shrinkage / momentum / ReLU
-elementwise work and the losses stay in torch autograd.  Adam is the reference's (torchopt)
+fp32 accumulation -- forward and both backward products); each LISTA layer's shrinkage +
+momentum is one fused HIP pass forward and one backward (``lista_step``); the residual layers'
+ReLU and the losses stay in torch autograd.  Adam is the reference's (torchopt)
 update applied to the stacked tensors with a per-model learning rate.  Off the GPU, or when a
 shape is not tiled by the kernels (B, n, d multiples of 128), the products fall back to fp32
 ``torch.matmul`` -- the CPU tests pin the engine against ``FunctionalEnsemble`` that way.
@@ -97,6 +98,52 @@ def grouped_mm(a: torch.Tensor, b: torch.Tensor, tb: bool = False) -> torch.Tens
     return torch.matmul(a, b.transpose(-1, -2) if tb else b)
 
 
+class _ListaStep(torch.autograd.Function):
+    """One LISTA layer's elementwise part in one HIP pass each way (csrc/elementwise.hip):
+    r = y + a, x_ = shrink(r, theta), y' = x_ + m (x_ - xs); returns (y', x_)."""
+
+    @staticmethod
+    def forward(ctx, y, a, xs, theta, m):
+        from ..ops import _lib
+
+        ctx.set_materialize_grads(False)
+        y, a, xs, theta, m = (t.contiguous() for t in (y, a, xs, theta, m))
+        G, B, n = y.shape
+        xo, yo = torch.empty_like(y), torch.empty_like(y)
+        p = _lib.ptr
+        _lib.check(_lib.lib().sc_lista_fwd(p(y), p(a), p(xs), p(theta), p(m), p(xo), p(yo), G, B, n,
+                                           _lib.stream_handle()), "sc_lista_fwd")
+        ctx.save_for_backward(y, a, xs, theta, m)
+        return yo, xo
+
+    @staticmethod
+    def backward(ctx, gy, gx):
+        from ..ops import _lib
+
+        y, a, xs, theta, m = ctx.saved_tensors
+        G, B, n = y.shape
+        if gy is None:
+            gy = torch.zeros_like(y)
+        rb = 64 if B % 64 == 0 else 4
+        gr, gxs = torch.empty_like(y), torch.empty_like(y)
+        gth = torch.empty(G, B // rb, n, device=y.device)
+        gm = torch.empty(G, B // rb, n // 256, device=y.device)
+        p = _lib.ptr
+        _lib.check(_lib.lib().sc_lista_bwd(p(gy.contiguous()), p(gx.contiguous() if gx is not None else None), p(y),
+                                           p(a), p(xs), p(theta), p(m), p(gr), p(gxs), p(gth), p(gm), G, B, n, rb,
+                                           _lib.stream_handle()), "sc_lista_bwd")
+        return gr, gr, gxs, gth.sum(1), gm.sum((1, 2))
+
+
+def lista_step(y, a, xs, theta, m):
+    """(y', x_) of a LISTA layer for stacked [G, B, n] tensors (theta [G, n], m [G] clamped)."""
+    G, B, n = y.shape
+    if y.is_cuda and n % 256 == 0 and B % 4 == 0:
+        return _ListaStep.apply(y, a, xs, theta, m)
+    x_ = shrinkage(y + a, theta.unsqueeze(1))
+    return x_ + m.view(-1, 1, 1) * (x_ - xs), x_
+
+
 _KINDS = {FunctionalLISTADenoisingSAE: "lista", FunctionalResidualDenoisingSAE: "residual"}
 
 
@@ -143,10 +190,9 @@ class UnrolledEnsemble:
         if self.kind == "lista":
             xs = y
             for i in range(self.n_layers):
-                m = torch.clamp(self._layer(i, "rho"), 0.0, 1.0).view(-1, 1, 1)
-                r = y + grouped_mm(x - grouped_mm(y, D), self._layer(i, "W"), tb=True)
-                x_ = shrinkage(r, self._layer(i, "theta").unsqueeze(1))
-                y, xs = x_ + m * (x_ - xs), x_
+                m = torch.clamp(self._layer(i, "rho"), 0.0, 1.0)
+                a = grouped_mm(x - grouped_mm(y, D), self._layer(i, "W"), tb=True)
+                y, xs = lista_step(y, a, xs, self._layer(i, "theta"), m)
             return y
         c = y
         for i in range(self.n_layers):
@@ -180,6 +226,13 @@ class UnrolledEnsemble:
         for k, p in self.params.items():
             g = grads[k]
             m, v = self.m[k], self.v[k]
+            if p.is_cuda and p.dim() == 3 and p.shape[-1] % 256 == 0 and p.shape[-1] <= 4096:
+                # matrices: the row-Adam kernel (one HBM pass; the torch form below is ~10)
+                from ..ops import adam as adam_ops
+
+                adam_ops.adam_rows([dict(p=p.data, g=g.contiguous(), m=m, v=v, shadow=None, norms=None, norm=False)],
+                                   self.lr, self.step_count, b1, b2, self.eps)
+                continue
             m.mul_(b1).add_(g, alpha=1.0 - b1)
             v.mul_(b2).addcmul_(g, g, value=1.0 - b2)
             lr = self.lr.view(-1, *([1] * (p.dim() - 1)))

@@ -6,9 +6,102 @@
 // gather_rows_kernel: the step's batch fetch from the HBM activation ring, out[i] = buf[idx[i]]
 //   for 16-byte-multiple rows: one wave per row, every lane one dwordx4 per 1 KiB of the row
 //   (the torch index_select took 5.3 us for 2048 x 1 KiB rows, mostly its launch tail).
+// lista_fwd_kernel / lista_bwd_kernel: one LISTA layer's elementwise part for a stacked
+//   ensemble (reference autoencoders/residual_denoising_autoencoder.py:26-36):
+//   r = y + a (a = (x - y D) W^T from the GEMMs), x_ = sign(r) relu(|r| - theta),
+//   y' = x_ + m (x_ - xs).  Forward: one pass (the torch chain was ~10 passes over [G, B, n]);
+//   backward: one pass producing dr (= dy = da), dxs and per-block partials of dtheta / dm.
 #include "common.h"
 
 namespace scamd {
+
+__global__ __launch_bounds__(256) void lista_fwd_kernel(const float4* __restrict__ y, const float4* __restrict__ a,
+                                                        const float4* __restrict__ xs, const float* __restrict__ theta,
+                                                        const float* __restrict__ m, float4* __restrict__ xo,
+                                                        float4* __restrict__ yo, int B, int n, long total4) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= total4) return;
+  const long e = t * 4;
+  const int g = (int)(e / ((long)B * n));
+  const int j = (int)(e % n);
+  const float4 yv = y[t], av = a[t], xv = xs[t];
+  const float4 th = *reinterpret_cast<const float4*>(theta + (long)g * n + j);
+  const float mm = m[g];
+  float4 xn, yn;
+  auto one = [&](float yy, float aa, float x0, float tt, float& xo_, float& yo_) {
+    const float r = yy + aa;
+    const float mag = fmaxf(fabsf(r) - tt, 0.f);
+    xo_ = r > 0.f ? mag : (r < 0.f ? -mag : 0.f);
+    yo_ = xo_ + mm * (xo_ - x0);
+  };
+  one(yv.x, av.x, xv.x, th.x, xn.x, yn.x);
+  one(yv.y, av.y, xv.y, th.y, xn.y, yn.y);
+  one(yv.z, av.z, xv.z, th.z, xn.z, yn.z);
+  one(yv.w, av.w, xv.w, th.w, xn.w, yn.w);
+  xo[t] = xn;
+  yo[t] = yn;
+}
+
+// grid (n / 256, B / rb, G), 256 threads = 4 row lanes x 64 column lanes of 4 columns each.
+__global__ __launch_bounds__(256) void lista_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ gx,
+                                                        const float* __restrict__ y, const float* __restrict__ a,
+                                                        const float* __restrict__ xs, const float* __restrict__ theta,
+                                                        const float* __restrict__ m, float* __restrict__ gr,
+                                                        float* __restrict__ gxs, float* __restrict__ gth_part,
+                                                        float* __restrict__ gm_part, int B, int n, int rb) {
+  __shared__ float4 red4[4][64];
+  __shared__ float redm[256];
+  const int g = blockIdx.z, rbk = blockIdx.y;
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int j = blockIdx.x * 256 + cl * 4;
+  const float mm = m[g];
+  const float4 th = *reinterpret_cast<const float4*>(theta + (long)g * n + j);
+  float4 gt = make_float4(0.f, 0.f, 0.f, 0.f);
+  float gmv = 0.f;
+  for (int r = rbk * rb + rl; r < (rbk + 1) * rb; r += 4) {
+    const long o = ((long)g * B + r) * n + j;
+    const float4 gyv = *reinterpret_cast<const float4*>(gy + o);
+    const float4 gxv = gx ? *reinterpret_cast<const float4*>(gx + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 yv = *reinterpret_cast<const float4*>(y + o);
+    const float4 av = *reinterpret_cast<const float4*>(a + o);
+    const float4 xv = *reinterpret_cast<const float4*>(xs + o);
+    float4 gro, gxo;
+    auto one = [&](float gyy, float gxx, float yy, float aa, float x0, float tt, float& gro_, float& gxo_, float& gtt) {
+      const float r_ = yy + aa;
+      const float mag = fabsf(r_) - tt;
+      const float on = mag > 0.f ? 1.f : 0.f;
+      const float sg = r_ > 0.f ? 1.f : (r_ < 0.f ? -1.f : 0.f);
+      const float xo_ = sg * fmaxf(mag, 0.f);
+      const float gtot = (1.f + mm) * gyy + gxx;   // dL/dx_
+      gro_ = gtot * on * (sg != 0.f ? 1.f : 0.f);  // d x_/d r = 1 where |r| > theta (0 at r = 0)
+      gxo_ = -mm * gyy;
+      gtt -= gtot * sg * on;                        // d x_/d theta = -sign(r) where |r| > theta
+      gmv += gyy * (xo_ - x0);                      // d y'/d m = x_ - xs
+    };
+    one(gyv.x, gxv.x, yv.x, av.x, xv.x, th.x, gro.x, gxo.x, gt.x);
+    one(gyv.y, gxv.y, yv.y, av.y, xv.y, th.y, gro.y, gxo.y, gt.y);
+    one(gyv.z, gxv.z, yv.z, av.z, xv.z, th.z, gro.z, gxo.z, gt.z);
+    one(gyv.w, gxv.w, yv.w, av.w, xv.w, th.w, gro.w, gxo.w, gt.w);
+    *reinterpret_cast<float4*>(gr + o) = gro;
+    *reinterpret_cast<float4*>(gxs + o) = gxo;
+  }
+  red4[rl][cl] = gt;
+  redm[threadIdx.x] = gmv;
+  __syncthreads();
+  if (rl == 0) {
+    float4 s = red4[0][cl];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      s.x += red4[k][cl].x; s.y += red4[k][cl].y; s.z += red4[k][cl].z; s.w += red4[k][cl].w;
+    }
+    *reinterpret_cast<float4*>(gth_part + ((long)g * gridDim.y + rbk) * n + j) = s;
+  }
+  for (int w = 128; w > 0; w >>= 1) {
+    __syncthreads();
+    if (threadIdx.x < w) redm[threadIdx.x] += redm[threadIdx.x + w];
+  }
+  if (threadIdx.x == 0) gm_part[((long)g * gridDim.y + rbk) * gridDim.x + blockIdx.x] = redm[0];
+}
 
 __global__ __launch_bounds__(256) void center_rows_kernel(const uint16_t* __restrict__ x, const float* __restrict__ c,
                                                           uint16_t* __restrict__ out, int G, int B, int d) {
@@ -46,6 +139,27 @@ int sc_center_rows(const void* x, const float* c, void* out, int G, int B, int d
   const long total = (long)G * B * d / 4;
   hipLaunchKernelGGL(center_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
                      reinterpret_cast<const uint16_t*>(x), c, reinterpret_cast<uint16_t*>(out), G, B, d);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_lista_fwd(const float* y, const float* a, const float* xs, const float* theta, const float* m, float* xo,
+                 float* yo, int G, int B, int n, hipStream_t stream) {
+  if (n % 4 || G < 1 || B < 1) return 1;
+  const long total4 = (long)G * B * n / 4;
+  hipLaunchKernelGGL(lista_fwd_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const float4*>(y), reinterpret_cast<const float4*>(a),
+                     reinterpret_cast<const float4*>(xs), theta, m, reinterpret_cast<float4*>(xo),
+                     reinterpret_cast<float4*>(yo), B, n, total4);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// gth_part: [G][B / rb][n], gm_part: [G][B / rb][n / 256]
+int sc_lista_bwd(const float* gy, const float* gx, const float* y, const float* a, const float* xs,
+                 const float* theta, const float* m, float* gr, float* gxs, float* gth_part, float* gm_part,
+                 int G, int B, int n, int rb, hipStream_t stream) {
+  if (n % 256 || rb < 4 || rb % 4 || B % rb || G < 1) return 1;
+  hipLaunchKernelGGL(lista_bwd_kernel, dim3(n / 256, B / rb, G), dim3(256), 0, stream, gy, gx, y, a, xs, theta, m,
+                     gr, gxs, gth_part, gm_part, B, n, rb);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -51,3 +51,52 @@ def test_unrolled_hip_grads_match_fp32(sig):
             e = _rel(gh[k][g], gr[k][g])
             assert e <= 3e-2, (k, g, e)
     assert grouped_mm(x.to(DEV), hip.params["decoder"].detach(), tb=True).is_cuda
+
+
+def test_lista_step_kernel_matches_torch_autograd():
+    from sparse_coding__amd.engine.unrolled import _ListaStep
+    from sparse_coding__amd.models.lista import shrinkage
+
+    torch.manual_seed(5)
+    G, B, n = 3, 128, 512
+    y, a, xs = (torch.randn(G, B, n, device=DEV, requires_grad=True) for _ in range(3))
+    theta = (torch.randn(G, n, device=DEV) * 0.3).requires_grad_()
+    m = torch.tensor([0.1, 0.5, 0.9], device=DEV, requires_grad=True)
+    yo, xo = _ListaStep.apply(y, a, xs, theta, m)
+    x_ = shrinkage(y + a, theta.unsqueeze(1))
+    yr = x_ + m.view(-1, 1, 1) * (x_ - xs)
+    torch.testing.assert_close(yo, yr)
+    torch.testing.assert_close(xo, x_)
+    gy, gx = torch.randn_like(yo), torch.randn_like(xo)
+    got = torch.autograd.grad([yo, xo], [y, a, xs, theta, m], [gy, gx])
+    ref = torch.autograd.grad([yr, x_], [y, a, xs, theta, m], [gy, gx], retain_graph=True)
+    for gg, rr in zip(got, ref):
+        torch.testing.assert_close(gg, rr, rtol=1e-4, atol=1e-3)
+    got1 = torch.autograd.grad(_ListaStep.apply(y, a, xs, theta, m)[0], [theta, m], gy)  # x_ unused
+    ref1 = torch.autograd.grad(yr, [theta, m], gy)
+    for gg, rr in zip(got1, ref1):
+        torch.testing.assert_close(gg, rr, rtol=1e-4, atol=1e-3)
+
+
+def test_unrolled_adam_kernel_matches_torch_adam():
+    """The engine's Adam (row-Adam kernel for the matrices, torch for vectors) == torchopt Adam
+    in torch on the same gradients, over two steps."""
+    torch.manual_seed(6)
+    d, n, B = 256, 256, 256
+    models = [FunctionalLISTADenoisingSAE.init(d, n, 2, l1) for l1 in (1e-3, 1e-2)]
+    eng = UnrolledEnsemble(models, FunctionalLISTADenoisingSAE, lr=1e-3, device=DEV)
+    p = {k: v.detach().clone() for k, v in eng.params.items()}
+    m = {k: torch.zeros_like(v) for k, v in p.items()}
+    v_ = {k: torch.zeros_like(v) for k, v in p.items()}
+    for t in (1, 2):
+        grads, _ = eng.grads(torch.randn(B, d, device=DEV))
+        eng.apply_grads(grads)
+        for k in p:
+            g = grads[k]
+            m[k] = 0.9 * m[k] + 0.1 * g
+            v_[k] = 0.999 * v_[k] + 0.001 * g * g
+            lr = eng.lr.view(-1, *([1] * (p[k].dim() - 1)))
+            p[k] = p[k] - lr * (m[k] / (1 - 0.9 ** t)) / ((v_[k] / (1 - 0.999 ** t)).sqrt() + 1e-8)
+    torch.cuda.synchronize()
+    for k in p:
+        torch.testing.assert_close(eng.params[k].detach(), p[k], rtol=1e-5, atol=1e-6)
