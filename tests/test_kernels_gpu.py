@@ -262,6 +262,18 @@ def _fused_step_matches(kind, fuse_adam):
         torch.testing.assert_close(out[:, 0], loss_ref["loss"], rtol=3e-2, atol=1e-4)
         torch.testing.assert_close(out[:, 1], loss_ref["l_reconstruction"], rtol=3e-2, atol=1e-4)
         torch.testing.assert_close(out[:, 2], loss_ref["l_l1"], rtol=3e-2, atol=1e-5)
+        if step == 0:
+            # gradient level: after one step Adam's first moment is (1 - b1) * g in both engines;
+            # per model relative Frobenius error (the oracle runs fp32 weights, the kernels the
+            # bf16-rounded encoder: ReLU mask flips near zero, ~2% at l1 = 1e-4)
+            mu = ref.optim_states.mu if hasattr(ref.optim_states, "mu") else ref.optim_states[0].mu
+            for k in fused.m:
+                if k not in mu:
+                    continue
+                for g in range(G):
+                    a, b = fused.m[k][g].float(), mu[k][g].float().reshape(fused.m[k][g].shape)
+                    e = float((a - b).norm() / b.norm().clamp_min(1e-30))
+                    assert e <= 5e-2, (k, g, e)
     for k, v in fused.params.items():
         init = torch.stack([m[0][k] for m in models]).to(DEV)
         mv_f, mv_r = (v - init).flatten(), (ref.params[k] - init).flatten()
