@@ -95,6 +95,9 @@ class FusedTopKEnsemble:
         self.g_all = torch.empty(self.wg_split, G, n, d, device=dev, dtype=bf if gbf else torch.float32)
         self.g = self.g_all[0]
         self.idx = self.val = None
+        # fold the dense-buffer clear into the next step's decode (SC_TOPK_FOLD_CLEAR, default on)
+        self.fold_clear = os.environ.get("SC_TOPK_FOLD_CLEAR", "1") not in ("", "0")
+        self._prev_idx = None
         # decode: "gather" (sparse, one wave per row) or "gemm" (dense codes through the decoder and
         # code-gradient epilogue GEMMs); chosen from measurement (profiles/config4_topk_r2.json)
         self.decode = decode
@@ -130,7 +133,7 @@ class FusedTopKEnsemble:
         else:
             # gather decode: one wave per row, k dictionary rows gathered twice from L2 / MALL
             topk_ops.decode_grad(self.idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
-                                 self.dscbuf, dscv=self.dscv)
+                                 self.dscbuf, dscv=self.dscv, prev_idx=self._prev_idx if self.fold_clear else None)
             torch.sum(self.row_se, dim=1, out=self._se)
         gs = self.sparse_g if self.decode == "gather" else 0
         if gs:
@@ -149,7 +152,12 @@ class FusedTopKEnsemble:
                 gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g], 2.0 / (B * d))
         else:
             gemm_ops.weight_grads([[(self.codebuf, self.r), (self.dscbuf, x)]], [self.g], 2.0 / (B * d))
-        topk_ops.clear(self.idx, self.codebuf, self.dscbuf)
+        if self.fold_clear and self.decode == "gather":
+            # the next step's decode zeroes these picks (one launch less per step); the idx tensor
+            # must survive until then (in the one-shot path topk_select returns a fresh one per step)
+            self._prev_idx = self.idx.clone() if self.g_chunk < G else self.idx
+        else:
+            topk_ops.clear(self.idx, self.codebuf, self.dscbuf)
         adam_ops.adam_rows([dict(p=self.params["dict"], g=self.g, m=self.m["dict"], v=self.v["dict"],
                                  shadow=self.shadow, norms=self.norms, norm=True)],
                            self.lr, self.step_count + 1, *self.betas, self.eps, step_dev=self.step_dev,

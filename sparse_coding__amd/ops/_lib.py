@@ -62,7 +62,7 @@ def _declare(lib):
         "sc_topk_select": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                            c_void_p],
         "sc_topk_decode_grad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
-                                c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+                                c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
         "sc_topk_sparse_wgrad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
                                  c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
         "sc_topk_clear": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p],

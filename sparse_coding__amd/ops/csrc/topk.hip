@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
     const int* __restrict__ idx, const float* __restrict__ val, const int* __restrict__ kv,
     const uint16_t* __restrict__ D, const uint16_t* __restrict__ X, long sx, uint16_t* __restrict__ R,
     float* __restrict__ row_se, uint16_t* __restrict__ codebuf, uint16_t* __restrict__ dscbuf, int G, int B,
-    int n, int d, int kmax, float* __restrict__ dscv) {
+    int n, int d, int kmax, float* __restrict__ dscv, const int* __restrict__ prev_idx) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)G * B) return;
@@ -692,6 +692,18 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
   // code gradients (units of R): dscore_j = 1[v_j > 0] <R, D[idx_j]>; scatter code and dscore
   uint16_t* Cb = codebuf + row * (long)n;
   uint16_t* Sb = dscbuf + row * (long)n;
+  if (prev_idx) {
+    // the previous step's picks of this row go back to zero here (replaces a separate clear
+    // launch after the weight gradient); the wait keeps them ordered before the new picks'
+    // stores, which may hit the same columns from other lanes of this wave
+    const int* P = prev_idx + row * kmax;
+    for (int j = lane; j < kmax; j += 64) {
+      const int c = P[j];
+      Cb[c] = 0;
+      Sb[c] = 0;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+  }
   for (int j0 = 0; j0 < k; j0 += DOTS) {
     float p[DOTS];
 #pragma unroll
@@ -863,14 +875,14 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
 
 int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const void* D, const void* X, long sx,
                         void* R, float* row_se, void* codebuf, void* dscbuf, int G, int B, int n, int d, int kmax,
-                        hipStream_t stream, float* dscv) {
+                        hipStream_t stream, float* dscv, const int* prev_idx) {
   if (d % 4) return 1;
   const int nv = (d + 255) / 256;
   dim3 grid(((long)G * B + 3) / 4);
 #define SC_D(V) \
   if (nv <= V) { hipLaunchKernelGGL((topk_decode_grad_kernel<V>), grid, dim3(256), 0, stream, idx, val, k, \
       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx, reinterpret_cast<uint16_t*>(R), \
-      row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv); \
+      row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   static const int ru = getenv("SC_TOPK_RU") ? atoi(getenv("SC_TOPK_RU")) : 0;
   static const int occ = getenv("SC_TOPK_OCC") ? atoi(getenv("SC_TOPK_OCC")) : 0;
@@ -879,7 +891,7 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
     hipLaunchKernelGGL((topk_decode_grad_kernel<3, RUV, OCCV, DV>), grid, dim3(256), 0, stream, idx, val, k,  \
                        reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,    \
                        reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),      \
-                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv);                            \
+                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx);                            \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                       \
   }
   if (nv == 3 && occ) {  // A/B knob: cap registers for more resident waves (SC_TOPK_OCC = waves / SIMD)
@@ -895,14 +907,14 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
     hipLaunchKernelGGL((topk_decode_grad_kernel<3, 16>), grid, dim3(256), 0, stream, idx, val, k,
                        reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,
                        reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),
-                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv);
+                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   if (nv == 3 && ru == 4) {
     hipLaunchKernelGGL((topk_decode_grad_kernel<3, 4>), grid, dim3(256), 0, stream, idx, val, k,
                        reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,
                        reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),
-                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv);
+                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx);
     return hipGetLastError() == hipSuccess ? 0 : 3;
   }
   SC_D(1) SC_D(2) SC_D(3) SC_D(4) SC_D(8) SC_D(16)

@@ -34,16 +34,21 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
     return idx, val
 
 
-def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dscv=None):
+def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dscv=None, prev_idx=None):
     """Sparse decode + residual (bf16 r_out [G, B, d]) + per-row squared error; with the dense
     buffers, also scatter codes and code gradients <R, D[idx]> (units of R) for the wgrad GEMM;
-    with ``dscv`` ([G, B, kmax] fp32) also the per-slot code gradients for ``sparse_wgrad``."""
+    with ``dscv`` ([G, B, kmax] fp32) also the per-slot code gradients for ``sparse_wgrad``.
+    ``prev_idx``: the previous step's picks ([G, B, kmax]), zeroed in the dense buffers first
+    (instead of a ``clear`` after the previous weight gradient)."""
+    if prev_idx is not None and (prev_idx.shape != idx.shape or prev_idx.dtype != torch.int32
+                                 or not prev_idx.is_contiguous()):
+        raise ValueError("prev_idx must be contiguous int32 of idx's shape")
     G, B, kmax = idx.shape
     n, d = D.shape[1], D.shape[2]
     sx = 0 if x.dim() == 2 else B * d
     rc = _lib.lib().sc_topk_decode_grad(_lib.ptr(idx), _lib.ptr(val), _lib.ptr(k), _lib.ptr(D), _lib.ptr(x), sx,
                                         _lib.ptr(r_out), _lib.ptr(row_se), _lib.ptr(codebuf), _lib.ptr(dscbuf),
-                                        G, B, n, d, kmax, _lib.stream_handle(), _lib.ptr(dscv))
+                                        G, B, n, d, kmax, _lib.stream_handle(), _lib.ptr(dscv), _lib.ptr(prev_idx))
     _lib.check(rc, "sc_topk_decode_grad")
 
 

@@ -437,6 +437,28 @@ def test_fused_overlapped_tail_bit_identical(monkeypatch, graph):
     assert int(engs[0].step_dev) == int(engs[1].step_dev) == 4
 
 
+def test_fused_topk_folded_clear_bit_identical(monkeypatch):
+    """Zeroing the previous picks inside the next decode == the separate clear launch."""
+    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
+    from sparse_coding__amd.models.topk import TopKEncoder
+
+    torch.manual_seed(13)
+    d, n, B = 256, 1024, 256
+    models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
+    engs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SC_TOPK_FOLD_CLEAR", flag)
+        engs.append(FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3))
+    assert engs[0].fold_clear and not engs[1].fold_clear
+    for s in range(4):
+        x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
+        mse = [e.step_batch(x).clone() for e in engs]
+        torch.cuda.synchronize()
+        assert torch.equal(mse[0], mse[1]), s
+        assert torch.equal(engs[0].g, engs[1].g), s
+    assert torch.equal(engs[0].params["dict"], engs[1].params["dict"])
+
+
 def test_gather_rows_matches_index_select():
     from sparse_coding__amd.data.ring import DeviceRing
     from sparse_coding__amd.ops.rows import gather_rows
