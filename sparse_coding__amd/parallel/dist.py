@@ -59,6 +59,13 @@ def init_distributed(backend: str | None = None, timeout_s: int = 600, device=No
         kw = dict(backend=be, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kw["device_id"] = device
+            if os.environ.get("SC_RCCL_HIGH_PRIORITY", "1") not in ("", "0"):
+                # RCCL's internal stream at high priority: the collectives that run under the
+                # step's GEMMs (ensemble-sharded batch all-gather, chunked DP all-reduce) get
+                # their workgroups dispatched ahead of the compute stream's
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                kw["pg_options"] = opts
         dist.init_process_group(**kw)
         return DistInfo(rank, world, local, device, be)
     if dist.is_initialized():
