@@ -136,11 +136,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
         const int row = 8 * k + (lane >> 3);
         uint4 v = *reinterpret_cast<const uint4*>(stage + row * STAGE_ROW + (((ch ^ (row >> 1)) & 7) << 4));
         if (row & 1) v = make_uint4(v.z, v.w, v.x, v.y);  // halves stored swapped on odd rows
-        if (p.dbg & 4)  // A/B knob (SC_GEMM_DBG bit 2): non-temporal output stores
-          __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
-                                      reinterpret_cast<u32x4_t*>(Cw + (long)row * p.ldc + ch * 8));
-        else
-          *reinterpret_cast<uint4*>(Cw + (long)row * p.ldc + ch * 8) = v;
+        *reinterpret_cast<uint4*>(Cw + (long)row * p.ldc + ch * 8) = v;
       }
     }
   };
