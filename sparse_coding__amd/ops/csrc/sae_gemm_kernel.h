@@ -103,7 +103,7 @@ __device__ __forceinline__ int stage_at(int row, int byte) {  // 8-byte granule 
 template <class S>
 constexpr int stage_bytes() { return STAGE_OFF + S::NW * STAGE_WAVE; }
 
-template <class S, int EPI, bool AUX_EARLY, bool STAGE = false>
+template <class S, int EPI, bool AUX_EARLY, bool STAGE = false, bool FSTAGE = false>
 __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)[S::WI][S::WJ],
                                              const uint2 (&auxv)[S::WI][S::WJ], float* red, int pi, int g, int m0,
                                              int n0, int tn, int tiles_n, void* cptr, float alpha, bool dead = false) {
@@ -197,6 +197,37 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
 
   if constexpr (EPI == EPI_F32) {
     float* C = reinterpret_cast<float*>(cptr) + (long)g * p.sc;
+    if constexpr (FSTAGE) {
+      if (!(p.dbg & 8)) {  // A/B knob (SC_GEMM_DBG bit 3): the direct MFMA-layout stores below
+        // LDS-staged row-contiguous fp32 stores (tile kernel, ring free after the K loop): the
+        // MFMA layout puts 16 rows x 64 B in one store; instead each wave parks 32 columns of
+        // its sub-tile (128-byte rows, the bf16 staging's swizzle) and streams whole 128-byte
+        // row segments, 8 rows per dwordx4 store; two passes cover the 64 columns.
+        char* st = reinterpret_cast<char*>(red) + wid * (WI * 16 * STAGE_ROW);
+        float* Cw = C + (long)(m0 + wr * (WI * 16)) * p.ldc + n0 + wc * (WJ * 16);
+        const int q = lane >> 4, r16 = lane & 15, ch = lane & 7;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int i = 0; i < WI; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+              const f32x4_t v = acc[i][2 * h + jj] * alpha;
+              const int row = i * 16 + r16, byte = (jj * 16 + 4 * q) * 4;
+              *reinterpret_cast<float2*>(st + stage_at(row, byte)) = make_float2(v[0], v[1]);
+              *reinterpret_cast<float2*>(st + stage_at(row, byte + 8)) = make_float2(v[2], v[3]);
+            }
+#pragma unroll
+          for (int k = 0; k < WI * 2; ++k) {
+            const int row = 8 * k + (lane >> 3);
+            uint4 u = *reinterpret_cast<const uint4*>(st + row * STAGE_ROW + (((ch ^ (row >> 1)) & 7) << 4));
+            if (row & 1) u = make_uint4(u.z, u.w, u.x, u.y);
+            *reinterpret_cast<uint4*>(Cw + (long)row * p.ldc + h * 32 + ch * 4) = u;
+          }
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < WI; ++i)
 #pragma unroll
@@ -903,7 +934,8 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
 #undef SC_ISSUE
   lds_barrier();  // all reads of the ring done before smem is reused below
   constexpr bool STAGE = S::WI == 4 && S::WJ == 4 && NST * STG >= stage_bytes<S>();
-  sae_epilogue<S, EPI, AUX_EARLY, STAGE>(p, acc, auxv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn, tiles_n,
+  constexpr bool FSTAGE = EPI == EPI_F32 && S::WJ == 4 && NST * STG >= S::NW * S::WI * 16 * STAGE_ROW;
+  sae_epilogue<S, EPI, AUX_EARLY, STAGE, FSTAGE>(p, acc, auxv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn, tiles_n,
                                          cptr, alpha, dead);
 }
 
