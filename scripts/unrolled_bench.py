@@ -32,6 +32,9 @@ models = [S.init(d, n, L, float(l1), device="cuda") for l1 in torch.logspace(-4,
 x = torch.randn(B, d, device="cuda")
 eng = UnrolledEnsemble(models, S, device="cuda")
 ms = timeit(lambda: eng.step_batch(x))
+if "--only-unrolled" in sys.argv:
+    print(json.dumps({"unrolled_ms_per_step": round(ms, 3)}))
+    sys.exit(0)
 ens = FunctionalEnsemble(models, S, adam, {"lr": 1e-3}, device="cuda")
 ms_e = timeit(lambda: ens.step_batch(x))
 print(json.dumps({"config": f"LISTA {G} models d={d} n={n} layers={L} B={B}", "unrolled_ms_per_step": round(ms, 3),

@@ -31,6 +31,26 @@ def _hip_ok(*dims) -> bool:
     return all(int(x) % 128 == 0 for x in dims)
 
 
+# bf16 copies of the step's weight operands (D and the layer matrices feed several products
+# forward and backward): one cast per tensor per step instead of one per product.  Keyed on
+# storage pointer, shape and autograd version, and active only inside ``UnrolledEnsemble.grads``
+# (every weight operand stays alive until its backward is done; the cache is cleared after).
+_BF16_CACHE: dict = {}
+_CACHE_ON = [False]
+
+
+def _bf16_operand(t: torch.Tensor, cache: bool) -> torch.Tensor:
+    if t.dtype == torch.bfloat16:
+        return t.contiguous()
+    if not (cache and _CACHE_ON[0]):
+        return t.to(torch.bfloat16).contiguous()
+    key = (t.data_ptr(), tuple(t.shape), t.stride(), t._version)
+    hit = _BF16_CACHE.get(key)
+    if hit is None:
+        hit = _BF16_CACHE[key] = t.to(torch.bfloat16).contiguous()
+    return hit
+
+
 def _gemm(a, b, tb: bool):
     """fp32 [G, M, N] = a @ (b^T if tb else b) with bf16 operands on the MFMA kernel.
     a: [G, M, K] (or [M, K] shared by every model); b: [G, N, K] if tb else [G, K, N]."""
@@ -40,8 +60,8 @@ def _gemm(a, b, tb: bool):
     M = a.shape[-2]
     N = b.shape[1] if tb else b.shape[2]
     out = torch.empty(G, M, N, device=b.device, dtype=torch.float32)
-    ab = a.to(torch.bfloat16).contiguous()
-    bb = b.to(torch.bfloat16).contiguous()
+    ab = _bf16_operand(a, cache=False)
+    bb = _bf16_operand(b, cache=True)  # b is always a weight operand (D or a layer matrix)
     if tb:
         gemm_ops.matmul_nt(ab, bb, out)
     else:
@@ -211,9 +231,15 @@ class UnrolledEnsemble:
     def grads(self, x: torch.Tensor):
         """Gradients of every model's loss (models are independent: d(sum)/dθ_g = dL_g/dθ_g)."""
         x = x.to(self.device, torch.float32)
-        total, l_rec, l_l1, c = self.losses(x)
-        keys = list(self.params)
-        gs = torch.autograd.grad(total.sum(), [self.params[k] for k in keys])
+        _BF16_CACHE.clear()
+        _CACHE_ON[0] = True
+        try:
+            total, l_rec, l_l1, c = self.losses(x)
+            keys = list(self.params)
+            gs = torch.autograd.grad(total.sum(), [self.params[k] for k in keys])
+        finally:
+            _CACHE_ON[0] = False
+            _BF16_CACHE.clear()
         return dict(zip(keys, gs)), (total.detach(), l_rec.detach(), l_l1.detach(), c.detach())
 
     @torch.no_grad()
