@@ -38,6 +38,8 @@ _CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_
 _CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
 if os.environ.get("SC_ADAM_EPI_CFG"):  # A/B knob: block shape of the Adam-fused weight gradient
     _CFG_DEFAULT[EPI_ADAM] = int(os.environ["SC_ADAM_EPI_CFG"])
+if os.environ.get("SC_F32_CFG"):  # A/B knob: block shape of the plain fp32 GEMMs (weight gradient)
+    _CFG_DEFAULT[EPI_F32] = int(os.environ["SC_F32_CFG"])
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 # cfg bits 2-3 select the K pipeline: 0 BK64 x 2-stage LDS ring (default), 1 BK32 x 4,
 # 2 BK32 x 2 (smallest LDS footprint: most co-resident blocks), 3 BK32 x 3 (the
