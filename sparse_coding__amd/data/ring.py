@@ -97,9 +97,11 @@ class DeviceRing:
             self._new_epoch()
         idx = self._perm[self._cursor + rank * batch_size:self._cursor + (rank + 1) * batch_size]
         self._cursor += batch_size * world
-        if self.buf.is_cuda and (self.buf[0].numel() * self.buf.element_size()) % 16 == 0 and idx.dtype == torch.int64:
+        if (self.buf.is_cuda and (self.buf[0].numel() * self.buf.element_size()) % 16 == 0
+                and idx.dtype == torch.int64 and _kernels_available()):
             from ..ops.rows import gather_rows  # one wave per row (HIP); torch index_select elsewhere
 
+            # (indices come from this ring's own permutation of [0, size): always in bounds)
             rows = gather_rows(self.buf, idx, out=out)
         else:
             rows = self.buf.index_select(0, idx) if out is None else torch.index_select(self.buf, 0, idx, out=out)
@@ -110,3 +112,9 @@ class DeviceRing:
 
     def view(self) -> torch.Tensor:
         return self.buf[: self.size]
+
+
+def _kernels_available() -> bool:
+    from ..ops import _lib
+
+    return _lib.available()

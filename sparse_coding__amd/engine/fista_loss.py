@@ -8,7 +8,8 @@ adjoint run on the kernels (``ops.fista.unrolled_fista_residual``: direct-form H
 saving the bf16 iterate slabs, adjoint sweep of grouped MFMA GEMMs + one elementwise kernel
 per iteration, one K = T B GEMM for the dictionary gradient); eta = 1 / lambda_max(w w^T)
 per model comes from the warm ``EtaTracker`` (power iteration, exact refresh every 50
-calls) instead of an eigvalsh per call.  The rest of the graph (two bmm, the norms) is
+calls) instead of an eigvalsh per call, and -- like the reference's undetached eigvalsh --
+carries its gradient (d lambda_max / dw = 2 (w u) u^T, ``ops.fista.tracked_eta``).  The rest of the graph (two bmm, the norms) is
 ordinary autograd, and Adam is torch's fused multi-tensor Adam over the stacked tensors
 (elementwise, so per-model exact).
 """
@@ -49,7 +50,8 @@ class FistaLossEnsemble:
         l_rec = (torch.bmm(c, w) - x).pow(2).mean(dim=(1, 2))
         l_l1 = self.l1 * c.abs().sum(-1).mean(-1)
         l_bd = self.bias_decay * b.norm(dim=-1)
-        eta = self.eta(w.detach())
+        # eta = 1/lambda_max(w w^T) is differentiable in w, as in the reference (not detached)
+        eta = fista_ops.tracked_eta(w, self.eta)
         R = fista_ops.unrolled_fista_residual(x, w, self.l1, c, self.num_iter, eta, backend=self.backend)
         l_fista = R.pow(2).mean(dim=(1, 2))
         return l_rec + l_fista + l_l1 + l_bd, {"l_reconstruction": l_rec, "l_fista": l_fista, "l_l1": l_l1}

@@ -51,7 +51,8 @@ class FusedSAEEnsemble:
 
     def __init__(self, models, sig, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999),
                  eps=1e-8, track_feature_counts=True, kind: Optional[str] = None, fuse_adam: bool = False,
-                 count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None):
+                 count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None,
+                 fused_bwd: Optional[bool] = None):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
         # FunctionalTiedCenteredSAE (sae_ensemble.py:162-228): the tied kernels on x - center
@@ -217,6 +218,15 @@ class FusedSAEEnsemble:
         # MI355X (the streaming Adam crowds the GEMM's CUs), kept as an option.
         self.overlap_adam = False
         self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        # Weight gradients + Adam in ONE kernel (csrc/sae_bwd.hip: a workgroup owns 64 dictionary
+        # rows of a model over the whole batch, the fp32 gradients never reach HBM).  Auto: plain
+        # ReLU SAEs (untied / tied) whose ensemble has >= 256 such row blocks, on one device (data
+        # parallel paths reduce the gradients between the two halves and use the split kernels).
+        bwd_ok = (self.kind in ("untied", "tied") and not fuse_adam and adam_ops.shape_ok(B, n, d)
+                  and (self.nactive is None or bool((self.nactive % 64 == 0).all())))
+        if fused_bwd and not bwd_ok:
+            raise ValueError(f"fused_bwd: unsupported configuration (kind {self.kind}, B={B}, n={n}, d={d})")
+        self.fused_bwd = bwd_ok if fused_bwd else (fused_bwd is None and bwd_ok and adam_ops.bwd_fills_gpu(G, n))
         self.dotpart = torch.zeros(G, tm, n, device=dev)        # norm-Jacobian row-dot partials
         self.sqpart = torch.zeros(G, n, d // 128, device=dev)   # updated-row |w|^2 partials
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)  # graph input buffer
@@ -395,7 +405,13 @@ class FusedSAEEnsemble:
             return dict(nsplit=self.wsplit, gstride=self.n_models * self.n * self.d)
         return {}
 
-    def adam_first(self):
+    def adam_first(self, reduced: bool = True):
+        """Dictionary Adam (decoder for untied SAEs).  Threshold / learned-centering SAEs first
+        update their scale and centering vectors: those gradients read the dictionary and must
+        see it BEFORE this step's update (reference: every gradient from the same parameters,
+        vmap(grad), autoencoders/ensemble.py:119-123)."""
+        if self.kind == "threshold" or self.learned_center:
+            self._threshold_extra_adam(reduced=reduced)
         adam_ops.adam_rows(self._adam_sets()[:1], self.lr, self.step_count + 1, *self.betas, self.eps,
                            step_dev=self.step_dev, live=self.nactive)
 
@@ -404,8 +420,6 @@ class FusedSAEEnsemble:
         if self.kind == "untied":
             adam_ops.adam_rows(self._adam_sets()[1:], self.lr, self.step_count + 1, *self.betas, self.eps,
                                step_dev=self.step_dev, live=self.nactive)
-        if self.kind == "threshold" or self.learned_center:
-            self._threshold_extra_adam(reduced=reduced_bias)
         self._bias_loss(update=True, reduced=reduced_bias)
         self._host_step()
 
@@ -415,11 +429,12 @@ class FusedSAEEnsemble:
         self._host_step()
 
     def _apply_update_kernels(self):
+        # scale / centering first: their gradients read the pre-update dictionary (adam_first)
+        if self.kind == "threshold" or self.learned_center:
+            self._threshold_extra_adam()
         if not self.fuse_adam:  # with fuse_adam the weights were already updated in wgrad_adam
             adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
                                step_dev=self.step_dev, live=self.nactive, **self._adam_split_kw())
-        if self.kind == "threshold" or self.learned_center:
-            self._threshold_extra_adam()
         self._bias_loss(update=True, reduced=False)
 
     def _threshold_extra_adam(self, reduced: bool = False):
@@ -443,6 +458,7 @@ class FusedSAEEnsemble:
             g_c += (self._x_rsum if reduced else self.rcol.sum(dim=1)) * a
         else:
             g_c = torch.bmm(self._gsum.unsqueeze(1).to(torch.bfloat16), self.enc_shadow).squeeze(1).float() * (-a)
+        self.last_center_grad = g_c  # (inspection / tests: the centering gradient of this step)
         if self.learned_center:
             upd = (("center", g_c),)
         else:
@@ -552,10 +568,26 @@ class FusedSAEEnsemble:
                                step_dev=self.step_dev, live=self.nactive, **self._adam_split_kw())
             main.wait_stream(self._side)
             self.step_dev += 1
+        elif self.fused_bwd and self.grad_scale == 1.0:
+            self.forward(x, count, target)
+            self._bwd_adam(x)
         else:
             self.forward(x, count, target)
             self.backward_weights(x)
             self._apply_update_kernels()
+
+    def _bwd_adam(self, x):
+        """Fused weight gradients + Adam (+ shadows, norms), then bias Adam and the losses."""
+        if self.learned_center:
+            self._threshold_extra_adam()  # reads the pre-update dictionary
+        if self.kind == "untied":
+            sets = [dict(p=self.params["encoder"], m=self.m["encoder"], v=self.v["encoder"], shadow=self.enc_shadow),
+                    dict(p=self.params["decoder"], m=self.m["decoder"], v=self.v["decoder"], shadow=self.dec_shadow)]
+        else:
+            sets = [dict(p=self.params["encoder"], m=self.m["encoder"], v=self.v["encoder"], shadow=self.enc_shadow)]
+        adam_ops.bwd_adam(self.kind != "untied", self.c, self.dpre, self.r, x, self._alpha, sets, self.norms,
+                          self.lr, self.step_dev, *self.betas, self.eps, nactive=self.nactive)
+        self._bias_loss(update=True, reduced=False)
 
     def _overlap_tail(self) -> bool:
         """Side-stream tail (SC_OVERLAP_TAIL=1, opt-in) for plain untied / tied steps.  A/B on

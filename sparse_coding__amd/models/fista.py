@@ -101,11 +101,18 @@ class FunctionalFista(DictSignature):
 
 
 def _unrolled_fista_residual(X, D, lam, A0, iters, eta=None):
-    """Differentiable FISTA residual X - A_T D (eta via eigvalsh, detached, as upstream) through
-    ``ops.fista.unrolled_fista_residual``: an explicit adjoint sweep (HIP slabs + MFMA GEMMs on
-    the GPU, fp32 torch otherwise) instead of autograd through every iteration."""
+    """Differentiable FISTA residual X - A_T D.  eta = 1 / eigvalsh(D D^T).max() is computed from
+    the differentiable dictionary and NOT detached, as upstream (reference fista.py:104-106), so
+    the gradient includes the path through the step size.  Plain tensors go through
+    ``ops.fista.unrolled_fista_residual`` (explicit adjoint sweep: HIP slabs + MFMA GEMMs on the
+    GPU, fp32 torch otherwise); under functorch transforms (``FunctionalEnsemble``'s
+    vmap(grad(loss))) the iterations run as plain differentiable torch ops."""
     if eta is None:
-        eta = 1.0 / torch.linalg.eigvalsh(D @ D.T).max().detach()
+        eta = 1.0 / torch.linalg.eigvalsh(D @ D.T).max()
+    wrapped = any(torch.is_tensor(t) and torch._C._functorch.is_functorch_wrapped_tensor(t)
+                  for t in (X, D, A0, eta, lam))
+    if wrapped:
+        return fista_ops.unrolled_fista_plain(X, D[None], lam, A0[None], iters, eta)[0]
     R = fista_ops.unrolled_fista_residual(X, D[None], lam, A0[None], iters, eta)
     return R[0]
 

@@ -89,6 +89,9 @@ def _declare(lib):
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
         "sc_basis_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int,
                            c_void_p],
+        "sc_bwd_adam": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_float,
+                        C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
+                        c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_void_p, c_void_p],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -102,8 +105,22 @@ def _declare(lib):
     return lib
 
 
+def verify_provenance(path: Path = _LIB_PATH) -> str:
+    """Check that the library at ``path`` was built from this tree's kernel sources (the sha256
+    ``build.source_hash()`` compiled into it); raises ``KernelError`` otherwise.  Returns the hash."""
+    from . import build as _build
+
+    want = _build.source_hash()
+    have = _build.embedded_hash(path)
+    if have != want:
+        raise KernelError(f"{path.name} was built from different kernel sources (library {have[:12] or 'untagged'}, "
+                          f"tree {want[:12]}): rebuild with `python -m sparse_coding__amd.ops.build`")
+    return want
+
+
 def lib():
-    """Return the loaded kernel library, building it in-tree if needed."""
+    """Return the loaded kernel library, building it in-tree if it is missing.  A library built
+    from other sources than this tree's is refused (``verify_provenance``), never loaded."""
     global _lib
     if _lib is not None:
         return _lib
@@ -116,7 +133,13 @@ def lib():
             from . import build as _build
 
             _build.build(verbose=False)
-        _lib = _declare(C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL))
+        want = verify_provenance(_LIB_PATH)
+        lib_ = C.CDLL(str(_LIB_PATH), mode=C.RTLD_GLOBAL)
+        lib_.sc_source_hash.restype = C.c_char_p
+        got = lib_.sc_source_hash().decode()
+        if got != want:  # (the bytes check above and the loaded symbol must agree)
+            raise KernelError(f"loaded {_LIB_PATH.name} reports source hash {got[:12]}, tree is {want[:12]}")
+        _lib = _declare(lib_)
         return _lib
 
 

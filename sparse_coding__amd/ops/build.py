@@ -2,7 +2,10 @@
 
 The kernels are plain HIP (no torch headers) exposed through a C ABI, so each
 translation unit compiles in seconds with ``hipcc --offload-arch=gfx950`` and
-the resulting ``_sc_kernels.so`` travels with the repository snapshot.  The
+the resulting ``_sc_kernels.so`` travels with the repository snapshot.  A sha256
+of every source, header and flag is compiled into the library (``sc_source_hash``);
+objects are rebuilt when their inputs' digest changes (not only their mtimes), and the
+loader refuses a library whose hash does not match the tree (``_lib.lib()``).  The
 library is loaded with ctypes *after* ``import torch`` so its NEEDED
 ``libamdhip64.so.7`` resolves to the HIP runtime torch already mapped (one
 runtime per process).
@@ -17,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -50,9 +54,43 @@ def _headers():
     return sorted(CSRC.glob("*.h")) + sorted((CSRC / "runtime").glob("*.h"))
 
 
-def _stale(target: Path, deps) -> bool:
+HASH_TAG = b"SC_SOURCE_HASH:"
+
+
+def _digest(paths, extra: str = "") -> str:
+    h = hashlib.sha256(extra.encode())
+    for p in paths:
+        h.update(p.relative_to(CSRC).as_posix().encode() + b"\0")
+        h.update(p.read_bytes())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def source_hash() -> str:
+    """sha256 over every kernel source, header and build flag: the identity of the library
+    that ``build()`` produces from this tree.  It is compiled INTO ``_sc_kernels.so``
+    (``sc_source_hash()``), and ``_lib.lib()`` refuses a library whose hash differs."""
+    return _digest(_kernel_sources() + _headers(), f"{ARCH}|{sorted(EXTRA_FLAGS.items())}")
+
+
+def embedded_hash(path: Path = None) -> str:
+    """The source hash baked into a built library (read from its bytes, without loading it)."""
+    data = Path(path or LIB).read_bytes()
+    i = data.find(HASH_TAG)
+    if i < 0:
+        return ""
+    return data[i + len(HASH_TAG): i + len(HASH_TAG) + 64].decode("ascii", "replace")
+
+
+def _stale(target: Path, deps, key: str = None) -> bool:
+    """Rebuild when the target is missing, older than a dependency, or (``key``) built from
+    different contents (a sidecar ``.hash`` records the digest the object was built from)."""
     if not target.exists():
         return True
+    if key is not None:
+        side = target.with_suffix(target.suffix + ".hash")
+        if not side.exists() or side.read_text() != key:
+            return True
     t = target.stat().st_mtime
     return any(d.stat().st_mtime > t for d in deps)
 
@@ -65,7 +103,8 @@ EXTRA_FLAGS = {"sae_gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 def _compile_one(src: Path, force: bool) -> Path:
     obj = BUILD / (src.stem + ".o")
-    if not force and not _stale(obj, [src, *_headers()]):
+    key = _digest([src, *_headers()], f"{ARCH}|{EXTRA_FLAGS.get(src.name, [])}")
+    if not force and not _stale(obj, [src, *_headers()], key):
         return obj
     cmd = [
         _hipcc(),
@@ -84,6 +123,21 @@ def _compile_one(src: Path, force: bool) -> Path:
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{res.stderr}")
+    obj.with_suffix(obj.suffix + ".hash").write_text(key)
+    return obj
+
+
+def _provenance_object(digest: str) -> Path:
+    """A one-function host object carrying the source hash (``sc_source_hash()``)."""
+    src = BUILD / "provenance.cpp"
+    src.write_text('extern "C" const char* sc_source_hash() {\n'
+                   f'  static const char tag[] = "{HASH_TAG.decode()}{digest}";\n'
+                   f'  return tag + {len(HASH_TAG)};\n}}\n')
+    obj = BUILD / "provenance.o"
+    cxx = shutil.which("g++") or "c++"
+    res = subprocess.run([cxx, "-O2", "-fPIC", "-c", str(src), "-o", str(obj)], capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"provenance object failed:\n{res.stderr}")
     return obj
 
 
@@ -107,7 +161,9 @@ def build(force: bool = False, verbose: bool = True) -> Path:
     with cf.ThreadPoolExecutor(workers) as ex:
         objs = list(ex.map(lambda s: _compile_one(s, force), srcs))
         rt_objs = list(ex.map(lambda s: _compile_host(s, force), rt_srcs))
-    if force or _stale(LIB, objs):
+    digest = source_hash()
+    if force or _stale(LIB, objs) or embedded_hash(LIB) != digest:
+        objs = objs + [_provenance_object(digest)]
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB)]
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:

@@ -236,11 +236,66 @@ def quadratic_basis_update(D, Res, A, H, lowest_activation=0.001, step=0.001, no
 
 
 # --------------------------------------------------------------------- FISTA in the loss
+class _TrackedEta(torch.autograd.Function):
+    """eta = 1 / lambda_max(D D^T) from an ``EtaTracker`` (warm power iteration), differentiable
+    in D: with u the top right singular vector of D (the tracker's eigenvector of D^T D),
+    d lambda_max / dD = 2 (D u) u^T, so dD = etabar * (-eta^2) * 2 (D u) u^T."""
+
+    @staticmethod
+    def forward(ctx, D, tracker):
+        eta = tracker(D.detach())
+        u = tracker.v.detach().to(D.dtype)  # [G, d, 1]
+        ctx.save_for_backward(D.detach(), u, eta)
+        return eta
+
+    @staticmethod
+    def backward(ctx, etabar):
+        D, u, eta = ctx.saved_tensors
+        Du = torch.bmm(D, u)                                          # [G, n, 1]
+        scale = (-2.0 * etabar * eta * eta).to(D.dtype)[:, None, None]
+        return scale * torch.bmm(Du, u.transpose(1, 2)), None
+
+
+def tracked_eta(D, tracker: "EtaTracker"):
+    """Differentiable eta for the FISTA-in-the-loss objective (reference fista.py:104-106 computes
+    it from the differentiable normalised encoder and does not detach it)."""
+    return _TrackedEta.apply(D, tracker)
+
+
+def exact_eta(D):
+    """eta = 1 / eigvalsh(D D^T).max() per model, differentiable (torch's eigvalsh backward)."""
+    return 1.0 / torch.linalg.eigvalsh(D @ D.transpose(-1, -2)).amax(dim=-1)
+
+
+def unrolled_fista_plain(X, D, lam, A0, iters: int, eta):
+    """The unrolled iterations as plain differentiable torch ops (reference fista.py:141-172
+    verbatim semantics): used under functorch transforms (vmap / grad of a signature loss),
+    where the explicit-adjoint autograd Function does not apply.  D [G, n, d], X [B, d] or
+    [G, B, d], A0 [G, B, n], lam / eta [G]."""
+    G = D.shape[0]
+    e = torch.as_tensor(eta, dtype=D.dtype, device=D.device).reshape(-1)
+    e = e.expand(G)[:, None, None] if e.numel() == 1 else e[:, None, None]
+    lam = torch.as_tensor(lam, dtype=D.dtype, device=D.device).reshape(-1)
+    thr = e * (lam.expand(G)[:, None, None] if lam.numel() == 1 else lam[:, None, None])
+    Dt = D.transpose(1, 2)
+    mom = momentum_schedule(max(iters, 1)).tolist()
+    A = A0
+    Y = A0
+    for t in range(iters):
+        A_prev = A
+        res = X - Y @ D
+        A = torch.relu(Y + e * (res @ Dt) - thr)
+        Y = A + (A - A_prev) * mom[t]
+    return X - A @ D
+
+
 def unrolled_fista_residual(X, D, lam, A0, iters: int = 50, eta=None, backend: str = "auto"):
     """R = X - A_T D after ``iters`` unrolled FISTA iterations warm-started at A0, differentiable
-    in D and A0 -- the "FISTA in the loss" term of reference autoencoders/fista.py:141-172 for
-    every model at once (D [G, n, d], X [B, d] or [G, B, d], A0 [G, B, n], lam / eta [G]; eta is
-    a constant, as the reference's detached eigvalsh).
+    in D, A0 and eta -- the "FISTA in the loss" term of reference autoencoders/fista.py:141-172
+    for every model at once (D [G, n, d], X [B, d] or [G, B, d], A0 [G, B, n], lam / eta [G]).
+    ``eta=None`` computes 1 / lambda_max(D D^T) differentiably, as the reference does (its
+    eigvalsh is not detached); a given ``eta`` tensor that requires grad receives
+    dL/deta = sum_t <Vbar_t, Res_t D^T - lam> from the adjoint sweep.
 
     Forward: the direct-form HIP solver saving the bf16 iterate slabs Y_t, Res_t, A_{t+1}
     ([G][T][B][*], 288 GB of HBM makes storing every iterate the cheap option).  Backward: the
@@ -252,7 +307,7 @@ def unrolled_fista_residual(X, D, lam, A0, iters: int = 50, eta=None, backend: s
     G = D.shape[0]
     lam = torch.as_tensor(lam, dtype=torch.float32, device=D.device).reshape(-1).expand(G).contiguous()
     if eta is None:
-        eta = step_size(D.detach())
+        eta = exact_eta(D.float())
     eta = torch.as_tensor(eta, dtype=torch.float32, device=D.device).reshape(-1).expand(G).contiguous()
     return _UnrolledFista.apply(X, D, A0, lam, eta, int(iters), backend)
 
@@ -281,13 +336,13 @@ class _UnrolledFista(torch.autograd.Function):
         if _unrolled_hip_ok(X, D, A0, backend):
             R, Db, Ys, Rs, As = unrolled_forward_hip(X, D.detach(), A0.detach(), lam, eta, iters, mom)
             ctx.hip = True
-            ctx.save_for_backward(Db, Ys, Rs, As, eta)
+            ctx.save_for_backward(Db, Ys, Rs, As, eta.detach(), lam)
             return R
         ctx.hip = False
         Df = D.detach().float()
         Xf = X.detach().float()
-        e = eta[:, None, None]
-        thr = (eta * lam)[:, None, None]
+        e = eta.detach()[:, None, None]
+        thr = (eta.detach() * lam)[:, None, None]
         A = A0.detach().float()
         Y = A
         Ys, Rs, As = [], [], []
@@ -301,24 +356,29 @@ class _UnrolledFista(torch.autograd.Function):
             Y = A + (A - A_prev) * ctx.mom[t]
         R = Xf - A @ Df
         ctx.save_for_backward(Df, torch.stack(Ys, 1) if Ys else None, torch.stack(Rs, 1) if Rs else None,
-                              torch.stack(As, 1) if As else None, eta, A)
+                              torch.stack(As, 1) if As else None, eta.detach(), A, lam)
         return R
 
     @staticmethod
     def backward(ctx, Rbar):
+        want_eta = ctx.needs_input_grad[4]
         if ctx.hip:
-            Db, Ys, Rs, As, eta = ctx.saved_tensors
-            Dbar, cbar = unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, ctx.mom, ctx.iters)
-            return None, Dbar, cbar, None, None, None, None
-        Df, Ys, Rs, As, eta, A_T = ctx.saved_tensors
-        Dbar, cbar = unrolled_backward_torch(Rbar, Df, Ys, Rs, As, eta, ctx.mom, ctx.iters, A_T)
-        return None, Dbar, cbar, None, None, None, None
+            Db, Ys, Rs, As, eta, lam = ctx.saved_tensors
+            Dbar, cbar, etabar = unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, ctx.mom, ctx.iters,
+                                                       lam=lam if want_eta else None)
+            return None, Dbar, cbar, None, etabar, None, None
+        Df, Ys, Rs, As, eta, A_T, lam = ctx.saved_tensors
+        Dbar, cbar, etabar = unrolled_backward_torch(Rbar, Df, Ys, Rs, As, eta, ctx.mom, ctx.iters, A_T,
+                                                     lam=lam if want_eta else None)
+        return None, Dbar, cbar, None, etabar, None, None
 
 
-def unrolled_backward_torch(Rbar, Df, Ys, Rs, As, eta, mom, T, A_T=None):
+def unrolled_backward_torch(Rbar, Df, Ys, Rs, As, eta, mom, T, A_T=None, lam=None):
     """fp32 adjoint sweep over saved iterate slabs ([G][T][B][*], any float dtype): the
     reference arithmetic for ``_unrolled_backward_hip`` (given the same slabs, the two differ
-    only by the bf16 rounding of Vbar / S and of the GEMM operands)."""
+    only by the bf16 rounding of Vbar / S and of the GEMM operands).  Returns (Dbar, cbar,
+    etabar); etabar = sum_t <S_t, Res_t> - lam sum Vbar_t (S_t = Vbar_t D: iteration t's
+    pre-activation is Y_t + eta (Res_t D^T - lam)) when ``lam`` is given, else None."""
     Df = Df.float()
     e = eta[:, None, None]
     Rbar = Rbar.float()
@@ -326,13 +386,16 @@ def unrolled_backward_torch(Rbar, Df, Ys, Rs, As, eta, mom, T, A_T=None):
     if A_T is None:
         A_T = As[:, T - 1]
     Dbar = -A_T.float().transpose(1, 2) @ Rbar
+    etabar = torch.zeros_like(eta) if lam is not None else None
     if T == 0:
-        return Dbar, -Rbar @ Dt
+        return Dbar, -Rbar @ Dt, etabar
     Vbar = -(Rbar @ Dt) * (As[:, T - 1] > 0)
     Ynext = torch.zeros_like(Vbar)
     cbar = None
     for t in range(T - 1, -1, -1):
         S = Vbar @ Df
+        if etabar is not None:
+            etabar = etabar + (S * Rs[:, t].float()).sum((1, 2)) - lam * Vbar.sum((1, 2))
         Dbar = Dbar + e * (Vbar.transpose(1, 2) @ Rs[:, t].float() - Ys[:, t].float().transpose(1, 2) @ S)
         Yb = Vbar - e * (S @ Dt)
         if t >= 1:
@@ -340,7 +403,7 @@ def unrolled_backward_torch(Rbar, Df, Ys, Rs, As, eta, mom, T, A_T=None):
         else:
             cbar = Yb - mom[0] * Ynext
         Ynext = Yb
-    return Dbar, cbar
+    return Dbar, cbar, etabar
 
 
 def unrolled_forward_hip(X, D, A0, lam, eta, iters, mom=None):
@@ -382,7 +445,9 @@ def _strided_mm(epi, layout, M, N, K, a, lda, sa, b, ldb, sb, out, ldc, sc, alph
                  [alpha], ldc, sc)
 
 
-def unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, mom, T):
+def unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, mom, T, lam=None):
+    """Adjoint sweep on the kernels; returns (Dbar, cbar, etabar) -- etabar (when ``lam`` is
+    given) = sum_t <S_t, Res_t> - lam sum Vbar_t from the saved slabs (nS_t = -S_t in Ss)."""
     from . import gemm
 
     G, n, d = Db.shape
@@ -430,7 +495,13 @@ def unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, mom, T):
     Dfin = torch.empty(G, n, d, device=dev)
     gemm.weight_grads([[(As[:, T - 1].contiguous(), Rb)]], [Dfin], -1.0)
     Dbar.mul_(eta[:, None, None]).add_(Dfin)
-    return Dbar, cbar
+    etabar = None
+    if lam is not None:
+        etabar = torch.zeros(G, device=dev)
+        for t in range(T):  # slab by slab (fp32 temporaries of one iterate, not of all T)
+            etabar -= (Ss[:, t].float() * Rs[:, t].float()).sum((1, 2))
+            etabar -= lam * Vs[:, t].float().sum((1, 2))
+    return Dbar, cbar, etabar
 
 
 # --------------------------------------------------------------------- direct coefficient search

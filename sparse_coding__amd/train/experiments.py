@@ -386,9 +386,7 @@ def run_fista_in_loss(argv=None):
 def run_synthetic_test(argv=None):
     """Synthetic ground-truth grid: n_ground_truth in {1024, 2048} x nonzero in {10, 50, 100},
     noise 0.1 (reference ``synthetic_test`` :817-851)."""
-    import shutil
-
-    from .sweep import sweep
+    from .sweep import remove_synthetic_dataset, sweep
 
     for noise, nz, ngt in product([0.1], [10, 50, 100], [1024, 2048]):
         cfg = _cfg(argv, cls=SyntheticEnsembleArgs, use_synthetic_dataset=True,
@@ -396,7 +394,7 @@ def run_synthetic_test(argv=None):
                    activation_width=512, feature_prob_decay=1.0, lr=1e-3, n_chunks=10, correlated_components=False,
                    noise_magnitude_scale=noise, n_ground_truth_components=ngt, feature_num_nonzero=nz,
                    output_folder=f"output_synthetic_{noise:.2E}_{ngt}_{nz}")
-        shutil.rmtree(cfg.dataset_folder, ignore_errors=True)  # regenerate per ground-truth setting
+        remove_synthetic_dataset(cfg.dataset_folder)  # regenerate per setting (only our own generated chunks)
         sweep(synthetic_linear_range, cfg)
 
 

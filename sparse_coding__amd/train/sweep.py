@@ -248,6 +248,23 @@ def sweep(ensemble_init_func, cfg, info: Optional[DistInfo] = None) -> List[Tupl
     return learned_dicts
 
 
+SYNTHETIC_MARKER = ".sc_synthetic_dataset"
+
+
+def remove_synthetic_dataset(folder: str) -> bool:
+    """Delete ``folder`` only if this package generated it (marker file present); a folder of
+    harvested or user activations is never touched.  Returns True when something was removed."""
+    import shutil
+
+    if not os.path.isdir(folder):
+        return False
+    if not os.path.exists(os.path.join(folder, SYNTHETIC_MARKER)):
+        raise RuntimeError(f"refusing to delete {folder!r}: it was not written by the synthetic dataset "
+                           f"generator (no {SYNTHETIC_MARKER} marker)")
+    shutil.rmtree(folder)
+    return True
+
+
 def _create_dataset(cfg, device):
     """Reference init_synthetic_dataset / init_model_dataset (big_sweep.py:271-338)."""
     from ..data.chunks import save_chunk
@@ -268,6 +285,9 @@ def _create_dataset(cfg, device):
                 parts.append(gen.send(None).half())
                 have += parts[-1].shape[0]
             save_chunk(torch.cat(parts)[:rows], cfg.dataset_folder, i)
+        # marker: this folder holds generated chunks only (runners may delete it to regenerate)
+        with open(os.path.join(cfg.dataset_folder, SYNTHETIC_MARKER), "w") as f:
+            f.write("synthetic chunks written by sparse_coding__amd.train.sweep\n")
         torch.save({"feats": gen.sparse_component_dict.cpu(), "probs": gen.sparse_component_probs.cpu()},
                    os.path.join(cfg.output_folder, "generator.pt"))
     else:

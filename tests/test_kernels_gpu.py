@@ -857,8 +857,8 @@ def test_unrolled_fista_hip_adjoint_matches_fp32():
     R_ref = F.unrolled_fista_residual(X, D, lam, c, T, eta, backend="torch")
     mom = F.momentum_schedule(T)
     R, Db, Ys, Rs, As = F.unrolled_forward_hip(X, D, c, lam, eta, T, mom)
-    Dh, ch = F.unrolled_backward_hip(W, Db, Ys, Rs, As, eta, mom.tolist(), T)
-    Dr, cr = F.unrolled_backward_torch(W, Db.float(), Ys, Rs, As, eta, mom.tolist(), T)
+    Dh, ch, _ = F.unrolled_backward_hip(W, Db, Ys, Rs, As, eta, mom.tolist(), T)
+    Dr, cr, _ = F.unrolled_backward_torch(W, Db.float(), Ys, Rs, As, eta, mom.tolist(), T)
     torch.cuda.synchronize()
     for g in range(G):
         rel = lambda a, b: ((a[g] - b[g]).norm() / b[g].norm()).item()  # noqa: E731
@@ -938,8 +938,9 @@ def test_fused_topk_encode_matches_reference_encode():
 def test_tied_centered_center_update_direction_at_dense_codes():
     """Learned-centre tied SAE with dense codes (bias 0, about half the atoms on): the two
     terms of the centre gradient largely cancel, so they come from fp32 data (the decoder
-    epilogue's fp32 residual column sums, fp32 masters).  One Adam step from zero moments moves
-    the centre by ~lr sign(g): the signs must agree with the eager fp32 ensemble's."""
+    epilogue's fp32 residual column sums, fp32 masters of the PRE-update dictionary).  The
+    gradient must match autograd of the eager fp32 ensemble, and one Adam step from zero
+    moments (~lr sign(g)) must move the centre the same way."""
     from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
     from sparse_coding__amd.engine.fused import FusedSAEEnsemble
     from sparse_coding__amd.engine.optim import adam
@@ -956,10 +957,16 @@ def test_tied_centered_center_update_direction_at_dense_codes():
     fused = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=DEV)
     feats = torch.nn.functional.normalize(torch.randn(1024, d, device=DEV), dim=-1)
     x = ((torch.relu(torch.randn(B, 1024, device=DEV) - 1.0) * 2.0) @ feats + 0.3).to(torch.bfloat16)
+    grads, _ = ref.compute_grads(x.float())
     ref.step_batch(x.float())
     out = fused.step_batch(x)
     torch.cuda.synchronize()
     assert float(out[:, 4].min()) > 0.3 * n, "codes must be dense for this test"
+    # the gradient itself (from the PRE-update dictionary, as vmap(grad) in the reference)
+    g_ref, g_fused = grads["center"].float(), fused.last_center_grad.float()
+    for g in range(len(models)):
+        rel = ((g_fused[g] - g_ref[g]).norm() / g_ref[g].norm()).item()
+        assert rel < 5e-2, (g, rel)
     init = torch.stack([m[0]["center"] for m in models]).to(DEV)
     mf, mr = fused.params["center"] - init, ref.params["center"] - init
     big = mr.abs() > 0.5e-3  # Adam's first step: ~lr where the gradient is not tiny

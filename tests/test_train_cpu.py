@@ -155,7 +155,16 @@ def test_sweep_synthetic_end_to_end(tmp_path):
     cfg = _sweep_cfg(tmp_path)
     lds = sweep(_tiny_init, cfg)
     assert len(lds) == 4
-    assert sorted(os.listdir(cfg.dataset_folder)) == ["0.pt", "1.pt"]
+    assert sorted(f for f in os.listdir(cfg.dataset_folder) if not f.startswith(".")) == ["0.pt", "1.pt"]
+    # generated by us: a runner may delete it; a user's folder is refused
+    from sparse_coding__amd.train.sweep import remove_synthetic_dataset
+
+    user = tmp_path / "user_acts"
+    user.mkdir()
+    (user / "0.pt").write_bytes(b"not ours")
+    with pytest.raises(RuntimeError, match="refusing"):
+        remove_synthetic_dataset(str(user))
+    assert (user / "0.pt").exists()
     last = os.path.join(cfg.output_folder, "_1", "learned_dicts.pt")
     loaded = ckpt.load_learned_dicts(last)
     np.testing.assert_allclose([hp["l1_alpha"] for _, hp in loaded], [1e-4, 1e-3, 1e-4, 1e-3], rtol=1e-6)
