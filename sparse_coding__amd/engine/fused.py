@@ -51,8 +51,7 @@ class FusedSAEEnsemble:
 
     def __init__(self, models, sig, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999),
                  eps=1e-8, track_feature_counts=True, kind: Optional[str] = None, fuse_adam: bool = False,
-                 count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None,
-                 fused_bwd: Optional[bool] = None):
+                 count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
         # FunctionalTiedCenteredSAE (sae_ensemble.py:162-228): the tied kernels on x - center
@@ -218,15 +217,6 @@ class FusedSAEEnsemble:
         # MI355X (the streaming Adam crowds the GEMM's CUs), kept as an option.
         self.overlap_adam = False
         self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
-        # Weight gradients + Adam in ONE kernel (csrc/sae_bwd.hip: a workgroup owns 64 dictionary
-        # rows of a model over the whole batch, the fp32 gradients never reach HBM).  Auto: plain
-        # ReLU SAEs (untied / tied) whose ensemble has >= 256 such row blocks, on one device (data
-        # parallel paths reduce the gradients between the two halves and use the split kernels).
-        bwd_ok = (self.kind in ("untied", "tied") and not fuse_adam and adam_ops.shape_ok(B, n, d)
-                  and (self.nactive is None or bool((self.nactive % 64 == 0).all())))
-        if fused_bwd and not bwd_ok:
-            raise ValueError(f"fused_bwd: unsupported configuration (kind {self.kind}, B={B}, n={n}, d={d})")
-        self.fused_bwd = bwd_ok if fused_bwd else (fused_bwd is None and bwd_ok and adam_ops.bwd_fills_gpu(G, n))
         self.dotpart = torch.zeros(G, tm, n, device=dev)        # norm-Jacobian row-dot partials
         self.sqpart = torch.zeros(G, n, d // 128, device=dev)   # updated-row |w|^2 partials
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)  # graph input buffer
@@ -415,6 +405,11 @@ class FusedSAEEnsemble:
         adam_ops.adam_rows(self._adam_sets()[:1], self.lr, self.step_count + 1, *self.betas, self.eps,
                            step_dev=self.step_dev, live=self.nactive)
 
+    def adam_rows_all(self):
+        """Row Adam on every dictionary set (data-parallel update after the reduction)."""
+        adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
+                           step_dev=self.step_dev, live=self.nactive)
+
     def adam_second(self, reduced_bias=True):
         """Encoder Adam (untied) and bias Adam + loss reduction (advances the step counter)."""
         if self.kind == "untied":
@@ -568,26 +563,10 @@ class FusedSAEEnsemble:
                                step_dev=self.step_dev, live=self.nactive, **self._adam_split_kw())
             main.wait_stream(self._side)
             self.step_dev += 1
-        elif self.fused_bwd and self.grad_scale == 1.0:
-            self.forward(x, count, target)
-            self._bwd_adam(x)
         else:
             self.forward(x, count, target)
             self.backward_weights(x)
             self._apply_update_kernels()
-
-    def _bwd_adam(self, x):
-        """Fused weight gradients + Adam (+ shadows, norms), then bias Adam and the losses."""
-        if self.learned_center:
-            self._threshold_extra_adam()  # reads the pre-update dictionary
-        if self.kind == "untied":
-            sets = [dict(p=self.params["encoder"], m=self.m["encoder"], v=self.v["encoder"], shadow=self.enc_shadow),
-                    dict(p=self.params["decoder"], m=self.m["decoder"], v=self.v["decoder"], shadow=self.dec_shadow)]
-        else:
-            sets = [dict(p=self.params["encoder"], m=self.m["encoder"], v=self.v["encoder"], shadow=self.enc_shadow)]
-        adam_ops.bwd_adam(self.kind != "untied", self.c, self.dpre, self.r, x, self._alpha, sets, self.norms,
-                          self.lr, self.step_dev, *self.betas, self.eps, nactive=self.nactive)
-        self._bias_loss(update=True, reduced=False)
 
     def _overlap_tail(self) -> bool:
         """Side-stream tail (SC_OVERLAP_TAIL=1, opt-in) for plain untied / tied steps.  A/B on

@@ -89,9 +89,6 @@ def _declare(lib):
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
         "sc_basis_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int,
                            c_void_p],
-        "sc_bwd_adam": [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_float,
-                        C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
-                        c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_void_p, c_void_p],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)

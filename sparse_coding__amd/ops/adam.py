@@ -107,55 +107,3 @@ def normalize_rows(shadow, sqpart, norms):
                                       _lib.stream_handle())
     _lib.check(rc, "sc_normalize_rows")
 
-
-def bwd_adam(tied: bool, c, dpre, R, x, alpha: float, sets, norms, lr, step_dev, b1=0.9, b2=0.999, eps=1e-8,
-             nactive=None):
-    """Fused weight gradient + Adam (``csrc/sae_bwd.hip``): dW_e = alpha dpre^T x and
-    dW_hat = alpha c^T R (tied: their sum) accumulated over the whole batch in registers, then
-    Adam with the norm Jacobian on the row-normalised set, bf16 shadows and new row norms --
-    the fp32 gradients never reach HBM.
-
-    c, dpre: bf16 [G, B, n]; R: bf16 [G, B, d]; x: bf16 [B, d] or [G, B, d].
-    sets: untied -> [encoder, decoder], tied -> [dictionary]; each a dict of fp32 p, m, v
-    [G, n, d] and a bf16 ``shadow``.  norms: fp32 [G, n] (written).  step_dev: int32 device
-    counter of completed steps.  d must be 256 or 512, B % 32 == 0, n % 64 == 0."""
-    G, B, n = c.shape
-    d = R.shape[-1]
-    if not shape_ok(B, n, d):
-        raise ValueError(f"bwd_adam: unsupported shape B={B} n={n} d={d} (d in 256/512, B % 32, n % 64)")
-    for t in (c, dpre, R, x):
-        if t.dtype != torch.bfloat16 or not t.is_contiguous():
-            raise ValueError("bwd_adam operands must be contiguous bf16")
-    if tuple(dpre.shape) != (G, B, n) or tuple(R.shape) != (G, B, d) or x.shape[-2:] != (B, d):
-        raise ValueError("bwd_adam: operand shapes disagree")
-    if len(sets) != (1 if tied else 2):
-        raise ValueError("bwd_adam: untied takes [encoder, decoder], tied [dictionary]")
-    for s in sets:
-        for k in ("p", "m", "v"):
-            t = s[k]
-            if t.dtype != torch.float32 or tuple(t.shape) != (G, n, d) or not t.is_contiguous():
-                raise ValueError(f"bwd_adam: {k} must be contiguous fp32 {(G, n, d)}")
-        sh = s["shadow"]
-        if sh.dtype != torch.bfloat16 or tuple(sh.shape) != (G, n, d) or not sh.is_contiguous():
-            raise ValueError("bwd_adam: shadow must be contiguous bf16 [G, n, d]")
-    if nactive is not None and bool((nactive.cpu() % 64 != 0).any()):
-        raise ValueError("bwd_adam: masked live sizes must be multiples of 64")
-    full = [sets[0], sets[0]] if tied else sets
-    sx = B * d if x.dim() == 3 else 0
-    rc = _lib.lib().sc_bwd_adam(int(bool(tied)), G, B, n, d, _lib.ptr(c), _lib.ptr(dpre), _lib.ptr(R), _lib.ptr(x),
-                                sx, float(alpha), _vp([s["p"] for s in full]), _vp([s["m"] for s in full]),
-                                _vp([s["v"] for s in full]), _vp([s["shadow"] for s in full]), _lib.ptr(norms),
-                                _lib.ptr(lr), _lib.ptr(step_dev), float(b1), float(b2), float(eps),
-                                _lib.ptr(nactive), _lib.stream_handle())
-    _lib.check(rc, "sc_bwd_adam")
-
-
-def shape_ok(B: int, n: int, d: int) -> bool:
-    """Shapes the fused weight-gradient + Adam kernel handles."""
-    return d in (256, 512) and B % 32 == 0 and n % 64 == 0
-
-
-def bwd_fills_gpu(G: int, n: int, n_cus: int = 256) -> bool:
-    """The fused kernel runs one workgroup (one CU) per 64 dictionary rows of a model; with
-    fewer rows than CUs in the ensemble the split-K GEMM + streaming Adam path is faster."""
-    return G * (n // 64) >= n_cus
