@@ -15,7 +15,9 @@ N > 1 GPUs (weak scaling: 2048 rows per GPU per step), ``--parallelism``:
       gradients;
   dp  data parallel: every rank holds all 8 models, gradients are all-reduced (RCCL over
       xGMI) in model chunks overlapped with the next chunk's compute (BASELINE config 3's
-      mechanism).
+      mechanism); each chunk's kernels replay from HIP graphs.
+  zero1  data parallel with ZeRO-1: reduce-scatter of the gradients onto row owners, Adam on
+      the owned rows only, all-gather of the bf16 shadows (parallel/zero.py).
 The run times the other strategy too (untimed for the headline) and reports it under
 ``alt_parallelism`` in the JSON line.
 
@@ -29,7 +31,6 @@ from __future__ import annotations
 import argparse
 import json
 import math
-import os
 import sys
 import time
 
@@ -69,11 +70,12 @@ def parse(argv=None):
                     help="after the timed region, keep training (untimed) until this many steps in total "
                          "before the FVU@L0 evaluation (the timed K steps alone are far from converged)")
     ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32")
-    ap.add_argument("--parallelism", choices=["auto", "es", "dp"], default="auto",
+    ap.add_argument("--parallelism", choices=["auto", "es", "dp", "zero1"], default="auto",
                     help="N>1: 'es' = ensemble-axis sharding (each GPU owns models/N models and trains "
                          "them on the all-gathered global batch: identical updates to data parallel on the "
                          "global batch, but only the 2 MB batch crosses xGMI instead of 67 MB of gradients); "
-                         "'dp' = data parallel with chunk-pipelined RCCL gradient all-reduce; "
+                         "'dp' = data parallel with chunk-pipelined RCCL gradient all-reduce; 'zero1' = data "
+                         "parallel with reduce-scatter, row-sharded Adam and a bf16 shadow all-gather; "
                          "auto = es when models %% N == 0")
     ap.add_argument("--dp-chunks", type=int, default=2,
                     help="N>1: split the ensemble into this many model chunks whose gradient all-reduce "
@@ -89,10 +91,7 @@ def parse(argv=None):
     ap.add_argument("--compare-parallelism", type=int, default=1,
                     help="N>1: after the headline run, also time the other strategy (es <-> dp) and report it "
                          "under alt_parallelism")
-    ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of a HIP graph")
-    ap.add_argument("--fuse-adam", type=int, default=-1,
-                    help="1: Adam inside the weight-gradient GEMM epilogue (single GPU); 0: separate streaming "
-                         "Adam kernel; -1: the engine default")
+    ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of HIP graphs")
     return ap.parse_args(argv)
 
 
@@ -148,49 +147,38 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
     if args.engine == "fused" and distributed:
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
+        from sparse_coding__amd.parallel.zero import ZeroFusedChunk
 
         engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device)
                    for m in split_models(models, args.dp_chunks)]
-        # cross-step: the last chunk's all-reduce overlaps the next step's first (encoder) GEMMs
-        trainer = ChunkedDataParallel([FusedChunk(e) for e in engines], info, grad_dtype, cross_step=True)
         xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
+        graph = not args.no_graph  # each chunk's compute and update replay from HIP graphs
+        if par == "zero1":
+            chunks = [ZeroFusedChunk(e, info, grad_dtype, graph=graph, x_static=xbuf) for e in engines]
+        else:
+            chunks = [FusedChunk(e, graph=graph, x_static=xbuf) for e in engines]
+        # cross-step: the last chunk's collectives overlap the next step's first (encoder) GEMMs
+        trainer = ChunkedDataParallel(chunks, info, grad_dtype, cross_step=True)
+
+        def dicts():
+            trainer.flush()
+            for c in chunks:  # ZeRO-1: every rank gathers the current masters before exporting
+                if hasattr(c, "gather_masters"):
+                    c.gather_masters()
+            return [ld for e in engines for ld in e.to_learned_dicts(device)]
+
         return Runner(lambda: trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf)),
-                      lambda: [ld for e in engines for ld in e.to_learned_dicts(device)],
-                      finish=trainer.flush, close=trainer.flush)
+                      dicts, finish=trainer.flush, close=trainer.flush)
     if args.engine == "fused":
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
 
-        kw = {} if args.fuse_adam < 0 else {"fuse_adam": bool(args.fuse_adam)}
-        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device, **kw)
+        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
         if not args.no_graph:
             eng.enable_graph()  # whole step = one HIP graph replay
-        if args.no_graph or os.environ.get("SC_BENCH_PREFETCH", "0") in ("", "0"):
-            def step():
-                ring.sample_shard(B, 0, 1, out=eng.x_static)
-                eng.step_static() if not args.no_graph else eng.step_batch(eng.x_static)
-
-            return Runner(step, lambda: eng.to_learned_dicts(device))
-        # double-buffered batch fetch (SC_BENCH_PREFETCH=1, opt-in): the gather of step t+1's rows
-        # runs on a side stream under step t's graph (two graphs, one per input buffer).  A/B'd
-        # slower on MI355X: 0.339 vs 0.325 ms/step (profiles/stream_overlap_ab_r2.json)
-        bufs = [eng.x_static, torch.empty_like(eng.x_static)]
-        eng.add_static_input(bufs[1])
-        fetch = torch.cuda.Stream(device=device)
-        st = {"cur": 0, "ev": None}
-        ring.sample_shard(B, 0, 1, out=bufs[0])
 
         def step():
-            main = torch.cuda.current_stream(device)
-            cur = st["cur"]
-            if st["ev"] is not None:
-                main.wait_event(st["ev"])       # this step's rows have landed
-            fetch.wait_stream(main)             # buffer 1-cur was last read by the previous step
-            with torch.cuda.stream(fetch):
-                ring.sample_shard(B, 0, 1, out=bufs[1 - cur])
-                st["ev"] = torch.cuda.Event()
-                st["ev"].record(fetch)
-            eng.step_static(cur)
-            st["cur"] = 1 - cur
+            ring.sample_shard(B, 0, 1, out=eng.x_static)
+            eng.step_static() if not args.no_graph else eng.step_batch(eng.x_static)
 
         return Runner(step, lambda: eng.to_learned_dicts(device))
     from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
@@ -201,6 +189,19 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
     trainer = DataParallelEnsemble(ens, info)
     return Runner(lambda: trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size).float()),
                   lambda: ens.to_learned_dicts(device))
+
+
+def comm_bytes(mode, args, world):
+    """Per-GPU bytes sent per step by the data-parallel modes at this config (parallel/zero.py):
+    dp all-reduces the weight + bias gradients, zero1 reduce-scatters them and all-gathers the
+    bf16 shadows, es all-gathers the batch."""
+    from sparse_coding__amd.parallel.zero import comm_bytes_per_step
+
+    n = args.d * args.ratio
+    params = args.models * (2 * n * args.d + n)
+    gbytes = 2 if args.grad_dtype == "bf16" else 4
+    return comm_bytes_per_step(mode, world, params * gbytes, shadow_bytes=args.models * 2 * n * args.d * 2,
+                               batch_bytes=args.batch * args.d * 2)
 
 
 def timed(runner, steps, info, B):
@@ -248,6 +249,8 @@ def main(argv=None):
         par = "es" if (distributed and args.models % info.world_size == 0) else "dp"
     if not distributed:
         par = "dp"  # one GPU: the plain fused step (no collectives)
+    if par == "es" and args.models % info.world_size:
+        raise SystemExit(f"--parallelism es needs models % N == 0 ({args.models} models, N={info.world_size})")
 
     runner = make_runner(par, args, info, sig, models, ring, device, grad_dtype)
     for _ in range(args.warmup):
@@ -272,7 +275,7 @@ def main(argv=None):
     # BASELINE config 3's mechanism -- and the ensemble-sharded path are on record)
     alt = None
     if distributed and args.compare_parallelism and args.models % info.world_size == 0:
-        other = "dp" if par == "es" else "es"
+        other = "dp" if par in ("es", "zero1") else "es"
         alt_models = [sig.init(args.d, n, float(l1), device=device) for l1 in l1s]
         alt_runner = make_runner(other, args, info, sig, alt_models, ring, device, grad_dtype)
         for _ in range(args.warmup):
@@ -280,7 +283,8 @@ def main(argv=None):
         a_ms, a_value = timed(alt_runner, args.steps, info, B)
         alt_runner.close()
         alt = {"parallelism": f"{other}{info.world_size}", "value": round(a_value, 1), "ms_per_step": round(a_ms, 4),
-               "dp_chunks": args.dp_chunks if other == "dp" else None}
+               "dp_chunks": args.dp_chunks if other == "dp" else None,
+               "comm_bytes_per_gpu_per_step": comm_bytes(other, args, info.world_size)}
 
     if info.is_main:
         rec = {
@@ -305,9 +309,12 @@ def main(argv=None):
                 "per_gpu_batch": B,
                 "parallelism": f"{par}{info.world_size}",
                 "engine": args.engine,
-                "dp_chunks": args.dp_chunks if par == "dp" and distributed else None,
+                "dp_chunks": args.dp_chunks if par in ("dp", "zero1") and distributed else None,
                 "grad_allreduce_dtype": args.grad_dtype,
             },
+            # ring-collective bytes each GPU sends per step in this mode (analytic; 0 on one GPU)
+            "comm_bytes_per_gpu_per_step": comm_bytes(par, args, info.world_size) if distributed else 0,
+            "comm_bytes_other_modes": {m: comm_bytes(m, args, max(info.world_size, 8)) for m in ("dp", "zero1", "es")},
             "model_activations_per_s": round(value * args.models, 1),
             "baseline_note": "vs_baseline divides by BASELINE.md row 12 (reference math, same shapes, "
                              "1.86k act/s, 8-vCPU sandbox); no published GPU throughput exists.  "

@@ -106,9 +106,7 @@ def main():
         "ntbf16": (lambda: gemm.matmul_nt(x, we, c), fl),
     }
     gemm.encode_relu(x, we, bias, c, part, None, None, mask_out=cmask)
-    modes = [("tile", lambda: gemm.force_persistent(False)),
-             ("p2", lambda: gemm.force_persistent(True, nst=2)),
-             ("p3", lambda: gemm.force_persistent(True, nst=3))]
+    modes = [("tile", lambda: gemm.force_shape(1))]
     if a.cfgs:  # explicit tile-kernel configurations (block shape | pipeline << 2) instead
         modes = [(f"cfg{c}", lambda c=int(c): gemm.force_shape(c)) for c in a.cfgs.split(",")]
     cases["step_torch_enc"] = (lambda: torch.matmul(x, we.transpose(1, 2), out=c), fl)

@@ -62,7 +62,6 @@ def main():
     res["enc_mask"] = (timeit(lambda: gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c,
                                                        e.enc_part, None, None, mask_out=e.cmask)), fl)
     res["wgrad_adam"] = (timeit(lambda: e.wgrad_adam(x)), 2 * fl)
-    e.fuse_adam = False
     e.overlap_adam = False
     res["step_no_overlap"] = (timeit(lambda: e.step_batch(x)), 5 * fl)
     e.overlap_adam = False

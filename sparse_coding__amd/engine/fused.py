@@ -50,7 +50,7 @@ class FusedSAEEnsemble:
     """Fused HIP training engine; API mirrors ``FunctionalEnsemble``."""
 
     def __init__(self, models, sig, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999),
-                 eps=1e-8, track_feature_counts=True, kind: Optional[str] = None, fuse_adam: bool = False,
+                 eps=1e-8, track_feature_counts=True, kind: Optional[str] = None,
                  count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
@@ -59,15 +59,11 @@ class FusedSAEEnsemble:
         self.learned_center = self.kind == "tied_centered"
         if self.learned_center:
             self.kind = "tied"
-            if fuse_adam:
-                raise ValueError("fuse_adam is not implemented for learned-centering SAEs")
         if self.kind not in _ACTS:
             raise ValueError(f"signature {sig} has no fused implementation")
         # code activation of the encoder / code-gradient epilogues: reverse and threshold
         # SAEs are tied dictionaries with another activation (sae_ensemble.py:230-303, 445-501)
         self.act = _ACTS[self.kind]
-        if self.act and fuse_adam:
-            raise ValueError(f"fuse_adam is not implemented for {self.kind} SAEs")
         # the per-feature vector that plays the encoder bias (threshold SAEs: the gain)
         self._bkey = "activation_gain" if self.kind == "threshold" else "encoder_bias"
         self.device = torch.device(device)
@@ -208,17 +204,9 @@ class FusedSAEEnsemble:
         self.feature_counts = torch.zeros(G, n, device=dev) if track_feature_counts else None
         self.rows_seen = 0
         self.out = torch.zeros(G, 6, device=dev)
-        # Optional: Adam fused into the weight-gradient GEMM (the fp32 gradients never reach
-        # HBM).  Off by default: on MI355X the epilogue's p/m/v traffic does not overlap the
-        # MFMA phase and the separate streaming Adam kernel is faster (profiles/).  Data
-        # parallel runs always use the separate kernel (gradients are all-reduced first).
-        self.fuse_adam = fuse_adam
-        # Side-stream overlap of the decoder Adam with the encoder wgrad: measured slower on
-        # MI355X (the streaming Adam crowds the GEMM's CUs), kept as an option.
-        self.overlap_adam = False
-        self._side = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
-        self.dotpart = torch.zeros(G, tm, n, device=dev)        # norm-Jacobian row-dot partials
-        self.sqpart = torch.zeros(G, n, d // 128, device=dev)   # updated-row |w|^2 partials
+        # threshold SAEs: per-feature partial sums of the code gradient on the activation's ramp
+        # (the scale gradient's source, written by the code-gradient epilogue)
+        self.dotpart = torch.zeros(G, tm, n, device=dev) if self.kind == "threshold" else None
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)  # graph input buffer
         self._static_inputs = [self.x_static]
         if self.centering is not None or self.kind == "threshold" or self.learned_center:
@@ -301,27 +289,7 @@ class FusedSAEEnsemble:
                                act=self.act, ascale=ascale, mask2=self.cmask2, nactive=self.nactive)
             return
         gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
-                           dotpart=self.dotpart if self.fuse_adam else None,
-                           tied_bias=self.params["encoder_bias"] if (self.fuse_adam and self.kind == "tied") else None,
                            mask=self.cmask, nactive=self.nactive)
-
-    def wgrad_adam(self, x):
-        """Weight gradients with Adam in the GEMM epilogue, then the decoder-row normalisation."""
-        B = self.batch_size
-        norm_state = dict(norm=True, dotpart=self.dotpart, norms=self.norms, sqpart=self.sqpart)
-        if self.kind == "untied":
-            states = [dict(p=self.params["decoder"], m=self.m["decoder"], v=self.v["decoder"],
-                           shadow=self.dec_shadow, **norm_state),
-                      dict(p=self.params["encoder"], m=self.m["encoder"], v=self.v["encoder"],
-                           shadow=self.enc_shadow, norm=False)]
-            pairs = [[(self.c, self.r)], [(self.dpre, x)]]
-        else:
-            states = [dict(p=self.params["encoder"], m=self.m["encoder"], v=self.v["encoder"],
-                           shadow=self.enc_shadow, **norm_state)]
-            pairs = [[(self.c, self.r), (self.dpre, x)]]
-        gemm_ops.weight_grads_adam(pairs, states, self._alpha, self.lr, self.step_dev, self.betas, self.eps,
-                                   dot_tm=B // 128)
-        adam_ops.normalize_rows(self.dec_shadow, self.sqpart, self.norms)
 
     @property
     def _alpha(self):
@@ -355,15 +323,11 @@ class FusedSAEEnsemble:
                 torch.sum(self.rcol, dim=1, out=self._x_rsum)
 
     def forward_backward(self, x):
-        """Kernels 1-4 for the single-device step (both weight gradients in one launch).
-        With ``fuse_adam`` the weight gradients are consumed by Adam inside the GEMM."""
+        """Kernels 1-4 for the single-device step (both weight gradients in one launch)."""
         self.forward(x)
         self.backward_weights(x)
 
     def backward_weights(self, x):
-        if self.fuse_adam:
-            self.wgrad_adam(x)
-            return
         split = self.g_parts is not None
         self._g_from_parts = split
         self._g_from_bf = gbf = self.g_bf is not None
@@ -427,9 +391,8 @@ class FusedSAEEnsemble:
         # scale / centering first: their gradients read the pre-update dictionary (adam_first)
         if self.kind == "threshold" or self.learned_center:
             self._threshold_extra_adam()
-        if not self.fuse_adam:  # with fuse_adam the weights were already updated in wgrad_adam
-            adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
-                               step_dev=self.step_dev, live=self.nactive, **self._adam_split_kw())
+        adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
+                           step_dev=self.step_dev, live=self.nactive, **self._adam_split_kw())
         self._bias_loss(update=True, reduced=False)
 
     def _threshold_extra_adam(self, reduced: bool = False):
@@ -530,51 +493,16 @@ class FusedSAEEnsemble:
         return self
 
     def _step_kernels(self, x, count=None):
-        """All kernels of one step.  Optionally (``overlap_adam``) untied models overlap the
-        memory-bound decoder Adam (side stream) with the compute-bound encoder wgrad GEMM."""
+        """All kernels of one step (captured as one HIP graph when enabled).  Side-stream
+        variants of this sequence -- decoder Adam beside the encoder weight gradient, the loss /
+        bias-Adam tail beside the weight gradient, Adam fused into the weight-gradient epilogue,
+        a fused weight-gradient + Adam kernel -- all measured slower on MI355X and were removed
+        (profiles/README.md)."""
         target = x if self.kind == "threshold" else None
         x = self.prepare(x)
-        if (self.kind == "untied" and self.overlap_adam and not self.fuse_adam
-                and os.environ.get("SC_SERIALIZE_STREAMS", "0") in ("", "0")):
-            main = torch.cuda.current_stream(self.device)
-            sets = self._adam_sets()
-            self.forward(x, count)
-            self.wgrad_first(x)
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
-                adam_ops.adam_rows(sets[:1], self.lr, self.step_count + 1, *self.betas, self.eps,
-                                   step_dev=self.step_dev, live=self.nactive)
-            self.wgrad_second(x, reduce_bias=False)
-            adam_ops.adam_rows(sets[1:], self.lr, self.step_count + 1, *self.betas, self.eps,
-                               step_dev=self.step_dev, live=self.nactive)
-            main.wait_stream(self._side)  # join before the step counter advances
-            self._bias_loss(update=True, reduced=False)
-        elif self._overlap_tail():
-            # the loss reduction + bias Adam (G and n/32 x G small blocks; they need only the
-            # forward's partials) run on a side stream under the weight-gradient GEMM and the
-            # row Adam; the device step counter advances after the join
-            self.forward(x, count, target)
-            main = torch.cuda.current_stream(self.device)
-            self._side.wait_stream(main)
-            with torch.cuda.stream(self._side):
-                self._bias_loss(update=True, reduced=False, defer_step=True)
-            self.backward_weights(x)
-            adam_ops.adam_rows(self._adam_sets(), self.lr, self.step_count + 1, *self.betas, self.eps,
-                               step_dev=self.step_dev, live=self.nactive, **self._adam_split_kw())
-            main.wait_stream(self._side)
-            self.step_dev += 1
-        else:
-            self.forward(x, count, target)
-            self.backward_weights(x)
-            self._apply_update_kernels()
-
-    def _overlap_tail(self) -> bool:
-        """Side-stream tail (SC_OVERLAP_TAIL=1, opt-in) for plain untied / tied steps.  A/B on
-        MI355X (profiles/stream_overlap_ab_r2.json): +7 us per step -- the cross-stream edges
-        of the captured graph cost more than the ~10 us of small kernels they hide."""
-        return (self._side is not None and not self.fuse_adam and self.kind in ("untied", "tied")
-                and not self.learned_center and os.environ.get("SC_OVERLAP_TAIL", "0") not in ("", "0")
-                and os.environ.get("SC_SERIALIZE_STREAMS", "0") in ("", "0"))
+        self.forward(x, count, target)
+        self.backward_weights(x)
+        self._apply_update_kernels()
 
     def add_static_input(self, t: torch.Tensor) -> int:
         """Register another persistent input buffer [B, d] bf16: ``step_batch(t)`` then replays

@@ -28,11 +28,6 @@ class ScOperand(C.Structure):
     _fields_ = [("ptr", c_void_p), ("ld", c_long), ("sg", c_long)]
 
 
-class ScAdamEpi(C.Structure):
-    _fields_ = [("p", c_void_p), ("m", c_void_p), ("v", c_void_p), ("sh", c_void_p),
-                ("dotpart", c_void_p), ("norms", c_void_p), ("sqpart", c_void_p), ("mode", c_int)]
-
-
 class KernelError(RuntimeError):
     pass
 
@@ -43,10 +38,9 @@ def _declare(lib):
                     C.POINTER(ScOperand), C.POINTER(ScOperand), C.POINTER(c_void_p), c_float_p,
                     c_long, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long,
                     c_void_p, c_void_p, c_void_p, c_float,
-                    c_void_p, c_int, C.POINTER(ScAdamEpi), c_void_p, c_void_p, c_float, c_float, c_float,
-                    c_int, c_float, c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                    c_void_p, c_int,
+                    c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                     c_void_p, c_void_p, c_void_p],
-        "sc_normalize_rows": [c_void_p, c_void_p, c_int, c_void_p, c_long, c_int, c_void_p],
         "sc_adam_rows": [c_int, C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
                          C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
                          C.POINTER(c_int), C.POINTER(c_int), c_int, c_int, c_void_p,

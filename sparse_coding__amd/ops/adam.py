@@ -96,14 +96,3 @@ def bias_loss(b, m, v, colpart, tm, enc_part, enc_tiles, dec_part, dec_tiles, l1
         bc1, bc2, int(update), _lib.ptr(step_dev), _lib.stream_handle(), int(bool(defer_step)),
     )
     _lib.check(rc, "sc_bias_loss")
-
-
-def normalize_rows(shadow, sqpart, norms):
-    """Finish an Adam-fused decoder update: shadow[row] /= sqrt(sum(sqpart[row])), norms[row] = |w|."""
-    d = shadow.shape[-1]
-    rows = shadow.numel() // d
-    ntile = sqpart.shape[-1]
-    rc = _lib.lib().sc_normalize_rows(_lib.ptr(shadow), _lib.ptr(sqpart), ntile, _lib.ptr(norms), rows, d,
-                                      _lib.stream_handle())
-    _lib.check(rc, "sc_normalize_rows")
-

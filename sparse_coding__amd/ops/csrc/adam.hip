@@ -48,13 +48,10 @@ __device__ __forceinline__ void bias_corrections(float b1, float b2, int t, floa
   bc2 = 1.f - __powf(b2, (float)t);
 }
 
-// NT: the fp32 state (p, m, v) is written with non-temporal stores and the gradient read with
-// non-temporal loads -- none of it is touched again this step, so it should not displace the
-// next GEMMs' operands from L2 / MALL or leave dirty lines for them to write back.
 // GBF: the gradient arrives in bf16 (the weight-gradient GEMM's bf16 epilogue): 1/7 of the
 // kernel's HBM bytes less to read and half the GEMM's output stores; the moments, the master
 // and the update arithmetic stay fp32.
-template <int NV, bool NT = false, bool GBF = false>
+template <int NV, bool GBF = false>
 __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   const int lane = threadIdx.x & 63;
   const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -86,12 +83,9 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
     if constexpr (GBF) {
       const ushort4 h = *reinterpret_cast<const ushort4*>(GH + e);
       gv[i] = make_float4(bf2f(h.x), bf2f(h.y), bf2f(h.z), bf2f(h.w));
-    } else if constexpr (NT) {
-      const f32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(G4 + e));
-      gv[i] = make_float4(t[0], t[1], t[2], t[3]);
-    }
-    else
+    } else {
       gv[i] = *reinterpret_cast<const float4*>(G4 + e);
+    }
     mv_[i] = *reinterpret_cast<const float4*>(R.m + base + e);
     vv_[i] = *reinterpret_cast<const float4*>(R.v + base + e);
   }
@@ -153,16 +147,9 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
       pp[k] -= step * mm[k] / (sqrtf(vvv[k] * rbc2) + a.eps);
       ss2 += pp[k] * pp[k];
     }
-    if constexpr (NT) {
-      __builtin_nontemporal_store(f32x4_t{mv.x, mv.y, mv.z, mv.w}, reinterpret_cast<f32x4_t*>(R.m + base + e));
-      __builtin_nontemporal_store(f32x4_t{vv.x, vv.y, vv.z, vv.w}, reinterpret_cast<f32x4_t*>(R.v + base + e));
-      __builtin_nontemporal_store(f32x4_t{pv[i].x, pv[i].y, pv[i].z, pv[i].w},
-                                  reinterpret_cast<f32x4_t*>(R.p + base + e));
-    } else {
-      *reinterpret_cast<float4*>(R.m + base + e) = mv;
-      *reinterpret_cast<float4*>(R.v + base + e) = vv;
-      *reinterpret_cast<float4*>(R.p + base + e) = pv[i];
-    }
+    *reinterpret_cast<float4*>(R.m + base + e) = mv;
+    *reinterpret_cast<float4*>(R.v + base + e) = vv;
+    *reinterpret_cast<float4*>(R.p + base + e) = pv[i];
   }
   float sc = 1.f;
   if (R.norm) {
@@ -338,33 +325,6 @@ __global__ __launch_bounds__(256) void bias_adam_kernel(BiasArgs a) {
   a.b[idx] = bj - (a.lr[g] / bc1) * mj / (sqrtf(vj / bc2) + a.eps);
 }
 
-// Finishes the decoder shadow after the Adam-fused weight-gradient GEMM: row
-// norm from the per-column-tile partial squares, bf16 shadow scaled in place,
-// norms stored for the next step's norm Jacobian.  One wave per row.
-__global__ __launch_bounds__(256) void normalize_rows_kernel(uint16_t* sh, const float* sqpart, int ntile,
-                                                             float* norms, long rows, int d) {
-  const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  float s2 = lane < ntile ? sqpart[row * ntile + lane] : 0.f;
-  s2 = wave_sum(s2);
-  const float nrm = fmaxf(sqrtf(s2), 1e-8f);
-  const float inv = 1.f / nrm;
-  if (lane == 0 && norms) norms[row] = nrm;
-  uint16_t* S = sh + row * d;
-  for (int e = lane * 8; e < d; e += 512) {
-    u32x4_t v = *reinterpret_cast<const u32x4_t*>(S + e);
-    u32x4_t o;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float lo = bf2f((uint16_t)(v[k] & 0xFFFF)) * inv;
-      const float hi = bf2f((uint16_t)(v[k] >> 16)) * inv;
-      o[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
-    }
-    *reinterpret_cast<u32x4_t*>(S + e) = o;
-  }
-}
-
 }  // namespace scamd
 
 using namespace scamd;
@@ -377,7 +337,6 @@ int sc_adam_rows(int nset, float* const* p, const void* const* g, float* const* 
                  float bc2, const int* step, int nsplit, long gstride, long row0, hipStream_t stream,
                  const int* live, int gbf16) {
   if (d % 256 || d > 4096 || nset < 1 || nset > 2 || nsplit < 1) return 1;
-  static const int nt = getenv("SC_ADAM_NT") ? atoi(getenv("SC_ADAM_NT")) : 0;
   AdamArgs a;
   long total = 0;
   for (int i = 0; i < nset; ++i) {
@@ -392,23 +351,14 @@ int sc_adam_rows(int nset, float* const* p, const void* const* g, float* const* 
   // bf16 gradients: plain loads only (the NT knob A/B'd slower, profiles/)
 #define SC_ADAM(NVV)                                                                                  \
   case NVV:                                                                                           \
-    if (gbf16) hipLaunchKernelGGL((adam_rows_kernel<NVV, false, true>), dim3(blocks), dim3(256), 0, stream, a); \
-    else if (nt) hipLaunchKernelGGL((adam_rows_kernel<NVV, true>), dim3(blocks), dim3(256), 0, stream, a);      \
-    else hipLaunchKernelGGL((adam_rows_kernel<NVV, false>), dim3(blocks), dim3(256), 0, stream, a);            \
+    if (gbf16) hipLaunchKernelGGL((adam_rows_kernel<NVV, true>), dim3(blocks), dim3(256), 0, stream, a); \
+    else hipLaunchKernelGGL((adam_rows_kernel<NVV>), dim3(blocks), dim3(256), 0, stream, a);            \
     break;
   switch (d / 256) {
     SC_ADAM(1) SC_ADAM(2) SC_ADAM(3) SC_ADAM(4) SC_ADAM(6) SC_ADAM(8) SC_ADAM(16)
     default: return 1;
   }
 #undef SC_ADAM
-  return hipGetLastError() == hipSuccess ? 0 : 3;
-}
-
-int sc_normalize_rows(void* sh, const float* sqpart, int ntile, float* norms, long rows, int d,
-                      hipStream_t stream) {
-  if (d % 8 || ntile > 64) return 1;
-  hipLaunchKernelGGL(normalize_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream,
-                     reinterpret_cast<uint16_t*>(sh), sqpart, ntile, norms, rows, d);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -20,7 +20,9 @@ using S256 = Shape<2, 4, 8, 4>;
 // consumers (loss / bias / Adam kernels) do not depend on the GEMM configuration.
 constexpr int PT = 128;
 
-enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ADAM = 5, EPI_ENC_CNT = 6,
+// (5 was EPI_ADAM, Adam fused into the weight-gradient epilogue: measured slower than the
+// separate streaming Adam kernel and removed)
+enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ENC_CNT = 6,
        EPI_DC_MASK = 7, EPI_ENC_ACT = 8, EPI_DC_ACT = 9, EPI_ROWMAX = 10 };
 
 // Activity bitmask of the codes: see mask_bit() in sae_gemm_kernel.h (one 64-bit word per lane
@@ -57,23 +59,6 @@ struct Problem {
   float alpha;
 };
 
-// Per-problem state for EPI_ADAM.  mode 1 = row-normalised parameter (decoder /
-// tied dictionary): the gradient reaching the raw rows goes through the norm
-// Jacobian, using the row dots accumulated by the code-gradient epilogue and
-// the current row norms; the updated rows are written unnormalised to the bf16
-// shadow together with per-(row, column-tile) partial squared norms, and a
-// small normalize pass finishes the shadow.
-struct AdamEpi {
-  float* p;
-  float* m;
-  float* v;
-  uint16_t* sh;
-  const float* dotpart;
-  const float* norms;
-  float* sqpart;
-  int mode;
-};
-
 struct GemmParams {
   Problem prob[2];
   int nprob;
@@ -92,20 +77,12 @@ struct GemmParams {
   float l1_add_scale;  // DC: multiplies l1[g] (= d/2 so dpre is in units of R)
   float* dotpart;      // DC (optional): [G][tiles_m][N] partials of the norm-Jacobian row dots
   int dc_tied;         // DC: tied dictionary -> dot also gets dpre * (c - b) (uses bias)
-  // --- EPI_ADAM: Adam fused into the weight-gradient epilogue -----------------
-  AdamEpi adam[2];
-  const float* lr;     // [G]
-  const int* step;     // device count of completed steps (t = *step + 1)
-  float b1, b2, eps;
-  int dot_tm;          // row tiles in dotpart
-  float dot_scale;     // converts dotpart sums to <w_hat, dL/dw_hat>
   uint64_t* cmask;     // ENC: optional activity-bitmask output; DC_MASK: its input
   // --- split-K (plain F32 / BF16 epilogues only): K-tile range split over `ksplit`
   // blocks per output tile; split s writes its partial product at c + s * split_stride
   // (the consumer -- the Adam kernel for weight gradients -- sums the slabs).
   int ksplit;
   long split_stride;
-  int dbg;  // diagnostics (SC_GEMM_DBG): bit 0 = EPI_BF16 skips its output stores
   // masked ensembles: per-group live extent of the n dimension when it is M / K (may be null)
   const int* nact_m;
   const int* nact_k;

@@ -3,48 +3,8 @@
 // sae_gemm_kernel.h; the 256-row block shapes are instantiated in sae_gemm_big.hip.
 #include "sae_gemm_kernel.h"
 
-#include <stdlib.h>
 
 using namespace scamd;
-
-namespace {
-
-// Persistent 128x128 launch (sae_gemm_pt_kernel): grid = workgroups resident at once (2 per
-// CU at NST 2, 1 at NST 3), each looping over tiles with a continuous LDS-DMA stream.
-template <int NST>
-int launch_pt(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t stream, int max_blocks) {
-  set_divisors<S128>(p);
-  const long total = n_blocks<S128>(p.M, p.N, p.G, nprob);
-  long nb = (NST == 2 ? 2 : 1) * 256;
-  if (max_blocks > 0 && max_blocks < nb) nb = max_blocks;
-  const dim3 grid((unsigned)(total < nb ? total : nb)), block(S128::NT);
-#define SC_LP(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_pt_kernel<S128, AKV, BKV, E, NST>), grid, block, 0, stream, p)
-  switch (epi) {
-    case EPI_ENC: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_ENC); break;
-    case EPI_ENC_CNT: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_ENC_CNT); break;
-    case EPI_ENC_ACT: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_ENC_ACT); break;
-    case EPI_DEC: if (!(ak && !bk)) return 5; SC_LP(true, false, EPI_DEC); break;
-    case EPI_DC_MASK: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_DC_MASK); break;
-    case EPI_DC_ACT: if (!(ak && bk)) return 5; SC_LP(true, true, EPI_DC_ACT); break;
-    case EPI_F32:
-      if (ak && bk) SC_LP(true, true, EPI_F32);
-      else if (ak) SC_LP(true, false, EPI_F32);
-      else if (bk) SC_LP(false, true, EPI_F32);
-      else SC_LP(false, false, EPI_F32);
-      break;
-    case EPI_BF16:
-      if (ak && bk) SC_LP(true, true, EPI_BF16);
-      else if (ak) SC_LP(true, false, EPI_BF16);
-      else if (bk) SC_LP(false, true, EPI_BF16);
-      else SC_LP(false, false, EPI_BF16);
-      break;
-    default: return 9;
-  }
-#undef SC_LP
-  return hipGetLastError() == hipSuccess ? 0 : 3;
-}
-
-}  // namespace
 
 // ------------------------------------------------------------------ C ABI
 extern "C" {
@@ -52,17 +12,6 @@ extern "C" {
 struct ScOperand {
   const void* ptr;
   long ld, sg;
-};
-
-struct ScAdamEpi {
-  float* p;
-  float* m;
-  float* v;
-  void* sh;
-  const float* dotpart;
-  const float* norms;
-  float* sqpart;
-  int mode;
 };
 
 
@@ -82,9 +31,7 @@ int sc_gemm_shape(int M, int N, int G, int nprob) {
 }
 
 // layout: bit0 = A is K-major, bit1 = B is K-major.
-// cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256; bit 4 (128x128
-// only): persistent tile loop with a continuous LDS-DMA stream (sae_gemm_pt_kernel), bits 8-23
-// then cap its grid (0 = one workgroup per CU slot);
+// cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256;
 // bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4 (128x128 blocks: BK64 x 3),
 // 2: BK32 x 2, 3: BK32 x 3).
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
@@ -92,9 +39,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             void* const* c /* [nprob] */, const float* alpha /* [nprob] */, long ldc, long sc,
             const float* bias, long sbias, const int* nactive, const void* aux, long ldaux,
             long saux, float* part, float* colpart, const float* l1, float l1_add_scale,
-            float* dotpart, int dc_tied, const ScAdamEpi* adam /* [nprob] or null */, const float* lr,
-            const int* step, float b1, float b2, float eps, int dot_tm, float dot_scale,
-            int cfg, int ksplit, long split_stride, void* cmask, int act, const float* ascale,
+            float* dotpart, int dc_tied, int cfg, int ksplit, long split_stride, void* cmask, int act, const float* ascale,
             void* cmask2, float* rcol, const int* nact_m, const int* nact_k, hipStream_t stream) {
   if (M % PT || N % PT || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
   if ((epi == EPI_DC_MASK || epi == EPI_DC_ACT) && !cmask) return 4;
@@ -118,18 +63,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.part = part; p.colpart = colpart; p.l1 = l1; p.l1_add_scale = l1_add_scale;
   p.dotpart = dotpart; p.dc_tied = dc_tied;
   p.cmask = reinterpret_cast<uint64_t*>(cmask);
-  for (int i = 0; i < 2; ++i) {
-    if (adam && i < nprob)
-      p.adam[i] = {adam[i].p, adam[i].m, adam[i].v, reinterpret_cast<uint16_t*>(adam[i].sh), adam[i].dotpart,
-                   adam[i].norms, adam[i].sqpart, adam[i].mode};
-    else
-      p.adam[i] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
-  }
-  if (epi == EPI_ADAM && (!adam || !lr || !step)) return 4;
-  p.lr = lr; p.step = step; p.b1 = b1; p.b2 = b2; p.eps = eps; p.dot_tm = dot_tm; p.dot_scale = dot_scale;
   p.ksplit = ksplit; p.split_stride = split_stride;
-  static const int dbg = getenv("SC_GEMM_DBG") ? atoi(getenv("SC_GEMM_DBG")) : 0;
-  p.dbg = dbg;
   p.act = act; p.ascale = ascale;
   p.cmask2 = reinterpret_cast<uint64_t*>(cmask2); p.rcol = rcol;
   p.nact_m = nact_m; p.nact_k = nact_k;
@@ -145,11 +79,6 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
       if (!fits<S256x128>(M, N)) return 6;
       return launch_big(2, pipe, epi, ak, bk, p, nprob, stream);
     default:
-      if (cfg & 16) {  // persistent tile loop (BK64 rings only, no split-K)
-        if (ksplit != 1 || (pipe != 0 && pipe != 1)) return 9;
-        const int mb = (cfg >> 8) & 0xFFFF;
-        return pipe == 1 ? launch_pt<3>(epi, ak, bk, p, nprob, stream, mb) : launch_pt<2>(epi, ak, bk, p, nprob, stream, mb);
-      }
       if (pipe == 1) return launch<S128, 64, 3, false>(epi, ak, bk, p, nprob, stream);  // 96 KB: 1 block/CU
       if (pipe == 2) return launch<S128, 32, 2, false>(epi, ak, bk, p, nprob, stream);  // 32 KB: 4-5 blocks/CU
       if (pipe == 3) return launch<S128, 32, 3, false>(epi, ak, bk, p, nprob, stream);

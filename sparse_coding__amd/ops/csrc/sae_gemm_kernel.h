@@ -95,8 +95,6 @@ constexpr int epi_scratch_floats() { return 2 * S::WGM * S::BN + S::NW; }
 // bank pairs (2-way, measured: 64 extra cycles per wave); the half swap makes them 16.
 // ds_read_b128 serves 16-lane groups on 64 banks: 2 rows x 8 chunks, distinct with the XOR.
 constexpr int STAGE_OFF = 4096, STAGE_ROW = 128, STAGE_WAVE = 64 * STAGE_ROW;
-// Adam-fused weight gradient: wave-private transpose pads past the epilogue's scratch floats
-constexpr int ADAM_PAD_OFF = 8192;
 __device__ __forceinline__ int stage_at(int row, int byte) {  // 8-byte granule of (row, byte)
   return row * STAGE_ROW + ((((byte >> 4) ^ (row >> 1)) & 7) << 4) + ((((byte >> 3) ^ row) & 1) << 3);
 }
@@ -141,8 +139,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
     }
   };
 
-  constexpr bool CAN_DIE = ENC || EPI == EPI_DC || EPI == EPI_DC_MASK || EPI == EPI_DC_ACT || EPI == EPI_F32 ||
-                           EPI == EPI_ADAM;
+  constexpr bool CAN_DIE = ENC || EPI == EPI_DC || EPI == EPI_DC_MASK || EPI == EPI_DC_ACT || EPI == EPI_F32;
   if (CAN_DIE && dead) {
     // A tile wholly past a model's live dictionary (masked ensembles): no MFMA work ran.  The
     // encoder still writes its zero codes and activity words and the weight gradient its
@@ -198,35 +195,33 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   if constexpr (EPI == EPI_F32) {
     float* C = reinterpret_cast<float*>(cptr) + (long)g * p.sc;
     if constexpr (FSTAGE) {
-      if (!(p.dbg & 8)) {  // A/B knob (SC_GEMM_DBG bit 3): the direct MFMA-layout stores below
-        // LDS-staged row-contiguous fp32 stores (tile kernel, ring free after the K loop): the
-        // MFMA layout puts 16 rows x 64 B in one store; instead each wave parks 32 columns of
-        // its sub-tile (128-byte rows, the bf16 staging's swizzle) and streams whole 128-byte
-        // row segments, 8 rows per dwordx4 store; two passes cover the 64 columns.
-        char* st = reinterpret_cast<char*>(red) + wid * (WI * 16 * STAGE_ROW);
-        float* Cw = C + (long)(m0 + wr * (WI * 16)) * p.ldc + n0 + wc * (WJ * 16);
-        const int q = lane >> 4, r16 = lane & 15, ch = lane & 7;
+      // LDS-staged row-contiguous fp32 stores (tile kernel, ring free after the K loop): the
+      // MFMA layout puts 16 rows x 64 B in one store; instead each wave parks 32 columns of
+      // its sub-tile (128-byte rows, the bf16 staging's swizzle) and streams whole 128-byte
+      // row segments, 8 rows per dwordx4 store; two passes cover the 64 columns.
+      char* st = reinterpret_cast<char*>(red) + wid * (WI * 16 * STAGE_ROW);
+      float* Cw = C + (long)(m0 + wr * (WI * 16)) * p.ldc + n0 + wc * (WJ * 16);
+      const int q = lane >> 4, r16 = lane & 15, ch = lane & 7;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < 2; ++h) {
 #pragma unroll
-          for (int i = 0; i < WI; ++i)
+        for (int i = 0; i < WI; ++i)
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-              const f32x4_t v = acc[i][2 * h + jj] * alpha;
-              const int row = i * 16 + r16, byte = (jj * 16 + 4 * q) * 4;
-              *reinterpret_cast<float2*>(st + stage_at(row, byte)) = make_float2(v[0], v[1]);
-              *reinterpret_cast<float2*>(st + stage_at(row, byte + 8)) = make_float2(v[2], v[3]);
-            }
-#pragma unroll
-          for (int k = 0; k < WI * 2; ++k) {
-            const int row = 8 * k + (lane >> 3);
-            uint4 u = *reinterpret_cast<const uint4*>(st + row * STAGE_ROW + (((ch ^ (row >> 1)) & 7) << 4));
-            if (row & 1) u = make_uint4(u.z, u.w, u.x, u.y);
-            *reinterpret_cast<uint4*>(Cw + (long)row * p.ldc + h * 32 + ch * 4) = u;
+          for (int jj = 0; jj < 2; ++jj) {
+            const f32x4_t v = acc[i][2 * h + jj] * alpha;
+            const int row = i * 16 + r16, byte = (jj * 16 + 4 * q) * 4;
+            *reinterpret_cast<float2*>(st + stage_at(row, byte)) = make_float2(v[0], v[1]);
+            *reinterpret_cast<float2*>(st + stage_at(row, byte + 8)) = make_float2(v[2], v[3]);
           }
+#pragma unroll
+        for (int k = 0; k < WI * 2; ++k) {
+          const int row = 8 * k + (lane >> 3);
+          uint4 u = *reinterpret_cast<const uint4*>(st + row * STAGE_ROW + (((ch ^ (row >> 1)) & 7) << 4));
+          if (row & 1) u = make_uint4(u.z, u.w, u.x, u.y);
+          *reinterpret_cast<uint4*>(Cw + (long)row * p.ldc + h * 32 + ch * 4) = u;
         }
-        return;
       }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < WI; ++i)
@@ -239,15 +234,6 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   }
   if constexpr (EPI == EPI_BF16) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-    if (p.dbg & 1) {  // diagnostics: main loop only (the sum keeps every accumulator live)
-      float s = 0.f;
-#pragma unroll
-      for (int i = 0; i < WI; ++i)
-#pragma unroll
-        for (int j = 0; j < WJ; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-      if (s == 1234.5f) C[0] = 0;
-      return;
-    }
 #pragma unroll
     for (int i = 0; i < WI; ++i)
 #pragma unroll
@@ -583,113 +569,6 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
     }
     return;
   }
-  if constexpr (EPI == EPI_ADAM) {
-    // Weight gradient -> Adam in registers; the fp32 gradient never touches HBM.
-    const AdamEpi E = p1 ? p.adam[1] : p.adam[0];
-    const long gb = (long)g * p.sc;
-    const float bc1 = 1.f - __powf(p.b1, (float)(*p.step + 1));
-    const float bc2 = 1.f - __powf(p.b2, (float)(*p.step + 1));
-    const float stp = p.lr[g] / bc1, rbc2 = 1.f / bc2, b1 = p.b1, b2 = p.b2, eps = p.eps;
-    if (E.mode) {  // per-row <w_hat, dW_hat> (code-gradient partials) and |w| into LDS
-      for (int r = tid; r < BM; r += NT) {
-        const int row = m0 + r;
-        float dsum = 0.f;
-        for (int t = 0; t < p.dot_tm; ++t) dsum += E.dotpart[((long)g * p.dot_tm + t) * p.M + row];
-        red[r] = dsum * p.dot_scale;
-        red[BM + r] = E.norms[(long)g * p.M + row];
-      }
-      lds_barrier();
-    }
-    // Row-contiguous streaming update.  In the MFMA layout one dwordx4 touches 16 rows x 64 B
-    // (16 half-used 128-byte lines of p, m and v); instead each 16-row group of the wave tile is
-    // transposed through a wave-private LDS pad (the ring is free after the K loop) so one
-    // dwordx4 covers 4 whole 256-byte row segments, and the p / m / v fragments of fragment
-    // f + D are loaded before fragment f is updated (D = 8: 24 x 1 KiB loads in flight per wave).
-    static_assert(WJ == 4, "row-contiguous Adam epilogue: 64-column wave tiles");
-    constexpr int PADW = 68;                     // floats per padded LDS row (16-byte skew)
-    constexpr int NF = WI * 4, D = NF < 8 ? NF : 8;
-    static_assert(ADAM_PAD_OFF + NW * 16 * PADW * 4 <= (S::BM + S::BN) * 64 * 2, "pad inside one ring stage");
-    float* pad = reinterpret_cast<float*>(reinterpret_cast<char*>(red) + ADAM_PAD_OFF) + wid * 16 * PADW;
-    float* ssr = red + 2 * BM;                   // per-(column wave, row) |w|^2 partials
-    static_assert((2 * BM + WGN * BM) * 4 <= ADAM_PAD_OFF, "scratch floats below the pads");
-    const int rsub = lane >> 4, cl = (lane & 15) * 4;
-    const int lrow0 = wr * (WI * 16);            // first tile-local row of the wave
-    const long rbase = gb + (long)(m0 + lrow0 + rsub) * p.ldc + n0 + wc * 64 + cl;
-    auto foff = [&](int f) { return rbase + (long)((f >> 2) * 16 + (f & 3) * 4) * p.ldc; };
-    f32x4_t pb[D], mb[D], vb[D];
-#pragma unroll
-    for (int f = 0; f < D; ++f) {
-      const long o = foff(f);
-      pb[f] = *reinterpret_cast<const f32x4_t*>(E.p + o);
-      mb[f] = *reinterpret_cast<const f32x4_t*>(E.m + o);
-      vb[f] = *reinterpret_cast<const f32x4_t*>(E.v + o);
-    }
-    f32x4_t gt[4];
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const int i = f >> 2, k = f & 3, sl = f % D;
-      if (k == 0) {  // transpose the 16 x 64 accumulator group i (wave-local LDS ops stay in order)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          *reinterpret_cast<f32x4_t*>(pad + (lane & 15) * PADW + 16 * j + 4 * (lane >> 4)) = acc[i][j];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) gt[kk] = *reinterpret_cast<const f32x4_t*>(pad + (4 * kk + rsub) * PADW + cl);
-      }
-      const long off = foff(f);
-      f32x4_t pv = pb[sl], mv = mb[sl], vv = vb[sl];
-      if (f + D < NF) {
-        const long o = foff(f + D);
-        pb[sl] = *reinterpret_cast<const f32x4_t*>(E.p + o);
-        mb[sl] = *reinterpret_cast<const f32x4_t*>(E.m + o);
-        vb[sl] = *reinterpret_cast<const f32x4_t*>(E.v + o);
-      }
-      const int lrow = lrow0 + i * 16 + 4 * k + rsub;
-      float a_ = alpha, c_ = 0.f;
-      if (E.mode) {  // norm Jacobian of this row: dW = dW_hat / |w| - w <w_hat, dW_hat> / |w|^2
-        const float dot = red[lrow], nrm = red[BM + lrow];
-        if (nrm > 1e-8f) {
-          const float inv = 1.f / nrm;
-          a_ = alpha * inv;
-          c_ = dot * inv * inv;
-        } else {
-          a_ = alpha * 1e8f;  // below the clamp floor the norm has zero derivative
-        }
-      }
-      float ss = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float gr = gt[k][r] * a_ - pv[r] * c_;
-        mv[r] = b1 * mv[r] + (1.f - b1) * gr;
-        vv[r] = b2 * vv[r] + (1.f - b2) * gr * gr;
-        pv[r] -= stp * mv[r] / (sqrtf(vv[r] * rbc2) + eps);
-        ss += pv[r] * pv[r];
-      }
-      *reinterpret_cast<f32x4_t*>(E.p + off) = pv;
-      *reinterpret_cast<f32x4_t*>(E.m + off) = mv;
-      *reinterpret_cast<f32x4_t*>(E.v + off) = vv;
-      *reinterpret_cast<ushort4*>(E.sh + off) = make_ushort4(f2bf(pv[0]), f2bf(pv[1]), f2bf(pv[2]), f2bf(pv[3]));
-      if (E.mode) {  // the row's 64-column |w|^2 partial: sum over the 16 lanes of the row
-        ss += __shfl_xor(ss, 1, 64);
-        ss += __shfl_xor(ss, 2, 64);
-        ss += __shfl_xor(ss, 4, 64);
-        ss += __shfl_xor(ss, 8, 64);
-        if ((lane & 15) == 0) ssr[wc * BM + lrow] = ss;
-      }
-    }
-    if (E.mode) {
-      // partial |w_j|^2 over each 128-column slot -> sqpart[g][row][slot]
-      constexpr int WPC = PT / (WJ * 16);  // wave columns per 128-column slot
-      lds_barrier();
-      for (int idx = tid; idx < (BN / PT) * BM; idx += NT) {
-        const int s = idx / BM, row = idx - s * BM;
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < WPC; ++w) v += ssr[(s * WPC + w) * BM + row];
-        E.sqpart[((long)g * p.M + m0 + row) * ptn + n0 / PT + s] = v;
-      }
-    }
-    return;
-  }
 }
 
 template <class S, bool AK, bool BKM, int EPI, int BKT, int NST>
@@ -733,7 +612,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
 
   // Only the weight-gradient style epilogues take a second K segment (K-concat);
   // the fused forward epilogues never do, and skipping its offsets saves VGPRs.
-  constexpr bool SEG2 = (EPI == EPI_F32 || EPI == EPI_BF16 || EPI == EPI_ADAM);
+  constexpr bool SEG2 = (EPI == EPI_F32 || EPI == EPI_BF16);
   constexpr bool ENC = (EPI == EPI_ENC || EPI == EPI_ENC_CNT || EPI == EPI_ENC_ACT);
   const int nk1 = p.K1 / BKT, nk_all = nk1 + (SEG2 ? p.K2 / BKT : 0);
   // this block's K-tile range [kbeg, nk) (the whole range unless split-K)
@@ -940,191 +819,6 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
 }
 
 
-// ------------------------------------------------------------------ persistent tile loop
-// 128x128 blocks, BK64 x NST LDS ring, one workgroup per (CU, slot) looping over output
-// tiles (tile lin = blockIdx.x + i * gridDim.x, XCD-remapped like the tile kernel).  The
-// LDS-DMA stream runs continuously ACROSS tiles: the K-tiles of tile i+1 are issued while
-// tile i's last K-steps compute, so the per-block start-up latency (measured ~15 us for
-// 2048 blocks in 4 rounds at K=64, scripts/dbg/store_lab.py) is paid once per workgroup,
-// and tile i's epilogue stores drain while tile i+1's MFMAs run.  The epilogue scratch is a
-// separate LDS area after the ring, and every barrier outside the K loop is LDS-only.
-//
-// vmcnt bookkeeping: stores count in vmcnt together with the DMAs.  At a K boundary whose
-// awaited DMA was issued BEFORE the previous tile's epilogue (kt <= NST-2 of a non-first
-// tile), that epilogue's stores are younger than it: the wait allows ST (a per-wave LOWER
-// bound of the epilogue's store instructions) more outstanding ops.  Under-counting only
-// over-waits.
-template <int EPI>
-constexpr int epi_min_stores(int wi, int wj) {
-  return (EPI == EPI_F32 || EPI == EPI_BF16 || EPI == EPI_ENC || EPI == EPI_ENC_CNT || EPI == EPI_ENC_ACT ||
-          EPI == EPI_DEC || EPI == EPI_DC || EPI == EPI_DC_MASK || EPI == EPI_DC_ACT)
-             ? wi * wj
-             : 0;
-}
-
-template <class S, bool AK, bool BKM, int EPI, int NST>
-__global__ __launch_bounds__(S::NT) void sae_gemm_pt_kernel(GemmParams p) {
-  constexpr int BKT = 64;
-  constexpr int BM = S::BM, BN = S::BN, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
-  constexpr int TA = BM * BKT * 2, TBB = BN * BKT * 2;
-  constexpr int PPWA = TA / 1024 / NW, PPWB = TBB / 1024 / NW;
-  constexpr int LPT = PPWA + PPWB;
-  constexpr int STG = TA + TBB;
-  constexpr int ST = epi_min_stores<EPI>(WI, WJ);
-  static_assert(S::BM == 128 && S::BN == 128, "persistent loop: 128x128 blocks");
-  __shared__ __attribute__((aligned(16))) char smem[NST * STG + epi_scratch_floats<S>() * 4];
-  float* red = reinterpret_cast<float*>(smem + NST * STG);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid / WGN, wc = wid % WGN;
-  const int tiles_m = p.M / BM, tiles_n = p.N / BN;
-  const int per_prob = tiles_m * tiles_n * p.G;  // ksplit == 1 (host-checked)
-  const int total = per_prob * p.nprob;
-  const int nmine = (total - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  constexpr bool SEG2 = (EPI == EPI_F32 || EPI == EPI_BF16);
-  const int nk1 = p.K1 / BKT, nk = nk1 + (SEG2 ? p.K2 / BKT : 0);
-  const int U = nmine * nk;  // this workgroup's K-tile stream
-
-  struct Tile { int pi, g, m0, n0, tn; };
-  auto tile_of = [&](int i) {
-    const int lin = xcd_remap((int)blockIdx.x + i * (int)gridDim.x, total);
-    Tile t;
-    t.pi = (int)fdiv(lin, p.f_prob);
-    int rem = lin - t.pi * per_prob;
-    t.g = (int)fdiv(rem, p.f_plane);
-    rem -= t.g * tiles_m * tiles_n;
-    const int tm = (int)fdiv(rem, p.f_tn);
-    t.tn = rem - tm * tiles_n;
-    t.m0 = tm * BM;
-    t.n0 = t.tn * BN;
-    return t;
-  };
-
-  // ---- DMA issue side: the operand context of the tile the next DMA belongs to
-  int iti = -1;
-  uint32_t va0[PPWA], vb0[PPWB], va1[SEG2 ? PPWA : 1], vb1[SEG2 ? PPWB : 1];
-  i32x4_t ra0, rb0, ra1, rb1;
-  uint32_t sa0 = 0, sa1 = 0, sb0 = 0, sb1 = 0;
-  auto set_issue_tile = [&](int ti) {
-    const Tile t = tile_of(ti);
-    const bool p1 = t.pi != 0;
-    const Operand oa0 = p1 ? p.prob[1].a[0] : p.prob[0].a[0];
-    const Operand ob0 = p1 ? p.prob[1].b[0] : p.prob[0].b[0];
-    piece_offsets<AK, BKT, PPWA>(va0, oa0.ld, t.m0, wid, lane);
-    piece_offsets<BKM, BKT, PPWB>(vb0, ob0.ld, t.n0, wid, lane);
-    ra0 = make_rsrc(oa0.ptr + (long)t.g * oa0.sg);
-    rb0 = make_rsrc(ob0.ptr + (long)t.g * ob0.sg);
-    sa0 = AK ? BKT * 2 : (uint32_t)(BKT * oa0.ld * 2);
-    sb0 = BKM ? BKT * 2 : (uint32_t)(BKT * ob0.ld * 2);
-    if constexpr (SEG2) {
-      const Operand oa1 = p1 ? p.prob[1].a[1] : p.prob[0].a[1];
-      const Operand ob1 = p1 ? p.prob[1].b[1] : p.prob[0].b[1];
-      piece_offsets<AK, BKT, PPWA>(va1, oa1.ld, t.m0, wid, lane);
-      piece_offsets<BKM, BKT, PPWB>(vb1, ob1.ld, t.n0, wid, lane);
-      ra1 = make_rsrc(oa1.ptr + (long)t.g * oa1.sg);
-      rb1 = make_rsrc(ob1.ptr + (long)t.g * ob1.sg);
-      sa1 = AK ? BKT * 2 : (uint32_t)(BKT * oa1.ld * 2);
-      sb1 = BKM ? BKT * 2 : (uint32_t)(BKT * ob1.ld * 2);
-    }
-  };
-  auto issue = [&](int u) {
-    const int ti = u / nk, kt = u - ti * nk;
-    if (ti != iti) {
-      set_issue_tile(ti);
-      iti = ti;
-    }
-    char* dst = smem + (u % NST) * STG;
-    if (!SEG2 || kt < nk1) {
-      issue_pieces<PPWA>(ra0, va0, (uint32_t)kt * sa0, dst, wid);
-      issue_pieces<PPWB>(rb0, vb0, (uint32_t)kt * sb0, dst + TA, wid);
-    } else if constexpr (SEG2) {
-      issue_pieces<PPWA>(ra1, va1, (uint32_t)(kt - nk1) * sa1, dst, wid);
-      issue_pieces<PPWB>(rb1, vb1, (uint32_t)(kt - nk1) * sb1, dst + TA, wid);
-    }
-  };
-
-  // ---- compute side (same pipelined K step as the tile kernel)
-  f32x4_t acc[WI][WJ];
-  auto mfmas = [&](const bf16x8_t (&fa)[WI], const bf16x8_t (&fb)[WJ]) {
-#pragma unroll
-    for (int i = 0; i < WI; ++i)
-#pragma unroll
-      for (int j = 0; j < WJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-  };
-  auto frags = [&](bf16x8_t (&fa)[WI], bf16x8_t (&fb)[WJ], int u, int ks) {
-    const char* la = smem + (u % NST) * STG;
-    const char* lb = la + TA;
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) fb[j] = load_frag<BKM, BKT>(lb, wc * (WJ * 16) + j * 16, ks, lane);
-#pragma unroll
-    for (int i = 0; i < WI; ++i) fa[i] = load_frag<AK, BKT>(la, wr * (WI * 16) + i * 16, ks, lane);
-  };
-  constexpr int RD = WI * (AK ? 1 : 2) + WJ * (BKM ? 1 : 2);
-  constexpr int MF = WI * WJ;
-  constexpr int MPR = MF / RD;
-  auto step = [&](bf16x8_t (&fan)[WI], bf16x8_t (&fbn)[WJ], int un, int ksn, const bf16x8_t (&fa)[WI],
-                  const bf16x8_t (&fb)[WJ]) {
-    __builtin_amdgcn_sched_barrier(0);
-    frags(fan, fbn, un, ksn);
-    mfmas(fa, fb);
-    sched_interleave<RD, MPR, MF - MPR * (RD - 1)>();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // wait until at most `younger` whole K-tiles of DMAs (+ `extra` younger ops) are in flight
-  auto wait_tiles = [&](int younger, bool stores_younger) {
-    if (stores_younger) {
-      if (NST >= 4 && younger >= 3) wait_vmcnt<(NST >= 4 ? 3 : 0) * LPT + ST>();
-      else if (NST >= 3 && younger >= 2) wait_vmcnt<(NST >= 3 ? 2 : 0) * LPT + ST>();
-      else if (younger >= 1) wait_vmcnt<LPT + ST>();
-      else wait_vmcnt<ST>();
-    } else {
-      if (NST >= 4 && younger >= 3) wait_vmcnt<(NST >= 4 ? 3 : 0) * LPT>();
-      else if (NST >= 3 && younger >= 2) wait_vmcnt<(NST >= 3 ? 2 : 0) * LPT>();
-      else if (younger >= 1) wait_vmcnt<LPT>();
-      else wait_vmcnt<0>();
-    }
-  };
-  auto tile_barrier = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  if (U == 0) return;  // (grid <= tiles on the host side; kept for safety: uniform exit)
-#pragma unroll
-  for (int t = 0; t < NST; ++t)
-    if (t < U) issue(t);
-  bf16x8_t fa0[WI], fb0[WJ], fa1[WI], fb1[WJ];
-  wait_tiles(min(NST - 1, U - 1), false);
-  tile_barrier();
-  frags(fa0, fb0, 0, 0);
-  uint2 noaux[WI][WJ];
-  for (int i = 0; i < nmine; ++i) {
-#pragma unroll
-    for (int a = 0; a < WI; ++a)
-#pragma unroll
-      for (int b = 0; b < WJ; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int kt = 0; kt < nk; ++kt) {
-      const int u = i * nk + kt;
-      step(fa1, fb1, u, 1, fa0, fb0);
-      // K-tile u+1 must have landed (for u = U-1 nothing is awaited and the fragment reads
-      // below fetch a stale stage that is never used)
-      wait_tiles(min(NST - 2, U - 2 - u), i > 0 && kt <= NST - 2);
-      tile_barrier();
-      if (u + NST < U) issue(u + NST);
-      step(fa0, fb0, u + 1, 0, fa1, fb1);
-    }
-    const Tile t = tile_of(i);
-    const bool p1 = t.pi != 0;
-    void* cptr = p1 ? p.prob[1].c : p.prob[0].c;
-    const float alpha = p1 ? p.prob[1].alpha : p.prob[0].alpha;
-    sae_epilogue<S, EPI, false>(p, acc, noaux, red, t.pi, t.g, t.m0, t.n0, t.tn, tiles_n, cptr, alpha);
-  }
-  wait_vmcnt<0>();  // no DMA may still target this workgroup's LDS when it exits
-}
-
 }  // namespace scamd
 
 namespace scamd {
@@ -1153,7 +847,7 @@ int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t strea
   set_divisors<S>(p);
   const dim3 grid((unsigned)(n_blocks<S>(p.M, p.N, p.G, nprob) * p.ksplit)), block(S::NT);
   if constexpr (!FULL) {
-    if (epi == EPI_ADAM || epi == EPI_BF16 || epi >= EPI_ENC_ACT || (epi == EPI_F32 && (ak || bk))) return 8;
+    if (epi == EPI_BF16 || epi >= EPI_ENC_ACT || (epi == EPI_F32 && (ak || bk))) return 8;
   }
 #define SC_L(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_kernel<S, AKV, BKV, E, BKT, NST>), grid, block, 0, stream, p)
   // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
@@ -1172,9 +866,6 @@ int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t strea
       break;
     case EPI_ROWMAX:
       if constexpr (FULL) { if (!(ak && bk)) return 5; SC_L(true, true, EPI_ROWMAX); }
-      break;
-    case EPI_ADAM:
-      if constexpr (FULL) { if (ak || bk) return 5; SC_L(false, false, EPI_ADAM); }
       break;
     case EPI_F32:
       if constexpr (FULL) {

@@ -11,13 +11,12 @@ n = dictionary size.  bf16 tensors are passed as torch.bfloat16.
 from __future__ import annotations
 
 import ctypes as C
-import os
 
 import torch
 
 from . import _lib
 
-EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16, EPI_ADAM, EPI_ENC_CNT, EPI_DC_MASK = 0, 1, 2, 3, 4, 5, 6, 7
+EPI_ENC, EPI_DEC, EPI_DC, EPI_F32, EPI_BF16, EPI_ENC_CNT, EPI_DC_MASK = 0, 1, 2, 3, 4, 6, 7
 EPI_ENC_ACT, EPI_DC_ACT, EPI_ROWMAX = 8, 9, 10
 # code activations of the ENC_ACT / DC_ACT epilogues
 ACT_RELU, ACT_REVERSE, ACT_THRESHOLD = 0, 1, 2
@@ -27,19 +26,17 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 #   0: automatic -- the largest shape that divides (M, N) and still launches >= 256 blocks
 #   1: 128x128, 4 waves of 64x64        2: 256x128, 4 waves of 128x64
 #   3: 256x256, 8 waves of 128x64 (one block per CU)
-# Per-epilogue defaults come from measurements on MI355X (profiles/); override with
-# SC_GEMM_CFG=<n> for all GEMMs.
+# Per-epilogue defaults come from measurements on MI355X (profiles/).
 # Measured at B=2048, d=512, n=2048, G=8 (profiles/kernel_bench_r1_v6.jsonl): the fused
 # epilogues are fastest on 128x128 blocks (two blocks per CU overlap one block's epilogue
 # with the other's MFMA loop: enc 61 vs 84 us on 256x256), the plain fp32 weight-gradient
-# GEMM (K = B = 2048) on 256x256 blocks (65 vs 74 us) -- "auto" picks that.
-_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ADAM: 0, EPI_ENC_CNT: 1,
+# GEMM (K = B = 2048) on 256x256 blocks (65 vs 74 us; 0.3311 vs 0.3460 ms per step) -- "auto"
+# picks that.  A persistent 128x128 tile loop with a continuous LDS-DMA stream across tiles
+# (bit-identical, not faster: two co-resident workgroups per CU already hide the same
+# latencies) and Adam fused into the weight-gradient epilogue were measured and removed.
+_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 1,
                 EPI_DC_MASK: 1, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
-_CFG_OVERRIDE = os.environ.get("SC_GEMM_CFG")
-if os.environ.get("SC_ADAM_EPI_CFG"):  # A/B knob: block shape of the Adam-fused weight gradient
-    _CFG_DEFAULT[EPI_ADAM] = int(os.environ["SC_ADAM_EPI_CFG"])
-if os.environ.get("SC_F32_CFG"):  # A/B knob: block shape of the plain fp32 GEMMs (weight gradient)
-    _CFG_DEFAULT[EPI_F32] = int(os.environ["SC_F32_CFG"])
+_CFG_OVERRIDE = None
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 # cfg bits 2-3 select the K pipeline: 0 BK64 x 2-stage LDS ring (default), 1 BK32 x 4,
 # 2 BK32 x 2 (smallest LDS footprint: most co-resident blocks), 3 BK32 x 3 (the
@@ -49,49 +46,6 @@ PIPES = {0: (64, 2), 1: (32, 4), 2: (32, 2), 3: (32, 3)}
 
 def set_config(epi: int, cfg: int):
     _CFG_DEFAULT[epi] = int(cfg)
-
-
-# Persistent 128x128 tile loop (cfg bit 4, csrc/sae_gemm_kernel.h sae_gemm_pt_kernel): one
-# workgroup per (CU, slot) walks several output tiles with a continuous LDS-DMA stream across
-# tile boundaries.  Bit-identical to the tile kernel (tests/test_gemm_persistent_gpu.py,
-# tests/test_gemm_pt_gpu.py); opt-in (SC_GEMM_PERSIST=1 / force_persistent) because on MI355X
-# two co-resident tile-kernel workgroups per CU already hide the same latencies (enc 64 vs
-# 60 us, profiles/gemm_lab_r2_v2.jsonl).  cfg bits 8-23 carry a grid cap (tests: many tiles
-# per workgroup).
-_PERSIST = os.environ.get("SC_GEMM_PERSIST", "0") not in ("", "0")
-_P_EPIS = {EPI_F32, EPI_BF16, EPI_ENC, EPI_ENC_CNT, EPI_ENC_ACT, EPI_DEC, EPI_DC_MASK, EPI_DC_ACT}
-_P_NST = int(os.environ.get("SC_GEMM_NST", "2"))
-_P_MAX_BLOCKS = 0
-
-
-class force_persistent:
-    """Context manager: route eligible GEMMs to the persistent tile loop (``on``) or to the tile
-    kernel; ``max_blocks`` caps the grid (tests: several tiles per workgroup); ``nst`` sets the
-    LDS ring depth (2: two workgroups per CU, 3: one)."""
-
-    def __init__(self, on: bool = True, max_blocks: int = 0, nst: int | None = None):
-        self.on, self.max_blocks, self.nst = bool(on), int(max_blocks), nst
-
-    def __enter__(self):
-        global _PERSIST, _P_MAX_BLOCKS, _P_NST
-        self._old = (_PERSIST, _P_MAX_BLOCKS, _P_NST)
-        _PERSIST, _P_MAX_BLOCKS = self.on, self.max_blocks
-        if self.nst is not None:
-            _P_NST = int(self.nst)
-        return self
-
-    def __exit__(self, *exc):
-        global _PERSIST, _P_MAX_BLOCKS, _P_NST
-        _PERSIST, _P_MAX_BLOCKS, _P_NST = self._old
-
-
-def _persistent_cfg(epi, M, N, ksplit, cfg_explicit):
-    """cfg word of the persistent loop for this GEMM, or None when it does not apply."""
-    if not _PERSIST or epi not in _P_EPIS or ksplit != 1 or cfg_explicit is not None or _CFG_OVERRIDE is not None:
-        return None
-    if M % 128 or N % 128 or _P_NST not in (2, 3):
-        return None
-    return 1 | 16 | (4 if _P_NST == 3 else 0) | (min(_P_MAX_BLOCKS, 0xFFFF) << 8)
 
 
 class force_shape:
@@ -132,19 +86,14 @@ def _bf16(t, name):
 
 def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *,
             bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
-            colpart=None, l1=None, l1_add_scale=0.0, dotpart=None, dc_tied=False, adam=None,
-            lr=None, step=None, betas=(0.9, 0.999), eps=1e-8, dot_tm=0, dot_scale=0.0, cfg=None,
+            colpart=None, l1=None, l1_add_scale=0.0, dotpart=None, dc_tied=False, cfg=None,
             ksplit=1, split_stride=0, cmask=None, act=0, ascale=None, cmask2=None, rcol=None, nact_m=None,
             nact_k=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
-    cfg_explicit = cfg
     cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
     _need((cfg & 3) == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg & 3)} does not tile M={M}, N={N}")
     nprob = len(outs)
-    pcfg = _persistent_cfg(epi, M, N, ksplit, cfg_explicit)
-    if pcfg is not None:
-        cfg = pcfg
     A = (_lib.ScOperand * (2 * nprob))(*a_ops)
     Bo = (_lib.ScOperand * (2 * nprob))(*b_ops)
     Cp = (C.c_void_p * nprob)(*[_lib.ptr(o) for o in outs])
@@ -153,8 +102,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
         epi, layout, nprob, M, N, K1, K2, G, A, Bo, Cp, al, ldc, sc,
         _lib.ptr(bias), sbias, _lib.ptr(nactive), _lib.ptr(aux), ldaux, saux,
         _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1), float(l1_add_scale),
-        _lib.ptr(dotpart), int(bool(dc_tied)), adam, _lib.ptr(lr), _lib.ptr(step),
-        float(betas[0]), float(betas[1]), float(eps), int(dot_tm), float(dot_scale),
+        _lib.ptr(dotpart), int(bool(dc_tied)),
         cfg, int(ksplit), int(split_stride), _lib.ptr(cmask), int(act), _lib.ptr(ascale),
         _lib.ptr(cmask2), _lib.ptr(rcol), _lib.ptr(nact_m), _lib.ptr(nact_k), _lib.stream_handle(),
     )
@@ -355,51 +303,6 @@ def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None):
     # skip their MFMAs and only write the zeros
     _launch(EPI_F32 if odt == torch.float32 else EPI_BF16, 0, n, d, K1, K2, G, a_ops, b_ops, list(outs),
             [alpha] * len(outs), d, n * d, cfg=cfg, ksplit=ksplit, split_stride=G * n * d, nact_m=nactive)
-
-
-def weight_grads_adam(pairs, states, alpha, lr, step_dev, betas=(0.9, 0.999), eps=1e-8, dot_tm=0):
-    """Weight gradients (as ``weight_grads``) with Adam applied in the epilogue.
-
-    states: one dict per problem with p/m/v (fp32 [G, n, d]), shadow (bf16 [G, n, d], written
-    UNNORMALISED for normalised rows), and for row-normalised parameters (``norm=True``):
-    dotpart [G, dot_tm, n] (from ``code_grad``), norms [G, n] (current row norms) and
-    sqpart [G, n, d/128] (receives partial squared norms; finish with ``adam.normalize_rows``).
-    """
-    _need(1 <= len(pairs) == len(states) <= 2, "1 or 2 problems")
-    G, n, d = states[0]["p"].shape
-    nseg = len(pairs[0])
-    a_ops, b_ops, ks = [], [], []
-    for p in pairs:
-        seg_a, seg_b = [], []
-        for (A, Bm) in p:
-            _bf16(A, "A"); _bf16(Bm, "B")
-            Bk = A.shape[-2]
-            _need(A.shape[-1] == n and Bm.shape[-1] == d and Bm.shape[-2] == Bk, "segment shapes")
-            seg_a.append(_op(A, n, 0 if A.dim() == 2 else Bk * n))
-            seg_b.append(_op(Bm, d, 0 if Bm.dim() == 2 else Bk * d))
-        if nseg == 1:
-            seg_a.append(seg_a[0]); seg_b.append(seg_b[0])
-        a_ops += seg_a; b_ops += seg_b
-        ks.append(tuple(x.shape[-2] for x, _ in p))
-    _need(len(set(ks)) == 1, "all problems must share K segments")
-    eps_arr = (_lib.ScAdamEpi * len(states))()
-    for i, st in enumerate(states):
-        for k in ("p", "m", "v"):
-            t = st[k]
-            _need(t.dtype == torch.float32 and tuple(t.shape) == (G, n, d) and t.is_contiguous(), f"adam {k}")
-        _need(st["shadow"].dtype == torch.bfloat16 and tuple(st["shadow"].shape) == (G, n, d), "shadow")
-        mode = int(bool(st.get("norm")))
-        if mode:
-            _need(st["dotpart"].numel() >= G * dot_tm * n, "dotpart")
-            _need(st["norms"].numel() == G * n and st["sqpart"].numel() >= G * n * (d // 128), "norms/sqpart")
-        eps_arr[i] = _lib.ScAdamEpi(_lib.ptr(st["p"]), _lib.ptr(st["m"]), _lib.ptr(st["v"]), _lib.ptr(st["shadow"]),
-                                    _lib.ptr(st.get("dotpart")), _lib.ptr(st.get("norms")),
-                                    _lib.ptr(st.get("sqpart")), mode)
-    K1 = ks[0][0]
-    K2 = ks[0][1] if nseg == 2 else 0
-    _launch(EPI_ADAM, 0, n, d, K1, K2, G, a_ops, b_ops, [st["p"] for st in states], [alpha] * len(states),
-            d, n * d, adam=eps_arr, lr=lr, step=step_dev, betas=betas, eps=eps, dot_tm=dot_tm,
-            dot_scale=alpha)
 
 
 def rowmax_nt(a, b, alpha=1.0, cfg=None):

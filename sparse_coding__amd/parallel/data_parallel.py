@@ -47,7 +47,6 @@ class DataParallelFused:
         self.grad_dtype = grad_dtype
         engine.grad_scale = 1.0 / info.world_size
         if info.enabled:
-            engine.fuse_adam = False  # gradients are all-reduced before the (separate) Adam kernels
             self.sync_params()
 
     def sync_params(self):
@@ -151,7 +150,6 @@ class FusedChunk:
     def __init__(self, engine, graph: bool = False, x_static=None):
         _check_kind(engine)
         self.engine = engine
-        engine.fuse_adam = False  # gradients are reduced before Adam
         self.graph = graph
         self.x_static = x_static
         self._graphs = {}
@@ -300,9 +298,14 @@ class ChunkedDataParallel:
     def _reduce(self, c, flat):
         # chunks with their own collective pattern (ZeRO-1: reduce-scatter + all-reduce of the
         # bias) return a pending handle; the default is one all-reduce of the flat gradient
-        if hasattr(c, "reduce_async"):
-            return c.reduce_async()
-        return self._reduce_async(flat)
+        h = c.reduce_async() if hasattr(c, "reduce_async") else self._reduce_async(flat)
+        if serialized():  # race debugging (utils.debug.serialize_streams): no overlap at all
+            torch.cuda.synchronize() if torch.cuda.is_available() else None
+            if hasattr(h, "wait") and not isinstance(h, tuple):
+                h.wait()
+            elif h[0] is not None:
+                h[0].wait()
+        return h
 
     def _complete(self, j, handle):
         c = self.chunks[j]
@@ -341,6 +344,14 @@ class ChunkedDataParallel:
             self._carry = None
             return self._complete(j, h)
         return None
+
+
+def serialized() -> bool:
+    """``SC_SERIALIZE_STREAMS=1`` (``utils.debug.serialize_streams``): every collective completes
+    before the next kernel is issued -- overlap-induced races show up as result differences."""
+    import os
+
+    return os.environ.get("SC_SERIALIZE_STREAMS", "0") not in ("", "0")
 
 
 def split_models(models, n_chunks: int):

@@ -57,6 +57,34 @@ def comm_bytes_per_step(mode: str, world: int, grad_bytes: int, shadow_bytes: in
     raise ValueError(mode)
 
 
+def _gloo_cuda(t) -> bool:
+    """gloo moves CUDA tensors for all-reduce / broadcast only (tests with several ranks sharing
+    one GPU): reduce-scatter and all-gather then go through an all-reduce."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def reduce_scatter_async(out, inp):
+    """out = this rank's 1/N slice of sum_ranks(inp) (async handle or None when completed)."""
+    if _gloo_cuda(inp):
+        tmp = inp.clone()
+        dist.all_reduce(tmp)
+        r = dist.get_rank()
+        out.copy_(tmp.view(dist.get_world_size(), -1)[r])
+        return None
+    return dist.reduce_scatter_tensor(out, inp, async_op=True)
+
+
+def all_gather_async(flat, lo, hi):
+    """Every rank's [lo, hi) slice of ``flat`` (its own slice is current) into all ranks' ``flat``."""
+    if _gloo_cuda(flat):
+        tmp = torch.zeros_like(flat)
+        tmp[lo:hi] = flat[lo:hi]
+        dist.all_reduce(tmp)
+        flat.copy_(tmp)
+        return None
+    return dist.all_gather_into_tensor(flat, flat[lo:hi], async_op=True)
+
+
 def graphed_region(chunk, key, fn):
     """Run ``fn`` (kernel launches only) -- from a HIP graph captured on first use when
     ``chunk.graph`` is set; one graph per (key, feature-counting step or not)."""
@@ -113,7 +141,6 @@ class ZeroFusedChunk:
         self.engine = e = engine
         self.info = info
         self.grad_dtype = grad_dtype
-        e.fuse_adam = False  # gradients are reduced between the weight-gradient GEMMs and Adam
         G, n, d = e.n_models, e.n, e.d
         self.lo, self.hi = shard_range(G * n, info.rank, info.world_size)
         rows = self.hi - self.lo
@@ -178,10 +205,10 @@ class ZeroFusedChunk:
         for i, (src, dst) in enumerate(zip(srcs, dsts)):
             if self._lowp:
                 self._rs_in[i].copy_(src.view(-1))
-                w = dist.reduce_scatter_tensor(self._rs_out[i], self._rs_in[i], async_op=True)
+                w = reduce_scatter_async(self._rs_out[i], self._rs_in[i])
                 pend.add(w, (lambda i=i, dst=dst: dst.view(-1).copy_(self._rs_out[i])))
             else:
-                pend.add(dist.reduce_scatter_tensor(dst.view(-1), src.reshape(-1), async_op=True))
+                pend.add(reduce_scatter_async(dst.view(-1), src.reshape(-1)))
         # untied: _g_flat = [g_enc | g_bias]; tied: [g_dict | g_bias | extras] -- the tail is small
         pend.add(dist.all_reduce(e._g_flat[G * n * d:], async_op=True))
         return pend
@@ -225,11 +252,9 @@ class ZeroFusedChunk:
         shadows = [e.dec_shadow] if e.kind == "untied" else []
         shadows.append(e.enc_shadow)
         for sh in shadows:
-            flat = sh.view(-1)
-            self._ag.add(dist.all_gather_into_tensor(flat, flat[lo * d:hi * d], async_op=True))
+            self._ag.add(all_gather_async(sh.view(-1), lo * d, hi * d))
         # norms travel too (cheap) so every rank's copy is valid for exports / refreshes
-        nf = e.norms.view(-1)
-        self._ag.add(dist.all_gather_into_tensor(nf, nf[lo:hi].clone(), async_op=True))
+        self._ag.add(all_gather_async(e.norms.view(-1), lo, hi))
 
     def gather_masters(self):
         """All-gather the fp32 masters and moments (exports / checkpoints): afterwards every
@@ -241,8 +266,9 @@ class ZeroFusedChunk:
         keys = ["decoder", "encoder"] if e.kind == "untied" else ["encoder"]
         for store in (e.params, e.m, e.v):
             for k in keys:
-                flat = store[k].view(-1)
-                dist.all_gather_into_tensor(flat, flat[lo * d:hi * d].clone())
+                w = all_gather_async(store[k].view(-1), lo * d, hi * d)
+                if w is not None:
+                    w.wait()
 
 
 class ZeroEagerChunk:

@@ -9,8 +9,8 @@ checks here are the ones that run on a normal build:
 * ``assert_deterministic(make_state, step)`` -- run one step twice from identical state
   and compare every output bit for bit (the GEMM epilogues, bias reduction and top-k
   select are designed to be deterministic; no float atomics on the training path);
-* ``serialize_streams()`` -- make side-stream work (Adam overlap, RCCL) wait for the
-  compute stream, to tell a stream-ordering race from a numerical bug.
+* ``serialize_streams()`` -- make the data-parallel collectives (RCCL stream) complete before the
+  next kernel is issued, to tell a stream-ordering race from a numerical bug.
 """
 
 from __future__ import annotations
@@ -54,7 +54,8 @@ def assert_deterministic(make_state: Callable[[], object], step: Callable[[objec
 
 @contextlib.contextmanager
 def serialize_streams():
-    """Run everything on the default stream: engines check ``SC_SERIALIZE_STREAMS``."""
+    """No compute / communication overlap: data-parallel collectives complete before the next
+    kernel is issued (``parallel.data_parallel.serialized`` checks ``SC_SERIALIZE_STREAMS``)."""
     old = os.environ.get("SC_SERIALIZE_STREAMS")
     os.environ["SC_SERIALIZE_STREAMS"] = "1"
     try:

@@ -131,7 +131,7 @@ def _sig(kind):
             "tied_centered": S.FunctionalTiedCenteredSAE, "tied": S.FunctionalTiedSAE}[kind]
 
 
-def _dp_gpu_worker(rank, world, port, x, init, kind, q, steps=3, grad_dtype=None):
+def _dp_gpu_worker(rank, world, port, x, init, kind, q, steps=3, grad_dtype=None, mode="dp"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     from sparse_coding__amd.engine.fused import FusedSAEEnsemble
@@ -145,12 +145,26 @@ def _dp_gpu_worker(rank, world, port, x, init, kind, q, steps=3, grad_dtype=None
         models = [(dict((k, torch.randn_like(v)) for k, v in p.items()), b) for p, b in models]
     engines = [FusedSAEEnsemble(m, _sig(kind), lr=1e-3, batch_size=x.shape[0] // world, device="cuda:0")
                for m in split_models(models, 2)]
-    dp = ChunkedDataParallel([FusedChunk(e) for e in engines], info, grad_dtype or torch.float32)
+    gdt = grad_dtype or torch.float32
+    graph = mode.endswith("_graph")
+    xbuf = torch.empty(x.shape[0] // world, x.shape[1], device="cuda:0", dtype=torch.bfloat16)
+    if mode.startswith("zero1"):
+        from sparse_coding__amd.parallel.zero import ZeroFusedChunk
+
+        chunks = [ZeroFusedChunk(e, info, gdt, graph=graph, x_static=xbuf) for e in engines]
+    else:
+        chunks = [FusedChunk(e, graph=graph, x_static=xbuf) for e in engines]
+    dp = ChunkedDataParallel(chunks, info, gdt, cross_step=mode != "dp")
     xall = x.cuda()
     nb = xall.shape[0] // (world * engines[0].batch_size)
     for s_ in range(steps):  # walk the batches so a long run sees fresh rows
         blk = xall.chunk(nb)[s_ % nb] if nb > 1 else xall
-        out = dp.step_batch(blk.chunk(world)[rank].contiguous())
+        xbuf.copy_(blk.chunk(world)[rank])
+        out = dp.step_batch(xbuf)
+    dp.flush()
+    for c in chunks:
+        if hasattr(c, "gather_masters"):  # ZeRO-1: each rank owns a row shard of the masters
+            c.gather_masters()
     torch.cuda.synchronize()
     res = {k: torch.cat([e.params[k] for e in engines]).cpu().numpy() for k in engines[0].params}
     if steps > 3:
@@ -203,6 +217,52 @@ def test_chunked_dp_fused_two_ranks_one_gpu(kind):
         du, dr = (res[0][k] - init_k).ravel(), (want - init_k).ravel()
         cos = float(du @ dr / (np.linalg.norm(du) * np.linalg.norm(dr) + 1e-30))
         assert cos > 0.99, (k, cos)
+
+
+@pytest.mark.parametrize("mode,kind", [("dp_graph", "untied"), ("zero1", "untied"), ("zero1_graph", "untied"),
+                                       ("zero1_graph", "tied")])
+def test_dp_modes_two_ranks_one_gpu(mode, kind):
+    """Graph-captured data parallel and ZeRO-1 (reduce-scatter -> row-sharded Adam -> shadow
+    all-gather) on two gloo ranks sharing cuda:0: replicas identical after gathering the
+    masters, updates match single-process training on the global batch."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+
+    torch.manual_seed(1)
+    d, n, B = 256, 512, 512
+    sig = _sig(kind)
+    init = [sig.init(d, n, l1) for l1 in (1e-4, 3e-4, 1e-3, 2e-3)]
+    feats = torch.nn.functional.normalize(torch.randn(1024, d), dim=-1)
+    x = (torch.relu(torch.randn(B, 1024) - 2.0) @ feats + 0.1).to(torch.bfloat16)
+    ref = FusedSAEEnsemble([({k: v.cuda() for k, v in p.items()}, {k: v.cuda() for k, v in b.items()})
+                            for p, b in init], sig, lr=1e-3, batch_size=B, device="cuda:0")
+    for _ in range(3):
+        ref.step_batch(x.cuda())
+    torch.cuda.synchronize()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_gpu_worker, args=(r, 2, port, x, init, kind, q, 3, None, mode))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in res[0]:
+        np.testing.assert_array_equal(res[0][k], res[1][k])
+        want = ref.params[k].cpu().numpy()
+        init_k = np.stack([p[k].numpy() for p, _ in init])
+        du, dr = (res[0][k] - init_k).ravel(), (want - init_k).ravel()
+        cos = float(du @ dr / (np.linalg.norm(du) * np.linalg.norm(dr) + 1e-30))
+        assert cos > 0.99, (mode, k, cos)
 
 
 def test_sweep_cli_ensemble_sharded_rccl(tmp_path):
