@@ -75,13 +75,15 @@ def cfg_topk(a):
     n = d * ratio
     ks = [8, 16, 24, 32, 48, 64, 96, 128][: a.models]
     models = [TopKEncoder.init(d, n, k, device=dev) for k in ks]
-    eng = FusedTopKEnsemble(models, lr=1e-3, batch_size=B, device=dev, decode=a.decode)
+    sk = a.sparse_k if a.sparse_k == "auto" else int(a.sparse_k)
+    eng = FusedTopKEnsemble(models, lr=1e-3, batch_size=B, device=dev, sparse_k=sk)
+    eng.enable_graph(not a.eager)
     ring = _ring(d, dev)
-    xbuf = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
-    el = _timed(lambda: eng.step_batch(ring.sample(B, out=xbuf)), a.steps, a.warmup, torch.cuda.synchronize)
-    return {"config": f"4: GPT-2-small residual d={d}, ratio {ratio} (n={n}), fused top-k, k={ks}, {a.decode} decode",
+    el = _timed(lambda: eng.step_batch(ring.sample(B, out=eng.x_static)), a.steps, a.warmup, torch.cuda.synchronize)
+    return {"config": f"4: GPT-2-small residual d={d}, ratio {ratio} (n={n}), fused top-k, k={ks}",
             "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
-            "batch": B, "models": len(ks), "dtype": "bf16", "data": "synthetic"}
+            "batch": B, "models": len(ks), "sparse_wgrad_models": eng.sparse_g, "graph": not a.eager,
+            "dtype": "bf16", "data": "synthetic"}
 
 
 def cfg_fista(a):
@@ -309,7 +311,8 @@ def main():
     ap.add_argument("--models", type=int, default=8)
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--ratio", type=float, default=1.0)
-    ap.add_argument("--decode", choices=["gather", "gemm"], default="gather", help="topk: decode path")
+    ap.add_argument("--sparse-k", default="auto", help="topk: models with k <= this take the slot-list wgrad")
+    ap.add_argument("--eager", action="store_true", help="topk: no HIP graph")
     ap.add_argument("--ring-gb", type=float, default=0.0, help="fista: ring size in GB of HBM (0: 512k rows)")
     a = ap.parse_args()
     rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "fistaloss": cfg_fistaloss, "mlp": cfg_mlp, "mlpout": cfg_mlpout, "masked": cfg_masked,

@@ -1,4 +1,4 @@
-"""Gram-form FISTA solve: 32-row vs 16-row workgroups (SC_FISTA_RT1), interleaved."""
+"""Gram-form FISTA solve: 32-row vs 16-row workgroups (fista(..., rows=16)), interleaved."""
 import json
 import os
 import statistics
@@ -24,19 +24,15 @@ def main():
         outs = {}
         for _ in range(5):
             for mode in ("rt2", "rt1"):
-                if mode == "rt1":
-                    os.environ["SC_FISTA_RT1"] = "1"
-                else:
-                    os.environ.pop("SC_FISTA_RT1", None)
                 torch.cuda.synchronize()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                A, _ = F.fista(X, D, lam, None, iters, eta, backend="hip", with_res=False, form="gram")
+                A, _ = F.fista(X, D, lam, None, iters, eta, backend="hip", with_res=False, form="gram",
+                                rows=16 if mode == "rt1" else 0)
                 e.record()
                 torch.cuda.synchronize()
                 res[mode].append(s.elapsed_time(e))
                 outs[mode] = A
-        os.environ.pop("SC_FISTA_RT1", None)
         diff = (outs["rt2"] - outs["rt1"]).abs().max().item()
         print(json.dumps({"n": n, "d": d, "G": G, "B": B, "iters": iters,
                           **{k: round(statistics.median(v), 3) for k, v in res.items()}, "max_abs_diff": diff}))

@@ -14,10 +14,10 @@
 #   pmc        three rocprofv3 --pmc passes over scripts/prof_step_kernels.py
 #   lab        scripts/gemm_lab.py (LAB_ARGS env passes flags)
 #   py:FILE    python -u FILE (PY_ARGS env passes flags), e.g. py:scripts/kernel_bench.py
-#   ab         alternating A/B of one env knob: AB_CMD (a python command line printing one JSON
-#              line), AB_VAR (env variable), AB_VALUES (space-separated), AB_ROUNDS (default 2);
-#              every run appends to gpurun_out/ab/<value>.jsonl, then a ms_per_step summary.
-#              e.g. AB_CMD="scripts/bench_configs.py topk --steps 40" AB_VAR=SC_TOPK_RU AB_VALUES="4 8"
+#   ab         alternating A/B of command-line variants: AB_CMD (a python command line printing one
+#              JSON line), AB_VALUES ('|'-separated extra flags, one set per variant), AB_ROUNDS
+#              (default 2); run i of variant v appends to gpurun_out/ab/v<v>.jsonl, then a summary.
+#              e.g. AB_CMD="scripts/bench_configs.py topk --steps 40" AB_VALUES="--sparse-k 0|--sparse-k auto"
 #   ktest:K    pytest tests/test_kernels_gpu.py tests/test_train_gpu.py -k K
 #   profile:CMD  rocprofv3 --kernel-trace --stats of "python3 CMD" (top-20 summary)
 # Extra bench flags: BENCH_ARGS env.
@@ -69,9 +69,10 @@ PY
       timeout -k 10 400 python -u scripts/gemm_lab.py ${LAB_ARGS} > "$O/gemm_lab.log" 2>&1; local rc=$?; cat "$O/gemm_lab.log"; return $rc ;;
     ab)
       mkdir -p "$O/ab"
+      local IFS_OLD="$IFS"; IFS='|' read -r -a variants <<< "${AB_VALUES}"; IFS="$IFS_OLD"
       for r in $(seq 1 "${AB_ROUNDS:-2}"); do
-        for v in ${AB_VALUES}; do
-          env "${AB_VAR}=$v" timeout -k 10 300 python ${AB_CMD} >> "$O/ab/$v.jsonl" 2>> "$O/ab/err.log" || { tail -20 "$O/ab/err.log"; return 1; }
+        for i in "${!variants[@]}"; do
+          timeout -k 10 300 python ${AB_CMD} ${variants[$i]} >> "$O/ab/v$i.jsonl" 2>> "$O/ab/err.log" || { tail -20 "$O/ab/err.log"; return 1; }
         done
       done
       grep -o '"ms_per_step": [0-9.]*\|"solve_ms_all_models": [0-9.]*' "$O"/ab/*.jsonl ;;

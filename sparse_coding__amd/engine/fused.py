@@ -182,11 +182,11 @@ class FusedSAEEnsemble:
         self.g_parts = (torch.empty(nprob, self.wsplit, G, n, d, device=dev, dtype=torch.float32)
                         if self.wsplit > 1 else None)
         self._g_from_parts = False
-        # bf16 weight gradients for the single-device step (``grad_dtype='bf16'``, or env
-        # SC_GRAD_DTYPE): the weight-gradient GEMM's bf16 epilogue and Adam's bf16-gradient loads
+        # bf16 weight gradients for the single-device step (``grad_dtype='bf16'``): the
+        # weight-gradient GEMM's bf16 epilogue and Adam's bf16-gradient loads
         # halve the gradient's HBM round trip; masters, moments and the update stay fp32.
         # Data-parallel paths keep the fp32 flat buffers (their all-reduce reads those).
-        gdt = grad_dtype or os.environ.get("SC_GRAD_DTYPE", "fp32")
+        gdt = grad_dtype or "fp32"
         if gdt not in ("fp32", "bf16"):
             raise ValueError(f"grad_dtype must be 'fp32' or 'bf16', got {gdt!r}")
         self.g_bf = (torch.empty(nprob, G, n, d, device=dev, dtype=bf)

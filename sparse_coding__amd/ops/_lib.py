@@ -58,12 +58,14 @@ def _declare(lib):
         "sc_topk_decode_grad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
         "sc_topk_sparse_wgrad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
-                                 c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
+                                 c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p],
+        "sc_topk_slot_lists": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                               c_int, c_int, c_void_p],
         "sc_topk_clear": [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_void_p],
         "sc_topk_scatter": [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int, c_int, c_int, c_void_p],
         "sc_fista": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                     c_void_p],
+                     c_void_p, c_int],
         "sc_center_rows": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
         "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_void_p],
         "sc_lista_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
@@ -77,7 +79,7 @@ def _declare(lib):
                              c_float, c_float, c_int, c_int, c_int, c_int, c_int, c_void_p],
         "sc_fista_adjoint_init": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
         "sc_fista_gram": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                          c_int, c_int, c_int, c_int, c_void_p],
+                          c_int, c_int, c_int, c_int, c_void_p, c_int],
         "sc_stream_create_cumask": [c_void_p, c_int, C.POINTER(c_void_p)],
         "sc_stream_destroy": [c_void_p],
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],

@@ -381,18 +381,18 @@ using namespace scamd;
 extern "C" {
 
 // Ysave / Rsave / Asave: the iterate slabs of FistaArgs, all three or none (then plain solve).
-static int launch_direct(const FistaArgs& a, int G, hipStream_t stream);
+static int launch_direct(const FistaArgs& a, int G, hipStream_t stream, int rows);
 
 int sc_fista(const void* X, const void* D, const void* Dt, const float* A0, const float* eta, const float* lam,
              const float* mom, float* A, float* Res, int G, int B, int n, int d, int T, void* Ysave, void* Rsave,
-             void* Asave, hipStream_t stream) {
+             void* Asave, hipStream_t stream, int rows) {
   if (B % FR || n % 128 || d % 128 || T < 0) return 1;
   if ((Ysave != nullptr) != (Asave != nullptr) || (Ysave != nullptr) != (Rsave != nullptr)) return 1;
   FistaArgs a{reinterpret_cast<const uint16_t*>(X), reinterpret_cast<const uint16_t*>(D),
               reinterpret_cast<const uint16_t*>(Dt), A0, eta, lam, mom, A, Res, B, n, d, T,
               reinterpret_cast<uint16_t*>(Ysave), reinterpret_cast<uint16_t*>(Rsave), reinterpret_cast<uint16_t*>(Asave),
               0, 0.f, 0.f};
-  return launch_direct(a, G, stream);
+  return launch_direct(a, G, stream, rows);
 }
 
 // Direct coefficient search (mode 1 of the direct solver): T projected-SGD-with-momentum steps
@@ -405,15 +405,15 @@ int sc_coef_search(const void* X, const void* D, const void* Dt, const float* A0
   FistaArgs a{reinterpret_cast<const uint16_t*>(X), reinterpret_cast<const uint16_t*>(D),
               reinterpret_cast<const uint16_t*>(Dt), A0, lr, lam, mom, A, Res, B, n, d, T,
               nullptr, nullptr, nullptr, 1, gscale, lscale};
-  return launch_direct(a, G, stream);
+  return launch_direct(a, G, stream, 0);
 }
 
-static int launch_direct(const FistaArgs& a, int G, hipStream_t stream) {
+static int launch_direct(const FistaArgs& a, int G, hipStream_t stream, int rows) {
   const int B = a.B, n = a.n, d = a.d;
   const int DW = d / 128, NW = n / 128;
   // 32-row workgroups where the doubled fp32 state fits (NW * DW small) and the LDS does
-  // (SC_FISTA_RT1 / SC_FISTA_RT2: force the 16- / 32-row form where it is legal -- tests, A/B)
-  const bool no_rt2 = getenv("SC_FISTA_RT1") != nullptr, force_rt2 = getenv("SC_FISTA_RT2") != nullptr;
+  // (rows = 16 / 32 forces that form where it is legal -- tests, A/B; 0 = this heuristic)
+  const bool no_rt2 = rows == 16, force_rt2 = rows == 32;
   const size_t lds1 = (size_t)FR * (2 * n + 4 * d), lds2 = 2 * lds1;
   const bool rt2 = !no_rt2 && B % (2 * FR) == 0 && lds2 <= 160 * 1024 &&
                    (force_rt2 || (long)G * (B / (2 * FR)) >= 256);
@@ -452,11 +452,11 @@ static int launch_direct(const FistaArgs& a, int G, hipStream_t stream) {
 // Gram-form solver: C = X D^T [G][B][n] fp32, Gm = D D^T bf16 in MFMA-fragment order
 // [G][n/16][n/32][64 lanes][8] (lane = 16 q + r holds Gm[16 tile + r][32 step + 8 q .. + 7]).
 int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* eta, const float* lam,
-                  const float* mom, float* A, int G, int B, int n, int T, hipStream_t stream) {
+                  const float* mom, float* A, int G, int B, int n, int T, hipStream_t stream, int rows) {
   if (B % FR || n % 128 || T < 0) return 1;
   const uint16_t* gm = reinterpret_cast<const uint16_t*>(Gm);
-  // 32-row workgroups when they still give >= 2 per CU (256 CUs); else 16 rows
-  const bool two = (B % (2 * FR) == 0) && (long)G * (B / (2 * FR)) >= 512 && !getenv("SC_FISTA_RT1");
+  // 32-row workgroups when they still give >= 2 per CU (256 CUs); else 16 rows (rows = 16 forces it)
+  const bool two = (B % (2 * FR) == 0) && (long)G * (B / (2 * FR)) >= 512 && rows != 16;
   const dim3 g2(G * (B / (2 * FR))), g1(G * (B / FR));
   // (NW, halves, ring depth) for 32-row, then 16-row workgroups: past n = 512 the fp32 iterates
   // need the column passes split, and the Gm ring shrinks to stay spill-free in 256 VGPRs
@@ -466,17 +466,8 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
     else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                        \
   }
-  static const int alt = getenv("SC_FISTA_GRAM_ALT") ? atoi(getenv("SC_FISTA_GRAM_ALT")) : 0;
-  // A/B knob: eight column passes with a 4- / 8-deep Gm ring (fewer accumulators live, more LDS
-  // re-reads of Y): 14.2 / 15.3 ms vs 12.9 ms for the default (4 passes, ring 2) -- kept off
-  if (n == 1024 && two && alt == 1) {
-    hipLaunchKernelGGL((fista_gram_kernel<8, 2, 8, 4>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T);
-    return hipGetLastError() == hipSuccess ? 0 : 3;
-  }
-  if (n == 1024 && two && alt == 2) {
-    hipLaunchKernelGGL((fista_gram_kernel<8, 2, 8, 8>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T);
-    return hipGetLastError() == hipSuccess ? 0 : 3;
-  }
+  // (eight column passes with a 4- / 8-deep Gm ring measured 14.2 / 15.3 ms vs 12.9 ms for
+  // n = 1024's four passes with ring 2 -- not instantiated)
   SC_G(2, 1, 4, 1, 4) SC_G(4, 1, 4, 1, 8) SC_G(6, 2, 2, 2, 4) SC_G(8, 4, 2, 2, 4)
 #undef SC_G
   return 2;

@@ -749,19 +749,161 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Feature-major slot lists on the device (a counting sort of the picks, no host round trip):
+//   slot_count   per (model, block of rows): LDS histogram of the picked features (slots s < k),
+//                then one global add per non-empty bin (a popular feature costs one atomic per
+//                block, not one per row)
+//   slot_offsets per model: exclusive scan of the counts -> list offsets (model bases from k);
+//                re-zeroes the counts for the next step
+//   slot_scatter per (model, block of rows): reserves each bin's range with one global add, then
+//                places the picks with LDS atomics (order within a list is arbitrary here)
+//   slot_sort    one wave per list: orders it by batch row -- a 64-lane bitonic sort for short
+//                lists, a presence bitmap over the rows for long ones -- so the weight
+//                gradient sums in a fixed order (deterministic)
+// Slot id = (g B + b) kmax + s: the flat index of the pick in idx / val (and dscv).
+__global__ __launch_bounds__(256) void topk_slot_count_kernel(const int* __restrict__ idx, const int* __restrict__ kv,
+                                                              int* __restrict__ cnt, int B, int n, int kmax, int rpb) {
+  extern __shared__ int hist[];
+  const int g = blockIdx.y, b0 = blockIdx.x * rpb, tid = threadIdx.x;
+  const int k = min(kv[g], kmax);
+  for (int j = tid; j < n; j += 256) hist[j] = 0;
+  __syncthreads();
+  const int rows = min(rpb, B - b0);
+  for (int t = tid; t < rows * k; t += 256) {
+    const int r = t / k, sl = t - r * k;
+    atomicAdd(&hist[idx[((long)g * B + b0 + r) * kmax + sl]], 1);
+  }
+  __syncthreads();
+  for (int j = tid; j < n; j += 256)
+    if (hist[j]) atomicAdd(&cnt[(long)g * n + j], hist[j]);
+}
+
+__global__ __launch_bounds__(1024) void topk_slot_offsets_kernel(int* __restrict__ cnt, const int* __restrict__ kv,
+                                                                 int* __restrict__ offs, int* __restrict__ cursor,
+                                                                 int Gs, int B, int n, int kmax) {
+  __shared__ int wsum[16];
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  long base = 0;  // slots of the models before g
+  for (int q = 0; q < g; ++q) base += (long)B * min(kv[q], kmax);
+  const int per = (n + 1023) / 1024;  // consecutive bins per thread
+  const int j0 = tid * per;
+  int local = 0;
+  for (int u = 0; u < per; ++u)
+    if (j0 + u < n) local += cnt[(long)g * n + j0 + u];
+  // block-wide exclusive scan of the per-thread sums
+  int incl = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int wbase = 0;
+  for (int q = 0; q < w; ++q) wbase += wsum[q];
+  int run = (int)base + wbase + incl - local;
+  for (int u = 0; u < per; ++u) {
+    const int j = j0 + u;
+    if (j >= n) break;
+    const long r = (long)g * n + j;
+    offs[r] = run;
+    cursor[r] = run;
+    run += cnt[r];
+    cnt[r] = 0;  // ready for the next step's counts
+  }
+  if (g == Gs - 1 && tid == 1023) offs[(long)Gs * n] = run;  // (the last bin's thread holds the end)
+}
+
+__global__ __launch_bounds__(256) void topk_slot_scatter_kernel(const int* __restrict__ idx, const int* __restrict__ kv,
+                                                                int* __restrict__ cursor, int* __restrict__ tmp, int B,
+                                                                int n, int kmax, int rpb) {
+  extern __shared__ int lds[];
+  int* hist = lds;        // [n] counts, then this block's next position per bin
+  const int g = blockIdx.y, b0 = blockIdx.x * rpb, tid = threadIdx.x;
+  const int k = min(kv[g], kmax);
+  for (int j = tid; j < n; j += 256) hist[j] = 0;
+  __syncthreads();
+  const int rows = min(rpb, B - b0);
+  for (int t = tid; t < rows * k; t += 256) {
+    const int r = t / k, sl = t - r * k;
+    atomicAdd(&hist[idx[((long)g * B + b0 + r) * kmax + sl]], 1);
+  }
+  __syncthreads();
+  for (int j = tid; j < n; j += 256)
+    if (hist[j]) hist[j] = atomicAdd(&cursor[(long)g * n + j], hist[j]);  // reserve this block's range
+  __syncthreads();
+  for (int t = tid; t < rows * k; t += 256) {
+    const int r = t / k, sl = t - r * k;
+    const int slot = ((g * B) + b0 + r) * kmax + sl;
+    tmp[atomicAdd(&hist[idx[slot]], 1)] = slot;
+  }
+}
+
+// LB: rows covered by the long-list bitmap path (B <= 64 * LB)
+template <int LB>
+__global__ __launch_bounds__(256) void topk_slot_sort_kernel(const int* __restrict__ tmp, const int* __restrict__ offs,
+                                                             int* __restrict__ perm, long lists, int B, int kmax) {
+  __shared__ unsigned long long bits[4][LB];
+  __shared__ unsigned char sof[4][64 * LB];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long row = (long)blockIdx.x * 4 + w;
+  if (row >= lists) return;
+  const int beg = offs[row], L = offs[row + 1] - beg;
+  if (L <= 64) {  // bitonic sort of the (unique) slot ids across the wave
+    int key = lane < L ? tmp[beg + lane] : 0x7FFFFFFF;
+#pragma unroll
+    for (int sz = 2; sz <= 64; sz <<= 1)
+#pragma unroll
+      for (int j = sz >> 1; j > 0; j >>= 1) {
+        const int other = __shfl_xor(key, j, 64);
+        const bool up = (lane & sz) == 0, low = (lane & j) == 0;
+        key = (low == up) ? min(key, other) : max(key, other);
+      }
+    if (lane < L) perm[beg + lane] = key;
+    return;
+  }
+  // long list: every batch row appears at most once -> presence bitmap over b, then compaction
+  // in b order (the slot's s is kept per row)
+  const int g_b0 = (tmp[beg] / kmax) / B * B;  // model row base (g B) of this list
+  for (int q = lane; q < LB; q += 64) bits[w][q] = 0ull;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  for (int i = lane; i < L; i += 64) {
+    const int slot = tmp[beg + i];
+    const int gb = slot / kmax, b = gb - g_b0;
+    sof[w][b] = (unsigned char)(slot - gb * kmax);
+    atomicOr(&bits[w][b >> 6], 1ull << (b & 63));
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  int pos = beg;
+  for (int q = 0; q < (B + 63) / 64; ++q) {
+    const unsigned long long m = bits[w][q];
+    const bool on = (m >> lane) & 1ull;
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (on) {
+      const int b = q * 64 + lane;
+      perm[pos + before] = (g_b0 + b) * kmax + sof[w][b];
+    }
+    pos += __popcll(m);
+  }
+}
+
 // Sparse weight gradient for top-k dictionaries with small k / n (the dense GEMM would multiply
 // mostly zeros): for dictionary row j of model g,
 //   G[g, j, :] = alpha * sum over the slots (b, s) that picked j of  val * R[g, b, :] + dscv * X[b, :]
-// Slot lists come from a stable sort of the picked indices (deterministic summation order).
-// One wave per dictionary row; rows nobody picked get zeros (Adam reads every row).
+// Slot lists come from the device counting sort above, ordered by batch row (deterministic
+// summation order).  One wave per dictionary row; rows nobody picked get zeros (Adam reads
+// every row).
 template <int NV>  // d == 256 * NV
-__global__ __launch_bounds__(256) void topk_sparse_wgrad_kernel(const long* __restrict__ perm, const int* __restrict__ offs,
+__global__ __launch_bounds__(256) void topk_sparse_wgrad_kernel(const int* __restrict__ perm, const int* __restrict__ offs,
                                                                 const float* __restrict__ val,
                                                                 const float* __restrict__ dscv,
                                                                 const uint16_t* __restrict__ R,
                                                                 const uint16_t* __restrict__ X, long sx,
-                                                                float* __restrict__ Gout, int Gs, int B, int n, int kmax,
-                                                                float alpha) {
+                                                                void* __restrict__ Gout, int Gs, int B, int n, int kmax,
+                                                                float alpha, int out_bf16) {
   constexpr int d = NV * 256;
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -772,7 +914,7 @@ __global__ __launch_bounds__(256) void topk_sparse_wgrad_kernel(const long* __re
 #pragma unroll
   for (int e = 0; e < NV * 4; ++e) acc[e] = 0.f;
   for (int e0 = beg; e0 < end; e0 += 2) {  // two slots in flight
-    long slot[2];
+    int slot[2];
     float cv[2], sv[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -803,7 +945,16 @@ __global__ __launch_bounds__(256) void topk_sparse_wgrad_kernel(const long* __re
         acc[v * 4 + 3] += cv[u] * bf2f(hr[u][v].w) + sv[u] * bf2f(hx[u][v].w);
       }
   }
-  float* Gr = Gout + row * d;
+  if (out_bf16) {  // the dense weight gradient's bf16 storage (Adam reads one dtype for all models)
+    uint16_t* Gr = reinterpret_cast<uint16_t*>(Gout) + row * d;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      *reinterpret_cast<ushort4*>(Gr + (v * 64 + lane) * 4) =
+          make_ushort4(f2bf(alpha * acc[v * 4 + 0]), f2bf(alpha * acc[v * 4 + 1]), f2bf(alpha * acc[v * 4 + 2]),
+                       f2bf(alpha * acc[v * 4 + 3]));
+    return;
+  }
+  float* Gr = reinterpret_cast<float*>(Gout) + row * d;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     *reinterpret_cast<float4*>(Gr + (v * 64 + lane) * 4) =
@@ -843,7 +994,7 @@ extern "C" {
 int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int G, int B, int n, int kmax,
                    int absolute, int relu, hipStream_t stream) {
   // wave bisection wins up to 64 keys per lane (measured: n = 2048 67 vs 147 us, n = 6144 310 vs 223 us)
-  if (n % 4 == 0 && n <= 64 * 64 && !getenv("SC_TOPK_RADIX")) {
+  if (n % 4 == 0 && n <= 64 * 64) {
     const long rows = (long)G * B;
     dim3 wgrid((unsigned)((rows + 3) / 4));
 #define SC_W(P) \
@@ -853,9 +1004,9 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
     SC_W(16) SC_W(32) SC_W(64)
 #undef SC_W
   }
-  if (n % 4 == 0 && n <= 256 * 64 && !getenv("SC_TOPK_RADIX")) {  // long rows: a block per row
+  if (n % 4 == 0 && n <= 256 * 64) {  // long rows: a block per row
     dim3 bgrid((unsigned)G * B);
-    static const int bracket = getenv("SC_TOPK_NOBRACKET") ? 0 : 1;
+    const int bracket = 1;  // bracketed select first (bracket_select; full bisection on heavy ties)
 #define SC_BK(P) \
     if (n <= 256 * P) { hipLaunchKernelGGL((topk_block_kernel<P>), bgrid, dim3(256), 0, stream, scores, k, idx, val, B, n, \
                                            kmax, absolute, relu, bracket); \
@@ -884,52 +1035,44 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx, reinterpret_cast<uint16_t*>(R), \
       row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
-  static const int ru = getenv("SC_TOPK_RU") ? atoi(getenv("SC_TOPK_RU")) : 0;
-  static const int occ = getenv("SC_TOPK_OCC") ? atoi(getenv("SC_TOPK_OCC")) : 0;
-#define SC_DO(RUV, OCCV, DV)                                                                              \
-  {                                                                                                       \
-    hipLaunchKernelGGL((topk_decode_grad_kernel<3, RUV, OCCV, DV>), grid, dim3(256), 0, stream, idx, val, k,  \
-                       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,    \
-                       reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),      \
-                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx);                            \
-    return hipGetLastError() == hipSuccess ? 0 : 3;                                                       \
-  }
-  if (nv == 3 && occ) {  // A/B knob: cap registers for more resident waves (SC_TOPK_OCC = waves / SIMD)
-    if (occ == 3) SC_DO(8, 3, 16)
-    if (occ == 4) SC_DO(8, 4, 16)
-    if (occ == 5) SC_DO(8, 5, 8)
-    if (occ == 6) SC_DO(4, 6, 8)
-    if (occ == 48) SC_DO(8, 4, 8)
-    if (occ == 44) SC_DO(4, 4, 8)
-  }
-#undef SC_DO
-  if (nv == 3 && ru == 16) {  // A/B knob (SC_TOPK_RU): 8 rows per iteration is the default for d <= 768
-    hipLaunchKernelGGL((topk_decode_grad_kernel<3, 16>), grid, dim3(256), 0, stream, idx, val, k,
-                       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,
-                       reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),
-                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx);
-    return hipGetLastError() == hipSuccess ? 0 : 3;
-  }
-  if (nv == 3 && ru == 4) {
-    hipLaunchKernelGGL((topk_decode_grad_kernel<3, 4>), grid, dim3(256), 0, stream, idx, val, k,
-                       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx,
-                       reinterpret_cast<uint16_t*>(R), row_se, reinterpret_cast<uint16_t*>(codebuf),
-                       reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx);
-    return hipGetLastError() == hipSuccess ? 0 : 3;
-  }
   SC_D(1) SC_D(2) SC_D(3) SC_D(4) SC_D(8) SC_D(16)
 #undef SC_D
   return 1;
 }
 
+// Feature-major slot lists of models [0, Gs): cnt [Gs n] (zero on entry, left zero), offs
+// [Gs n + 1], cursor [Gs n], tmp / perm [B sum_g k_g] int32.  Graph-capturable (no host reads).
+int sc_topk_slot_lists(const int* idx, const int* k, int* cnt, int* offs, int* cursor, int* tmp, int* perm, int Gs,
+                       int B, int n, int kmax, hipStream_t stream) {
+  if (n > 32768 || kmax > 256 || Gs < 1 || (long)Gs * B * kmax >= (1l << 31)) return 1;
+  const int rpb = 64;
+  const dim3 grid((unsigned)((B + rpb - 1) / rpb), (unsigned)Gs);
+  const size_t lds = (size_t)n * sizeof(int);
+  hipLaunchKernelGGL(topk_slot_count_kernel, grid, dim3(256), lds, stream, idx, k, cnt, B, n, kmax, rpb);
+  hipLaunchKernelGGL(topk_slot_offsets_kernel, dim3((unsigned)Gs), dim3(1024), 0, stream, cnt, k, offs, cursor, Gs, B, n,
+                     kmax);
+  hipLaunchKernelGGL(topk_slot_scatter_kernel, grid, dim3(256), lds, stream, idx, k, cursor, tmp, B, n, kmax, rpb);
+  const long lists = (long)Gs * n;
+  if (B <= 64 * 32) {
+    hipLaunchKernelGGL((topk_slot_sort_kernel<32>), dim3((unsigned)((lists + 3) / 4)), dim3(256), 0, stream, tmp, offs,
+                       perm, lists, B, kmax);
+  } else if (B <= 64 * 256) {
+    hipLaunchKernelGGL((topk_slot_sort_kernel<256>), dim3((unsigned)((lists + 3) / 4)), dim3(256), 0, stream, tmp, offs,
+                       perm, lists, B, kmax);
+  } else {
+    return 1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
 // G[0 .. Gs) rows of the weight gradient from the sorted slot lists (see the kernel).
-int sc_topk_sparse_wgrad(const long* perm, const int* offs, const float* val, const float* dscv, const void* R,
-                         const void* X, long sx, float* Gout, int Gs, int B, int n, int d, int kmax, float alpha,
-                         hipStream_t stream) {
+int sc_topk_sparse_wgrad(const int* perm, const int* offs, const float* val, const float* dscv, const void* R,
+                         const void* X, long sx, void* Gout, int Gs, int B, int n, int d, int kmax, float alpha,
+                         int out_bf16, hipStream_t stream) {
   dim3 grid((unsigned)(((long)Gs * n + 3) / 4));
 #define SC_SW(V) \
   if (d == 256 * V) { hipLaunchKernelGGL((topk_sparse_wgrad_kernel<V>), grid, dim3(256), 0, stream, perm, offs, val, dscv, \
-      reinterpret_cast<const uint16_t*>(R), reinterpret_cast<const uint16_t*>(X), sx, Gout, Gs, B, n, kmax, alpha); \
+      reinterpret_cast<const uint16_t*>(R), reinterpret_cast<const uint16_t*>(X), sx, Gout, Gs, B, n, kmax, alpha, out_bf16); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   SC_SW(1) SC_SW(2) SC_SW(3) SC_SW(4)
 #undef SC_SW

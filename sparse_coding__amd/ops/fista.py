@@ -115,7 +115,7 @@ DIRECT_TILES = {(2, 2), (2, 4), (2, 8), (2, 16), (4, 4), (4, 8), (4, 16), (6, 6)
 
 
 def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_res: bool = True,
-          form: str = "auto") -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+          form: str = "auto", rows: int = 0) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Solve min_A>=0 1/2|X - A D|^2 + lam |A|_1 (ISTA step eta) for every model.
 
     backend: "hip" (gfx950 kernel, bf16 GEMM operands, fp32 iterates), "torch" (fp32
@@ -123,7 +123,11 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
     form (hip only): "direct" -- two products per iteration, (Y D) then (Res D^T);
     "gram" -- Y += eta (X D^T - Y (D D^T)), one [B, n] x [n, n] product per iteration
     (2 B n^2 instead of 4 B n d FLOPs); "auto" picks gram for n <= d.
+    rows (hip only): batch rows per workgroup, 16 or 32 where that form is instantiated; 0 lets
+    the kernel library choose (32 when that still gives enough workgroups to fill the chip).
     """
+    if rows not in (0, 16, 32):
+        raise ValueError(f"rows must be 0, 16 or 32, got {rows}")
     G, n, d = D.shape
     B = X.shape[-2]
     use_hip = backend == "hip" or (backend == "auto" and D.is_cuda and _lib.available() and B % 16 == 0
@@ -159,7 +163,7 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
         # so every wave fragment load is 1 KB contiguous (8 full lines instead of 16 half lines)
         Gm = Gm.view(G, n // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
         rc = _lib.lib().sc_fista_gram(_lib.ptr(C), _lib.ptr(Gm), _lib.ptr(a0), _lib.ptr(eta), _lib.ptr(lam),
-                                      _lib.ptr(mom), _lib.ptr(A), G, B, n, iters, _lib.stream_handle())
+                                      _lib.ptr(mom), _lib.ptr(A), G, B, n, iters, _lib.stream_handle(), rows)
     else:
         # both operands in MFMA-fragment order (see the Gram form): D [G][n/16][d/32][64][8] for the
         # (Res D^T) product, D^T [G][d/16][n/32][64][8] for the (Y D) product
@@ -167,7 +171,7 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
         Dfb = Db.view(G, n // 16, 16, d // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
         rc = _lib.lib().sc_fista(_lib.ptr(Xb), _lib.ptr(Dfb), _lib.ptr(Dtb), _lib.ptr(a0), _lib.ptr(eta),
                                  _lib.ptr(lam), _lib.ptr(mom), _lib.ptr(A), 0, G, B, n, d, iters, None, None, None,
-                                 _lib.stream_handle())
+                                 _lib.stream_handle(), rows)
     if rc == 2 and backend == "auto":
         return fista_torch(X, D, lam, A0, iters, eta)
     _lib.check(rc, "sc_fista")
@@ -432,7 +436,7 @@ def unrolled_forward_hip(X, D, A0, lam, eta, iters, mom=None):
     mom_d = mom.to(dev)
     rc = _lib.lib().sc_fista(_lib.ptr(Xb), _lib.ptr(Dfb), _lib.ptr(Dtb), _lib.ptr(a0), _lib.ptr(eta),
                              _lib.ptr(lam), _lib.ptr(mom_d), _lib.ptr(A), _lib.ptr(R), G, B, n, d, iters,
-                             _lib.ptr(Ys), _lib.ptr(Rs), _lib.ptr(As), _lib.stream_handle())
+                             _lib.ptr(Ys), _lib.ptr(Rs), _lib.ptr(As), _lib.stream_handle(), 0)
     _lib.check(rc, "sc_fista (saving iterates)")
     return R, Db, Ys, Rs, As
 

@@ -52,37 +52,45 @@ def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dsc
     _lib.check(rc, "sc_topk_decode_grad")
 
 
-def sparse_wgrad(idx, val, dscv, ks, r, x, g_out, alpha, cache=None):
-    """Weight gradient of the first Gs = g_out.shape[0] models from their picked slots only:
-    g[g, j] = alpha * sum_{(b, s): idx[g, b, s] = j, s < ks[g]} val R[g, b] + dscv x[b]
-    (= codes^T R + dscores^T x of the dense path).  ``ks``: the models' k (host ints).  The
-    slots are ordered by sorting the unique keys ((g n + j) B + b) -- a fixed summation order per
-    row without a stable sort -- and the row offsets come from a binary search over the sorted
-    keys (no histogram atomics: padding and popular features made one hot bin).  ``cache``: a
-    dict reused across calls for the step-invariant index tensors."""
+class SlotLists:
+    """Device buffers of the feature-major slot lists for models [0, Gs) (``slot_lists``)."""
+
+    def __init__(self, Gs: int, B: int, n: int, ks, kmax: int, device):
+        total = B * sum(min(int(k), kmax) for k in ks[:Gs])
+        self.Gs, self.B, self.n, self.kmax = Gs, B, n, kmax
+        i32 = torch.int32
+        self.cnt = torch.zeros(Gs * n, device=device, dtype=i32)
+        self.offs = torch.zeros(Gs * n + 1, device=device, dtype=i32)
+        self.cursor = torch.zeros(Gs * n, device=device, dtype=i32)
+        self.tmp = torch.zeros(max(total, 1), device=device, dtype=i32)
+        self.perm = torch.zeros(max(total, 1), device=device, dtype=i32)
+
+
+def slot_lists(idx, k, lists: SlotLists):
+    """Counting sort of the first Gs models' picks by (model, feature) on the device: afterwards
+    ``lists.perm[offs[g n + j] : offs[g n + j + 1]]`` holds the slot ids (g B + b) kmax + s of
+    every row b that picked feature j (s < k[g]), in increasing b.  No host synchronisation (graph
+    capturable); replaces the torch sort / searchsorted of the previous host-built lists."""
+    G, B, kmax = idx.shape
+    if idx.dtype != torch.int32 or not idx.is_contiguous() or kmax != lists.kmax or B != lists.B:
+        raise ValueError("slot_lists: idx must be contiguous int32 [G, B, kmax] matching the buffers")
+    rc = _lib.lib().sc_topk_slot_lists(_lib.ptr(idx), _lib.ptr(k), _lib.ptr(lists.cnt), _lib.ptr(lists.offs),
+                                       _lib.ptr(lists.cursor), _lib.ptr(lists.tmp), _lib.ptr(lists.perm), lists.Gs,
+                                       B, lists.n, kmax, _lib.stream_handle())
+    _lib.check(rc, "sc_topk_slot_lists")
+
+
+def sparse_wgrad(lists: SlotLists, val, dscv, r, x, g_out, alpha):
+    """Weight gradient of the first Gs = lists.Gs models from their picked slots only:
+    g[g, j] = alpha * sum_{(b, s): idx[g, b, s] = j, s < k[g]} val R[g, b] + dscv x[b]
+    (= codes^T R + dscores^T x of the dense path), summed in increasing b.  ``g_out`` fp32 or
+    bf16 [Gs, n, d]."""
     Gs, n, d = g_out.shape
-    _, B, kmax = idx.shape
-    dev = idx.device
-    cache = {} if cache is None else cache
-    sig = (tuple(ks[:Gs]), B, kmax, n)
-    if cache.get("sig") != sig:
-        bcol = torch.arange(B, device=dev, dtype=torch.int64).view(B, 1)
-        base, slot = [], []
-        for g in range(Gs):
-            kg = int(ks[g])
-            base.append((torch.full((B, kg), g * n, device=dev, dtype=torch.int64) * B + bcol).reshape(-1))
-            slot.append(((g * B + bcol) * kmax + torch.arange(kg, device=dev, dtype=torch.int64).view(1, kg)).reshape(-1))
-        cache.update(sig=sig, base=torch.cat(base), slot=torch.cat(slot),
-                     rows=torch.arange(Gs * n + 1, device=dev, dtype=torch.int64))
-    picks = torch.cat([idx[g, :, : int(ks[g])].reshape(-1) for g in range(Gs)]).to(torch.int64)
-    key = picks * B + cache["base"]
-    skey, order = torch.sort(key)
-    perm = cache["slot"][order]
-    offs = torch.searchsorted(skey // B, cache["rows"]).to(torch.int32)
+    _, B, kmax = val.shape
     sx = 0 if x.dim() == 2 else B * d
-    rc = _lib.lib().sc_topk_sparse_wgrad(_lib.ptr(perm), _lib.ptr(offs), _lib.ptr(val), _lib.ptr(dscv), _lib.ptr(r),
-                                         _lib.ptr(x), sx, _lib.ptr(g_out), Gs, B, n, d, kmax, float(alpha),
-                                         _lib.stream_handle())
+    rc = _lib.lib().sc_topk_sparse_wgrad(_lib.ptr(lists.perm), _lib.ptr(lists.offs), _lib.ptr(val), _lib.ptr(dscv),
+                                         _lib.ptr(r), _lib.ptr(x), sx, _lib.ptr(g_out), Gs, B, n, d, kmax, float(alpha),
+                                         int(g_out.dtype == torch.bfloat16), _lib.stream_handle())
     _lib.check(rc, "sc_topk_sparse_wgrad")
 
 
