@@ -129,26 +129,33 @@ def cfg_fista(a):
 
 def cfg_fistaloss(a):
     """FISTA in the loss (reference autoencoders/fista.py:141-172, the fork's fista_13_10 runs):
-    8-model L1 sweep, d = n = 512 (dict_size 512), 50 unrolled iterations inside the loss."""
-    from sparse_coding__amd.engine.fista_loss import FistaLossEnsemble
+    8-model L1 sweep, d = n = 512 (dict_size 512), 50 unrolled iterations inside the loss.
+    The fused engine (tied SAE kernels + Gram-form solve / adjoint + row Adam) and, for
+    comparison, the autograd engine (HIP solve + adjoint, torch SAE half and Adam)."""
+    from sparse_coding__amd.engine.fista_loss import FistaLossEnsemble, FusedFistaLossEnsemble
     from sparse_coding__amd.models.fista import FunctionalFista
 
     dev = "cuda:0"
     torch.manual_seed(0)
     d, n, B = 512, int(512 * a.ratio), a.batch
     models = [FunctionalFista.init(d, n, float(l1), device=dev) for l1 in np.logspace(-4, -2, a.models)]
-    eng = FistaLossEnsemble(models, lr=1e-3, batch_size=B, device=dev, num_iter=a.iters, backend="hip")
     ring = _ring(d, dev)
     xbuf = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
-    losses = []
-    el = _timed(lambda: losses.append(eng.step_batch(ring.sample(B, out=xbuf))), a.steps, a.warmup,
-                torch.cuda.synchronize)
-    return {"config": f"FISTA-in-loss ensemble: d={d}, n={n}, {a.models} models, {a.iters} unrolled iterations, "
-                      "HIP solver + adjoint sweep",
-            "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
-            "batch": B, "loss_first": [round(float(v), 5) for v in losses[0]],
-            "loss_last": [round(float(v), 5) for v in losses[-1]], "dtype": "bf16 GEMM operands, fp32 iterates",
-            "data": "synthetic"}
+    out = {"config": f"FISTA-in-loss ensemble: d={d}, n={n}, {a.models} models, {a.iters} unrolled iterations",
+           "unit": "activations/s", "batch": B, "dtype": "bf16 GEMM operands, fp32 iterates", "data": "synthetic"}
+    for name, cls, kw in (("fused", FusedFistaLossEnsemble, {}), ("autograd", FistaLossEnsemble, {"backend": "hip"})):
+        eng = cls(models, lr=1e-3, batch_size=B, device=dev, num_iter=a.iters, **kw)
+        losses = []
+        el = _timed(lambda: losses.append(eng.step_batch(ring.sample(B, out=xbuf))), a.steps, a.warmup,
+                    torch.cuda.synchronize)
+        out[f"{name}_ms_per_step"] = round(1e3 * el / a.steps, 3)
+        out[f"{name}_loss_first"] = [round(float(v), 5) for v in losses[0]]
+        out[f"{name}_loss_last"] = [round(float(v), 5) for v in losses[-1]]
+        del eng
+        torch.cuda.empty_cache()
+    out["ms_per_step"] = out["fused_ms_per_step"]
+    out["value"] = round(B / out["fused_ms_per_step"] * 1e3, 1)
+    return out
 
 
 def cfg_mlpout(a):

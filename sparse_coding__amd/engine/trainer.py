@@ -88,11 +88,17 @@ class EnsembleTrainer:
             self.impl = self.es.engine
             self.kind = self._es_kind
         elif objective == "fista_loss":
-            from .fista_loss import FistaLossEnsemble
+            from .fista_loss import FistaLossEnsemble, FusedFistaLossEnsemble, fused_ok
 
-            self.impl = FistaLossEnsemble(models, lr=lr, batch_size=batch_size, device=device,
-                                          num_iter=fista_loss_iters, backend=fista_backend)
-            self.kind = "fista-loss"
+            if engine in ("auto", "fused") and fista_backend != "torch" and fused_ok(models, batch_size, device,
+                                                                                     fista_loss_iters):
+                self.impl = FusedFistaLossEnsemble(models, lr=lr, batch_size=batch_size, device=device,
+                                                   num_iter=fista_loss_iters)
+                self.kind = "fista-loss-fused"
+            else:
+                self.impl = FistaLossEnsemble(models, lr=lr, batch_size=batch_size, device=device,
+                                              num_iter=fista_loss_iters, backend=fista_backend)
+                self.kind = "fista-loss"
         elif ok and sig is TopKEncoder:
             from .topk import FusedTopKEnsemble
 

@@ -79,7 +79,7 @@ def _declare(lib):
                              c_float, c_float, c_int, c_int, c_int, c_int, c_int, c_void_p],
         "sc_fista_adjoint_init": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
         "sc_fista_gram": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                          c_int, c_int, c_int, c_int, c_void_p, c_int],
+                          c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
         "sc_stream_create_cumask": [c_void_p, c_int, C.POINTER(c_void_p)],
         "sc_stream_destroy": [c_void_p],
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],

@@ -256,11 +256,23 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
 // columns, then their FISTA update) so only half the accumulators are live, and the bf16
 // copy of Y is double-buffered in LDS (read the current iterate, write the next): one
 // barrier per iteration.
-template <int NW, int RT, int HALVES, int PF>
+//
+// MODE 1 (unrolled FISTA in the loss, forward): also store the bf16 iterate slabs
+//   Ysave [G][T][B][n] slot t = Y_t (the iterate multiplied at iteration t, Y_0 = A0) and
+//   Asave [G][T][B][n] slot t = A_{t+1} (its support masks the adjoint).
+// MODE 2 (its adjoint, reverse time t = T-1 .. 0), with Y holding Vbar_t and Ap the previous Yb:
+//   Yb = Vbar - eta Vbar Gm;  t >= 1: Vbar = ((1 + mom[t-1]) Yb - mom[t] Yb_prev) * 1[A_t > 0]
+//   t == 0: cbar = Yb - mom[0] Yb_prev (-> Aout);  A0 = Vbar_{T-1};  C unused.
+//   Ysave receives Vbar_t in slot t, Vsum = sum_t Vbar_t (fp32, [G][B][n]).  With these the
+//   dictionary gradient needs no residual slabs: Dbar = eta (Vsum^T X - (M + M^T) D) - A_T^T Rbar,
+//   M = sum_t Vbar_t^T Y_t (one K = T B GEMM over the two Y slabs, ops/fista.py).
+template <int NW, int RT, int HALVES, int PF, int MODE = 0>
 __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restrict__ C, const uint16_t* __restrict__ Gm,
                                                         const float* __restrict__ A0, const float* __restrict__ eta_,
                                                         const float* __restrict__ lam_, const float* __restrict__ mom,
-                                                        float* __restrict__ Aout, int B, int T) {
+                                                        float* __restrict__ Aout, int B, int T,
+                                                        uint16_t* __restrict__ Ysave, uint16_t* __restrict__ Asave,
+                                                        float* __restrict__ Vsum) {
   constexpr int n = NW * 128;  // 8 waves x NW 16-column tiles
   constexpr int nrb = n * 2;
   constexpr int R = FR * RT;   // rows per workgroup
@@ -272,11 +284,14 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int g = bid / rb, r0 = (bid % rb) * R;
   const uint16_t* Gg = Gm + (long)g * n * n;
-  const float eta = eta_[g], thr = eta_[g] * lam_[g];
+  const float eta = eta_[g], thr = MODE == 2 ? 0.f : eta_[g] * lam_[g];
   const int row = lane & 15, q = lane >> 4;
   const int nbase = w * NW * 16;
   const float* Cg = C + ((long)g * B + r0) * n;
+  // slot s of a slab for this workgroup's rows (wave-uniform base; lanes add a 32-bit offset)
+  auto slab = [&](uint16_t* base, int s) { return base + (((long)g * T + s) * B + r0) * n; };
   f32x4_t Y[RT][NW], Ap[RT][NW];
+  f32x4_t Vs[MODE == 2 ? RT : 1][MODE == 2 ? NW : 1];
 #pragma unroll
   for (int u = 0; u < RT; ++u)
 #pragma unroll
@@ -285,8 +300,12 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
       f32x4_t v = f32x4_t{0.f, 0.f, 0.f, 0.f};
       if (A0) v = *reinterpret_cast<const f32x4_t*>(A0 + ((long)g * B + r0 + u * FR + row) * n + col);
       Y[u][t] = v;
-      Ap[u][t] = v;
+      Ap[u][t] = MODE == 2 ? f32x4_t{0.f, 0.f, 0.f, 0.f} : v;
+      if constexpr (MODE == 2) Vs[u][t] = v;
       lds_put4(Ybuf, u * FR + row, col, nrb, v[0], v[1], v[2], v[3]);
+      if constexpr (MODE != 0)  // Y_0 (forward) / Vbar_{T-1} (adjoint)
+        *reinterpret_cast<ushort4*>(slab(Ysave, MODE == 2 ? T - 1 : 0) + (u * FR + row) * n + col) =
+            make_ushort4(f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3]));
     }
   __syncthreads();
   // Gm fragment stream: PF k-steps in flight per wave, one ring running continuously across
@@ -306,17 +325,30 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
   for (int it = 0; it < T; ++it) {
     const char* Ycur = Ybuf + (it & 1) * (R * nrb);
     char* Ynxt = Ybuf + ((it + 1) & 1) * (R * nrb);
-    const float mo = mom[it];
+    const int ts = MODE == 2 ? T - 1 - it : it;  // the adjoint runs backwards in time
+    const float mo = mom[ts];
+    const float m1 = MODE == 2 && ts >= 1 ? 1.f + mom[ts - 1] : 0.f;
     const bool final_iter = it + 1 == T;
+    const uint16_t* a_in = MODE == 2 && !final_iter ? slab(Asave, ts - 1) : nullptr;  // support of A_ts
+    uint16_t* y_out = MODE == 2 ? (final_iter ? nullptr : slab(Ysave, ts - 1))
+                                : MODE == 1 && !final_iter ? slab(Ysave, ts + 1) : nullptr;
+    uint16_t* a_out = MODE == 1 ? slab(Asave, ts) : nullptr;
 #pragma unroll
     for (int h = 0; h < HALVES; ++h) {
-      // C for this half's update, issued ahead of the half's GEMM
-      f32x4_t cv[RT][NH];
+      // C (forward) / the support of A_ts (adjoint) for this half's update, issued ahead of the GEMM
+      f32x4_t cv[MODE == 2 ? 1 : RT][MODE == 2 ? 1 : NH];
+      ushort4 mk[MODE == 2 ? RT : 1][MODE == 2 ? NH : 1];  // raw bf16 A_ts (half the registers)
 #pragma unroll
       for (int u = 0; u < RT; ++u)
 #pragma unroll
-        for (int t = 0; t < NH; ++t)
-          cv[u][t] = *reinterpret_cast<const f32x4_t*>(Cg + (long)(u * FR + row) * n + nbase + (h * NH + t) * 16 + 4 * q);
+        for (int t = 0; t < NH; ++t) {
+          const int col = nbase + (h * NH + t) * 16 + 4 * q;
+          if constexpr (MODE == 2) {
+            if (!final_iter) mk[u][t] = *reinterpret_cast<const ushort4*>(a_in + (u * FR + row) * n + col);
+          } else {
+            cv[u][t] = *reinterpret_cast<const f32x4_t*>(Cg + (long)(u * FR + row) * n + col);
+          }
+        }
       // Z[R, this half of n_w] = Ycur[R, n] x Gm[n, half]
       f32x4_t Z[RT][NH];
 #pragma unroll
@@ -351,14 +383,43 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
           const int tt = h * NH + t;
           const int col = nbase + tt * 16 + 4 * q;
           f32x4_t an;
+          if constexpr (MODE == 2) {
+            // Yb = Vbar - eta Vbar Gm; the next Vbar (or, at t = 0, cbar) from Yb and the previous Yb
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float y = Y[u][tt][r] + eta * (cv[u][t][r] - Z[u][t][r]);
-            an[r] = fmaxf(y - thr, 0.f);
-            Y[u][tt][r] = an[r] + (an[r] - Ap[u][tt][r]) * mo;
+            for (int r = 0; r < 4; ++r) {
+              const float yb = Y[u][tt][r] - eta * Z[u][t][r];
+              const uint16_t av = r == 0 ? mk[u][t].x : r == 1 ? mk[u][t].y : r == 2 ? mk[u][t].z : mk[u][t].w;
+              // A >= 0, so its support is "bf16 bits nonzero" (the slab stores relu outputs)
+              an[r] = final_iter ? yb - mo * Ap[u][tt][r] : ((av & 0x7fff) ? m1 * yb - mo * Ap[u][tt][r] : 0.f);
+              Ap[u][tt][r] = yb;
+            }
+            if (final_iter) {
+              Y[u][tt] = an;  // cbar
+            } else {
+              Y[u][tt] = an;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) Vs[u][tt][r] += an[r];
+              lds_put4(Ynxt, u * FR + row, col, nrb, an[0], an[1], an[2], an[3]);
+              *reinterpret_cast<ushort4*>(y_out + (u * FR + row) * n + col) =
+                  make_ushort4(f2bf(an[0]), f2bf(an[1]), f2bf(an[2]), f2bf(an[3]));
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float y = Y[u][tt][r] + eta * (cv[u][t][r] - Z[u][t][r]);
+              an[r] = fmaxf(y - thr, 0.f);
+              Y[u][tt][r] = an[r] + (an[r] - Ap[u][tt][r]) * mo;
+            }
+            Ap[u][tt] = an;
+            if (!final_iter) lds_put4(Ynxt, u * FR + row, col, nrb, Y[u][tt][0], Y[u][tt][1], Y[u][tt][2], Y[u][tt][3]);
+            if constexpr (MODE == 1) {
+              *reinterpret_cast<ushort4*>(a_out + (u * FR + row) * n + col) =
+                  make_ushort4(f2bf(an[0]), f2bf(an[1]), f2bf(an[2]), f2bf(an[3]));
+              if (!final_iter)
+                *reinterpret_cast<ushort4*>(y_out + (u * FR + row) * n + col) =
+                    make_ushort4(f2bf(Y[u][tt][0]), f2bf(Y[u][tt][1]), f2bf(Y[u][tt][2]), f2bf(Y[u][tt][3]));
+            }
           }
-          Ap[u][tt] = an;
-          if (!final_iter) lds_put4(Ynxt, u * FR + row, col, nrb, Y[u][tt][0], Y[u][tt][1], Y[u][tt][2], Y[u][tt][3]);
         }
     }
     // the next iterate is complete in Ynxt; nobody reads Ycur any more.  LDS-only barrier: the
@@ -370,7 +431,9 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
 #pragma unroll
     for (int t = 0; t < NW; ++t) {
       const int col = nbase + t * 16 + 4 * q;
-      *reinterpret_cast<f32x4_t*>(Aout + ((long)g * B + r0 + u * FR + row) * n + col) = Ap[u][t];
+      const long o = ((long)g * B + r0 + u * FR + row) * n + col;
+      *reinterpret_cast<f32x4_t*>(Aout + o) = MODE == 2 ? Y[u][t] : Ap[u][t];
+      if constexpr (MODE == 2) *reinterpret_cast<f32x4_t*>(Vsum + o) = Vs[u][t];
     }
 }
 
@@ -451,25 +514,50 @@ static int launch_direct(const FistaArgs& a, int G, hipStream_t stream, int rows
 
 // Gram-form solver: C = X D^T [G][B][n] fp32, Gm = D D^T bf16 in MFMA-fragment order
 // [G][n/16][n/32][64 lanes][8] (lane = 16 q + r holds Gm[16 tile + r][32 step + 8 q .. + 7]).
+// mode 0: solve; 1: solve saving the Y / A slabs (Ysave, Asave); 2: the adjoint sweep (A0 =
+// Vbar_{T-1}, A = cbar out, Ysave = Vbar slab out, Asave = the forward's A slab in, Vsum out).
 int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* eta, const float* lam,
-                  const float* mom, float* A, int G, int B, int n, int T, hipStream_t stream, int rows) {
-  if (B % FR || n % 128 || T < 0) return 1;
+                  const float* mom, float* A, int G, int B, int n, int T, hipStream_t stream, int rows, int mode,
+                  void* Ysave, void* Asave, float* Vsum) {
+  if (B % FR || n % 128 || T < 0 || mode < 0 || mode > 2) return 1;
+  if (mode && (!Ysave || !Asave || T < 1 || (mode == 2 && (!Vsum || !A0)))) return 1;
   const uint16_t* gm = reinterpret_cast<const uint16_t*>(Gm);
+  uint16_t* ys = reinterpret_cast<uint16_t*>(Ysave);
+  uint16_t* as = reinterpret_cast<uint16_t*>(Asave);
   // 32-row workgroups when they still give >= 2 per CU (256 CUs); else 16 rows (rows = 16 forces it)
   const bool two = (B % (2 * FR) == 0) && (long)G * (B / (2 * FR)) >= 512 && rows != 16;
   const dim3 g2(G * (B / (2 * FR))), g1(G * (B / FR));
   // (NW, halves, ring depth) for 32-row, then 16-row workgroups: past n = 512 the fp32 iterates
   // need the column passes split, and the Gm ring shrinks to stay spill-free in 256 VGPRs
-#define SC_G(NWV, H2, PF2, H1, PF1)                                                                                    \
-  if (n == NWV * 128) {                                                                                    \
-    if (two) hipLaunchKernelGGL((fista_gram_kernel<NWV, 2, H2, PF2>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
-    else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, T); \
+#define SC_GM(NWV, H2, PF2, H1, PF1, MV)                                                                   \
+  {                                                                                                        \
+    if (two) hipLaunchKernelGGL((fista_gram_kernel<NWV, 2, H2, PF2, MV>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, \
+                                mom, A, B, T, ys, as, Vsum);                                               \
+    else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1, MV>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, \
+                            mom, A, B, T, ys, as, Vsum);                                                   \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                        \
   }
-  // (eight column passes with a 4- / 8-deep Gm ring measured 14.2 / 15.3 ms vs 12.9 ms for
-  // n = 1024's four passes with ring 2 -- not instantiated)
-  SC_G(2, 1, 4, 1, 4) SC_G(4, 1, 4, 1, 8) SC_G(6, 2, 2, 2, 4) SC_G(8, 4, 2, 2, 4)
+  // (NW, halves, ring depth) of the 32-row and 16-row solve, then of the slab-saving solve and
+  // the adjoint (its Vbar sum needs registers: more halves, shallower rings; past n = 512 the
+  // adjoint's three fp32 row states only fit 16-row workgroups -- spill-free per
+  // -Rpass-analysis=kernel-resource-usage)
+#define SC_G(NWV, H2, PF2, H1, PF1, SAVE, ADJ)                                                             \
+  if (n == NWV * 128) {                                                                                    \
+    if (mode == 1) { SAVE }                                                                                \
+    if (mode == 2) { ADJ }                                                                                 \
+    SC_GM(NWV, H2, PF2, H1, PF1, 0)                                                                        \
+  }
+#define SC_G1(NWV, H1, PF1, MV)                                                                            \
+  hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1, MV>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, \
+                     T, ys, as, Vsum);                                                                     \
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+  SC_G(2, 1, 4, 1, 4, SC_GM(2, 1, 4, 1, 4, 1), SC_GM(2, 1, 4, 1, 4, 2))
+  SC_G(4, 1, 4, 1, 8, SC_GM(4, 1, 4, 1, 4, 1), SC_GM(4, 2, 2, 1, 2, 2))
+  SC_G(6, 2, 2, 2, 4, SC_GM(6, 2, 2, 2, 4, 1), SC_G1(6, 2, 2, 2))
+  SC_G(8, 4, 2, 2, 4, SC_G1(8, 2, 4, 1), SC_G1(8, 4, 2, 2))
 #undef SC_G
+#undef SC_G1
+#undef SC_GM
   return 2;
 }
 

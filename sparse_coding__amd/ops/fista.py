@@ -163,7 +163,8 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
         # so every wave fragment load is 1 KB contiguous (8 full lines instead of 16 half lines)
         Gm = Gm.view(G, n // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
         rc = _lib.lib().sc_fista_gram(_lib.ptr(C), _lib.ptr(Gm), _lib.ptr(a0), _lib.ptr(eta), _lib.ptr(lam),
-                                      _lib.ptr(mom), _lib.ptr(A), G, B, n, iters, _lib.stream_handle(), rows)
+                                      _lib.ptr(mom), _lib.ptr(A), G, B, n, iters, _lib.stream_handle(), rows, 0,
+                                      None, None, None)
     else:
         # both operands in MFMA-fragment order (see the Gram form): D [G][n/16][d/32][64][8] for the
         # (Res D^T) product, D^T [G][d/16][n/32][64][8] for the (Y D) product
@@ -338,6 +339,12 @@ class _UnrolledFista(torch.autograd.Function):
         ctx.iters, ctx.mom = iters, mom.tolist()
         ctx.x_shape = X.shape
         if _unrolled_hip_ok(X, D, A0, backend):
+            ctx.gram = _gram_unrolled_ok(D, A0) and iters >= 1
+            if ctx.gram:
+                R, st = unrolled_forward_gram(X.detach(), D.detach(), A0.detach(), lam, eta.detach(), iters, mom)
+                ctx.hip = True
+                ctx.save_for_backward(*st, eta.detach(), lam)
+                return R
             R, Db, Ys, Rs, As = unrolled_forward_hip(X, D.detach(), A0.detach(), lam, eta, iters, mom)
             ctx.hip = True
             ctx.save_for_backward(Db, Ys, Rs, As, eta.detach(), lam)
@@ -366,6 +373,11 @@ class _UnrolledFista(torch.autograd.Function):
     @staticmethod
     def backward(ctx, Rbar):
         want_eta = ctx.needs_input_grad[4]
+        if ctx.hip and ctx.gram:
+            *st, eta, lam = ctx.saved_tensors
+            Dbar, cbar, etabar = unrolled_backward_gram(Rbar, tuple(st), eta, ctx.mom, ctx.iters,
+                                                        lam=lam if want_eta else None)
+            return None, Dbar, cbar, None, etabar, None, None
         if ctx.hip:
             Db, Ys, Rs, As, eta, lam = ctx.saved_tensors
             Dbar, cbar, etabar = unrolled_backward_hip(Rbar, Db, Ys, Rs, As, eta, ctx.mom, ctx.iters,
@@ -439,6 +451,116 @@ def unrolled_forward_hip(X, D, A0, lam, eta, iters, mom=None):
                              _lib.ptr(Ys), _lib.ptr(Rs), _lib.ptr(As), _lib.stream_handle(), 0)
     _lib.check(rc, "sc_fista (saving iterates)")
     return R, Db, Ys, Rs, As
+
+
+def _gram_operands(Xb, Db):
+    """C = X D^T (fp32 [G, B, n]) and Gm = D D^T (bf16 [G, n, n], plus its MFMA-fragment-order
+    copy the Gram kernel streams)."""
+    from . import gemm
+
+    G, n, d = Db.shape
+    B = Xb.shape[-2]
+    C = torch.empty(G, B, n, device=Db.device)
+    gemm.matmul_nt(Xb, Db, C)
+    Gm = torch.empty(G, n, n, device=Db.device, dtype=torch.bfloat16)
+    gemm.matmul_nt(Db, Db, Gm)
+    Gmf = Gm.view(G, n // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
+    return C, Gm, Gmf
+
+
+def unrolled_forward_gram(X, D, A0, lam, eta, iters, mom=None):
+    """Gram-form HIP solve of ``iters`` iterations (Y += eta (C - Y Gm), one [B, n] x [n, n]
+    product per iteration) saving the bf16 Y / A slabs for ``unrolled_backward_gram``.
+    Returns (R = X - A_T D fp32 [G, B, d], state for the backward)."""
+    from . import gemm
+
+    G, n, d = D.shape
+    B = A0.shape[-2]
+    dev = D.device
+    mom = momentum_schedule(max(iters, 1)) if mom is None else mom
+    Xb = X.to(torch.bfloat16).contiguous()
+    Db = D.to(torch.bfloat16).contiguous()
+    C, Gm, Gmf = _gram_operands(Xb, Db)
+    T = int(iters)
+    Ys = torch.empty(G, T, B, n, device=dev, dtype=torch.bfloat16)
+    As = torch.empty(G, T, B, n, device=dev, dtype=torch.bfloat16)
+    A = torch.empty(G, B, n, device=dev)
+    a0 = A0.float().contiguous()
+    if tuple(a0.shape) != (G, B, n):
+        raise ValueError(f"A0 shape {tuple(A0.shape)} != {(G, B, n)}")
+    rc = _lib.lib().sc_fista_gram(_lib.ptr(C), _lib.ptr(Gmf), _lib.ptr(a0), _lib.ptr(eta), _lib.ptr(lam),
+                                  _lib.ptr(mom.to(dev)), _lib.ptr(A), G, B, n, T, _lib.stream_handle(), 0, 1,
+                                  _lib.ptr(Ys), _lib.ptr(As), None)
+    _lib.check(rc, "sc_fista_gram (saving iterates)")
+    # R = X - A_T D from the bf16 A_T in the last A slot (the direct form also multiplies bf16 A)
+    AD = torch.empty(G, B, d, device=dev)
+    _strided_mm(gemm.EPI_F32, 1, B, d, n, As[:, T - 1], n, T * B * n, Db, d, n * d, AD, d, B * d, 1.0)
+    R = (X.float() if X.dim() == 3 else X.float().expand(G, B, d)) - AD
+    return R, (Xb, Db, Gm, Gmf, Ys, As)
+
+
+def unrolled_backward_gram(Rbar, state, eta, mom, T, lam=None):
+    """Adjoint of ``unrolled_forward_gram``: the reverse sweep runs in the Gram kernel (mode 2:
+    Vbar_t in registers, Yb = Vbar - eta Vbar Gm, the support of A_t from the slab), writing the
+    Vbar slab and sum_t Vbar_t.  The dictionary gradient then needs no residual slabs:
+        Dbar = eta (Vsum^T X - (M + M^T) D) - A_T^T Rbar,   M = sum_t Vbar_t^T Y_t
+    (one K = T B GEMM, [n, n] out), and etabar = <Vsum^T X, D> - <M, Gm> - lam sum Vsum.
+    Returns (Dbar fp32 [G, n, d], cbar fp32 [G, B, n], etabar [G] or None)."""
+    from . import gemm
+
+    Xb, Db, Gm, Gmf, Ys, As = state
+    G, n, d = Db.shape
+    B = Ys.shape[2]
+    dev = Db.device
+    Rb = Rbar.to(torch.bfloat16)
+    Rb = (Rb if Rb.dim() == 3 else Rb.expand(G, B, d)).contiguous()
+    T2 = torch.empty(G, B, n, device=dev)
+    gemm.matmul_nt(Rb, Db, T2)                                     # Rbar D^T
+    Vs = torch.empty(G, T, B, n, device=dev, dtype=torch.bfloat16)
+    V0 = torch.empty(G, B, n, device=dev)
+    stream = _lib.stream_handle()
+    _lib.check(_lib.lib().sc_fista_adjoint_init(_lib.ptr(T2), _lib.ptr(V0), _lib.ptr(As), _lib.ptr(Vs), G, B, n, T,
+                                                stream), "sc_fista_adjoint_init")
+    cbar = torch.empty(G, B, n, device=dev)
+    Vsum = torch.empty(G, B, n, device=dev)
+    lam_t = lam if lam is not None else torch.zeros(G, device=dev)
+    rc = _lib.lib().sc_fista_gram(None, _lib.ptr(Gmf), _lib.ptr(V0), _lib.ptr(eta), _lib.ptr(lam_t),
+                                  _lib.ptr(torch.as_tensor(mom, dtype=torch.float32).to(dev)), _lib.ptr(cbar), G, B, n,
+                                  T, stream, 0, 2, _lib.ptr(Vs), _lib.ptr(As), _lib.ptr(Vsum))
+    _lib.check(rc, "sc_fista_gram (adjoint)")
+    # M = sum_t Vbar_t^T Y_t: G (n/256)^2 output tiles over K = T B -> split K to fill the chip
+    tiles = G * ((n + 255) // 256) ** 2
+    ks = 1
+    while ks < 16 and tiles * ks * 2 <= 512 and (T * B) % (64 * ks * 2) == 0:
+        ks *= 2
+    segs = [[(Vs.view(G, T * B, n), Ys.view(G, T * B, n))]]
+    if ks > 1:
+        slabs = torch.empty(ks, G, n, n, device=dev)
+        gemm.weight_grads(segs, [slabs], 1.0, ksplit=ks)
+        M = slabs.sum(dim=0)
+    else:
+        M = torch.empty(G, n, n, device=dev)
+        gemm.weight_grads(segs, [M], 1.0)
+    VX = torch.empty(G, n, d, device=dev)
+    gemm.weight_grads([[(Vsum.to(torch.bfloat16), Xb)]], [VX], 1.0)
+    AR = torch.empty(G, n, d, device=dev)
+    gemm.weight_grads([[(As[:, T - 1].contiguous(), Rb)]], [AR], 1.0)
+    Q = torch.empty(G, n, d, device=dev)
+    gemm.matmul_nn((M + M.transpose(1, 2)).to(torch.bfloat16), Db, Q)
+    e = eta[:, None, None]
+    Dbar = (VX - Q) * e - AR
+    etabar = None
+    if lam is not None:
+        etabar = ((VX * Db.float()).sum((1, 2)) - (M * Gm.float()).sum((1, 2)) - lam * Vsum.sum((1, 2)))
+    return Dbar, cbar, etabar
+
+
+def _gram_unrolled_ok(D, A0) -> bool:
+    """The Gram form pays for n <= d (2 B n^2 per iteration and a T B n^2 dictionary-gradient
+    GEMM against 4 B n d and 2 T B n d for the direct form)."""
+    G, n, d = D.shape
+    B = A0.shape[-2]
+    return n in GRAM_N and n <= d and B % 128 == 0 and d % 256 == 0
 
 
 def _strided_mm(epi, layout, M, N, K, a, lda, sa, b, ldb, sb, out, ldc, sc, alpha):

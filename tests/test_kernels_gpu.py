@@ -302,8 +302,8 @@ def test_graph_replay_matches_eager():
     torch.testing.assert_close(graph.out, eager.out, rtol=0, atol=0)
 
 
-# block-per-row, wave-per-row, block (PL=48), block-radix (n % 4 != 0), block-radix (n > 256 * 64)
-@pytest.mark.parametrize("n", [6144, 1000, 12288, 1002, 20000])
+# block-per-row, wave-per-row, block (PL=48), block-radix (n % 4 != 0), block (PL=64)
+@pytest.mark.parametrize("n", [6144, 1000, 12288, 1002, 16000])
 def test_topk_select_exact(n):
     from sparse_coding__amd.ops import topk as T
 
@@ -829,6 +829,43 @@ def test_unrolled_fista_hip_adjoint_matches_fp32():
     torch.testing.assert_close(D1.grad, Dh, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("G,B,n,d", [(2, 256, 512, 512), (4, 4096, 512, 512), (2, 256, 256, 512)])
+def test_unrolled_fista_gram_adjoint_matches_fp32(G, B, n, d):
+    """Gram-form FISTA in the loss: the slab-saving solve and the reverse sweep in the Gram
+    kernel (16- and 32-row workgroups) with the dictionary gradient from M = sum_t Vbar_t^T Y_t
+    (no residual slabs) against the fp32 adjoint over the same Y / A slabs (residual slabs
+    recomputed in fp32), including d loss / d eta."""
+    from sparse_coding__amd.ops import fista as F
+
+    torch.manual_seed(21)
+    T = 20
+    D = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1)
+    X = torch.randn(B, d, device=DEV)
+    c = torch.relu(torch.randn(G, B, n, device=DEV)) * 0.05
+    lam = torch.linspace(1e-3, 2e-2, G, device=DEV)
+    eta = F.step_size(D)
+    W = torch.randn(G, B, d, device=DEV)
+    mom = F.momentum_schedule(T)
+    R_ref = F.unrolled_fista_residual(X, D, lam, c, T, eta, backend="torch")
+    R, st = F.unrolled_forward_gram(X, D, c, lam, eta, T, mom)
+    Xb, Db, Gm, Gmf, Ys, As = st
+    Dg, cg, eg = F.unrolled_backward_gram(W, st, eta, mom.tolist(), T, lam=lam)
+    Df = Db.float()
+    Rs = (Xb.float() - Ys.float() @ Df.unsqueeze(1)).to(torch.bfloat16)  # Res_t = X - Y_t D per slot
+    Dr, cr, er = F.unrolled_backward_torch(W, Df, Ys, Rs, As, eta, mom.tolist(), T, lam=lam)
+    torch.cuda.synchronize()
+    for g in range(G):
+        rel = lambda a, b: ((a[g] - b[g]).norm() / b[g].norm()).item()  # noqa: E731
+        assert rel(R, R_ref) < 3e-2, rel(R, R_ref)
+        assert rel(Dg, Dr) < 1e-2, rel(Dg, Dr)
+        assert rel(cg, cr) < 1e-2, rel(cg, cr)
+    torch.testing.assert_close(eg, er, rtol=2e-2, atol=1e-2 * er.abs().max().item())
+    # the autograd Function routes to the Gram path for n <= d
+    D1, c1 = D.clone().requires_grad_(), c.clone().requires_grad_()
+    (F.unrolled_fista_residual(X, D1, lam, c1, T, eta, backend="hip") * W).sum().backward()
+    torch.testing.assert_close(D1.grad, Dg, rtol=1e-3, atol=1e-3)
+
+
 def test_fista_loss_ensemble_trains_on_gpu():
     from sparse_coding__amd.engine.fista_loss import FistaLossEnsemble
     from sparse_coding__amd.models.fista import FunctionalFista
@@ -841,6 +878,46 @@ def test_fista_loss_ensemble_trains_on_gpu():
     first = eng.step_batch(x)
     for _ in range(20):
         last = eng.step_batch(x)
+    torch.cuda.synchronize()
+    assert torch.isfinite(last).all() and (last < first).all(), (first, last)
+
+
+@pytest.mark.parametrize("T", [1, 5])
+def test_fused_fista_loss_gradients_match_autograd(T):
+    """FISTA in the loss on the fused engine (tied SAE kernels + Gram solve / adjoint + eta
+    term + warm-start gradient through the ReLU) against fp32 autograd of the reference's
+    loss2 (FistaLossEnsemble, torch backend) on the same bf16-rounded batch: the raw encoder
+    gradient (norm Jacobian applied to the engine's normalised-row gradient), the bias
+    gradient and the loss terms."""
+    from sparse_coding__amd.engine.fista_loss import FistaLossEnsemble, FusedFistaLossEnsemble
+    from sparse_coding__amd.models.fista import FunctionalFista
+
+    torch.manual_seed(22)
+    G, d, n, B = 2, 512, 512, 256
+    models = [FunctionalFista.init(d, n, l1, device=DEV) for l1 in (1e-3, 1e-2)]
+    feats = torch.nn.functional.normalize(torch.randn(1024, d, device=DEV), dim=-1)
+    x = ((torch.relu(torch.randn(B, 1024, device=DEV) - 1.0) * 2.0) @ feats).to(torch.bfloat16)
+    fused = FusedFistaLossEnsemble(models, lr=1e-3, batch_size=B, device=DEV, num_iter=T)
+    ref = FistaLossEnsemble(models, lr=1e-3, batch_size=B, device=DEV, num_iter=T, backend="torch")
+    total, parts = ref.losses(x.float())
+    total.sum().backward()
+    fused.compute_grads(x)
+    torch.cuda.synchronize()
+    e = fused.engine
+    w_hat = e.params["encoder"] / e.norms.unsqueeze(-1)
+    gw = e.g_dec
+    g_raw = (gw - (gw * w_hat).sum(-1, keepdim=True) * w_hat) / e.norms.unsqueeze(-1)
+    g_ref = ref.params["encoder"].grad
+    gb, gb_ref = e.g_bias.view(G, n), ref.params["encoder_bias"].grad
+    for g in range(G):
+        rel_w = ((g_raw[g] - g_ref[g]).norm() / g_ref[g].norm()).item()
+        rel_b = ((gb[g] - gb_ref[g]).norm() / gb_ref[g].norm()).item()
+        assert rel_w < 3e-2 and rel_b < 3e-2, (g, rel_w, rel_b)
+    torch.testing.assert_close(fused.l_fista, parts["l_fista"].detach(), rtol=2e-2, atol=1e-5)
+    # a few steps train
+    first = fused.step_batch(x).clone()
+    for _ in range(10):
+        last = fused.step_batch(x)
     torch.cuda.synchronize()
     assert torch.isfinite(last).all() and (last < first).all(), (first, last)
 
