@@ -208,9 +208,13 @@ def cfg_masked(a):
     out = {"config": f"masked: {len(sizes)} tied SAEs of sizes {sizes} stacked to {stack}, d={d}, batch {B}",
            "unit": "activations/s", "dtype": "bf16", "data": "synthetic",
            "live_fraction": round(sum(sizes) / (stack * len(sizes)), 4)}
-    for name, sig, models in (
-            ("masked", FunctionalMaskedTiedSAE, [FunctionalMaskedTiedSAE.init(d, s, stack, 1e-3, device=dev) for s in sizes]),
-            ("unmasked", FunctionalTiedSAE, [FunctionalTiedSAE.init(d, stack, 1e-3, device=dev) for _ in sizes])):
+    variants = (("masked", FunctionalMaskedTiedSAE, lambda: [FunctionalMaskedTiedSAE.init(d, s, stack, 1e-3, device=dev)
+                                                            for s in sizes]),
+                ("unmasked", FunctionalTiedSAE, lambda: [FunctionalTiedSAE.init(d, stack, 1e-3, device=dev) for _ in sizes]))
+    for name, sig, make in variants:
+        if a.variant not in ("both", name):
+            continue
+        models = make()
         eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=dev)
         eng.enable_graph()
         el = _timed(lambda: (ring.sample(B, out=eng.x_static), eng.step_static()), a.steps, a.warmup,
@@ -218,8 +222,9 @@ def cfg_masked(a):
         out[f"{name}_ms_per_step"] = round(1e3 * el / a.steps, 4)
         del eng
         torch.cuda.empty_cache()
-    out["time_ratio"] = round(out["masked_ms_per_step"] / out["unmasked_ms_per_step"], 4)
-    out["value"] = round(B / out["masked_ms_per_step"] * 1e3, 1)
+    if a.variant == "both":
+        out["time_ratio"] = round(out["masked_ms_per_step"] / out["unmasked_ms_per_step"], 4)
+    out["value"] = round(B / out[f"{'unmasked' if a.variant == 'unmasked' else 'masked'}_ms_per_step"] * 1e3, 1)
     return out
 
 
@@ -320,6 +325,7 @@ def main():
     ap.add_argument("--ratio", type=float, default=1.0)
     ap.add_argument("--sparse-k", default="auto", help="topk: models with k <= this take the slot-list wgrad")
     ap.add_argument("--eager", action="store_true", help="topk: no HIP graph")
+    ap.add_argument("--variant", default="both", choices=["both", "masked", "unmasked"], help="masked: which run")
     ap.add_argument("--ring-gb", type=float, default=0.0, help="fista: ring size in GB of HBM (0: 512k rows)")
     a = ap.parse_args()
     rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "fistaloss": cfg_fistaloss, "mlp": cfg_mlp, "mlpout": cfg_mlpout, "masked": cfg_masked,

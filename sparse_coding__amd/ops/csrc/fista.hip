@@ -263,7 +263,10 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
 // MODE 2 (its adjoint, reverse time t = T-1 .. 0), with Y holding Vbar_t and Ap the previous Yb:
 //   Yb = Vbar - eta Vbar Gm;  t >= 1: Vbar = ((1 + mom[t-1]) Yb - mom[t] Yb_prev) * 1[A_t > 0]
 //   t == 0: cbar = Yb - mom[0] Yb_prev (-> Aout);  A0 = Vbar_{T-1};  C unused.
-//   Ysave receives Vbar_t in slot t, Vsum = sum_t Vbar_t (fp32, [G][B][n]).  With these the
+//   Ysave receives Vbar_t in slot t, Vsum = sum_t Vbar_t (fp32, [G][B][n]), and epart [G][B / 16]
+//   the workgroups' sums of <Z_t, Y_t> (Z_t = Vbar_t Gm, Y_t from the forward's slab Yfwd): the
+//   eta gradient is <Vsum, C> - sum epart - lam sum Vsum, taken from fp32 data -- its terms cancel
+//   to ~1/10 of their size, so the bf16 GEMM form (<Vsum^T X, D> - <M, Gm>) is too coarse.  With these the
 //   dictionary gradient needs no residual slabs: Dbar = eta (Vsum^T X - (M + M^T) D) - A_T^T Rbar,
 //   M = sum_t Vbar_t^T Y_t (one K = T B GEMM over the two Y slabs, ops/fista.py).
 template <int NW, int RT, int HALVES, int PF, int MODE = 0>
@@ -272,7 +275,8 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
                                                         const float* __restrict__ lam_, const float* __restrict__ mom,
                                                         float* __restrict__ Aout, int B, int T,
                                                         uint16_t* __restrict__ Ysave, uint16_t* __restrict__ Asave,
-                                                        float* __restrict__ Vsum) {
+                                                        float* __restrict__ Vsum, const uint16_t* __restrict__ Yfwd,
+                                                        float* __restrict__ epart) {
   constexpr int n = NW * 128;  // 8 waves x NW 16-column tiles
   constexpr int nrb = n * 2;
   constexpr int R = FR * RT;   // rows per workgroup
@@ -289,7 +293,8 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
   const int nbase = w * NW * 16;
   const float* Cg = C + ((long)g * B + r0) * n;
   // slot s of a slab for this workgroup's rows (wave-uniform base; lanes add a 32-bit offset)
-  auto slab = [&](uint16_t* base, int s) { return base + (((long)g * T + s) * B + r0) * n; };
+  auto slab = [&](auto* base, int s) { return base + (((long)g * T + s) * B + r0) * n; };
+  float edot = 0.f;  // adjoint: this lane's share of sum_t <Z_t, Y_t>
   f32x4_t Y[RT][NW], Ap[RT][NW];
   f32x4_t Vs[MODE == 2 ? RT : 1][MODE == 2 ? NW : 1];
 #pragma unroll
@@ -330,6 +335,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
     const float m1 = MODE == 2 && ts >= 1 ? 1.f + mom[ts - 1] : 0.f;
     const bool final_iter = it + 1 == T;
     const uint16_t* a_in = MODE == 2 && !final_iter ? slab(Asave, ts - 1) : nullptr;  // support of A_ts
+    const uint16_t* y_in = MODE == 2 ? slab(Yfwd, ts) : nullptr;                     // Y_ts
     uint16_t* y_out = MODE == 2 ? (final_iter ? nullptr : slab(Ysave, ts - 1))
                                 : MODE == 1 && !final_iter ? slab(Ysave, ts + 1) : nullptr;
     uint16_t* a_out = MODE == 1 ? slab(Asave, ts) : nullptr;
@@ -338,6 +344,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
       // C (forward) / the support of A_ts (adjoint) for this half's update, issued ahead of the GEMM
       f32x4_t cv[MODE == 2 ? 1 : RT][MODE == 2 ? 1 : NH];
       ushort4 mk[MODE == 2 ? RT : 1][MODE == 2 ? NH : 1];  // raw bf16 A_ts (half the registers)
+      ushort4 yv[MODE == 2 ? RT : 1][MODE == 2 ? NH : 1];  // bf16 Y_ts
 #pragma unroll
       for (int u = 0; u < RT; ++u)
 #pragma unroll
@@ -345,6 +352,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
           const int col = nbase + (h * NH + t) * 16 + 4 * q;
           if constexpr (MODE == 2) {
             if (!final_iter) mk[u][t] = *reinterpret_cast<const ushort4*>(a_in + (u * FR + row) * n + col);
+            yv[u][t] = *reinterpret_cast<const ushort4*>(y_in + (u * FR + row) * n + col);
           } else {
             cv[u][t] = *reinterpret_cast<const f32x4_t*>(Cg + (long)(u * FR + row) * n + col);
           }
@@ -385,6 +393,8 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
           f32x4_t an;
           if constexpr (MODE == 2) {
             // Yb = Vbar - eta Vbar Gm; the next Vbar (or, at t = 0, cbar) from Yb and the previous Yb
+            edot += Z[u][t][0] * bf2f(yv[u][t].x) + Z[u][t][1] * bf2f(yv[u][t].y) + Z[u][t][2] * bf2f(yv[u][t].z) +
+                    Z[u][t][3] * bf2f(yv[u][t].w);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float yb = Y[u][tt][r] - eta * Z[u][t][r];
@@ -435,6 +445,11 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
       *reinterpret_cast<f32x4_t*>(Aout + o) = MODE == 2 ? Y[u][t] : Ap[u][t];
       if constexpr (MODE == 2) *reinterpret_cast<f32x4_t*>(Vsum + o) = Vs[u][t];
     }
+  if constexpr (MODE == 2) {
+    __shared__ float ered[FNT / 64];
+    const float tot = block_sum<FNT / 64>(edot, ered);
+    if (tid == 0) epart[(long)g * (B / FR) + bid % rb] = tot;  // [G][B / 16] slots, first B / R used
+  }
 }
 
 }  // namespace scamd
@@ -515,12 +530,14 @@ static int launch_direct(const FistaArgs& a, int G, hipStream_t stream, int rows
 // Gram-form solver: C = X D^T [G][B][n] fp32, Gm = D D^T bf16 in MFMA-fragment order
 // [G][n/16][n/32][64 lanes][8] (lane = 16 q + r holds Gm[16 tile + r][32 step + 8 q .. + 7]).
 // mode 0: solve; 1: solve saving the Y / A slabs (Ysave, Asave); 2: the adjoint sweep (A0 =
-// Vbar_{T-1}, A = cbar out, Ysave = Vbar slab out, Asave = the forward's A slab in, Vsum out).
+// Vbar_{T-1}, A = cbar out, Ysave = Vbar slab out, Asave / Yfwd = the forward's A / Y slabs in,
+// Vsum out, epart [G][B / 16] out: workgroup partials, zero-initialised by the caller).
 int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* eta, const float* lam,
                   const float* mom, float* A, int G, int B, int n, int T, hipStream_t stream, int rows, int mode,
-                  void* Ysave, void* Asave, float* Vsum) {
+                  void* Ysave, void* Asave, float* Vsum, const void* Yfwd, float* epart) {
   if (B % FR || n % 128 || T < 0 || mode < 0 || mode > 2) return 1;
-  if (mode && (!Ysave || !Asave || T < 1 || (mode == 2 && (!Vsum || !A0)))) return 1;
+  if (mode && (!Ysave || !Asave || T < 1 || (mode == 2 && (!Vsum || !A0 || !Yfwd || !epart)))) return 1;
+  const uint16_t* yf = reinterpret_cast<const uint16_t*>(Yfwd);
   const uint16_t* gm = reinterpret_cast<const uint16_t*>(Gm);
   uint16_t* ys = reinterpret_cast<uint16_t*>(Ysave);
   uint16_t* as = reinterpret_cast<uint16_t*>(Asave);
@@ -532,9 +549,9 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
 #define SC_GM(NWV, H2, PF2, H1, PF1, MV)                                                                   \
   {                                                                                                        \
     if (two) hipLaunchKernelGGL((fista_gram_kernel<NWV, 2, H2, PF2, MV>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, \
-                                mom, A, B, T, ys, as, Vsum);                                               \
+                                mom, A, B, T, ys, as, Vsum, yf, epart);                                               \
     else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1, MV>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, \
-                            mom, A, B, T, ys, as, Vsum);                                                   \
+                            mom, A, B, T, ys, as, Vsum, yf, epart);                                                   \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                        \
   }
   // (NW, halves, ring depth) of the 32-row and 16-row solve, then of the slab-saving solve and
@@ -549,12 +566,12 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
   }
 #define SC_G1(NWV, H1, PF1, MV)                                                                            \
   hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1, MV>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, \
-                     T, ys, as, Vsum);                                                                     \
+                     T, ys, as, Vsum, yf, epart);                                                                     \
   return hipGetLastError() == hipSuccess ? 0 : 3;
   SC_G(2, 1, 4, 1, 4, SC_GM(2, 1, 4, 1, 4, 1), SC_GM(2, 1, 4, 1, 4, 2))
-  SC_G(4, 1, 4, 1, 8, SC_GM(4, 1, 4, 1, 4, 1), SC_GM(4, 2, 2, 1, 2, 2))
+  SC_G(4, 1, 4, 1, 8, SC_GM(4, 1, 4, 1, 4, 1), SC_GM(4, 4, 1, 1, 2, 2))
   SC_G(6, 2, 2, 2, 4, SC_GM(6, 2, 2, 2, 4, 1), SC_G1(6, 2, 2, 2))
-  SC_G(8, 4, 2, 2, 4, SC_G1(8, 2, 4, 1), SC_G1(8, 4, 2, 2))
+  SC_G(8, 4, 2, 2, 4, SC_G1(8, 2, 4, 1), SC_G1(8, 4, 1, 2))
 #undef SC_G
 #undef SC_G1
 #undef SC_GM

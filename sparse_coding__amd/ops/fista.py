@@ -496,19 +496,22 @@ def unrolled_forward_gram(X, D, A0, lam, eta, iters, mom=None):
     AD = torch.empty(G, B, d, device=dev)
     _strided_mm(gemm.EPI_F32, 1, B, d, n, As[:, T - 1], n, T * B * n, Db, d, n * d, AD, d, B * d, 1.0)
     R = (X.float() if X.dim() == 3 else X.float().expand(G, B, d)) - AD
-    return R, (Xb, Db, Gm, Gmf, Ys, As)
+    return R, (Xb, Db, Gm, Gmf, Ys, As, C)
 
 
-def unrolled_backward_gram(Rbar, state, eta, mom, T, lam=None):
+def unrolled_backward_gram(Rbar, state, eta, mom, T, lam=None, rows: int = 0):
     """Adjoint of ``unrolled_forward_gram``: the reverse sweep runs in the Gram kernel (mode 2:
     Vbar_t in registers, Yb = Vbar - eta Vbar Gm, the support of A_t from the slab), writing the
     Vbar slab and sum_t Vbar_t.  The dictionary gradient then needs no residual slabs:
         Dbar = eta (Vsum^T X - (M + M^T) D) - A_T^T Rbar,   M = sum_t Vbar_t^T Y_t
-    (one K = T B GEMM, [n, n] out), and etabar = <Vsum^T X, D> - <M, Gm> - lam sum Vsum.
+    (one K = T B GEMM, [n, n] out).  The eta gradient, sum_t <Vbar_t, C - Y_t Gm> - lam sum Vbar_t,
+    is <Vsum, C> - sum_t <Vbar_t Gm, Y_t> - lam sum Vsum with the middle term accumulated in
+    fp32 inside the sweep (its terms cancel to ~1/10 of their size: the bf16 GEMM identity
+    <Vsum^T X, D> - <M, Gm> is off by ~10%).  ``rows``: 16 / 32 forces the workgroup height.
     Returns (Dbar fp32 [G, n, d], cbar fp32 [G, B, n], etabar [G] or None)."""
     from . import gemm
 
-    Xb, Db, Gm, Gmf, Ys, As = state
+    Xb, Db, Gm, Gmf, Ys, As, C = state
     G, n, d = Db.shape
     B = Ys.shape[2]
     dev = Db.device
@@ -523,10 +526,12 @@ def unrolled_backward_gram(Rbar, state, eta, mom, T, lam=None):
                                                 stream), "sc_fista_adjoint_init")
     cbar = torch.empty(G, B, n, device=dev)
     Vsum = torch.empty(G, B, n, device=dev)
+    epart = torch.zeros(G, B // 16, device=dev)  # per-workgroup partials (16- or 32-row workgroups)
     lam_t = lam if lam is not None else torch.zeros(G, device=dev)
     rc = _lib.lib().sc_fista_gram(None, _lib.ptr(Gmf), _lib.ptr(V0), _lib.ptr(eta), _lib.ptr(lam_t),
                                   _lib.ptr(torch.as_tensor(mom, dtype=torch.float32).to(dev)), _lib.ptr(cbar), G, B, n,
-                                  T, stream, 0, 2, _lib.ptr(Vs), _lib.ptr(As), _lib.ptr(Vsum))
+                                  T, stream, rows, 2, _lib.ptr(Vs), _lib.ptr(As), _lib.ptr(Vsum), _lib.ptr(Ys),
+                                  _lib.ptr(epart))
     _lib.check(rc, "sc_fista_gram (adjoint)")
     # M = sum_t Vbar_t^T Y_t: G (n/256)^2 output tiles over K = T B -> split K to fill the chip
     tiles = G * ((n + 255) // 256) ** 2
@@ -551,7 +556,7 @@ def unrolled_backward_gram(Rbar, state, eta, mom, T, lam=None):
     Dbar = (VX - Q) * e - AR
     etabar = None
     if lam is not None:
-        etabar = ((VX * Db.float()).sum((1, 2)) - (M * Gm.float()).sum((1, 2)) - lam * Vsum.sum((1, 2)))
+        etabar = (Vsum * C).sum((1, 2)) - epart.sum(1) - lam * Vsum.sum((1, 2))
     return Dbar, cbar, etabar
 
 

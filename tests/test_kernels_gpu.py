@@ -848,7 +848,7 @@ def test_unrolled_fista_gram_adjoint_matches_fp32(G, B, n, d):
     mom = F.momentum_schedule(T)
     R_ref = F.unrolled_fista_residual(X, D, lam, c, T, eta, backend="torch")
     R, st = F.unrolled_forward_gram(X, D, c, lam, eta, T, mom)
-    Xb, Db, Gm, Gmf, Ys, As = st
+    Xb, Db, Gm, Gmf, Ys, As, C = st
     Dg, cg, eg = F.unrolled_backward_gram(W, st, eta, mom.tolist(), T, lam=lam)
     Df = Db.float()
     Rs = (Xb.float() - Ys.float() @ Df.unsqueeze(1)).to(torch.bfloat16)  # Res_t = X - Y_t D per slot
@@ -859,7 +859,11 @@ def test_unrolled_fista_gram_adjoint_matches_fp32(G, B, n, d):
         assert rel(R, R_ref) < 3e-2, rel(R, R_ref)
         assert rel(Dg, Dr) < 1e-2, rel(Dg, Dr)
         assert rel(cg, cr) < 1e-2, rel(cg, cr)
-    torch.testing.assert_close(eg, er, rtol=2e-2, atol=1e-2 * er.abs().max().item())
+    torch.testing.assert_close(eg, er, rtol=1e-2, atol=1e-3 * er.abs().max().item())
+    # the 16-row adjoint (rows=16) gives the same gradients
+    D16, c16, e16 = F.unrolled_backward_gram(W, st, eta, mom.tolist(), T, lam=lam, rows=16)
+    torch.testing.assert_close(D16, Dg, rtol=1e-3, atol=1e-3 * Dg.abs().max().item())
+    torch.testing.assert_close(e16, eg, rtol=1e-3, atol=1e-3 * eg.abs().max().item())
     # the autograd Function routes to the Gram path for n <= d
     D1, c1 = D.clone().requires_grad_(), c.clone().requires_grad_()
     (F.unrolled_fista_residual(X, D1, lam, c1, T, eta, backend="hip") * W).sum().backward()
