@@ -127,6 +127,71 @@ def cfg_fista(a):
             "ring_gb": round(ring.capacity * d * 2 / 1e9, 1), "ring_fill_s": round(fill_s, 1)}
 
 
+def cfg_config5(a):
+    """Config 5 at machine scale (reference activation_dataset.py:326-391 harvest, big_sweep.py:176-198
+    + basic_l1_sweep.py:48-152 training): random-init Pythia-410m in bf16, layer-12 residual
+    (d = 1024) harvested into an HBM ring sized from free device memory (all but ``--reserve-gb``),
+    then the fork's loop -- ``EnsembleTrainer(..., FunctionalFista)``: one Adam step of the
+    8-model L1 sweep, then a 300-iteration FISTA solve + Hessian-preconditioned basis update per
+    step, all on device.  Progress lines go to stderr while the ring fills."""
+    from sparse_coding__amd.data.harvest import ActivationHarvester, build_model
+    from sparse_coding__amd.data.ring import DeviceRing, rows_for_budget
+    from sparse_coding__amd.engine.trainer import EnsembleTrainer
+    from sparse_coding__amd.models.fista import FunctionalFista
+    from sparse_coding__amd.ops import fista as F
+
+    dev = "cuda:0"
+    torch.manual_seed(0)
+    d, layer = 1024, 12
+    model = build_model("pythia-410m", device=dev, dtype=torch.bfloat16)
+    h = ActivationHarvester(model, [layer], "residual")
+    bs, seq = 64, 256
+    free, total = torch.cuda.mem_get_info()
+    budget = (a.ring_gb * 1e9) if a.ring_gb > 0 else free - a.reserve_gb * 1e9
+    ring = DeviceRing(rows_for_budget(d, int(budget)), d, device=dev, seed=1)
+    # Zipf token ids sampled on the device (offline stand-in for the Pile)
+    ranks = torch.arange(1, 50305, device=dev, dtype=torch.float64)
+    probs = (1.0 / ranks ** 1.1)
+    probs = (probs / probs.sum()).float()
+    gen = torch.Generator(device=dev).manual_seed(3)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = t0
+    while ring.size < ring.capacity:
+        toks = torch.multinomial(probs, bs * seq, replacement=True, generator=gen).view(bs, seq)
+        acts = h.run(toks)[layer]
+        ring.push(acts[: ring.capacity - ring.size])
+        if time.perf_counter() - last > 20:
+            torch.cuda.synchronize()
+            last = time.perf_counter()
+            print(f"[config5] ring {ring.size / ring.capacity:6.1%} of {ring.capacity} rows, "
+                  f"{ring.size / (last - t0):,.0f} act/s", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    fill_s = time.perf_counter() - t0
+    h.close()
+    del model, h
+    torch.cuda.empty_cache()
+    B, n = a.batch, int(d * a.ratio)
+    l1s = np.logspace(-4, -2, a.models)
+    models = [FunctionalFista.init(d, n, float(l1), device=dev) for l1 in l1s]
+    tr = EnsembleTrainer(models, FunctionalFista, batch_size=B, device=dev, fista_iters=a.iters, fista_backend="hip")
+    xbuf = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
+    el = _timed(lambda: tr.step(ring.sample(B, out=xbuf)), a.steps, a.warmup, torch.cuda.synchronize)
+    D = torch.nn.functional.normalize(torch.randn(a.models, n, d, device=dev), dim=-1)
+    x = ring.sample(B).float()
+    eta = F.step_size(D)
+    lam = torch.tensor(l1s, device=dev, dtype=torch.float32)
+    solve = _timed(lambda: F.fista(x, D, lam, None, a.iters, eta, backend="hip", with_res=False), 3, 1,
+                   torch.cuda.synchronize) / 3
+    return {"config": f"5: FISTA {a.iters}-step dictionary learning on harvested random-init Pythia-410m layer-{layer} "
+                      f"residual (d={d}), n={n}, {a.models} models, batch {B}",
+            "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
+            "solve_ms_all_models": round(1e3 * solve, 3), "engine": tr.kind,
+            "ring_rows": ring.capacity, "ring_gb": round(ring.capacity * d * 2 / 1e9, 1),
+            "device_total_gb": round(total / 1e9, 1), "ring_fill_s": round(fill_s, 1),
+            "harvest_act_per_s": round(ring.capacity / fill_s, 1), "dtype": "bf16", "data": "harvested (random-init LM)"}
+
+
 def cfg_fistaloss(a):
     """FISTA in the loss (reference autoencoders/fista.py:141-172, the fork's fista_13_10 runs):
     8-model L1 sweep, d = n = 512 (dict_size 512), 50 unrolled iterations inside the loss.
@@ -316,7 +381,8 @@ def cfg_harvest(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["cpu", "topk", "fista", "fistaloss", "mlp", "mlpout", "masked", "harvest"])
+    ap.add_argument("which", choices=["cpu", "topk", "fista", "config5", "fistaloss", "mlp", "mlpout", "masked",
+                                      "harvest"])
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=2048)
@@ -326,9 +392,11 @@ def main():
     ap.add_argument("--sparse-k", default="auto", help="topk: models with k <= this take the slot-list wgrad")
     ap.add_argument("--eager", action="store_true", help="topk: no HIP graph")
     ap.add_argument("--variant", default="both", choices=["both", "masked", "unmasked"], help="masked: which run")
-    ap.add_argument("--ring-gb", type=float, default=0.0, help="fista: ring size in GB of HBM (0: 512k rows)")
+    ap.add_argument("--ring-gb", type=float, default=0.0,
+                    help="fista: ring size in GB of HBM (0: 512k rows); config5: 0 = free memory - reserve")
+    ap.add_argument("--reserve-gb", type=float, default=24.0, help="config5: HBM left outside the ring")
     a = ap.parse_args()
-    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "fistaloss": cfg_fistaloss, "mlp": cfg_mlp, "mlpout": cfg_mlpout, "masked": cfg_masked,
+    rec = {"cpu": cfg_cpu, "topk": cfg_topk, "fista": cfg_fista, "config5": cfg_config5, "fistaloss": cfg_fistaloss, "mlp": cfg_mlp, "mlpout": cfg_mlpout, "masked": cfg_masked,
            "harvest": cfg_harvest}[a.which](a)
     print(json.dumps(rec), flush=True)
 

@@ -32,7 +32,8 @@ class KernelError(RuntimeError):
     pass
 
 
-def _declare(lib):
+def signatures():
+    """(required, optional) C signatures of the kernel library: name -> argument types."""
     sig = {
         "sc_gemm": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                     C.POINTER(ScOperand), C.POINTER(ScOperand), C.POINTER(c_void_p), c_float_p,
@@ -79,13 +80,19 @@ def _declare(lib):
                              c_float, c_float, c_int, c_int, c_int, c_int, c_int, c_void_p],
         "sc_fista_adjoint_init": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
         "sc_fista_gram": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                          c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+                          c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                          c_void_p, c_void_p],
         "sc_stream_create_cumask": [c_void_p, c_int, C.POINTER(c_void_p)],
         "sc_stream_destroy": [c_void_p],
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
         "sc_basis_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int,
                            c_void_p],
     }
+    return sig, optional
+
+
+def _declare(lib):
+    sig, optional = signatures()
     for name, args in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = args
@@ -95,7 +102,31 @@ def _declare(lib):
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = c_int
-    return lib
+    return _Checked(lib)
+
+
+class _Checked:
+    """The loaded library with arity-checked entry points: ctypes passes surplus arguments
+    with default conversions (a Python int becomes a 32-bit C int), so a call with more
+    arguments than the declared signature would silently truncate pointers.  Refuse instead."""
+
+    def __init__(self, lib):
+        self._lib = lib
+        self._fns = {}
+
+    def __getattr__(self, name):
+        fn = self._fns.get(name)
+        if fn is None:
+            raw = getattr(self._lib, name)
+            nargs = len(raw.argtypes) if raw.argtypes is not None else None
+
+            def fn(*args, _raw=raw, _n=nargs, _name=name):
+                if _n is not None and len(args) != _n:
+                    raise TypeError(f"{_name} takes {_n} arguments, got {len(args)}")
+                return _raw(*args)
+
+            self._fns[name] = fn
+        return fn
 
 
 def verify_provenance(path: Path = _LIB_PATH) -> str:

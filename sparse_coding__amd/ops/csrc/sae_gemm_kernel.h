@@ -593,9 +593,21 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   int rem = bid - pi * per_prob;
   const int ksi = (int)fdiv(rem, p.f_split);
   rem -= ksi * per_split;
-  const int g = (int)fdiv(rem, p.f_plane);
-  rem -= g * tiles_m * tiles_n;
-  const int tm = (int)fdiv(rem, p.f_tn), tn = rem - tm * tiles_n;
+  int g, tm, tn;
+  if (p.nactive || p.nact_m || p.nact_k) {
+    // masked ensembles: models carry different live sizes, so the model index varies fastest --
+    // with model-major order the XCD-aware remap hands each XCD one model's tiles and the XCD
+    // holding the largest model bounds the launch (measured 0.83x of unmasked at 60% live)
+    g = rem % p.G;
+    const int t = rem / p.G;
+    tm = (int)fdiv(t, p.f_tn);
+    tn = t - tm * tiles_n;
+  } else {
+    g = (int)fdiv(rem, p.f_plane);
+    rem -= g * tiles_m * tiles_n;
+    tm = (int)fdiv(rem, p.f_tn);
+    tn = rem - tm * tiles_n;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
 
   // Resolve the problem's operands with selects (a dynamically indexed kernarg

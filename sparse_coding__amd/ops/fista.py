@@ -164,7 +164,7 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
         Gm = Gm.view(G, n // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
         rc = _lib.lib().sc_fista_gram(_lib.ptr(C), _lib.ptr(Gm), _lib.ptr(a0), _lib.ptr(eta), _lib.ptr(lam),
                                       _lib.ptr(mom), _lib.ptr(A), G, B, n, iters, _lib.stream_handle(), rows, 0,
-                                      None, None, None)
+                                      None, None, None, None, None)
     else:
         # both operands in MFMA-fragment order (see the Gram form): D [G][n/16][d/32][64][8] for the
         # (Res D^T) product, D^T [G][d/16][n/32][64][8] for the (Y D) product
@@ -490,7 +490,7 @@ def unrolled_forward_gram(X, D, A0, lam, eta, iters, mom=None):
         raise ValueError(f"A0 shape {tuple(A0.shape)} != {(G, B, n)}")
     rc = _lib.lib().sc_fista_gram(_lib.ptr(C), _lib.ptr(Gmf), _lib.ptr(a0), _lib.ptr(eta), _lib.ptr(lam),
                                   _lib.ptr(mom.to(dev)), _lib.ptr(A), G, B, n, T, _lib.stream_handle(), 0, 1,
-                                  _lib.ptr(Ys), _lib.ptr(As), None)
+                                  _lib.ptr(Ys), _lib.ptr(As), None, None, None)
     _lib.check(rc, "sc_fista_gram (saving iterates)")
     # R = X - A_T D from the bf16 A_T in the last A slot (the direct form also multiplies bf16 A)
     AD = torch.empty(G, B, d, device=dev)
