@@ -258,15 +258,17 @@ __global__ __launch_bounds__(FNT, 1) void fista_kernel(FistaArgs a) {
 // barrier per iteration.
 //
 // MODE 1 (unrolled FISTA in the loss, forward): also store the bf16 iterate slabs
-//   Ysave [G][T][B][n] slot t = Y_t (the iterate multiplied at iteration t, Y_0 = A0) and
-//   Asave [G][T][B][n] slot t = A_{t+1} (its support masks the adjoint).
+//   Ysave [G][T][B][n] slot t = Y_t (the iterate multiplied at iteration t, Y_0 = A0),
+//   Asave [G][T][B][n] slot t = A_{t+1} (its support masks the adjoint) and
+//   Qslab [G][T][B][n] slot t = Q_t = C - Y_t Gm (= Res_t D^T, the step direction; fp32 in registers
+//   here, small -- the eta gradient is sum_t <Vbar_t, Q_t>, which from C and Y_t Gm separately
+//   would be a difference of terms ~10x its size).
 // MODE 2 (its adjoint, reverse time t = T-1 .. 0), with Y holding Vbar_t and Ap the previous Yb:
 //   Yb = Vbar - eta Vbar Gm;  t >= 1: Vbar = ((1 + mom[t-1]) Yb - mom[t] Yb_prev) * 1[A_t > 0]
 //   t == 0: cbar = Yb - mom[0] Yb_prev (-> Aout);  A0 = Vbar_{T-1};  C unused.
 //   Ysave receives Vbar_t in slot t, Vsum = sum_t Vbar_t (fp32, [G][B][n]), and epart [G][B / 16]
-//   the workgroups' sums of <Z_t, Y_t> (Z_t = Vbar_t Gm, Y_t from the forward's slab Yfwd): the
-//   eta gradient is <Vsum, C> - sum epart - lam sum Vsum, taken from fp32 data -- its terms cancel
-//   to ~1/10 of their size, so the bf16 GEMM form (<Vsum^T X, D> - <M, Gm>) is too coarse.  With these the
+//   the workgroups' sums of <Vbar_t, Q_t> (fp32 Vbar, Q from the forward's slab): the eta
+//   gradient is sum epart - lam sum Vsum.  With these the
 //   dictionary gradient needs no residual slabs: Dbar = eta (Vsum^T X - (M + M^T) D) - A_T^T Rbar,
 //   M = sum_t Vbar_t^T Y_t (one K = T B GEMM over the two Y slabs, ops/fista.py).
 template <int NW, int RT, int HALVES, int PF, int MODE = 0>
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
                                                         const float* __restrict__ lam_, const float* __restrict__ mom,
                                                         float* __restrict__ Aout, int B, int T,
                                                         uint16_t* __restrict__ Ysave, uint16_t* __restrict__ Asave,
-                                                        float* __restrict__ Vsum, const uint16_t* __restrict__ Yfwd,
+                                                        float* __restrict__ Vsum, uint16_t* __restrict__ Qslab,
                                                         float* __restrict__ epart) {
   constexpr int n = NW * 128;  // 8 waves x NW 16-column tiles
   constexpr int nrb = n * 2;
@@ -294,7 +296,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
   const float* Cg = C + ((long)g * B + r0) * n;
   // slot s of a slab for this workgroup's rows (wave-uniform base; lanes add a 32-bit offset)
   auto slab = [&](auto* base, int s) { return base + (((long)g * T + s) * B + r0) * n; };
-  float edot = 0.f;  // adjoint: this lane's share of sum_t <Z_t, Y_t>
+  float edot = 0.f;  // adjoint: this lane's share of sum_t <Vbar_t, Q_t>
   f32x4_t Y[RT][NW], Ap[RT][NW];
   f32x4_t Vs[MODE == 2 ? RT : 1][MODE == 2 ? NW : 1];
 #pragma unroll
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
     const float m1 = MODE == 2 && ts >= 1 ? 1.f + mom[ts - 1] : 0.f;
     const bool final_iter = it + 1 == T;
     const uint16_t* a_in = MODE == 2 && !final_iter ? slab(Asave, ts - 1) : nullptr;  // support of A_ts
-    const uint16_t* y_in = MODE == 2 ? slab(Yfwd, ts) : nullptr;                     // Y_ts
+    uint16_t* q_sl = MODE != 0 ? slab(Qslab, ts) : nullptr;  // Q_ts: written (forward) / read (adjoint)
     uint16_t* y_out = MODE == 2 ? (final_iter ? nullptr : slab(Ysave, ts - 1))
                                 : MODE == 1 && !final_iter ? slab(Ysave, ts + 1) : nullptr;
     uint16_t* a_out = MODE == 1 ? slab(Asave, ts) : nullptr;
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
       // C (forward) / the support of A_ts (adjoint) for this half's update, issued ahead of the GEMM
       f32x4_t cv[MODE == 2 ? 1 : RT][MODE == 2 ? 1 : NH];
       ushort4 mk[MODE == 2 ? RT : 1][MODE == 2 ? NH : 1];  // raw bf16 A_ts (half the registers)
-      ushort4 yv[MODE == 2 ? RT : 1][MODE == 2 ? NH : 1];  // bf16 Y_ts
+      ushort4 qv[MODE == 2 ? RT : 1][MODE == 2 ? NH : 1];  // bf16 Q_ts
 #pragma unroll
       for (int u = 0; u < RT; ++u)
 #pragma unroll
@@ -352,7 +354,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
           const int col = nbase + (h * NH + t) * 16 + 4 * q;
           if constexpr (MODE == 2) {
             if (!final_iter) mk[u][t] = *reinterpret_cast<const ushort4*>(a_in + (u * FR + row) * n + col);
-            yv[u][t] = *reinterpret_cast<const ushort4*>(y_in + (u * FR + row) * n + col);
+            qv[u][t] = *reinterpret_cast<const ushort4*>(q_sl + (u * FR + row) * n + col);
           } else {
             cv[u][t] = *reinterpret_cast<const f32x4_t*>(Cg + (long)(u * FR + row) * n + col);
           }
@@ -393,8 +395,8 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
           f32x4_t an;
           if constexpr (MODE == 2) {
             // Yb = Vbar - eta Vbar Gm; the next Vbar (or, at t = 0, cbar) from Yb and the previous Yb
-            edot += Z[u][t][0] * bf2f(yv[u][t].x) + Z[u][t][1] * bf2f(yv[u][t].y) + Z[u][t][2] * bf2f(yv[u][t].z) +
-                    Z[u][t][3] * bf2f(yv[u][t].w);
+            edot += Y[u][tt][0] * bf2f(qv[u][t].x) + Y[u][tt][1] * bf2f(qv[u][t].y) +
+                    Y[u][tt][2] * bf2f(qv[u][t].z) + Y[u][tt][3] * bf2f(qv[u][t].w);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float yb = Y[u][tt][r] - eta * Z[u][t][r];
@@ -414,13 +416,18 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
                   make_ushort4(f2bf(an[0]), f2bf(an[1]), f2bf(an[2]), f2bf(an[3]));
             }
           } else {
+            f32x4_t qd;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float y = Y[u][tt][r] + eta * (cv[u][t][r] - Z[u][t][r]);
+              qd[r] = cv[u][t][r] - Z[u][t][r];
+              const float y = Y[u][tt][r] + eta * qd[r];
               an[r] = fmaxf(y - thr, 0.f);
               Y[u][tt][r] = an[r] + (an[r] - Ap[u][tt][r]) * mo;
             }
             Ap[u][tt] = an;
+            if constexpr (MODE == 1)
+              *reinterpret_cast<ushort4*>(q_sl + (u * FR + row) * n + col) =
+                  make_ushort4(f2bf(qd[0]), f2bf(qd[1]), f2bf(qd[2]), f2bf(qd[3]));
             if (!final_iter) lds_put4(Ynxt, u * FR + row, col, nrb, Y[u][tt][0], Y[u][tt][1], Y[u][tt][2], Y[u][tt][3]);
             if constexpr (MODE == 1) {
               *reinterpret_cast<ushort4*>(a_out + (u * FR + row) * n + col) =
@@ -530,14 +537,14 @@ static int launch_direct(const FistaArgs& a, int G, hipStream_t stream, int rows
 // Gram-form solver: C = X D^T [G][B][n] fp32, Gm = D D^T bf16 in MFMA-fragment order
 // [G][n/16][n/32][64 lanes][8] (lane = 16 q + r holds Gm[16 tile + r][32 step + 8 q .. + 7]).
 // mode 0: solve; 1: solve saving the Y / A slabs (Ysave, Asave); 2: the adjoint sweep (A0 =
-// Vbar_{T-1}, A = cbar out, Ysave = Vbar slab out, Asave / Yfwd = the forward's A / Y slabs in,
+// Vbar_{T-1}, A = cbar out, Ysave = Vbar slab out, Asave / Qslab = the forward's A / Q slabs in,
 // Vsum out, epart [G][B / 16] out: workgroup partials, zero-initialised by the caller).
 int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* eta, const float* lam,
                   const float* mom, float* A, int G, int B, int n, int T, hipStream_t stream, int rows, int mode,
-                  void* Ysave, void* Asave, float* Vsum, const void* Yfwd, float* epart) {
+                  void* Ysave, void* Asave, float* Vsum, void* Qslab, float* epart) {
   if (B % FR || n % 128 || T < 0 || mode < 0 || mode > 2) return 1;
-  if (mode && (!Ysave || !Asave || T < 1 || (mode == 2 && (!Vsum || !A0 || !Yfwd || !epart)))) return 1;
-  const uint16_t* yf = reinterpret_cast<const uint16_t*>(Yfwd);
+  if (mode && (!Ysave || !Asave || !Qslab || T < 1 || (mode == 2 && (!Vsum || !A0 || !epart)))) return 1;
+  uint16_t* qs = reinterpret_cast<uint16_t*>(Qslab);
   const uint16_t* gm = reinterpret_cast<const uint16_t*>(Gm);
   uint16_t* ys = reinterpret_cast<uint16_t*>(Ysave);
   uint16_t* as = reinterpret_cast<uint16_t*>(Asave);
@@ -549,9 +556,9 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
 #define SC_GM(NWV, H2, PF2, H1, PF1, MV)                                                                   \
   {                                                                                                        \
     if (two) hipLaunchKernelGGL((fista_gram_kernel<NWV, 2, H2, PF2, MV>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, \
-                                mom, A, B, T, ys, as, Vsum, yf, epart);                                               \
+                                mom, A, B, T, ys, as, Vsum, qs, epart);                                               \
     else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1, MV>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, \
-                            mom, A, B, T, ys, as, Vsum, yf, epart);                                                   \
+                            mom, A, B, T, ys, as, Vsum, qs, epart);                                                   \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                        \
   }
   // (NW, halves, ring depth) of the 32-row and 16-row solve, then of the slab-saving solve and
@@ -566,12 +573,12 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
   }
 #define SC_G1(NWV, H1, PF1, MV)                                                                            \
   hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1, MV>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, \
-                     T, ys, as, Vsum, yf, epart);                                                                     \
+                     T, ys, as, Vsum, qs, epart);                                                                     \
   return hipGetLastError() == hipSuccess ? 0 : 3;
   SC_G(2, 1, 4, 1, 4, SC_GM(2, 1, 4, 1, 4, 1), SC_GM(2, 1, 4, 1, 4, 2))
   SC_G(4, 1, 4, 1, 8, SC_GM(4, 1, 4, 1, 4, 1), SC_GM(4, 4, 1, 1, 2, 2))
-  SC_G(6, 2, 2, 2, 4, SC_GM(6, 2, 2, 2, 4, 1), SC_G1(6, 2, 2, 2))
-  SC_G(8, 4, 2, 2, 4, SC_G1(8, 2, 4, 1), SC_G1(8, 4, 1, 2))
+  SC_G(6, 2, 2, 2, 4, SC_GM(6, 2, 2, 2, 4, 1), SC_G1(6, 3, 1, 2))
+  SC_G(8, 4, 2, 2, 4, SC_G1(8, 2, 4, 1), SC_G1(8, 8, 1, 2))  // adjoint spills ~180 B/lane at n = 1024
 #undef SC_G
 #undef SC_G1
 #undef SC_GM

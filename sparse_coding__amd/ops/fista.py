@@ -484,19 +484,20 @@ def unrolled_forward_gram(X, D, A0, lam, eta, iters, mom=None):
     T = int(iters)
     Ys = torch.empty(G, T, B, n, device=dev, dtype=torch.bfloat16)
     As = torch.empty(G, T, B, n, device=dev, dtype=torch.bfloat16)
+    Qs = torch.empty(G, T, B, n, device=dev, dtype=torch.bfloat16)
     A = torch.empty(G, B, n, device=dev)
     a0 = A0.float().contiguous()
     if tuple(a0.shape) != (G, B, n):
         raise ValueError(f"A0 shape {tuple(A0.shape)} != {(G, B, n)}")
     rc = _lib.lib().sc_fista_gram(_lib.ptr(C), _lib.ptr(Gmf), _lib.ptr(a0), _lib.ptr(eta), _lib.ptr(lam),
                                   _lib.ptr(mom.to(dev)), _lib.ptr(A), G, B, n, T, _lib.stream_handle(), 0, 1,
-                                  _lib.ptr(Ys), _lib.ptr(As), None, None, None)
+                                  _lib.ptr(Ys), _lib.ptr(As), None, _lib.ptr(Qs), None)
     _lib.check(rc, "sc_fista_gram (saving iterates)")
     # R = X - A_T D from the bf16 A_T in the last A slot (the direct form also multiplies bf16 A)
     AD = torch.empty(G, B, d, device=dev)
     _strided_mm(gemm.EPI_F32, 1, B, d, n, As[:, T - 1], n, T * B * n, Db, d, n * d, AD, d, B * d, 1.0)
     R = (X.float() if X.dim() == 3 else X.float().expand(G, B, d)) - AD
-    return R, (Xb, Db, Gm, Gmf, Ys, As, C)
+    return R, (Xb, Db, Gm, Gmf, Ys, As, Qs)
 
 
 def unrolled_backward_gram(Rbar, state, eta, mom, T, lam=None, rows: int = 0):
@@ -504,14 +505,15 @@ def unrolled_backward_gram(Rbar, state, eta, mom, T, lam=None, rows: int = 0):
     Vbar_t in registers, Yb = Vbar - eta Vbar Gm, the support of A_t from the slab), writing the
     Vbar slab and sum_t Vbar_t.  The dictionary gradient then needs no residual slabs:
         Dbar = eta (Vsum^T X - (M + M^T) D) - A_T^T Rbar,   M = sum_t Vbar_t^T Y_t
-    (one K = T B GEMM, [n, n] out).  The eta gradient, sum_t <Vbar_t, C - Y_t Gm> - lam sum Vbar_t,
-    is <Vsum, C> - sum_t <Vbar_t Gm, Y_t> - lam sum Vsum with the middle term accumulated in
-    fp32 inside the sweep (its terms cancel to ~1/10 of their size: the bf16 GEMM identity
-    <Vsum^T X, D> - <M, Gm> is off by ~10%).  ``rows``: 16 / 32 forces the workgroup height.
+    (one K = T B GEMM, [n, n] out).  The eta gradient, sum_t <Vbar_t, Q_t> - lam sum Vbar_t with
+    Q_t = C - Y_t Gm the forward's step direction (saved as a bf16 slab: from C and Y_t Gm
+    separately it would be a difference of terms ~10x its size -- the bf16 GEMM identity
+    <Vsum^T X, D> - <M, Gm> is off by ~10%), is accumulated in fp32 inside the sweep.
+    ``rows``: 16 / 32 forces the workgroup height.
     Returns (Dbar fp32 [G, n, d], cbar fp32 [G, B, n], etabar [G] or None)."""
     from . import gemm
 
-    Xb, Db, Gm, Gmf, Ys, As, C = state
+    Xb, Db, Gm, Gmf, Ys, As, Qs = state
     G, n, d = Db.shape
     B = Ys.shape[2]
     dev = Db.device
@@ -530,7 +532,7 @@ def unrolled_backward_gram(Rbar, state, eta, mom, T, lam=None, rows: int = 0):
     lam_t = lam if lam is not None else torch.zeros(G, device=dev)
     rc = _lib.lib().sc_fista_gram(None, _lib.ptr(Gmf), _lib.ptr(V0), _lib.ptr(eta), _lib.ptr(lam_t),
                                   _lib.ptr(torch.as_tensor(mom, dtype=torch.float32).to(dev)), _lib.ptr(cbar), G, B, n,
-                                  T, stream, rows, 2, _lib.ptr(Vs), _lib.ptr(As), _lib.ptr(Vsum), _lib.ptr(Ys),
+                                  T, stream, rows, 2, _lib.ptr(Vs), _lib.ptr(As), _lib.ptr(Vsum), _lib.ptr(Qs),
                                   _lib.ptr(epart))
     _lib.check(rc, "sc_fista_gram (adjoint)")
     # M = sum_t Vbar_t^T Y_t: G (n/256)^2 output tiles over K = T B -> split K to fill the chip
@@ -556,7 +558,7 @@ def unrolled_backward_gram(Rbar, state, eta, mom, T, lam=None, rows: int = 0):
     Dbar = (VX - Q) * e - AR
     etabar = None
     if lam is not None:
-        etabar = (Vsum * C).sum((1, 2)) - epart.sum(1) - lam * Vsum.sum((1, 2))
+        etabar = epart.sum(1) - lam * Vsum.sum((1, 2))
     return Dbar, cbar, etabar
 
 
