@@ -323,10 +323,10 @@ def _unrolled_hip_ok(X, D, A0, backend):
     G, n, d = D.shape
     B = A0.shape[-2]
     ok = (_hip_ok(D) and B % 128 == 0 and n % 128 == 0 and d % 128 == 0
-          and (d // 128, n // 128) in DIRECT_TILES)
+          and ((d // 128, n // 128) in DIRECT_TILES or _gram_unrolled_ok(D, A0)))
     if backend == "hip" and not ok:
         raise ValueError(f"unrolled FISTA HIP path needs B % 128 == 0 and (d/128, n/128) in {sorted(DIRECT_TILES)} "
-                         f"(B={B}, n={n}, d={d})")
+                         f"or the Gram form (n in {GRAM_N}, n <= d, d % 256 == 0) (B={B}, n={n}, d={d})")
     return ok
 
 
