@@ -76,6 +76,29 @@ __device__ __forceinline__ long mask_word(const GemmParams& p, int g, int row0, 
   return (((long)g * (p.M >> 6) + (row0 >> 6)) * (p.N >> 6) + (col0 >> 6)) * 64 + lane;
 }
 
+// ------------------------------------------------------------------ phase stamps (lab builds only)
+// scripts/lab/gemm_phases.hip defines SC_PHASE_STAMPS to time the phases of every workgroup
+// (start, first K-tile landed, K loop done, epilogue done) into a buffer of its own; product
+// builds compile these to nothing.
+#ifdef SC_PHASE_STAMPS
+__device__ long long* sc_stamp_buf;
+#define SC_STAMP(k)                                                                      \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && sc_stamp_buf) {                                              \
+      long long* st_ = sc_stamp_buf + (long)blockIdx.x * 8;                              \
+      st_[k] = (long long)__builtin_amdgcn_s_memtime();                                  \
+      if ((k) == 0) {                                                                    \
+        st_[4] = (long long)__builtin_amdgcn_s_memrealtime();                            \
+        st_[6] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);                   \
+        st_[7] = (long long)__builtin_amdgcn_s_getreg((15 << 11) | 20);                  \
+      }                                                                                  \
+      if ((k) == 3) st_[5] = (long long)__builtin_amdgcn_s_memrealtime();                \
+    }                                                                                    \
+  } while (0)
+#else
+#define SC_STAMP(k) do {} while (0)
+#endif
+
 // ------------------------------------------------------------------ epilogues
 // The fused epilogue of one output tile (shared by the tile kernel and the persistent
 // kernel).  `red` is LDS scratch of at least epi_scratch_floats<S>() floats; every
@@ -580,6 +603,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   constexpr int STG = TA + TBB;
   static_assert(PPWA * NW * 1024 == TA && PPWB * NW * 1024 == TBB, "tile must split into whole pieces");
   __shared__ __attribute__((aligned(16))) char smem[NST * STG];
+  SC_STAMP(0);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -762,6 +786,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
     // (the host guarantees ksplit <= number of K tiles, so every block has nk > kbeg)
     wait_tiles(min(NST - 1, nk - 1 - kbeg));  // tile kbeg landed
     tile_barrier();
+    SC_STAMP(1);
     frags(fa0, fb0, kbeg, 0);
     // Steady state (a DMA issued at every boundary, NST-2 tiles younger than kt+1 in
     // flight), then the drain (no more DMAs), then the last tile peeled: neither loop body
@@ -799,6 +824,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
     // (no implicit vmcnt(0)) so younger DMAs stay in flight; "memory" keeps hipcc from
     // moving LDS reads across it.
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kt == kbeg) SC_STAMP(1);
     if (kt + NST - 1 < nk) SC_ISSUE(kt + NST - 1);
     const char* la = smem + (kt % NST) * STG;
     const char* lb = la + TA;
@@ -823,11 +849,13 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   }
   }  // !dead
 #undef SC_ISSUE
+  SC_STAMP(2);
   lds_barrier();  // all reads of the ring done before smem is reused below
   constexpr bool STAGE = S::WI == 4 && S::WJ == 4 && NST * STG >= stage_bytes<S>();
   constexpr bool FSTAGE = EPI == EPI_F32 && S::WJ == 4 && NST * STG >= S::NW * S::WI * 16 * STAGE_ROW;
   sae_epilogue<S, EPI, AUX_EARLY, STAGE, FSTAGE>(p, acc, auxv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn, tiles_n,
                                          cptr, alpha, dead);
+  SC_STAMP(3);
 }
 
 
