@@ -51,7 +51,8 @@ class FusedSAEEnsemble:
 
     def __init__(self, models, sig, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999),
                  eps=1e-8, track_feature_counts=True, kind: Optional[str] = None,
-                 count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None):
+                 count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None,
+                 rowblock: Optional[bool] = None):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
         # FunctionalTiedCenteredSAE (sae_ensemble.py:162-228): the tied kernels on x - center
@@ -193,14 +194,30 @@ class FusedSAEEnsemble:
                      if gdt == "bf16" and self.wsplit == 1 else None)
         self._g_from_bf = False
         self.grad_scale = 1.0  # data parallel: 1 / world_size (gradients are then summed)
-        self.enc_part = torch.zeros(G, tm * (n // 128), 2, device=dev)
-        self.dec_part = torch.zeros(G, tm * (d // 128), device=dev)
-        self.colpart = torch.zeros(G, tm, n, device=dev)
+        # Kernels 1-3 as ONE row-block launch (csrc/sae_rowblock.hip: encoder -> decoder -> code
+        # gradient per 64 batch rows, c and R never re-read from HBM) for ReLU SAEs at d = 512,
+        # opt-in (``rowblock=True``): on MI355X it is still slower than the three grouped GEMMs
+        # (profiles/README.md, round 3).  Its partial sums use 64-row (scalars) and 32-row
+        # (column sums) slots instead of the GEMMs' 128x128 grid.
+        eligible = (self.act == gemm_ops.ACT_RELU and self.nactive is None and not self.learned_center
+                    and gemm_ops.rowblock_supported(B, n, d))
+        self.rowblock = False if rowblock is None else bool(rowblock)
+        if self.rowblock and not eligible:
+            raise ValueError("row-block forward needs a ReLU SAE without masks / learned centre, d = 512, "
+                             "n % 256 == 0, B % 64 == 0")
+        slots = B // 32 if self.rowblock else tm
+        if self.rowblock:
+            self.enc_part = torch.zeros(G, B // 64, 2, device=dev)
+            self.dec_part = torch.zeros(G, B // 64, device=dev)
+        else:
+            self.enc_part = torch.zeros(G, tm * (n // 128), 2, device=dev)
+            self.dec_part = torch.zeros(G, tm * (d // 128), device=dev)
+        self.colpart = torch.zeros(G, slots, n, device=dev)
         self.track_feature_counts = track_feature_counts
         # per-feature activation counts are sampled every `count_every` steps (the column
         # reduction costs ~15% of the encoder GEMM); `rows_seen` counts only sampled rows
         self.count_every = max(1, int(count_every))
-        self.cnt_part = torch.zeros(G, tm, n, device=dev) if track_feature_counts else None
+        self.cnt_part = torch.zeros(G, slots, n, device=dev) if track_feature_counts else None
         self.feature_counts = torch.zeros(G, n, device=dev) if track_feature_counts else None
         self.rows_seen = 0
         self.out = torch.zeros(G, 6, device=dev)
@@ -277,6 +294,11 @@ class FusedSAEEnsemble:
             raise ValueError(f"batch has {x.shape[-2]} rows, engine was built for {self.batch_size}")
         count = self._counting() if count is None else count
         self._counted = count
+        if self.rowblock and target is None:
+            gemm_ops.sae_forward_rowblock(x, self.enc_shadow, self.dec_shadow, self.params[self._bkey], self.l1,
+                                          self.c, self.r, self.dpre, self.cmask, self.enc_part, self.dec_part,
+                                          self.colpart, self.cnt_part if count else None)
+            return
         ascale = self.s2 if self.kind == "threshold" else None
         gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part,
                              self.cnt_part if count else None, self.nactive, mask_out=self.cmask,
@@ -458,7 +480,7 @@ class FusedSAEEnsemble:
         if reduced:  # bias gradient already summed (and possibly all-reduced) into g_bias
             colpart, tm, gscale = self.g_bias, 1, 1.0
         else:
-            colpart, tm, gscale = self.colpart, B // 128, self._alpha
+            colpart, tm, gscale = self.colpart, self.colpart.shape[1], self._alpha
         adam_ops.bias_loss(self.params[self._bkey], self.m[self._bkey], self.v[self._bkey],
                            colpart, tm, self.enc_part, self.enc_part.shape[1], self.dec_part,
                            self.dec_part.shape[1], self.l1, self.bias_decay, self.lr, self.out, B, d,
@@ -555,12 +577,15 @@ class FusedSAEEnsemble:
         for i in range(0, N, B):
             xin = self._x_bf16(rows[i:i + B])
             x = self.prepare(xin)
-            gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part, None,
-                                 self.nactive, mask_out=self.cmask, act=self.act,
-                                 ascale=self.s2 if self.kind == "threshold" else None)
-            if self.kind == "threshold":  # reconstructs the uncentred rows
-                x = xin
-            gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
+            if self.rowblock:
+                self.forward(x, count=False)
+            else:
+                gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part, None,
+                                     self.nactive, mask_out=self.cmask, act=self.act,
+                                     ascale=self.s2 if self.kind == "threshold" else None)
+                if self.kind == "threshold":  # reconstructs the uncentred rows
+                    x = xin
+                gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
             se += self.dec_part.sum(1).double()
             l0 += self.enc_part[..., 1].sum(1).double()
             xf = x.double() if x.dim() == 3 else x.double().expand(G, B, self.d)
