@@ -92,6 +92,8 @@ def parse(argv=None):
                     help="N>1: after the headline run, also time the other strategy (es <-> dp) and report it "
                          "under alt_parallelism")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of HIP graphs")
+    ap.add_argument("--rowblock", action="store_true",
+                    help="single-GPU fused engine: encoder/decoder/code gradient as one row-block kernel")
     return ap.parse_args(argv)
 
 
@@ -172,7 +174,8 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
     if args.engine == "fused":
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
 
-        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
+        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device,
+                               rowblock=True if args.rowblock else None)
         if not args.no_graph:
             eng.enable_graph()  # whole step = one HIP graph replay
 

@@ -15,8 +15,8 @@ for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursiv
     for r in csv.DictReader(open(f)):
         name = r.get("Kernel_Name", "?")
         short = name.split("(")[0].replace("void ", "").replace("scamd::", "")
-        if "sae_gemm_kernel" in name or "adam" in name or "topk" in name or "bias_loss" in name:
-            key = name[:160]
+        if any(t in name for t in ("sae_gemm_kernel", "adam", "topk", "bias_loss", "rowblock")):
+            key = name[:160] + (f" grid={r.get('Grid_Size')}" if "rowblock" in name else "")
             vals[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
             meta[key] = (r.get("VGPR_Count"), r.get("Accum_VGPR_Count"), r.get("LDS_Block_Size"), r.get("Grid_Size"),
                          r.get("Workgroup_Size"))
