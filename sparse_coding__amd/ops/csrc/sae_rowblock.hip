@@ -113,10 +113,13 @@ __global__ __launch_bounds__(rb::NT) void sae_rowblock_kernel(RowBlockParams p) 
   //                      w = 16..31  dec: W_hat_j[32 k-rows t = (w-16)/2][256 cols h = w&1] (N-major)
   //   phase C, chunk j:  s = 0..15   dc:  W_hat_j[256][32 k of slice s] + R[64][32 k]  (K-major)
   // per-lane LDS-DMA source offsets are unit-invariant; the unit adds a scalar soffset
-  uint32_t vB[2], vA[1], vT[2];
-  piece_offsets<true, 32, 2>(vB, D, 0, wid, lane);               // [256 rows][32 k]: 16 pieces
-  piece_offsets<true, 32, 1>(vA, D, m0, wid & 3, lane);          // [64 rows][32 k]: 4 pieces (waves 0-3)
-  piece_offsets<false, 32, 2>(vT, D, 0, wid, lane);              // [32 k][256 cols]: 16 pieces
+  // Only waves 0-3 (one per SIMD) issue DMAs: the per-piece scalar bookkeeping runs on the CU's
+  // single scalar unit, and with all 8 waves issuing the loop was scalar-issue bound.
+  const bool dma_wave = wid < 4;
+  uint32_t vB[4], vA[1], vT[4];
+  piece_offsets<true, 32, 4>(vB, D, 0, wid & 3, lane);           // [256 rows][32 k]: 16 pieces
+  piece_offsets<true, 32, 1>(vA, D, m0, wid & 3, lane);          // [64 rows][32 k]: 4 pieces
+  piece_offsets<false, 32, 4>(vT, D, 0, wid & 3, lane);          // [32 k][256 cols]: 16 pieces
   const i32x4_t rWe = make_rsrc(p.we + (long)g * n * D);
   const i32x4_t rWd = make_rsrc(p.wd + (long)g * n * D);
   const i32x4_t rX = make_rsrc(p.x + (long)g * p.x_sg);
@@ -133,17 +136,17 @@ __global__ __launch_bounds__(rb::NT) void sae_rowblock_kernel(RowBlockParams p) 
     if (u < UA) {
       const int j = u >> 5, w = u & 31;
       if (w < 16) {
-        issue_pieces<2>(rWe, vB, (uint32_t)(j * NC * D + 32 * w) * 2u, slot, wid);
-        if (wid < 4) issue_pieces<1>(rX, vA, (uint32_t)(32 * w) * 2u, slot + SLOT_A, wid);
-        else if (w == 15 && wid == 4) issue_pieces<1>(rBias, &vBias, (uint32_t)(j * NC * 4), slot + SLOT_BIAS, 0);
+        issue_pieces<4>(rWe, vB, (uint32_t)(j * NC * D + 32 * w) * 2u, slot, wid);
+        issue_pieces<1>(rX, vA, (uint32_t)(32 * w) * 2u, slot + SLOT_A, wid);
+        if (w == 15 && wid == 0) issue_pieces<1>(rBias, &vBias, (uint32_t)(j * NC * 4), slot + SLOT_BIAS, 0);
       } else {
         const int t = (w - 16) >> 1, h = w & 1;
-        issue_pieces<2>(rWd, vT, (uint32_t)((j * NC + 32 * t) * D + 256 * h) * 2u, slot, wid);
+        issue_pieces<4>(rWd, vT, (uint32_t)((j * NC + 32 * t) * D + 256 * h) * 2u, slot, wid);
       }
     } else {
       const int v = u - UA, j = v >> 4, sl = v & 15;
-      issue_pieces<2>(rWd, vB, (uint32_t)(j * NC * D + 32 * sl) * 2u, slot, wid);
-      if (wid < 4) issue_pieces<1>(rR, vA, (uint32_t)(32 * sl) * 2u, slot + SLOT_A, wid);
+      issue_pieces<4>(rWd, vB, (uint32_t)(j * NC * D + 32 * sl) * 2u, slot, wid);
+      issue_pieces<1>(rR, vA, (uint32_t)(32 * sl) * 2u, slot + SLOT_A, wid);
     }
   };
 
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(rb::NT) void sae_rowblock_kernel(RowBlockParams p) 
   int issued = 0, islot = 0, limit = UA;
   auto refill = [&](int upto) {  // issue units up to `upto` (inclusive) within the phase limit
     while (issued <= upto && issued < limit) {
-      issue(issued, islot);
+      if (dma_wave) issue(issued, islot);
       ++issued;
       islot = islot == NSLOT - 1 ? 0 : islot + 1;
     }
@@ -271,10 +274,13 @@ __global__ __launch_bounds__(rb::NT) void sae_rowblock_kernel(RowBlockParams p) 
       refill(b + NSLOT - 3);
     }
     RB_STAMP(b, 0);
-    // Units b, b+1 must have landed.  Every unit puts >= 2 DMA instructions per wave in flight, so
-    // with the two younger units issued vmcnt(4) is a safe (slightly conservative) bound.
-    if (issued - 2 - b >= 2) wait_vmcnt<4>();
-    else wait_vmcnt<0>();
+    // Units b, b+1 must have landed (the DMA waves wait for their own pieces; the barrier then
+    // publishes them to all).  Every unit puts >= 4 DMA instructions per DMA wave in flight, so
+    // with the two younger units issued vmcnt(8) is a safe (slightly conservative) bound.
+    if (dma_wave) {
+      if (issued - 2 - b >= 2) wait_vmcnt<8>();
+      else wait_vmcnt<0>();
+    }
     RB_STAMP(b, 1);
     lds_barrier();
     RB_STAMP(b, 2);
