@@ -121,8 +121,10 @@ class FusedSAEEnsemble:
         lrs = lr if isinstance(lr, (list, tuple)) else [lr] * G
         self.lr = torch.tensor([float(x) for x in lrs], device=dev, dtype=torch.float32)
         self.nactive = None
+        self._live = None  # host copy of the live sizes: masked launches cover only live tiles
         if "dict_size" in b0:
-            self.nactive = torch.tensor([int(m[1]["dict_size"]) for m in models], device=dev, dtype=torch.int32)
+            self._live = [int(m[1]["dict_size"]) for m in models]
+            self.nactive = torch.tensor(self._live, device=dev, dtype=torch.int32)
 
         # ----- bf16 shadows read by the GEMMs
         bf = torch.bfloat16
@@ -133,7 +135,10 @@ class FusedSAEEnsemble:
 
         # ----- workspaces
         tm = B // 128
-        self.c = torch.empty(G, B, n, device=dev, dtype=bf)
+        # masked ensembles: the compacted launches never write past a model's live size, so the
+        # buffers read there (codes, gradients) start, and stay, zero
+        alloc = torch.zeros if self.nactive is not None else torch.empty
+        self.c = alloc(G, B, n, device=dev, dtype=bf)
         self.r = torch.empty(G, B, d, device=dev, dtype=bf)
         self.dpre = torch.empty(G, B, n, device=dev, dtype=bf)
         # activity bitmask of c written by the encoder epilogue, read by the code-gradient
@@ -147,7 +152,7 @@ class FusedSAEEnsemble:
         if self.kind == "untied":
             # one allocation [g_dec | g_enc | g_bias]: data-parallel runs can reduce all of a
             # chunk's gradients with one collective (grad_all) or in two ([g_dec], [g_enc|g_bias])
-            self.grad_all = torch.empty(2 * G * n * d + G * n, device=dev, dtype=torch.float32)
+            self.grad_all = alloc(2 * G * n * d + G * n, device=dev, dtype=torch.float32)
             self.g_dec = self.grad_all[: G * n * d].view(G, n, d)
             self._g_flat = self.grad_all[G * n * d:]
             self.g_enc = self._g_flat[: G * n * d].view(G, n, d)
@@ -158,7 +163,7 @@ class FusedSAEEnsemble:
             self._n_extra = 0
             if self.kind == "threshold" or self.learned_center:
                 self._n_extra = G * n + (G * n if self.kind == "threshold" else 0) + (G * d if self.learned_center else 0)
-            self._g_flat = torch.empty(G * n * d + G * n + self._n_extra, device=dev, dtype=torch.float32)
+            self._g_flat = alloc(G * n * d + G * n + self._n_extra, device=dev, dtype=torch.float32)
             self.grad_all = self._g_flat
             self.g_dec = self._g_flat[: G * n * d].view(G, n, d)
             self.g_enc = None
@@ -179,8 +184,9 @@ class FusedSAEEnsemble:
         # Adam kernel sums the partial slabs.  (Data-parallel paths use the flat buffers.)
         nprob = 2 if self.kind == "untied" else 1
         kdim = B if self.kind == "untied" else 2 * B
-        self.wsplit = (gemm_ops.wgrad_split(G, n, d, kdim, nprob) if wgrad_split == "auto" else int(wgrad_split))
-        self.g_parts = (torch.empty(nprob, self.wsplit, G, n, d, device=dev, dtype=torch.float32)
+        self.wsplit = (gemm_ops.wgrad_split(G, n, d, kdim, nprob, live=self._live) if wgrad_split == "auto"
+                       else int(wgrad_split))
+        self.g_parts = (alloc(nprob, self.wsplit, G, n, d, device=dev, dtype=torch.float32)
                         if self.wsplit > 1 else None)
         self._g_from_parts = False
         # bf16 weight gradients for the single-device step (``grad_dtype='bf16'``): the
@@ -190,7 +196,7 @@ class FusedSAEEnsemble:
         gdt = grad_dtype or "fp32"
         if gdt not in ("fp32", "bf16"):
             raise ValueError(f"grad_dtype must be 'fp32' or 'bf16', got {gdt!r}")
-        self.g_bf = (torch.empty(nprob, G, n, d, device=dev, dtype=bf)
+        self.g_bf = (alloc(nprob, G, n, d, device=dev, dtype=bf)
                      if gdt == "bf16" and self.wsplit == 1 else None)
         self._g_from_bf = False
         self.grad_scale = 1.0  # data parallel: 1 / world_size (gradients are then summed)
@@ -302,16 +308,17 @@ class FusedSAEEnsemble:
         ascale = self.s2 if self.kind == "threshold" else None
         gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part,
                              self.cnt_part if count else None, self.nactive, mask_out=self.cmask,
-                             act=self.act, ascale=ascale, mask2_out=self.cmask2)
+                             act=self.act, ascale=ascale, mask2_out=self.cmask2, live_host=self._live)
         gemm_ops.decode_residual(self.c, self.dec_shadow, x if target is None else target, self.r, self.dec_part,
                                  rcol=self.rcol, nactive=self.nactive)
         if self.act:
             gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                                dotpart=self.dotpart if self.kind == "threshold" else None, mask=self.cmask,
-                               act=self.act, ascale=ascale, mask2=self.cmask2, nactive=self.nactive)
+                               act=self.act, ascale=ascale, mask2=self.cmask2, nactive=self.nactive,
+                               live_host=self._live)
             return
         gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
-                           mask=self.cmask, nactive=self.nactive)
+                           mask=self.cmask, nactive=self.nactive, live_host=self._live)
 
     @property
     def _alpha(self):
@@ -321,16 +328,18 @@ class FusedSAEEnsemble:
         """Untied: dW_hat = c^T R (decoder).  Tied: the whole dictionary gradient + bias grad."""
         self._g_from_parts = self._g_from_bf = False
         if self.kind == "untied":
-            gemm_ops.weight_grads([[(self.c, self.r)]], [self.g_dec], self._alpha, nactive=self.nactive)
+            gemm_ops.weight_grads([[(self.c, self.r)]], [self.g_dec], self._alpha, nactive=self.nactive,
+                                  live_host=self._live)
         else:
             gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], [self.g_dec], self._alpha,
-                                  nactive=self.nactive)
+                                  nactive=self.nactive, live_host=self._live)
             self._reduce_bias_grad()
 
     def wgrad_second(self, x, reduce_bias=True):
         """Untied: dW_e = dpre^T x (encoder) + bias grad.  Tied: nothing."""
         if self.kind == "untied":
-            gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha, nactive=self.nactive)
+            gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha, nactive=self.nactive,
+                                  live_host=self._live)
             if reduce_bias:
                 self._reduce_bias_grad()
 
@@ -357,11 +366,11 @@ class FusedSAEEnsemble:
             outs = ([self.g_parts[0], self.g_parts[1]] if split else
                     [self.g_bf[0], self.g_bf[1]] if gbf else [self.g_dec, self.g_enc])
             gemm_ops.weight_grads([[(self.c, self.r)], [(self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit,
-                                  nactive=self.nactive)
+                                  nactive=self.nactive, live_host=self._live)
         else:
             outs = [self.g_parts[0]] if split else [self.g_bf[0]] if gbf else [self.g_dec]
             gemm_ops.weight_grads([[(self.c, self.r), (self.dpre, x)]], outs, self._alpha, ksplit=self.wsplit,
-                                  nactive=self.nactive)
+                                  nactive=self.nactive, live_host=self._live)
 
     def _adam_sets(self):
         parts = self._g_from_parts
@@ -582,7 +591,7 @@ class FusedSAEEnsemble:
             else:
                 gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part, None,
                                      self.nactive, mask_out=self.cmask, act=self.act,
-                                     ascale=self.s2 if self.kind == "threshold" else None)
+                                     ascale=self.s2 if self.kind == "threshold" else None, live_host=self._live)
                 if self.kind == "threshold":  # reconstructs the uncentred rows
                     x = xin
                 gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)

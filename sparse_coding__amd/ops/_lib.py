@@ -41,7 +41,7 @@ def signatures():
                     c_void_p, c_void_p, c_void_p, c_float,
                     c_void_p, c_int,
                     c_int, c_int, c_long, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
-                    c_void_p, c_void_p, c_void_p],
+                    c_void_p, c_void_p, c_void_p, c_void_p],
         "sc_adam_rows": [c_int, C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
                          C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
                          C.POINTER(c_int), C.POINTER(c_int), c_int, c_int, c_void_p,

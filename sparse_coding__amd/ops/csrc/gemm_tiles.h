@@ -97,6 +97,17 @@ struct GemmParams {
   // DEC (optional): fp32 column sums of the residual per 128-row tile [G][tiles_m][N],
   // taken before the bf16 rounding (learned-centering gradient)
   float* rcol;
+  // --- masked ensembles, compacted grid (set by the launcher from host copies of the live sizes):
+  // only live tiles are launched.  cdim 0: the masked dimension is N (encoder / code gradient),
+  // 1: it is M (weight-gradient rows).  Model g owns tl[g] tiles along it and logical tiles
+  // [tpre[g], tpre[g+1]) of each problem; fl[g] divides by tl[g].  Dead outputs are never written
+  // (the engine zero-initialises them once).
+  int want_comp;      // host: nact_h holds the live sizes
+  int nact_h[16];
+  int ncomp, cdim, ctotal;  // ctotal: live tiles per problem
+  int tpre[17];
+  int tl[16];
+  FDiv fl[16];
 };
 
 // LDS image of a K-major tile [128 rows][BKT k] bf16.

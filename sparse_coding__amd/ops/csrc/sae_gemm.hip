@@ -40,7 +40,8 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             const float* bias, long sbias, const int* nactive, const void* aux, long ldaux,
             long saux, float* part, float* colpart, const float* l1, float l1_add_scale,
             float* dotpart, int dc_tied, int cfg, int ksplit, long split_stride, void* cmask, int act, const float* ascale,
-            void* cmask2, float* rcol, const int* nact_m, const int* nact_k, hipStream_t stream) {
+            void* cmask2, float* rcol, const int* nact_m, const int* nact_k, const int* nact_host,
+            hipStream_t stream) {
   if (M % PT || N % PT || K1 % 64 || K2 % 64 || nprob < 1 || nprob > 2 || G < 1) return 1;
   if ((epi == EPI_DC_MASK || epi == EPI_DC_ACT) && !cmask) return 4;
   if (epi == EPI_DC_ACT && (!aux || !colpart || !l1)) return 4;
@@ -67,6 +68,10 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.act = act; p.ascale = ascale;
   p.cmask2 = reinterpret_cast<uint64_t*>(cmask2); p.rcol = rcol;
   p.nact_m = nact_m; p.nact_k = nact_k;
+  // masked launches with host copies of the live sizes launch only their live tiles
+  p.want_comp = nact_host != nullptr && G <= 16;
+  p.ncomp = 0;
+  for (int g = 0; g < 16; ++g) p.nact_h[g] = (nact_host && g < G) ? nact_host[g] : 0;
   const bool ak = layout & 1, bk = layout & 2;
   int shape = cfg & 3;
   const int pipe = (cfg >> 2) & 3;  // 0: BK64 x 2 stages, 1: BK32 x 4, 2: BK32 x 2, 3: BK32 x 3

@@ -48,6 +48,8 @@
 #pragma once
 #include "gemm_tiles.h"
 
+#include <algorithm>
+
 namespace scamd {
 
 // Scheduling-group pattern for one pipelined K-step: N x (MPR MFMAs, then one DS read), the
@@ -610,7 +612,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   const int wr = wid / WGN, wc = wid % WGN;
   const int tiles_m = p.M / BM, tiles_n = p.N / BN;
   const int ptm = p.M / PT, ptn = p.N / PT;  // partial-buffer grid (128 x 128 sub-tiles)
-  const int per_split = tiles_m * tiles_n * p.G;
+  const int per_split = p.ncomp ? p.ctotal : tiles_m * tiles_n * p.G;
   const int per_prob = per_split * p.ksplit;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int pi = (int)fdiv(bid, p.f_prob);
@@ -618,7 +620,23 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   const int ksi = (int)fdiv(rem, p.f_split);
   rem -= ksi * per_split;
   int g, tm, tn;
-  if (p.nactive || p.nact_m || p.nact_k) {
+  if (p.ncomp) {
+    // compacted masked grid: find the model owning logical tile `rem` (static kernarg indices)
+    g = 0;
+    int base = 0, tlg = p.tl[0];
+    FDiv flg = p.fl[0];
+#pragma unroll
+    for (int k = 1; k < 16; ++k)
+      if (k < p.G && rem >= p.tpre[k]) { g = k; base = p.tpre[k]; tlg = p.tl[k]; flg = p.fl[k]; }
+    const int local = rem - base;
+    if (p.cdim == 0) {  // N masked: tl[g] column tiles per row tile
+      tm = (int)fdiv(local, flg);
+      tn = local - tm * tlg;
+    } else {            // M masked: all column tiles of tl[g] row tiles
+      tm = (int)fdiv(local, p.f_tn);
+      tn = local - tm * tiles_n;
+    }
+  } else if (p.nactive || p.nact_m || p.nact_k) {
     // masked ensembles: models carry different live sizes, so the model index varies fastest --
     // with model-major order the XCD-aware remap hands each XCD one model's tiles and the XCD
     // holding the largest model bounds the launch (measured 0.83x of unmasked at 60% live)
@@ -882,10 +900,42 @@ void set_divisors(GemmParams& p) {
   p.f_ksplit = make_fdiv(p.ksplit);
 }
 
+// Host: compact a masked launch to its live tiles (see GemmParams::ncomp).  Returns the number of
+// blocks per problem, or 0 when the launch stays uncompacted.
+template <class S>
+long compact_tiles(int epi, GemmParams& p) {
+  p.ncomp = 0;
+  if (!p.want_comp || p.G > 16) return 0;
+  const bool ncols = p.nactive && (epi == EPI_ENC || epi == EPI_ENC_CNT || epi == EPI_ENC_ACT || epi == EPI_DC ||
+                                   epi == EPI_DC_MASK || epi == EPI_DC_ACT);
+  const bool nrows = p.nact_m && (epi == EPI_F32 || epi == EPI_BF16);
+  if (!ncols && !nrows) return 0;
+  const int per = ncols ? S::BN : S::BM, full = ncols ? p.N / S::BN : p.M / S::BM;
+  const int other = ncols ? p.M / S::BM : p.N / S::BN;
+  long total = 0;
+  for (int g = 0; g < p.G; ++g) {
+    const int live = std::min(full, std::max(1, (p.nact_h[g] + per - 1) / per));
+    p.tl[g] = live;
+    p.fl[g] = make_fdiv((uint32_t)live);
+    p.tpre[g] = (int)total;
+    total += (long)live * other;
+  }
+  p.tpre[p.G] = (int)total;
+  p.ctotal = (int)total;
+  p.ncomp = 1;
+  p.cdim = ncols ? 0 : 1;
+  return total;
+}
+
 template <class S, int BKT, int NST, bool FULL = true>
 int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t stream) {
   set_divisors<S>(p);
-  const dim3 grid((unsigned)(n_blocks<S>(p.M, p.N, p.G, nprob) * p.ksplit)), block(S::NT);
+  const long comp = compact_tiles<S>(epi, p);
+  if (comp) {
+    p.f_split = make_fdiv((uint32_t)comp);
+    p.f_prob = make_fdiv((uint32_t)(comp * p.ksplit));
+  }
+  const dim3 grid((unsigned)((comp ? comp * nprob : n_blocks<S>(p.M, p.N, p.G, nprob)) * p.ksplit)), block(S::NT);
   if constexpr (!FULL) {
     if (epi == EPI_BF16 || epi >= EPI_ENC_ACT || (epi == EPI_F32 && (ak || bk))) return 8;
   }

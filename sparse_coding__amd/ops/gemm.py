@@ -88,7 +88,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
             bias=None, sbias=0, nactive=None, aux=None, ldaux=0, saux=0, part=None,
             colpart=None, l1=None, l1_add_scale=0.0, dotpart=None, dc_tied=False, cfg=None,
             ksplit=1, split_stride=0, cmask=None, act=0, ascale=None, cmask2=None, rcol=None, nact_m=None,
-            nact_k=None):
+            nact_k=None, nact_host=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
@@ -98,13 +98,16 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
     Bo = (_lib.ScOperand * (2 * nprob))(*b_ops)
     Cp = (C.c_void_p * nprob)(*[_lib.ptr(o) for o in outs])
     al = (C.c_float * nprob)(*alphas)
+    # host copy of a masked ensemble's live sizes: the launcher then launches only live tiles
+    nh = (C.c_int * len(nact_host))(*[int(v) for v in nact_host]) if nact_host is not None else None
     rc = _lib.lib().sc_gemm(
         epi, layout, nprob, M, N, K1, K2, G, A, Bo, Cp, al, ldc, sc,
         _lib.ptr(bias), sbias, _lib.ptr(nactive), _lib.ptr(aux), ldaux, saux,
         _lib.ptr(part), _lib.ptr(colpart), _lib.ptr(l1), float(l1_add_scale),
         _lib.ptr(dotpart), int(bool(dc_tied)),
         cfg, int(ksplit), int(split_stride), _lib.ptr(cmask), int(act), _lib.ptr(ascale),
-        _lib.ptr(cmask2), _lib.ptr(rcol), _lib.ptr(nact_m), _lib.ptr(nact_k), _lib.stream_handle(),
+        _lib.ptr(cmask2), _lib.ptr(rcol), _lib.ptr(nact_m), _lib.ptr(nact_k),
+        C.cast(nh, C.c_void_p) if nh is not None else None, _lib.stream_handle(),
     )
     _lib.check(rc, f"sc_gemm(epi={epi})")
 
@@ -125,7 +128,7 @@ def code_mask_shape(G, B, n):
 
 
 def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=None, act=ACT_RELU, ascale=None,
-                mask2_out=None):
+                mask2_out=None, live_host=None):
     """c[g] = relu(x[g] @ w[g]^T + bias[g]) with L1/L0 partials.
 
     ``act`` selects another code activation of the same GEMM:
@@ -140,6 +143,10 @@ def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=No
     can read instead of the codes.
     mask2_out (``ACT_THRESHOLD``): the same layout, 1 where the code is on the threshold's ramp
     (decided on the fp32 pre-activation; ``code_grad(mask2=...)`` reads it).
+    live_host (with ``nactive``): the same live sizes as host ints -- only live tiles are then
+    launched and nothing past a model's live size is written (``c_out`` / ``colpart`` / ``part``
+    must hold zeros there, as the engine's zero-initialised buffers do); ``code_grad`` and
+    ``weight_grads`` take it too.
     """
     G, n, d = w.shape
     B = c_out.shape[1]
@@ -167,7 +174,7 @@ def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=No
     epi = EPI_ENC_ACT if act != ACT_RELU else (EPI_ENC_CNT if colpart is not None else EPI_ENC)
     _launch(epi, 3, B, n, d, 0, G, a, b, [c_out], [1.0], n, B * n,
             bias=bias, sbias=n, nactive=nactive, part=part, colpart=colpart, cmask=mask_out, act=act,
-            ascale=ascale, cmask2=mask2_out)
+            ascale=ascale, cmask2=mask2_out, nact_host=live_host if nactive is not None else None)
 
 
 def decode_residual(c, w_hat, x, r_out, part, rcol=None, nactive=None):
@@ -195,7 +202,7 @@ def decode_residual(c, w_hat, x, r_out, part, rcol=None, nactive=None):
 
 
 def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, mask=None, act=ACT_RELU,
-              ascale=None, mask2=None, nactive=None):
+              ascale=None, mask2=None, nactive=None, live_host=None):
     """dpre_s[g] = 1[c>0] * (r[g] @ w_hat[g]^T + l1[g] * d / 2).
 
     dpre_s is the code gradient in units of the residual: dL/dpre = 2/(B d) * dpre_s.
@@ -235,12 +242,14 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, 
                   and tuple(mask2.shape) == code_mask_shape(G, B, n), "mask2 must match the encoder's mask2_out")
         _launch(EPI_DC_ACT, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
                 aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0,
-                dotpart=dotpart, cmask=mask, act=act, ascale=ascale, sbias=n, cmask2=mask2, nactive=nactive)
+                dotpart=dotpart, cmask=mask, act=act, ascale=ascale, sbias=n, cmask2=mask2, nactive=nactive,
+                nact_host=live_host if nactive is not None else None)
         return
     if mask is not None and dotpart is None:
         _need(mask.dtype == torch.int64 and tuple(mask.shape) == code_mask_shape(G, B, n), "mask shape")
         _launch(EPI_DC_MASK, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
-                colpart=colpart, l1=l1, l1_add_scale=d / 2.0, cmask=mask, nactive=nactive)
+                colpart=colpart, l1=l1, l1_add_scale=d / 2.0, cmask=mask, nactive=nactive,
+                nact_host=live_host if nactive is not None else None)
         return
     _launch(EPI_DC, 3, B, n, d, 0, G, a, b, [dpre_out], [1.0], n, B * n,
             aux=c, ldaux=n, saux=B * n, colpart=colpart, l1=l1, l1_add_scale=d / 2.0,
@@ -294,19 +303,22 @@ def sae_forward_rowblock(x, w_enc, w_dec, bias, l1, c_out, r_out, dpre_out, mask
     _lib.check(rc, "sc_sae_rowblock")
 
 
-def wgrad_split(G, n, d, K, nprob):
+def wgrad_split(G, n, d, K, nprob, live=None):
     """Split-K factor for the weight-gradient GEMM: 1 while the 256x256 grid already fills
     the 256 CUs; otherwise the smallest power of two that reaches 256 blocks and keeps
     >= 1024 rows of K per split (few models on a large gathered batch, e.g. one model per
     GPU with ensemble sharding at N = 8)."""
-    tiles = nprob * G * max(1, n // 256) * max(1, d // 256)
+    if live is not None:  # masked ensembles launch only their live row tiles
+        tiles = nprob * sum(min(max(1, n // 256), max(1, -(-int(s) // 256))) for s in live) * max(1, d // 256)
+    else:
+        tiles = nprob * G * max(1, n // 256) * max(1, d // 256)
     s = 1
     while tiles * s < 256 and K // (2 * s) >= 1024 and K % (2 * s * 64) == 0:
         s *= 2
     return s
 
 
-def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None):
+def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None, live_host=None):
     """out_i[g] = alpha * sum_segments A_s[g]^T @ B_s[g]   (reduction over batch rows).
 
     pairs: list (one per problem, 1 or 2 problems) of lists of (A, B) segments
@@ -347,9 +359,10 @@ def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None):
     if ksplit > 1:
         cfg = 3 if shape_fits(3, n, d) else 1
     # nactive (masked ensembles): gradient rows past a model's live size are zero -- those tiles
-    # skip their MFMAs and only write the zeros
+    # skip their MFMAs and only write the zeros; with live_host they are not launched at all
     _launch(EPI_F32 if odt == torch.float32 else EPI_BF16, 0, n, d, K1, K2, G, a_ops, b_ops, list(outs),
-            [alpha] * len(outs), d, n * d, cfg=cfg, ksplit=ksplit, split_stride=G * n * d, nact_m=nactive)
+            [alpha] * len(outs), d, n * d, cfg=cfg, ksplit=ksplit, split_stride=G * n * d, nact_m=nactive,
+            nact_host=live_host if nactive is not None else None)
 
 
 def rowmax_nt(a, b, alpha=1.0, cfg=None):
