@@ -77,9 +77,10 @@ def parse(argv=None):
                          "'dp' = data parallel with chunk-pipelined RCCL gradient all-reduce; 'zero1' = data "
                          "parallel with reduce-scatter, row-sharded Adam and a bf16 shadow all-gather; "
                          "auto = es when models %% N == 0")
-    ap.add_argument("--dp-chunks", type=int, default=2,
-                    help="N>1: split the ensemble into this many model chunks whose gradient all-reduce "
-                         "overlaps the next chunk's compute (1 = one reduction per step)")
+    ap.add_argument("--dp-chunks", type=int, default=None,
+                    help="dp / zero1: split the ensemble into this many model chunks whose gradient all-reduce "
+                         "overlaps the next chunk's compute (1 = one reduction per step; default 2, or 1 on "
+                         "one rank, where there is no communication to hide)")
     ap.add_argument("--dist-backend", choices=["auto", "nccl", "gloo"], default="auto",
                     help="auto = RCCL ('nccl') on GPUs; gloo only for rehearsals")
     ap.add_argument("--shared-gpu", action="store_true",
@@ -245,6 +246,8 @@ def main(argv=None):
 
     grad_dtype = torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32
     distributed = info.world_size > 1 or args.force_dist
+    if args.dp_chunks is None:
+        args.dp_chunks = 2 if info.world_size > 1 else 1
     par = args.parallelism
     if par == "auto":
         # N > 1: ensemble-axis sharding (per model identical to data parallel on the global batch;

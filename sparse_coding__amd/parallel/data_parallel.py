@@ -279,7 +279,7 @@ class ChunkedDataParallel:
                 c.after_param_sync()
 
     def _reduce_async(self, flat):
-        if not dist.is_initialized():
+        if not dist.is_initialized() or self.info.world_size <= 1:  # one rank: the sum is the gradient
             return None, flat
         if self.grad_dtype == torch.float32 or flat.dtype == self.grad_dtype:
             return dist.all_reduce(flat, async_op=True), flat

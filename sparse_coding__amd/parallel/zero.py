@@ -145,10 +145,17 @@ class ZeroFusedChunk:
         self.lo, self.hi = shard_range(G * n, info.rank, info.world_size)
         rows = self.hi - self.lo
         dev = e.device
+        # one rank: every collective is an identity, so the shard IS the whole gradient (views,
+        # no reduce-scatter / all-gather / copies)
+        self._solo = info.world_size <= 1
         # reduce-scatter targets: the owned rows' summed gradients (fp32 for Adam)
-        self.g_dec_shard = torch.empty(rows, d, device=dev)
-        self.g_enc_shard = torch.empty(rows, d, device=dev) if kind == "untied" else None
-        self._lowp = grad_dtype != torch.float32
+        if self._solo:
+            self.g_dec_shard = e.g_dec.view(G * n, d)
+            self.g_enc_shard = e.g_enc.view(G * n, d) if kind == "untied" else None
+        else:
+            self.g_dec_shard = torch.empty(rows, d, device=dev)
+            self.g_enc_shard = torch.empty(rows, d, device=dev) if kind == "untied" else None
+        self._lowp = grad_dtype != torch.float32 and not self._solo
         if self._lowp:  # reduce in bf16, widen the owned shard afterwards
             self._rs_in = [torch.empty(G * n * d, device=dev, dtype=grad_dtype) for _ in range(2 if kind == "untied" else 1)]
             self._rs_out = [torch.empty(rows * d, device=dev, dtype=grad_dtype) for _ in self._rs_in]
@@ -199,6 +206,8 @@ class ZeroFusedChunk:
         loss-side extras); returns a _Pending whose completion means the shards are ready."""
         e = self.engine
         pend = _Pending()
+        if self._solo:
+            return pend
         G, n, d = e.n_models, e.n, e.d
         srcs = [e.g_dec] + ([e.g_enc] if e.kind == "untied" else [])
         dsts = [self.g_dec_shard] + ([self.g_enc_shard] if e.kind == "untied" else [])
@@ -246,6 +255,8 @@ class ZeroFusedChunk:
                            row0=lo, live=e.nactive)
 
     def _issue_gathers(self):
+        if self._solo:
+            return
         e = self.engine
         G, n, d = e.n_models, e.n, e.d
         lo, hi = self.lo, self.hi
@@ -260,6 +271,8 @@ class ZeroFusedChunk:
         """All-gather the fp32 masters and moments (exports / checkpoints): afterwards every
         rank holds the complete, current optimizer state."""
         self._ag.wait()
+        if self._solo:
+            return
         e = self.engine
         G, n, d = e.n_models, e.n, e.d
         lo, hi = self.lo, self.hi
