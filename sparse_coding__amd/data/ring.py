@@ -107,11 +107,52 @@ class DeviceRing:
             rows = self.buf.index_select(0, idx) if out is None else torch.index_select(self.buf, 0, idx, out=out)
         return (rows, idx) if return_index else rows
 
+    def graph_source(self, batch_size: int) -> "RingGraphSource":
+        """A batch source whose fetch can run INSIDE a training engine's HIP graph (see
+        ``RingGraphSource``); it walks this ring's permutations like ``sample``."""
+        return RingGraphSource(self, batch_size)
+
     def batches_per_epoch(self, batch_size: int) -> int:
         return self.size // batch_size
 
     def view(self) -> torch.Tensor:
         return self.buf[: self.size]
+
+
+class RingGraphSource:
+    """In-graph batch fetch from a ``DeviceRing`` (single process).
+
+    Step t of an engine reads rows ``perm[(t - ep0) * B : (t - ep0 + 1) * B]`` of a permutation kept
+    in a persistent device buffer; t is the engine's device step counter (advanced inside the
+    captured step), ep0 a device scalar.  Between replays ``prepare(t)`` rolls a fresh permutation
+    into the same buffer (and sets ep0 = t) when the epoch is exhausted -- the same
+    without-replacement epochs as ``DeviceRing.sample``.  The fetch itself is one gather kernel
+    that is part of the step's graph, so no plain launch sits between graph replays."""
+
+    def __init__(self, ring: DeviceRing, batch_size: int):
+        if ring.size < batch_size:
+            raise ValueError("ring holds fewer rows than one batch")
+        self.ring, self.B = ring, int(batch_size)
+        dev = ring.device
+        self.perm = torch.empty(ring.size, device=dev, dtype=torch.int64)
+        self.ep0 = torch.zeros(1, device=dev, dtype=torch.int32)
+        self._ep0_host = None  # step at which the current permutation started
+
+    def prepare(self, step: int, steps: int = 1):
+        """Host bookkeeping before replaying steps ``step .. step + steps - 1``: a new permutation
+        when they would run past the current one (a multi-step replay may start the next epoch
+        up to ``steps - 1`` batches early: every epoch is still a without-replacement pass)."""
+        if self._ep0_host is None or (step - self._ep0_host + steps) * self.B > self.perm.numel():
+            self.perm.copy_(torch.randperm(self.ring.size, device=self.ring.device, generator=self.ring.gen))
+            self.ep0.fill_(int(step))
+            self._ep0_host = int(step)
+            self.ring.epoch += 1
+
+    def gather(self, out: torch.Tensor, step_dev: torch.Tensor):
+        """The capturable fetch: ``out`` [B, ...] <- this step's rows."""
+        from ..ops.rows import gather_rows_perm
+
+        return gather_rows_perm(self.ring.buf, self.perm, step_dev, self.ep0, out)
 
 
 def _kernels_available() -> bool:

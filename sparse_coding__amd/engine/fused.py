@@ -99,6 +99,7 @@ class FusedSAEEnsemble:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # completed Adam steps
         self.use_graph = False
         self._graph = None
+        self._source = None  # in-graph batch source (attach_source)
         self._counted = False
 
         # ----- parameters (fp32 masters) and Adam state
@@ -556,6 +557,47 @@ class FusedSAEEnsemble:
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     self._step_kernels(xin, count)
                 self._graph[(count, i)] = g
+
+    def attach_source(self, source):
+        """Fetch each step's batch INSIDE the captured graph from ``source`` (e.g.
+        ``DeviceRing.graph_source(batch_size)``, indexed by the device step counter); then call
+        ``step_source()`` per step.  Removes the plain gather launch between graph replays
+        (an ~9 us idle gap per step on MI355X, profiles/README.md)."""
+        self._source = source
+        self._graph = None
+        return self
+
+    def _counting_at(self, t: int) -> bool:
+        return self.track_feature_counts and (t % self.count_every == 0)
+
+    def step_source(self, steps: int = 1):
+        """``steps`` optimizer steps, each on the next batch of the attached source, as ONE graph
+        replay (each step: batch gather + the step's kernels; the device step counter indexes the
+        batches).  Consecutive graph replays are separated by a ~9 us idle gap on MI355X, so a
+        multi-step graph pays it once per ``steps`` steps.  Graphs are captured per pattern of
+        feature-counting steps (usually one pattern: ``steps`` divides ``count_every``)."""
+        if self._source is None:
+            raise RuntimeError("attach_source() first")
+        if self._graph is None:
+            self._capture()
+        t = self.step_count
+        pattern = tuple(self._counting_at(t + s) for s in range(int(steps)))
+        self._source.prepare(t, len(pattern))
+        key = ("src", pattern)
+        g = self._graph.get(key)
+        if g is None:
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for count in pattern:
+                    self._source.gather(self.x_static, self.step_dev)  # the step's first kernel
+                    self._step_kernels(self.x_static, count)
+            self._graph[key] = g
+        g.replay()
+        for count in pattern:
+            self._counted = count
+            self._host_step()
+        return self.out
 
     def step_static(self, which: int = 0):
         """Replay the captured step on whatever is in ``x_static`` (fill it first, e.g. with

@@ -69,6 +69,8 @@ def signatures():
                      c_void_p, c_int],
         "sc_center_rows": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
         "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_void_p],
+        "sc_gather_rows_perm": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_long, c_long,
+                                c_void_p],
         "sc_lista_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                          c_int, c_void_p],
         "sc_lista_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

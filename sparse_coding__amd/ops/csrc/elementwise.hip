@@ -128,6 +128,26 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const u32x4_t* __restr
   for (int v = lane; v < row_vec; v += 64) o[v] = s[v];
 }
 
+// gather_rows_perm_kernel: the same fetch with the indices taken from a ring permutation at a
+//   DEVICE cursor, (step - epoch_start) * rows, so the batch fetch can live inside the step's
+//   HIP graph (the engine's device step counter advances in the graph; the host only rolls a
+//   new permutation between replays at epoch ends).  Out-of-range positions read row 0.
+__global__ __launch_bounds__(256) void gather_rows_perm_kernel(const u32x4_t* __restrict__ buf, long nbuf,
+                                                               const long* __restrict__ perm, long nperm,
+                                                               const int* __restrict__ step,
+                                                               const int* __restrict__ ep0,
+                                                               u32x4_t* __restrict__ out, long rows, int row_vec) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const long j = (long)(step[0] - ep0[0]) * rows + r;
+  long src = (j >= 0 && j < nperm) ? perm[j] : 0;
+  src = (src >= 0 && src < nbuf) ? src : 0;
+  const u32x4_t* s = buf + src * row_vec;
+  u32x4_t* o = out + r * row_vec;
+  for (int v = lane; v < row_vec; v += 64) o[v] = s[v];
+}
+
 }  // namespace scamd
 
 using namespace scamd;
@@ -169,6 +189,16 @@ int sc_gather_rows(const void* buf, const long* idx, void* out, long rows, long 
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
                      reinterpret_cast<const u32x4_t*>(buf), idx, reinterpret_cast<u32x4_t*>(out), rows,
                      (int)(row_bytes / 16));
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_gather_rows_perm(const void* buf, long nbuf, const long* perm, long nperm, const int* step, const int* ep0,
+                        void* out, long rows, long row_bytes, hipStream_t stream) {
+  if (row_bytes % 16 || rows < 0 || nbuf < 1) return 1;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(gather_rows_perm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
+                     reinterpret_cast<const u32x4_t*>(buf), nbuf, perm, nperm, step, ep0,
+                     reinterpret_cast<u32x4_t*>(out), rows, (int)(row_bytes / 16));
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -27,3 +27,24 @@ def gather_rows(buf: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None =
                                    _lib.stream_handle())
     _lib.check(rc, "sc_gather_rows")
     return out
+
+
+def gather_rows_perm(buf: torch.Tensor, perm: torch.Tensor, step: torch.Tensor, ep0: torch.Tensor,
+                     out: torch.Tensor) -> torch.Tensor:
+    """out[i] = buf[perm[(step - ep0) * rows + i]] with ``step`` / ``ep0`` int32 [1] DEVICE scalars, so
+    the fetch can be captured in a HIP graph and still walk the permutation (rows = out.shape[0]).
+    Positions past ``perm`` (a host bookkeeping error) read row 0 instead of faulting."""
+    if not (buf.is_cuda and buf.is_contiguous() and out.is_contiguous()):
+        raise ValueError("gather_rows_perm needs contiguous GPU buffers")
+    row_bytes = buf[0].numel() * buf.element_size()
+    if row_bytes % 16 or tuple(out.shape[1:]) != tuple(buf.shape[1:]) or out.dtype != buf.dtype:
+        raise ValueError("out rows must match buf rows (16-byte multiples)")
+    if perm.dtype != torch.int64 or not perm.is_contiguous():
+        raise ValueError("perm must be contiguous int64")
+    for t in (step, ep0):
+        if t.dtype != torch.int32 or t.numel() < 1 or t.device != buf.device:
+            raise ValueError("step / ep0 must be int32 device scalars")
+    rc = _lib.lib().sc_gather_rows_perm(_lib.ptr(buf), buf.shape[0], _lib.ptr(perm), perm.numel(), _lib.ptr(step),
+                                        _lib.ptr(ep0), _lib.ptr(out), out.shape[0], row_bytes, _lib.stream_handle())
+    _lib.check(rc, "sc_gather_rows_perm")
+    return out

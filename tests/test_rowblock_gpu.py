@@ -140,3 +140,70 @@ def test_rowblock_graph_replay_matches_eager():
     for k in eager.params:
         torch.testing.assert_close(graph.params[k], eager.params[k], rtol=0, atol=0)
     torch.testing.assert_close(graph.out, eager.out, rtol=0, atol=0)
+
+
+def test_in_graph_ring_source_matches_host_sampling():
+    """Batch fetch inside the step's HIP graph (DeviceRing.graph_source, indexed by the device
+    step counter) == host-driven sampling + graph replay, across permutation (epoch) rollovers."""
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+
+    torch.manual_seed(9)
+    d, n, B = 512, 1024, 256
+    rows = (torch.randn(B * 7 // 2, d, device=DEV) * 2).to(torch.bfloat16)  # 3.5 batches: 3-step epochs
+    rings = []
+    for _ in range(2):
+        r = DeviceRing(rows.shape[0], d, device=DEV, seed=5)
+        r.push(rows)
+        rings.append(r)
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3)]
+    a = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    a.attach_source(rings[0].graph_source(B))
+    b = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    for _ in range(8):
+        a.step_source()
+        rings[1].sample_shard(B, 0, 1, out=b.x_static)
+        b.step_static()
+    torch.cuda.synchronize()
+    assert rings[0].epoch == rings[1].epoch >= 3
+    torch.testing.assert_close(a.x_static, b.x_static, rtol=0, atol=0)
+    for k in a.params:
+        torch.testing.assert_close(a.params[k], b.params[k], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("group", [8, 3])
+def test_multi_step_graph_replay_matches_single_steps(group):
+    """``step_source(k)``: k optimizer steps (batch gathers included) in ONE graph replay equal k
+    single-step replays on host-sampled batches: parameters, losses, feature counts."""
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+
+    torch.manual_seed(10)
+    d, n, B, steps = 512, 1024, 256, 16
+    rows = (torch.randn(B * 40, d, device=DEV) * 2).to(torch.bfloat16)
+    rings = []
+    for _ in range(2):
+        r = DeviceRing(rows.shape[0], d, device=DEV, seed=3)
+        r.push(rows)
+        rings.append(r)
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3, 1e-2)]
+    a = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    a.attach_source(rings[0].graph_source(B))
+    b = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    done = 0
+    while done < steps:
+        k = min(group, steps - done)
+        a.step_source(k)
+        done += k
+    for _ in range(steps):
+        rings[1].sample_shard(B, 0, 1, out=b.x_static)
+        b.step_static()
+    torch.cuda.synchronize()
+    assert a.step_count == b.step_count == steps and int(a.step_dev.item()) == steps
+    for k in a.params:
+        torch.testing.assert_close(a.params[k], b.params[k], rtol=0, atol=0)
+    torch.testing.assert_close(a.out, b.out, rtol=0, atol=0)
+    torch.testing.assert_close(a.feature_counts, b.feature_counts, rtol=0, atol=0)
+    assert a.rows_seen == b.rows_seen
