@@ -128,8 +128,9 @@ constexpr int stage_bytes() { return STAGE_OFF + S::NW * STAGE_WAVE; }
 
 template <class S, int EPI, bool AUX_EARLY, bool STAGE = false, bool FSTAGE = false>
 __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)[S::WI][S::WJ],
-                                             const uint2 (&auxv)[S::WI][S::WJ], float* red, int pi, int g, int m0,
-                                             int n0, int tn, int tiles_n, void* cptr, float alpha, bool dead = false) {
+                                             const uint2 (&auxv)[S::WI][S::WJ], const f32x4_t (&biasv)[S::WJ],
+                                             float* red, int pi, int g, int m0, int n0, int tn, int tiles_n,
+                                             void* cptr, float alpha, bool dead = false) {
   constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
   constexpr bool ENC = (EPI == EPI_ENC || EPI == EPI_ENC_CNT || EPI == EPI_ENC_ACT);
   constexpr int RED_SUM = 2 * S::WGM * BN;  // block_sum scratch after the two column-sum regions
@@ -325,7 +326,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
       const int col = colb + j * 16;
-      const f32x4_t bj = *reinterpret_cast<const f32x4_t*>(bias + col);
+      const f32x4_t bj = ACTV ? *reinterpret_cast<const f32x4_t*>(bias + col) : biasv[j];  // (ReLU: loaded before the K loop)
       f32x4_t s2 = f32x4_t{1.f, 1.f, 1.f, 1.f}, is2 = s2;
       if (ACTV && act == 2) {
         s2 = *reinterpret_cast<const f32x4_t*>(p.ascale + (long)g * p.sbias + col);
@@ -734,6 +735,15 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
         auxv[i][j] = *reinterpret_cast<const uint2*>(X + (long)(rowb + i * 16) * p.ldaux + colb + j * 16);
   }
 
+  // The ReLU encoder epilogue's bias: loaded here, before the K-loop prologue issues its DMAs (so
+  // the counted vmcnt waits below still see only tile DMAs as younger), its latency hidden.
+  f32x4_t biasv[WJ];
+  if constexpr (EPI == EPI_ENC || EPI == EPI_ENC_CNT) {
+    const float* bias = p.bias + (long)g * p.sbias;
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) biasv[j] = *reinterpret_cast<const f32x4_t*>(bias + colb + j * 16);
+  }
+
   if (!dead) {  // ---------------------------------------------------------------- K loop
 #pragma unroll
   for (int t = 0; t < NST - 1; ++t)
@@ -871,8 +881,8 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
   lds_barrier();  // all reads of the ring done before smem is reused below
   constexpr bool STAGE = S::WI == 4 && S::WJ == 4 && NST * STG >= stage_bytes<S>();
   constexpr bool FSTAGE = EPI == EPI_F32 && S::WJ == 4 && NST * STG >= S::NW * S::WI * 16 * STAGE_ROW;
-  sae_epilogue<S, EPI, AUX_EARLY, STAGE, FSTAGE>(p, acc, auxv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn, tiles_n,
-                                         cptr, alpha, dead);
+  sae_epilogue<S, EPI, AUX_EARLY, STAGE, FSTAGE>(p, acc, auxv, biasv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn,
+                                                 tiles_n, cptr, alpha, dead);
   SC_STAMP(3);
 }
 
