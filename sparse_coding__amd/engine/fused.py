@@ -567,23 +567,12 @@ class FusedSAEEnsemble:
         self._graph = None
         return self
 
-    def _counting_at(self, t: int) -> bool:
-        return self.track_feature_counts and (t % self.count_every == 0)
-
-    def step_source(self, steps: int = 1):
-        """``steps`` optimizer steps, each on the next batch of the attached source, as ONE graph
-        replay (each step: batch gather + the step's kernels; the device step counter indexes the
-        batches).  Consecutive graph replays are separated by a ~9 us idle gap on MI355X, so a
-        multi-step graph pays it once per ``steps`` steps.  Graphs are captured per pattern of
-        feature-counting steps (usually one pattern: ``steps`` divides ``count_every``)."""
+    def _source_graph(self, pattern):
         if self._source is None:
             raise RuntimeError("attach_source() first")
         if self._graph is None:
             self._capture()
-        t = self.step_count
-        pattern = tuple(self._counting_at(t + s) for s in range(int(steps)))
-        self._source.prepare(t, len(pattern))
-        key = ("src", pattern)
+        key = ("src", tuple(pattern))
         g = self._graph.get(key)
         if g is None:
             torch.cuda.synchronize(self.device)
@@ -593,7 +582,30 @@ class FusedSAEEnsemble:
                     self._source.gather(self.x_static, self.step_dev)  # the step's first kernel
                     self._step_kernels(self.x_static, count)
             self._graph[key] = g
-        g.replay()
+        return g
+
+    def prime_source(self, steps: int):
+        """Capture (without running anything) every graph that ``step_source(steps)`` groups
+        starting at the current step, and single-step remainders, will replay -- so no capture
+        happens later inside a timed region."""
+        t = self.step_count
+        self._source_graph(tuple(self._counting_at(t + s) for s in range(int(steps))))
+        for count in (True, False):
+            self._source_graph((count,))
+
+    def _counting_at(self, t: int) -> bool:
+        return self.track_feature_counts and (t % self.count_every == 0)
+
+    def step_source(self, steps: int = 1):
+        """``steps`` optimizer steps, each on the next batch of the attached source, as ONE graph
+        replay (each step: batch gather + the step's kernels; the device step counter indexes the
+        batches).  Consecutive graph replays are separated by a ~9 us idle gap on MI355X, so a
+        multi-step graph pays it once per ``steps`` steps.  Graphs are captured per pattern of
+        feature-counting steps (usually one pattern: ``steps`` divides ``count_every``)."""
+        t = self.step_count
+        pattern = tuple(self._counting_at(t + s) for s in range(int(steps)))
+        self._source.prepare(t, len(pattern))
+        self._source_graph(pattern).replay()
         for count in pattern:
             self._counted = count
             self._host_step()

@@ -207,3 +207,33 @@ def test_multi_step_graph_replay_matches_single_steps(group):
     torch.testing.assert_close(a.out, b.out, rtol=0, atol=0)
     torch.testing.assert_close(a.feature_counts, b.feature_counts, rtol=0, atol=0)
     assert a.rows_seen == b.rows_seen
+
+
+def test_prime_source_captures_without_running():
+    """``prime_source`` captures the group / single-step graphs at the current step without
+    executing any step (parameters and counters unchanged); later replays reuse them."""
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+
+    torch.manual_seed(12)
+    d, n, B = 512, 512, 256
+    ring = DeviceRing(B * 20, d, device=DEV, seed=1)
+    ring.push((torch.randn(B * 20, d, device=DEV)).to(torch.bfloat16))
+    models = [FunctionalSAE.init(d, n, 1e-3, device=DEV)]
+    e = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    e.attach_source(ring.graph_source(B))
+    e.step_source(1)
+    e.step_source(1)
+    torch.cuda.synchronize()
+    before = {k: v.clone() for k, v in e.params.items()}
+    e.prime_source(8)
+    torch.cuda.synchronize()
+    n_graphs = len(e._graph)
+    assert e.step_count == 2 and int(e.step_dev.item()) == 2
+    for k in before:
+        assert torch.equal(before[k], e.params[k])
+    e.step_source(8)
+    e.step_source(1)
+    torch.cuda.synchronize()
+    assert len(e._graph) == n_graphs and e.step_count == 11 and int(e.step_dev.item()) == 11
