@@ -1,4 +1,6 @@
-"""Headline benchmark: activations/sec of a Pythia-70m residual-stream SAE ensemble.
+"""ROUND-3 HARNESS, kept for A/B against bench.py (graph capture after warmup, 8+8+1+1+1+1 tiling).
+
+Headline benchmark: activations/sec of a Pythia-70m residual-stream SAE ensemble.
 
 BASELINE.json config 2/3: an 8-way L1 sweep (l1 = logspace(-4, -2, 8)) of untied
 SAEs on d_model = 512 activations with dict_ratio 4 (n = 2048), bf16 MFMA compute
@@ -36,6 +38,9 @@ import time
 
 import numpy as np
 import torch
+
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 
 # the reference's untied 8-model d=512 n=2048 step (its own math,
 # vmap(grad)+Adam) -- the only measured throughput for this exact config (no GPU number
@@ -93,6 +98,8 @@ def parse(argv=None):
                     help="N>1: after the headline run, also time the other strategy (es <-> dp) and report it "
                          "under alt_parallelism")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of HIP graphs")
+    ap.add_argument("--rowblock", action="store_true",
+                    help="single-GPU fused engine: encoder/decoder/code gradient as one row-block kernel")
     return ap.parse_args(argv)
 
 
@@ -117,32 +124,21 @@ def fvu_l0(dicts, x):
     return [(float(mean_l0(ld, x)), float(fraction_variance_unexplained(ld, x))) for ld in dicts]
 
 
-# single-GPU fused step: at most this many optimizer steps per HIP graph replay (each replay
-# boundary costs an ~9 us idle gap on MI355X); engine/graph_plan.py picks the group size so that
-# the warmup replays every graph the timed region replays
+# single-GPU fused step: optimizer steps per HIP graph replay (each replay boundary costs an
+# ~9 us idle gap on MI355X; 8 = the feature-count sampling period, so one graph pattern)
 GRAPH_STEPS = 8
 
 
 class Runner:
-    """One training configuration.
+    """One training configuration: ``step()`` (one full optimizer step on a fresh device batch),
+    ``finish()`` (complete cross-step work), ``dicts()`` (LearnedDicts), ``close()``."""
 
-    ``setup(tiling)``: capture (and upload) every graph the run will replay -- before warmup;
-    ``run(groups)``: one full optimizer step per entry of ``sum(groups)``, replayed as one graph per
-    group where the runner has graphs; ``finish()``: complete cross-step work in flight;
-    ``dicts()``: LearnedDicts; ``close()``."""
-
-    def __init__(self, step, dicts, finish=None, close=None, run=None, setup=None):
+    def __init__(self, step, dicts, finish=None, close=None, prime=None):
         self.step, self.dicts = step, dicts
         self.finish = finish or (lambda: None)
         self.close = close or (lambda: None)
-        self._run = run
-        self.setup = setup or (lambda tiling: None)
-
-    def run(self, groups):
-        if self._run is not None:
-            return self._run(groups)
-        for _ in range(sum(groups)):
-            self.step()
+        # prime(): capture every graph the timed steps will replay (no work runs), untimed
+        self.prime = prime or (lambda: None)
 
 
 def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
@@ -152,32 +148,17 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.parallel.ensemble_shard import EnsembleSharded
 
-        from sparse_coding__amd.engine.graph_plan import count_pattern
-
         es = EnsembleSharded(models, lambda m, bs: FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=bs, device=device),
                              info, batch_per_rank=B, d=args.d)
+        if not args.no_graph:
+            es.enable_graph()
         metas = [b for _, b in models]
 
         def sample(out):
             return ring.sample_shard(B, info.rank, info.world_size, out=out)
 
-        def dicts():
-            return es.to_learned_dicts(metas, sig, device)
-
-        if args.no_graph:
-            return Runner(lambda: es.step_sampled(sample), dicts, close=es.flush)
-
-        def sample_steps(out, s):  # this rank's rows of the next s steps, one gather kernel
-            return ring.sample_shard_steps(B, info.rank, info.world_size, s, out)
-
-        def pattern(s):
-            return count_pattern(s, GRAPH_STEPS)
-
-        # multi-step groups: per group one local-row gather, s batch all-gathers (RCCL stream, issued
-        # under the previous group's replay) and ONE HIP graph replay of the s steps
-        return Runner(lambda: es.run_groups([1], sample_steps, pattern), dicts, close=es.flush,
-                      run=lambda groups: es.run_groups(groups, sample_steps, pattern),
-                      setup=lambda tiling: es.prime_groups(tiling.sizes, pattern))
+        return Runner(lambda: es.step_sampled(sample), lambda: es.to_learned_dicts(metas, sig, device),
+                      close=es.flush)
     if args.engine == "fused" and distributed:
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
@@ -206,27 +187,38 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
     if args.engine == "fused":
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
 
-        from sparse_coding__amd.engine.graph_plan import count_pattern
-
         eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
-        if args.no_graph:
-            def step():
+        if not args.no_graph:
+            # every step (ring batch gather included) runs from HIP graphs of GRAPH_STEPS steps:
+            # step() queues a step, a full group replays as one graph, finish() (inside the timed
+            # region) runs the remainder -- so exactly the requested steps execute, once each
+            eng.enable_graph().attach_source(ring.graph_source(B))
+        queued = [0]
+
+        def step():
+            if args.no_graph:
                 ring.sample_shard(B, 0, 1, out=eng.x_static)
                 eng.step_batch(eng.x_static)
+                return
+            queued[0] += 1
+            if queued[0] == GRAPH_STEPS:
+                eng.step_source(GRAPH_STEPS)
+                queued[0] = 0
 
-            return Runner(step, lambda: eng.to_learned_dicts(device))
-        # every step (ring batch gather included) runs from HIP graphs of up to GRAPH_STEPS steps;
-        # feature counts are sampled on the first step of each replay (every <= 8 steps)
-        eng.enable_graph().attach_source(ring.graph_source(B))
+        def finish():
+            while queued[0]:
+                eng.step_source(1)
+                queued[0] -= 1
 
-        def run(groups):
-            for s in groups:
-                eng.step_source(s, count_pattern(s, GRAPH_STEPS))
+        def dicts():
+            finish()
+            return eng.to_learned_dicts(device)
 
-        def setup(tiling):
-            eng.prime_source(patterns=[count_pattern(s, GRAPH_STEPS) for s in tiling.sizes])
+        def prime():
+            if not args.no_graph:
+                eng.prime_source(GRAPH_STEPS)
 
-        return Runner(lambda: run([1]), lambda: eng.to_learned_dicts(device), run=run, setup=setup)
+        return Runner(step, dicts, finish=finish, prime=prime)
     from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
     from sparse_coding__amd.engine.optim import adam
     from sparse_coding__amd.parallel.data_parallel import DataParallelEnsemble
@@ -250,33 +242,20 @@ def comm_bytes(mode, args, world):
                                batch_bytes=args.batch * args.d * 2)
 
 
-def timed(runner, groups, info, B):
-    """Exactly ``sum(groups)`` steps between barrier + synchronize on both sides; max over ranks."""
+def timed(runner, steps, info, B):
+    """Exactly ``steps`` steps between barrier + synchronize on both sides; max over ranks."""
     from sparse_coding__amd.parallel.dist import all_reduce_max, barrier
 
-    steps = sum(groups)
     barrier(info)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    runner.run(groups)
+    for _ in range(steps):
+        runner.step()
     runner.finish()  # work the last timed step still has in flight (cross-step pipelining)
     torch.cuda.synchronize()
     barrier(info)
     elapsed = all_reduce_max(time.perf_counter() - t0, info)
     return 1e3 * elapsed / steps, B * info.world_size * steps / elapsed
-
-
-def warm_and_time(runner, args, info, B):
-    """Capture every graph first, run the warmup through those same graphs (the last warmup replay
-    is a timed-size group), then time exactly ``args.steps`` steps (engine/graph_plan.py)."""
-    from sparse_coding__amd.engine.graph_plan import tile
-
-    tiling = tile(args.steps, args.warmup, GRAPH_STEPS)
-    runner.setup(tiling)
-    runner.run(list(tiling.warm))
-    runner.finish()  # no warmup work may spill into the timed region
-    ms, value = timed(runner, list(tiling.timed), info, B)
-    return ms, value, tiling
 
 
 def main(argv=None):
@@ -314,16 +293,18 @@ def main(argv=None):
         raise SystemExit(f"--parallelism es needs models % N == 0 ({args.models} models, N={info.world_size})")
 
     runner = make_runner(par, args, info, sig, models, ring, device, grad_dtype)
-    ms, value, tiling = warm_and_time(runner, args, info, B)
+    for _ in range(args.warmup):
+        runner.step()
+    runner.finish()  # no warmup work may spill into the timed region
+    runner.prime()   # nor any graph capture
+    ms, value = timed(runner, args.steps, info, B)
 
     quality = None
     trained = args.warmup + args.steps
     if not args.no_eval:
-        if trained < args.quality_steps:  # untimed: train on toward convergence before evaluating
-            from sparse_coding__amd.engine.graph_plan import chunks
-
-            runner.run(chunks(args.quality_steps - trained, tiling.group))
-            trained = args.quality_steps
+        while trained < args.quality_steps:  # untimed: train on toward convergence before evaluating
+            runner.step()
+            trained += 1
         runner.finish()
         torch.cuda.synchronize()
         lds = runner.dicts()  # collective in the sharded mode: every rank takes part
@@ -339,7 +320,11 @@ def main(argv=None):
         other = "dp" if par in ("es", "zero1") else "es"
         alt_models = [sig.init(args.d, n, float(l1), device=device) for l1 in l1s]
         alt_runner = make_runner(other, args, info, sig, alt_models, ring, device, grad_dtype)
-        a_ms, a_value, _ = warm_and_time(alt_runner, args, info, B)
+        for _ in range(args.warmup):
+            alt_runner.step()
+        alt_runner.finish()
+        alt_runner.prime()
+        a_ms, a_value = timed(alt_runner, args.steps, info, B)
         alt_runner.close()
         alt = {"parallelism": f"{other}{info.world_size}", "value": round(a_value, 1), "ms_per_step": round(a_ms, 4),
                "dp_chunks": args.dp_chunks if other == "dp" else None,
@@ -379,11 +364,6 @@ def main(argv=None):
                              "1.86k act/s, 8-vCPU sandbox); no published GPU throughput exists.  "
                              "vs_eager_same_box divides by this repo's PyTorch-eager vmap(grad)+Adam "
                              "engine on the same MI355X (profiles/bench_eager_r2.json)",
-            # how the steps were cut into HIP graph replays: all graphs captured + uploaded before
-            # warmup; the warmup replays every graph the timed region replays (engine/graph_plan.py)
-            "graph_replays": {"timed": list(tiling.timed), "warmup": list(tiling.warm),
-                              "warm_covered": tiling.covered} if par == "dp" and not distributed
-            and not args.no_graph and args.engine == "fused" else None,
             "vs_eager_same_box": round(value / (EAGER_SAME_BOX_ACT_PER_S * info.world_size), 2)
             if EAGER_SAME_BOX_ACT_PER_S and args.engine == "fused" and args.d == 512 and args.ratio == 4
             and args.models == 8 and B == 2048 else None,

@@ -4,7 +4,7 @@
 #ifndef NO_STAMPS
 #define SC_RB_STAMPS 1
 #endif
-#include "../../sparse_coding__amd/ops/csrc/sae_rowblock.hip"
+#include "sae_rowblock.hip"
 #include <stdio.h>
 #include <string.h>
 #include <vector>

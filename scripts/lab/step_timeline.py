@@ -1,0 +1,49 @@
+"""Per-step timeline of the last N training steps in a rocprofv3 kernel trace.
+
+A step starts at its ring-gather kernel.  Prints per step: wall from its gather to the next
+step's gather, busy time (sum of kernel durations), idle gaps, and per-kernel durations, so a
+short timed region (--steps 20) can be compared with the steady state kernel by kernel.
+Usage: python step_timeline.py TRACE_DIR [N_STEPS]
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def short(name):
+    n = name.split("(")[0]
+    if "sae_gemm_kernel" in n:
+        return "gemm" + name[name.index("Shape"):].split(">")[0][5:] + "," + name.split(">,")[1].split(">")[0]
+    return n.split("::")[-1][-30:]
+
+
+def main():
+    f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
+    nsteps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    rows = [r for r in csv.DictReader(open(f)) if "scamd" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if "gather_rows_perm" in r["Kernel_Name"]]
+    sel = starts[-nsteps:]
+    out = []
+    for k, i0 in enumerate(sel):
+        i1 = sel[k + 1] if k + 1 < len(sel) else len(rows)
+        seg = rows[i0:i1]
+        t0 = int(seg[0]["Start_Timestamp"])
+        t1 = int(rows[i1]["Start_Timestamp"]) if i1 < len(rows) else int(seg[-1]["End_Timestamp"])
+        busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg)
+        kern = collections.OrderedDict()
+        for r in seg:
+            kern[short(r["Kernel_Name"])] = round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000, 1)
+        out.append({"step": k, "wall_us": round((t1 - t0) / 1000, 1), "busy_us": round(busy / 1000, 1),
+                    "kernels": kern})
+    for o in out:
+        print(json.dumps(o))
+    walls = [o["wall_us"] for o in out[:-1]]
+    print(json.dumps({"mean_wall_us": round(sum(walls) / max(1, len(walls)), 1),
+                      "mean_busy_us": round(sum(o["busy_us"] for o in out) / len(out), 1)}))
+
+
+if __name__ == "__main__":
+    main()

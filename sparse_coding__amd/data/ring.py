@@ -107,6 +107,34 @@ class DeviceRing:
             rows = self.buf.index_select(0, idx) if out is None else torch.index_select(self.buf, 0, idx, out=out)
         return (rows, idx) if return_index else rows
 
+    def sample_shard_steps(self, batch_size: int, rank: int, world: int, steps: int, out: torch.Tensor):
+        """This rank's rows of the next ``steps`` data-parallel steps into ``out`` [steps * batch_size, d]
+        in one gather: step s's shard is the same permutation block ``sample_shard`` would return at
+        its s-th call.  When the group would run past the epoch's permutation, a new epoch starts at
+        the group (up to ``steps - 1`` global batches of the old one are skipped -- every epoch is
+        still a without-replacement pass)."""
+        if self.size == 0:
+            raise RuntimeError("ring is empty")
+        steps = int(steps)
+        need = batch_size * world * steps
+        if out.shape[0] != steps * batch_size:
+            raise ValueError(f"out has {out.shape[0]} rows, need {steps * batch_size}")
+        if self._perm is None or self._cursor + need > self._perm.numel():
+            self._new_epoch()
+            if need > self._perm.numel():
+                raise ValueError(f"{steps} steps of {batch_size} x {world} rows exceed the ring ({self.size} rows)")
+        base = self._cursor + rank * batch_size
+        if (self.buf.is_cuda and (self.buf[0].numel() * self.buf.element_size()) % 16 == 0
+                and _kernels_available()):
+            from ..ops.rows import gather_rows_blocks
+
+            gather_rows_blocks(self.buf, self._perm, base, batch_size * world, batch_size, out)
+        else:
+            idx = self._perm[self._cursor:self._cursor + need].view(steps, world, batch_size)[:, rank].reshape(-1)
+            torch.index_select(self.buf, 0, idx, out=out)
+        self._cursor += need
+        return out
+
     def graph_source(self, batch_size: int) -> "RingGraphSource":
         """A batch source whose fetch can run INSIDE a training engine's HIP graph (see
         ``RingGraphSource``); it walks this ring's permutations like ``sample``."""
@@ -134,7 +162,10 @@ class RingGraphSource:
             raise ValueError("ring holds fewer rows than one batch")
         self.ring, self.B = ring, int(batch_size)
         dev = ring.device
-        self.perm = torch.empty(ring.size, device=dev, dtype=torch.int64)
+        # the permutation covers the rows valid at attach time (the captured gather reads this
+        # buffer, so its size is fixed); rows appended later are walked after ``resize()``
+        self.rows = int(ring.size)
+        self.perm = torch.empty(self.rows, device=dev, dtype=torch.int64)
         self.ep0 = torch.zeros(1, device=dev, dtype=torch.int32)
         self._ep0_host = None  # step at which the current permutation started
 
@@ -143,7 +174,7 @@ class RingGraphSource:
         when they would run past the current one (a multi-step replay may start the next epoch
         up to ``steps - 1`` batches early: every epoch is still a without-replacement pass)."""
         if self._ep0_host is None or (step - self._ep0_host + steps) * self.B > self.perm.numel():
-            self.perm.copy_(torch.randperm(self.ring.size, device=self.ring.device, generator=self.ring.gen))
+            self.perm.copy_(torch.randperm(self.rows, device=self.ring.device, generator=self.ring.gen))
             self.ep0.fill_(int(step))
             self._ep0_host = int(step)
             self.ring.epoch += 1

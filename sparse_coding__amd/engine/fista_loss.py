@@ -93,7 +93,7 @@ class FistaLossEnsemble:
 
     def state_dict(self):
         return {"params": {k: v.detach().clone() for k, v in self.params.items()}, "optim": self.opt.state_dict(),
-                "step": self.step_count}
+                "step": self.step_count, "eta": self.eta.state_dict()}
 
     def load_state_dict(self, st):
         with torch.no_grad():
@@ -101,6 +101,8 @@ class FistaLossEnsemble:
                 self.params[k].copy_(v)
         self.opt.load_state_dict(st["optim"])
         self.step_count = int(st["step"])
+        if "eta" in st:
+            self.eta.load_state_dict(st["eta"])
 
 
 class FusedFistaLossEnsemble:
@@ -207,3 +209,13 @@ class FusedFistaLossEnsemble:
         from ..models.learned_dict import TiedSAE
 
         return [TiedSAE(p["encoder"], p["encoder_bias"], norm_encoder=True) for p, _ in self.unstack(device)]
+
+    def state_dict(self):
+        """Masters, Adam moments, step counters (host and device) of the kernel engine, plus this
+        objective's own step count and the warm power-iteration state of the eta tracker."""
+        return {"engine": self.engine.state_dict(), "step": self.step_count, "eta": self.eta.state_dict()}
+
+    def load_state_dict(self, st):
+        self.engine.load_state_dict(st["engine"])  # also rebuilds the bf16 shadows and row norms
+        self.step_count = int(st["step"])
+        self.eta.load_state_dict(st["eta"])

@@ -42,6 +42,14 @@ _ACTS = {"untied": gemm_ops.ACT_RELU, "tied": gemm_ops.ACT_RELU, "reverse": gemm
          "threshold": gemm_ops.ACT_THRESHOLD}
 
 
+def _upload(g, device):
+    """Upload a freshly captured graph so its first replay does not pay the upload inline."""
+    from ..ops import _lib
+
+    with torch.cuda.device(device):
+        _lib.upload_graph(g, device)
+
+
 def _stack(models, key, which=0, device=None):
     return torch.stack([m[which][key].detach().float() for m in models]).to(device).contiguous()
 
@@ -51,8 +59,7 @@ class FusedSAEEnsemble:
 
     def __init__(self, models, sig, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999),
                  eps=1e-8, track_feature_counts=True, kind: Optional[str] = None,
-                 count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None,
-                 rowblock: Optional[bool] = None):
+                 count_every: int = 8, wgrad_split="auto", grad_dtype: Optional[str] = None):
         self.sig = sig
         self.kind = kind or getattr(sig, "fused_kind", None)
         # FunctionalTiedCenteredSAE (sae_ensemble.py:162-228): the tied kernels on x - center
@@ -141,7 +148,9 @@ class FusedSAEEnsemble:
         alloc = torch.zeros if self.nactive is not None else torch.empty
         self.c = alloc(G, B, n, device=dev, dtype=bf)
         self.r = torch.empty(G, B, d, device=dev, dtype=bf)
-        self.dpre = torch.empty(G, B, n, device=dev, dtype=bf)
+        # (masked: the wgrad GEMM's 256-row tiles read dpre columns past a model's live size that
+        # the compacted 128-column code-gradient launch never writes -- they must read zero)
+        self.dpre = alloc(G, B, n, device=dev, dtype=bf)
         # activity bitmask of c written by the encoder epilogue, read by the code-gradient
         # epilogue instead of c itself (1/16 of the bytes)
         self.cmask = torch.empty(gemm_ops.code_mask_shape(G, B, n), device=dev, dtype=torch.int64)
@@ -201,24 +210,9 @@ class FusedSAEEnsemble:
                      if gdt == "bf16" and self.wsplit == 1 else None)
         self._g_from_bf = False
         self.grad_scale = 1.0  # data parallel: 1 / world_size (gradients are then summed)
-        # Kernels 1-3 as ONE row-block launch (csrc/sae_rowblock.hip: encoder -> decoder -> code
-        # gradient per 64 batch rows, c and R never re-read from HBM) for ReLU SAEs at d = 512,
-        # opt-in (``rowblock=True``): on MI355X it is still slower than the three grouped GEMMs
-        # (profiles/README.md, round 3).  Its partial sums use 64-row (scalars) and 32-row
-        # (column sums) slots instead of the GEMMs' 128x128 grid.
-        eligible = (self.act == gemm_ops.ACT_RELU and self.nactive is None and not self.learned_center
-                    and gemm_ops.rowblock_supported(B, n, d))
-        self.rowblock = False if rowblock is None else bool(rowblock)
-        if self.rowblock and not eligible:
-            raise ValueError("row-block forward needs a ReLU SAE without masks / learned centre, d = 512, "
-                             "n % 256 == 0, B % 64 == 0")
-        slots = B // 32 if self.rowblock else tm
-        if self.rowblock:
-            self.enc_part = torch.zeros(G, B // 64, 2, device=dev)
-            self.dec_part = torch.zeros(G, B // 64, device=dev)
-        else:
-            self.enc_part = torch.zeros(G, tm * (n // 128), 2, device=dev)
-            self.dec_part = torch.zeros(G, tm * (d // 128), device=dev)
+        slots = tm
+        self.enc_part = torch.zeros(G, tm * (n // 128), 2, device=dev)
+        self.dec_part = torch.zeros(G, tm * (d // 128), device=dev)
         self.colpart = torch.zeros(G, slots, n, device=dev)
         self.track_feature_counts = track_feature_counts
         # per-feature activation counts are sampled every `count_every` steps (the column
@@ -301,11 +295,6 @@ class FusedSAEEnsemble:
             raise ValueError(f"batch has {x.shape[-2]} rows, engine was built for {self.batch_size}")
         count = self._counting() if count is None else count
         self._counted = count
-        if self.rowblock and target is None:
-            gemm_ops.sae_forward_rowblock(x, self.enc_shadow, self.dec_shadow, self.params[self._bkey], self.l1,
-                                          self.c, self.r, self.dpre, self.cmask, self.enc_part, self.dec_part,
-                                          self.colpart, self.cnt_part if count else None)
-            return
         ascale = self.s2 if self.kind == "threshold" else None
         gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part,
                              self.cnt_part if count else None, self.nactive, mask_out=self.cmask,
@@ -556,6 +545,7 @@ class FusedSAEEnsemble:
                 # collectives while this thread captures (ensemble-sharded runs)
                 with torch.cuda.graph(g, capture_error_mode="thread_local"):
                     self._step_kernels(xin, count)
+                _upload(g, self.device)
                 self._graph[(count, i)] = g
 
     def attach_source(self, source):
@@ -563,6 +553,12 @@ class FusedSAEEnsemble:
         ``DeviceRing.graph_source(batch_size)``, indexed by the device step counter); then call
         ``step_source()`` per step.  Removes the plain gather launch between graph replays
         (an ~9 us idle gap per step on MI355X, profiles/README.md)."""
+        ring = getattr(source, "ring", None)
+        if ring is not None and (ring.buf.dtype != self.x_static.dtype or ring.buf.shape[-1] != self.d
+                                 or getattr(source, "B", self.batch_size) != self.batch_size):
+            raise ValueError(f"source rows are {ring.buf.dtype} [*, {ring.buf.shape[-1]}] in batches of "
+                             f"{getattr(source, 'B', '?')}; the engine takes {self.x_static.dtype} "
+                             f"[{self.batch_size}, {self.d}]")
         self._source = source
         self._graph = None
         return self
@@ -581,31 +577,80 @@ class FusedSAEEnsemble:
                 for count in pattern:
                     self._source.gather(self.x_static, self.step_dev)  # the step's first kernel
                     self._step_kernels(self.x_static, count)
+            _upload(g, self.device)
             self._graph[key] = g
         return g
 
-    def prime_source(self, steps: int):
-        """Capture (without running anything) every graph that ``step_source(steps)`` groups
-        starting at the current step, and single-step remainders, will replay -- so no capture
-        happens later inside a timed region."""
-        t = self.step_count
-        self._source_graph(tuple(self._counting_at(t + s) for s in range(int(steps))))
-        for count in (True, False):
-            self._source_graph((count,))
+    def prime_source(self, steps: Optional[int] = None, patterns: Sequence[Sequence[bool]] = ()):
+        """Capture and upload (without running anything) the graphs later replays will use: the
+        ``steps``-step group starting at the current step plus the single-step remainders, and/or
+        every explicit counting ``pattern`` -- so no capture happens inside a timed region."""
+        if steps is not None:
+            t = self.step_count
+            self._source_graph(tuple(self._counting_at(t + s) for s in range(int(steps))))
+            for count in (True, False):
+                self._source_graph((count,))
+        for p in patterns:
+            self._source_graph(tuple(bool(c) for c in p))
 
     def _counting_at(self, t: int) -> bool:
         return self.track_feature_counts and (t % self.count_every == 0)
 
-    def step_source(self, steps: int = 1):
+    def step_source(self, steps: int = 1, pattern: Optional[Sequence[bool]] = None):
         """``steps`` optimizer steps, each on the next batch of the attached source, as ONE graph
         replay (each step: batch gather + the step's kernels; the device step counter indexes the
         batches).  Consecutive graph replays are separated by a ~9 us idle gap on MI355X, so a
         multi-step graph pays it once per ``steps`` steps.  Graphs are captured per pattern of
-        feature-counting steps (usually one pattern: ``steps`` divides ``count_every``)."""
+        feature-counting steps: by default step t counts when ``t % count_every == 0``;
+        ``pattern`` (one bool per step) fixes it per replay instead, e.g. count on the first step
+        of every group, so one graph serves every group whatever step it starts at."""
         t = self.step_count
-        pattern = tuple(self._counting_at(t + s) for s in range(int(steps)))
+        if pattern is None:
+            pattern = tuple(self._counting_at(t + s) for s in range(int(steps)))
+        else:
+            pattern = tuple(bool(c) and self.track_feature_counts for c in pattern)
+            if len(pattern) != int(steps):
+                raise ValueError(f"pattern has {len(pattern)} entries for {steps} steps")
         self._source.prepare(t, len(pattern))
         self._source_graph(pattern).replay()
+        for count in pattern:
+            self._counted = count
+            self._host_step()
+        return self.out
+
+    def _inputs_graph(self, xs, pattern):
+        key = ("inp", tuple(x.data_ptr() for x in xs), tuple(pattern))
+        if self._graph is None:
+            self._graph = {}
+        g = self._graph.get(key)
+        if g is None:
+            for x in xs:
+                if x.dtype != torch.bfloat16 or tuple(x.shape) != (self.batch_size, self.d) or not x.is_contiguous():
+                    raise ValueError("graph inputs must be contiguous bf16 [batch_size, d] buffers")
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for x, count in zip(xs, pattern):
+                    self._step_kernels(x, count)
+            _upload(g, self.device)
+            self._graph[key] = g
+        return g
+
+    def prime_inputs(self, xs: Sequence[torch.Tensor], pattern: Sequence[bool]):
+        """Capture + upload (nothing runs) the multi-step graph ``step_inputs(xs, pattern)`` replays."""
+        self._inputs_graph(list(xs), tuple(bool(c) and self.track_feature_counts for c in pattern))
+
+    def step_inputs(self, xs: Sequence[torch.Tensor], pattern: Optional[Sequence[bool]] = None):
+        """``len(xs)`` optimizer steps as ONE graph replay, step s on the persistent batch buffer
+        ``xs[s]`` (e.g. the all-gathered global batches of a multi-step group under ensemble
+        sharding); ``pattern`` = feature counting per step (default: the first step only)."""
+        xs = list(xs)
+        if pattern is None:
+            pattern = [i == 0 for i in range(len(xs))]
+        pattern = tuple(bool(c) and self.track_feature_counts for c in pattern)
+        if len(pattern) != len(xs):
+            raise ValueError("one counting flag per step")
+        self._inputs_graph(xs, pattern).replay()
         for count in pattern:
             self._counted = count
             self._host_step()
@@ -640,15 +685,12 @@ class FusedSAEEnsemble:
         for i in range(0, N, B):
             xin = self._x_bf16(rows[i:i + B])
             x = self.prepare(xin)
-            if self.rowblock:
-                self.forward(x, count=False)
-            else:
-                gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part, None,
-                                     self.nactive, mask_out=self.cmask, act=self.act,
-                                     ascale=self.s2 if self.kind == "threshold" else None, live_host=self._live)
-                if self.kind == "threshold":  # reconstructs the uncentred rows
-                    x = xin
-                gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
+            gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part, None,
+                                 self.nactive, mask_out=self.cmask, act=self.act,
+                                 ascale=self.s2 if self.kind == "threshold" else None, live_host=self._live)
+            if self.kind == "threshold":  # reconstructs the uncentred rows
+                x = xin
+            gemm_ops.decode_residual(self.c, self.dec_shadow, x, self.r, self.dec_part)
             se += self.dec_part.sum(1).double()
             l0 += self.enc_part[..., 1].sum(1).double()
             xf = x.double() if x.dim() == 3 else x.double().expand(G, B, self.d)

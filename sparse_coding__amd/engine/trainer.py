@@ -77,10 +77,11 @@ class EnsembleTrainer:
             raise ValueError(f"objective must be 'loss' or 'fista_loss', got {objective!r}")
         if objective == "fista_loss" and (sig is not FunctionalFista or parallel != "none"):
             raise ValueError("objective='fista_loss' needs the FunctionalFista signature and parallel='none'")
-        ok, why = _fused_ok(models, sig, batch_size, device) if engine in ("auto", "fused") else (False, "eager")
         if objective == "fista_loss":
-            ok, why = False, "fista-in-loss engine"
-        if engine == "fused" and not ok:
+            ok, why = False, "fista-in-loss engine"  # its own engines below (fused or autograd)
+        else:
+            ok, why = _fused_ok(models, sig, batch_size, device) if engine in ("auto", "fused") else (False, "eager")
+        if engine == "fused" and not ok and objective != "fista_loss":
             raise ValueError(f"fused engine requested but unavailable: {why}")
         self.engine_reason = why
         self.kind = "eager"
@@ -90,11 +91,15 @@ class EnsembleTrainer:
         elif objective == "fista_loss":
             from .fista_loss import FistaLossEnsemble, FusedFistaLossEnsemble, fused_ok
 
-            if engine in ("auto", "fused") and fista_backend != "torch" and fused_ok(models, batch_size, device,
-                                                                                     fista_loss_iters):
+            fok = fista_backend != "torch" and fused_ok(models, batch_size, device, fista_loss_iters)
+            if engine == "fused" and not fok:
+                raise ValueError("fused FISTA-in-loss engine requested but unavailable (needs the GPU kernels, "
+                                 "B % 128 == 0, d % 256 == 0, n <= d and n in the Gram kernel's sizes)")
+            if engine in ("auto", "fused") and fok:
                 self.impl = FusedFistaLossEnsemble(models, lr=lr, batch_size=batch_size, device=device,
                                                    num_iter=fista_loss_iters)
                 self.kind = "fista-loss-fused"
+                self.engine_reason = "fused fista-in-loss"
             else:
                 self.impl = FistaLossEnsemble(models, lr=lr, batch_size=batch_size, device=device,
                                               num_iter=fista_loss_iters, backend=fista_backend)
@@ -187,7 +192,7 @@ class EnsembleTrainer:
             mse = self.impl.step_batch(batch)
             self.last_losses = {"loss": mse}
             codes = None
-        elif self.kind == "fista-loss":
+        elif self.kind in ("fista-loss", "fista-loss-fused"):
             total = self.impl.step_batch(batch)
             self.last_losses = {"loss": total, **self.impl.last}
             codes = None
@@ -255,7 +260,7 @@ class EnsembleTrainer:
         elif self.kind == "fused-topk":
             st["impl"] = {"params": self.impl.params, "m": self.impl.m, "v": self.impl.v,
                           "step": self.impl.step_count}
-        elif self.kind in ("analytic", "fista-loss", "unrolled"):
+        elif self.kind in ("analytic", "fista-loss", "fista-loss-fused", "unrolled"):
             st["impl"] = self.impl.state_dict()
         else:
             st["impl"] = {"params": self.impl.params, "optim": self.impl.optim_states}
@@ -268,7 +273,7 @@ class EnsembleTrainer:
             raise ValueError(f"checkpoint engine {st['kind']} != {self.kind}")
         self.steps = int(st["steps"])
         imp = st["impl"]
-        if self.kind in ("fused-sae", "analytic", "fista-loss", "unrolled"):
+        if self.kind in ("fused-sae", "analytic", "fista-loss", "fista-loss-fused", "unrolled"):
             self.impl.load_state_dict(imp)
         elif self.kind == "fused-topk":
             for d_ in ("params", "m", "v"):

@@ -71,6 +71,8 @@ def signatures():
         "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_void_p],
         "sc_gather_rows_perm": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_long, c_long,
                                 c_void_p],
+        "sc_gather_rows_blocks": [c_void_p, c_long, c_void_p, c_long, c_long, c_long, c_long, c_long, c_void_p,
+                                  c_long, c_void_p],
         "sc_lista_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                          c_int, c_void_p],
         "sc_lista_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -86,9 +88,7 @@ def signatures():
                           c_void_p, c_void_p],
         "sc_stream_create_cumask": [c_void_p, c_int, C.POINTER(c_void_p)],
         "sc_stream_destroy": [c_void_p],
-        "sc_sae_rowblock": [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
-                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                            c_int, c_int, c_int, c_int, c_void_p],
+        "sc_graph_upload": [c_void_p, c_void_p],
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
         "sc_basis_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int,
                            c_void_p],
@@ -221,3 +221,10 @@ def cu_mask_stream(cus, n_cus: int = 256, device=None):
 
 def stream_handle(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def upload_graph(g: "torch.cuda.CUDAGraph", device=None):
+    """hipGraphUpload a captured graph on the current stream, so its first ``replay()`` does not
+    pay the upload (csrc/streams.hip)."""
+    rc = lib().sc_graph_upload(g.raw_cuda_graph_exec(), stream_handle(device))
+    check(rc, "sc_graph_upload")

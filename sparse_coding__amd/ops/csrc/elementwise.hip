@@ -148,6 +148,26 @@ __global__ __launch_bounds__(256) void gather_rows_perm_kernel(const u32x4_t* __
   for (int v = lane; v < row_vec; v += 64) o[v] = s[v];
 }
 
+// gather_rows_blocks_kernel: out[o * inner + i] = buf[perm[base + o * stride + i]] -- several
+//   steps' shards of a data-parallel permutation in one launch (rank r of N, step t: the block at
+//   perm[(t N + r) B, +B)), so a multi-step group's local batches fill one send buffer.
+//   Out-of-range positions read row 0.
+__global__ __launch_bounds__(256) void gather_rows_blocks_kernel(const u32x4_t* __restrict__ buf, long nbuf,
+                                                                 const long* __restrict__ perm, long nperm, long base,
+                                                                 long stride, long inner, u32x4_t* __restrict__ out,
+                                                                 long rows, int row_vec) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const long o = r / inner;
+  const long j = base + o * stride + (r - o * inner);
+  long src = (j >= 0 && j < nperm) ? perm[j] : 0;
+  src = (src >= 0 && src < nbuf) ? src : 0;
+  const u32x4_t* s = buf + src * row_vec;
+  u32x4_t* dst = out + r * row_vec;
+  for (int v = lane; v < row_vec; v += 64) dst[v] = s[v];
+}
+
 }  // namespace scamd
 
 using namespace scamd;
@@ -198,6 +218,17 @@ int sc_gather_rows_perm(const void* buf, long nbuf, const long* perm, long nperm
   if (rows == 0) return 0;
   hipLaunchKernelGGL(gather_rows_perm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
                      reinterpret_cast<const u32x4_t*>(buf), nbuf, perm, nperm, step, ep0,
+                     reinterpret_cast<u32x4_t*>(out), rows, (int)(row_bytes / 16));
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_gather_rows_blocks(const void* buf, long nbuf, const long* perm, long nperm, long base, long stride,
+                          long inner, long outer, void* out, long row_bytes, hipStream_t stream) {
+  if (row_bytes % 16 || inner < 1 || outer < 0 || nbuf < 1) return 1;
+  const long rows = inner * outer;
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(gather_rows_blocks_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
+                     reinterpret_cast<const u32x4_t*>(buf), nbuf, perm, nperm, base, stride, inner,
                      reinterpret_cast<u32x4_t*>(out), rows, (int)(row_bytes / 16));
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }

@@ -19,4 +19,13 @@ int sc_stream_destroy(void* s) {
   return hipStreamDestroy(reinterpret_cast<hipStream_t>(s)) == hipSuccess ? 0 : 3;
 }
 
+// Upload an instantiated graph to the device ahead of its first launch.  Without it the first
+// hipGraphLaunch of a freshly captured multi-step graph pays the upload inline (on MI355X several
+// hundred microseconds for a 40-60 node graph), which lands inside whatever region times it.
+int sc_graph_upload(void* exec, void* stream) {
+  if (hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec), reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+    return 3;
+  return 0;
+}
+
 }  // extern "C"

@@ -84,6 +84,13 @@ class EtaTracker:
         lam = (v.transpose(1, 2) @ gram @ v).reshape(-1)
         return 1.0 / ((1.0 + self.margin) * lam)
 
+    def state_dict(self):
+        return {"v": None if self.v is None else self.v.detach().clone(), "calls": self.calls}
+
+    def load_state_dict(self, st):
+        self.v = None if st.get("v") is None else st["v"].clone()
+        self.calls = int(st.get("calls", 0))
+
 
 def fista_torch(X, D, lam, A0=None, iters=500, eta=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Batched fp32 oracle: identical arithmetic to the reference loop, all models at once."""

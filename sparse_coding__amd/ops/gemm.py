@@ -256,53 +256,6 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, 
             dotpart=dotpart, dc_tied=tied_bias is not None, bias=tied_bias, sbias=n)
 
 
-ROWBLOCK_D = 512  # d of the row-block kernel's register / LDS layout (csrc/sae_rowblock.hip)
-
-
-def rowblock_supported(B, n, d):
-    """Shapes the fused row-block forward (``sae_forward_rowblock``) handles."""
-    return d == ROWBLOCK_D and n % 256 == 0 and 0 < n <= 2048 and B % 64 == 0 and B > 0
-
-
-def sae_forward_rowblock(x, w_enc, w_dec, bias, l1, c_out, r_out, dpre_out, mask_out, enc_part, dec_part,
-                         colpart, cnt_part=None):
-    """Encoder, decoder and code gradient of a ReLU SAE step in one launch (csrc/sae_rowblock.hip):
-
-        c    = relu(x w_enc^T + bias)               -> c_out  [G, B, n] bf16, mask_out (activity bits)
-        R    = c w_dec - x                          -> r_out  [G, B, d] bf16
-        dpre = 1[c > 0] (R w_dec^T + l1 d / 2)      -> dpre_out [G, B, n] bf16
-
-    the same quantities (and rounding points) as ``encode_relu`` -> ``decode_residual`` ->
-    ``code_grad(mask=...)``.  Partials: enc_part [G, B/64, 2] (sum c, active count), dec_part
-    [G, B/64] (sum R^2), colpart / cnt_part [G, B/32, n] (bias-gradient sums / on-counts per
-    32-row slot).  w_dec may be w_enc itself (tied dictionaries)."""
-    G, n, d = w_enc.shape
-    B = c_out.shape[1]
-    _need(rowblock_supported(B, n, d), f"row-block forward needs d={ROWBLOCK_D}, n%256==0, n<=2048, B%64==0 "
-          f"(got B={B}, n={n}, d={d})")
-    for t, name in ((x, "x"), (w_enc, "w_enc"), (w_dec, "w_dec"), (c_out, "c_out"), (r_out, "r_out"),
-                    (dpre_out, "dpre_out")):
-        _bf16(t, name)
-    sx = _x_stride(x, B, d, G)
-    _need(tuple(w_dec.shape) == (G, n, d), "w_dec shape")
-    _need(tuple(c_out.shape) == (G, B, n) and tuple(dpre_out.shape) == (G, B, n), "c/dpre shape")
-    _need(tuple(r_out.shape) == (G, B, d), "r_out shape")
-    _need(tuple(bias.shape) == (G, n) and bias.dtype == torch.float32 and bias.is_contiguous(), "bias")
-    _need(l1.dtype == torch.float32 and l1.numel() == G, "l1 must be fp32[G]")
-    _need(mask_out.dtype == torch.int64 and tuple(mask_out.shape) == code_mask_shape(G, B, n)
-          and mask_out.is_contiguous(), "mask_out")
-    for t, shape, name in ((enc_part, (G, B // 64, 2), "enc_part"), (dec_part, (G, B // 64), "dec_part"),
-                           (colpart, (G, B // 32, n), "colpart"), (cnt_part, (G, B // 32, n), "cnt_part")):
-        if t is None and name == "cnt_part":
-            continue
-        _need(t.dtype == torch.float32 and tuple(t.shape) == shape and t.is_contiguous(), f"{name} must be fp32 {shape}")
-    rc = _lib.lib().sc_sae_rowblock(
-        _lib.ptr(x), sx, _lib.ptr(w_enc), _lib.ptr(w_dec), _lib.ptr(bias), _lib.ptr(l1), d / 2.0,
-        _lib.ptr(c_out), _lib.ptr(r_out), _lib.ptr(dpre_out), _lib.ptr(mask_out), _lib.ptr(enc_part),
-        _lib.ptr(dec_part), _lib.ptr(colpart), _lib.ptr(cnt_part), G, B, n, d, _lib.stream_handle())
-    _lib.check(rc, "sc_sae_rowblock")
-
-
 def wgrad_split(G, n, d, K, nprob, live=None):
     """Split-K factor for the weight-gradient GEMM: 1 while the 256x256 grid already fills
     the 256 CUs; otherwise the smallest power of two that reaches 256 blocks and keeps

@@ -48,3 +48,23 @@ def gather_rows_perm(buf: torch.Tensor, perm: torch.Tensor, step: torch.Tensor, 
                                         _lib.ptr(ep0), _lib.ptr(out), out.shape[0], row_bytes, _lib.stream_handle())
     _lib.check(rc, "sc_gather_rows_perm")
     return out
+
+
+def gather_rows_blocks(buf: torch.Tensor, perm: torch.Tensor, base: int, stride: int, inner: int,
+                       out: torch.Tensor) -> torch.Tensor:
+    """out[o * inner + i] = buf[perm[base + o * stride + i]] for o < out.shape[0] // inner (one launch;
+    e.g. rank r's shards of several consecutive data-parallel steps).  Positions past ``perm`` read
+    row 0 instead of faulting."""
+    if not (buf.is_cuda and buf.is_contiguous() and out.is_contiguous()):
+        raise ValueError("gather_rows_blocks needs contiguous GPU buffers")
+    row_bytes = buf[0].numel() * buf.element_size()
+    rows = out.numel() // max(1, buf[0].numel())
+    if row_bytes % 16 or out.dtype != buf.dtype or out.numel() != rows * buf[0].numel() or rows % inner:
+        raise ValueError("out must hold whole rows of buf, a multiple of `inner` of them")
+    if perm.dtype != torch.int64 or not perm.is_contiguous() or perm.device != buf.device:
+        raise ValueError("perm must be contiguous int64 on the buffer's device")
+    rc = _lib.lib().sc_gather_rows_blocks(_lib.ptr(buf), buf.shape[0], _lib.ptr(perm), perm.numel(), int(base),
+                                          int(stride), int(inner), rows // inner, _lib.ptr(out), row_bytes,
+                                          _lib.stream_handle())
+    _lib.check(rc, "sc_gather_rows_blocks")
+    return out

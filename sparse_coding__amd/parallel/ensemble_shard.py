@@ -84,19 +84,18 @@ class EnsembleSharded:
         return self
 
     # ------------------------------------------------------------------ batch assembly
-    def _gather(self, local: torch.Tensor, i: int, async_op: bool):
+    def _gather(self, local: torch.Tensor, i: Optional[int], async_op: bool, out: Optional[torch.Tensor] = None):
+        out = self.gbuf[i] if out is None else out
         if not dist.is_initialized():
-            self.gbuf[i].copy_(local)
+            out.copy_(local)
             return None
         if self.info.backend == "gloo":  # gloo: list all_gather through host memory (tests, rehearsals)
             host = local.detach().cpu()
             parts = [torch.empty_like(host) for _ in range(self.info.world_size)]
             dist.all_gather(parts, host)
-            self.gbuf[i].copy_(torch.cat(parts))
+            out.copy_(torch.cat(parts))
             return None
-        else:
-            work = dist.all_gather_into_tensor(self.gbuf[i], local.contiguous(), async_op=async_op)
-        return work
+        return dist.all_gather_into_tensor(out, local.contiguous(), async_op=async_op)
 
     def step_batch(self, local: torch.Tensor):
         """One step on this rank's ``local`` rows [B, d] (gathered synchronously)."""
@@ -124,6 +123,65 @@ class EnsembleSharded:
         self._pending = (nxt, self._gather(self.lbuf[nxt], nxt, async_op=True))
         self._cur = nxt
         return self.engine.step_batch(self.gbuf[i])
+
+    # ------------------------------------------------------------------ multi-step groups
+    def _group_buffers(self, s: int):
+        """Per parity: a send buffer [s_max B, d] (this rank's rows of a group's steps) and the
+        gathered global batches [s_max, N B, d], one contiguous [N B, d] buffer per step."""
+        have = getattr(self, "_gsend", None)
+        if have is None or have[0].shape[0] < s * self.B:
+            dev, dt = self.gbuf[0].device, self.gbuf[0].dtype
+            self._gsend = [torch.empty(s * self.B, self.d, device=dev, dtype=dt) for _ in range(2)]
+            self._gglob = [torch.empty(s, self.global_batch, self.d, device=dev, dtype=dt) for _ in range(2)]
+        return self._gsend, self._gglob
+
+    def _issue_group(self, par: int, s: int, sample_steps):
+        send, glob = self._group_buffers(s)
+        sample_steps(send[par][: s * self.B], s)
+        works = [self._gather(send[par][k * self.B:(k + 1) * self.B], None, async_op=True, out=glob[par][k])
+                 for k in range(s)]
+        return par, s, works
+
+    def prime_groups(self, sizes: Sequence[int], pattern_fn):
+        """Fused engine: capture + upload every multi-step graph ``run_groups`` will replay (both
+        buffer parities), before any collective is in flight."""
+        if not hasattr(self.engine, "prime_inputs"):
+            return
+        _, glob = self._group_buffers(max(sizes))
+        for s in sorted(set(sizes)):
+            for par in (0, 1):
+                self.engine.prime_inputs([glob[par][k] for k in range(s)], pattern_fn(s))
+
+    def run_groups(self, groups: Sequence[int], sample_steps, pattern_fn=None):
+        """``sum(groups)`` steps as multi-step groups: per group ONE ``sample_steps(out, s)`` call (this
+        rank's rows of the group's s steps, e.g. ``DeviceRing.sample_shard_steps``), s batch
+        all-gathers on RCCL's stream, and ONE graph replay of the s steps (fused engine; other engines
+        step each batch).  The next group's sample and gathers are issued before this group's replay,
+        so they run under it; a replay waits (stream-ordered, no host sync) for its own gathers."""
+        groups = [int(s) for s in groups if int(s) > 0]
+        if not groups:
+            return None
+        pattern_fn = pattern_fn or (lambda s: [i == 0 for i in range(s)])
+        self.flush()  # (a single-step prefetch of step_sampled would hold stale rows)
+        self._group_buffers(max(groups))  # (re)allocated before anything is gathered into them
+        par = self._gpar = getattr(self, "_gpar", 0)
+        pend = self._issue_group(par, groups[0], sample_steps)
+        out = None
+        for k, s in enumerate(groups):
+            p, _, works = pend
+            for w in works:
+                if w is not None:
+                    w.wait()
+            if k + 1 < len(groups):
+                pend = self._issue_group(1 - p, groups[k + 1], sample_steps)
+            glob = self._gglob[p]
+            if hasattr(self.engine, "step_inputs"):
+                out = self.engine.step_inputs([glob[p_k] for p_k in range(s)], pattern_fn(s))
+            else:
+                for i in range(s):
+                    out = self.engine.step_batch(glob[i])
+        self._gpar = 1 - pend[0]
+        return out
 
     def flush(self):
         """Complete an outstanding prefetch (call before tearing the process group down)."""

@@ -332,8 +332,8 @@ class ZeroEagerChunk:
 
     def reduce_async(self):
         pend = _Pending()
-        if dist.is_initialized():
-            pend.add(dist.reduce_scatter_tensor(self._gshard, self._pad_grad, async_op=True))
+        if dist.is_initialized():  # (gloo with CUDA tensors: through an all-reduce)
+            pend.add(reduce_scatter_async(self._gshard, self._pad_grad))
         else:
             self._gshard.copy_(self._pad_grad[self.lo:self.hi])
         return pend
@@ -350,7 +350,9 @@ class ZeroEagerChunk:
         shard = self.flat[self.lo:self.hi]
         shard.add_(-self.lr * (self.m / bc1) / (torch.sqrt(self.v / bc2 + self.eps_root) + self.eps))
         if dist.is_initialized():
-            dist.all_gather_into_tensor(self.flat, shard.clone())
+            w = all_gather_async(self.flat, self.lo, self.hi)
+            if w is not None:
+                w.wait()
         off = 0
         for t in leaves:
             k = t.numel()

@@ -1,0 +1,114 @@
+"""HIP graph replays of the fused step: the in-graph ring batch fetch, multi-step graphs (k optimizer
+steps per replay) and priming (capture + upload without running), against host-driven steps."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from sparse_coding__amd.ops import _lib as L
+
+    L.lib()  # must load: no silent fallback on a GPU box
+    yield
+
+
+def test_in_graph_ring_source_matches_host_sampling():
+    """Batch fetch inside the step's HIP graph (DeviceRing.graph_source, indexed by the device
+    step counter) == host-driven sampling + graph replay, across permutation (epoch) rollovers."""
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+
+    torch.manual_seed(9)
+    d, n, B = 512, 1024, 256
+    rows = (torch.randn(B * 7 // 2, d, device=DEV) * 2).to(torch.bfloat16)  # 3.5 batches: 3-step epochs
+    rings = []
+    for _ in range(2):
+        r = DeviceRing(rows.shape[0], d, device=DEV, seed=5)
+        r.push(rows)
+        rings.append(r)
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3)]
+    a = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    a.attach_source(rings[0].graph_source(B))
+    b = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    for _ in range(8):
+        a.step_source()
+        rings[1].sample_shard(B, 0, 1, out=b.x_static)
+        b.step_static()
+    torch.cuda.synchronize()
+    assert rings[0].epoch == rings[1].epoch >= 3
+    torch.testing.assert_close(a.x_static, b.x_static, rtol=0, atol=0)
+    for k in a.params:
+        torch.testing.assert_close(a.params[k], b.params[k], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("group", [8, 3])
+def test_multi_step_graph_replay_matches_single_steps(group):
+    """``step_source(k)``: k optimizer steps (batch gathers included) in ONE graph replay equal k
+    single-step replays on host-sampled batches: parameters, losses, feature counts."""
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+
+    torch.manual_seed(10)
+    d, n, B, steps = 512, 1024, 256, 16
+    rows = (torch.randn(B * 40, d, device=DEV) * 2).to(torch.bfloat16)
+    rings = []
+    for _ in range(2):
+        r = DeviceRing(rows.shape[0], d, device=DEV, seed=3)
+        r.push(rows)
+        rings.append(r)
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3, 1e-2)]
+    a = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    a.attach_source(rings[0].graph_source(B))
+    b = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    done = 0
+    while done < steps:
+        k = min(group, steps - done)
+        a.step_source(k)
+        done += k
+    for _ in range(steps):
+        rings[1].sample_shard(B, 0, 1, out=b.x_static)
+        b.step_static()
+    torch.cuda.synchronize()
+    assert a.step_count == b.step_count == steps and int(a.step_dev.item()) == steps
+    for k in a.params:
+        torch.testing.assert_close(a.params[k], b.params[k], rtol=0, atol=0)
+    torch.testing.assert_close(a.out, b.out, rtol=0, atol=0)
+    torch.testing.assert_close(a.feature_counts, b.feature_counts, rtol=0, atol=0)
+    assert a.rows_seen == b.rows_seen
+
+
+def test_prime_source_captures_without_running():
+    """``prime_source`` captures the group / single-step graphs at the current step without
+    executing any step (parameters and counters unchanged); later replays reuse them."""
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+
+    torch.manual_seed(12)
+    d, n, B = 512, 512, 256
+    ring = DeviceRing(B * 20, d, device=DEV, seed=1)
+    ring.push((torch.randn(B * 20, d, device=DEV)).to(torch.bfloat16))
+    models = [FunctionalSAE.init(d, n, 1e-3, device=DEV)]
+    e = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
+    e.attach_source(ring.graph_source(B))
+    e.step_source(1)
+    e.step_source(1)
+    torch.cuda.synchronize()
+    before = {k: v.clone() for k, v in e.params.items()}
+    e.prime_source(8)
+    torch.cuda.synchronize()
+    n_graphs = len(e._graph)
+    assert e.step_count == 2 and int(e.step_dev.item()) == 2
+    for k in before:
+        assert torch.equal(before[k], e.params[k])
+    e.step_source(8)
+    e.step_source(1)
+    torch.cuda.synchronize()
+    assert len(e._graph) == n_graphs and e.step_count == 11 and int(e.step_dev.item()) == 11

@@ -1,5 +1,7 @@
 """Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references."""
 
+import io
+
 import pytest
 import torch
 
@@ -941,6 +943,46 @@ def test_fused_fista_loss_gradients_match_autograd(T):
         last = fused.step_batch(x)
     torch.cuda.synchronize()
     assert torch.isfinite(last).all() and (last < first).all(), (first, last)
+
+
+@pytest.mark.parametrize("engine", ["auto", "fused"])
+def test_trainer_fista_loss_fused_steps_and_resumes(engine):
+    """EnsembleTrainer(objective='fista_loss') on a GPU takes the fused FISTA-in-loss engine (auto
+    and explicit), trains, and a checkpoint round trip continues bit-identically."""
+    from sparse_coding__amd.engine.trainer import EnsembleTrainer
+    from sparse_coding__amd.models.fista import FunctionalFista
+
+    torch.manual_seed(23)
+    d, n, B = 512, 512, 256
+    models = [FunctionalFista.init(d, n, l1, device=DEV) for l1 in (1e-3, 3e-3)]
+    feats = torch.nn.functional.normalize(torch.randn(1024, d, device=DEV), dim=-1)
+    xs = [((torch.relu(torch.randn(B, 1024, device=DEV) - 1.0) * 2.0) @ feats).to(torch.bfloat16)
+          for _ in range(4)]
+
+    def make():
+        return EnsembleTrainer(models, FunctionalFista, lr=1e-3, batch_size=B, device=DEV, engine=engine,
+                               objective="fista_loss", fista_loss_iters=5)
+
+    tr = make()
+    assert tr.kind == "fista-loss-fused", tr.engine_reason
+    first = tr.step(xs[0]).clone()
+    for i in range(6):
+        last = tr.step(xs[1 + i % 3])
+    torch.cuda.synchronize()
+    assert torch.isfinite(last).all()
+    buf = io.BytesIO()
+    torch.save(tr.state_dict(), buf)  # what a checkpoint file holds (copies, not live views)
+    buf.seek(0)
+    st = torch.load(buf, weights_only=True)
+    tr2 = make()
+    tr2.load_state_dict(st)
+    a = tr.step(xs[0]).clone()
+    b = tr2.step(xs[0]).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), (a, b)
+    assert torch.equal(tr.impl.params["encoder"], tr2.impl.params["encoder"])
+    assert torch.equal(tr.impl.params["encoder_bias"], tr2.impl.params["encoder_bias"])
+    assert (a <= first).all(), (first, a)
 
 
 def test_coef_search_hip_matches_torch():

@@ -532,6 +532,68 @@ def test_ensemble_sharded_gloo_matches_global_batch():
         np.testing.assert_allclose(res[0][k], single.params[k].numpy(), atol=2e-5, rtol=1e-4)
 
 
+def _ring(rows, seed=7):
+    from sparse_coding__amd.data.ring import DeviceRing
+
+    r = DeviceRing(rows.shape[0], rows.shape[1], device="cpu", dtype=torch.float32, seed=seed)
+    r.push(rows)
+    return r
+
+
+def _es_groups_worker(rank, world, port, rows, init, groups, B, out_q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from sparse_coding__amd.engine.analytic import AnalyticSAEEnsemble
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
+    from sparse_coding__amd.parallel.ensemble_shard import EnsembleSharded
+
+    info = init_distributed("gloo")
+    ring = _ring(rows)  # every rank walks the same permutation and keeps its own shard of it
+    es = EnsembleSharded(init, lambda m, bs: AnalyticSAEEnsemble(m, FunctionalSAE, lr=1e-2), info,
+                         batch_per_rank=B, d=rows.shape[1], dtype=torch.float32)
+    for chunk in groups:  # several calls, several groups per call (the bench's warmup / timed split)
+        es.run_groups(chunk, lambda out, s: ring.sample_shard_steps(B, rank, world, s, out))
+    full = es.gather_params()
+    out_q.put((rank, {k: v.numpy().copy() for k, v in full.items()}))
+    shutdown(info)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ensemble_sharded_multistep_groups_gloo(world):
+    """Multi-step groups (one local-row gather per group, per-step batch all-gathers issued under the
+    previous group, one replay per group) over 2 and 4 gloo ranks == one process training every model
+    on the same global batches (the ring's data-parallel permutation, rank-ordered shards)."""
+    from sparse_coding__amd.engine.analytic import AnalyticSAEEnsemble
+
+    torch.manual_seed(3)
+    d, B = 16, 8
+    init = [FunctionalSAE.init(d, 32, l1) for l1 in (1e-4, 3e-4, 1e-3, 3e-3)]
+    rows = torch.randn(400, d)
+    groups = [[3, 2], [3], [1, 4]]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_es_groups_worker, args=(r, world, port, rows, init, groups, B, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = AnalyticSAEEnsemble([(dict(p), dict(b)) for p, b in init], FunctionalSAE, lr=1e-2)
+    ring = _ring(rows)
+    for chunk in groups:
+        for s in chunk:
+            xs = ring.sample_shard_steps(B * world, 0, 1, s, torch.empty(s * B * world, d))
+            for x in xs.view(s, B * world, d):
+                single.step_batch(x)
+    for k in single.params:
+        for r in range(1, world):
+            np.testing.assert_array_equal(res[0][k], res[r][k])
+        np.testing.assert_allclose(res[0][k], single.params[k].numpy(), atol=2e-5, rtol=1e-4)
+
+
 def _trainer_es_worker(rank, world, port, xs, init, out_q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
