@@ -45,6 +45,11 @@ BASELINE_ACT_PER_S = 1.86e3
 # Adam, fp32, the reference's algorithm) on ONE MI355X at the same config, measured with
 # ``bench.py --engine eager`` (profiles/bench_eager_r2.json: 2.63 ms/step).
 EAGER_SAME_BOX_ACT_PER_S = 779054.6
+# single-GPU step and per-rank ensemble-sharded steps measured on one MI355X (inputs of the
+# comm model's prediction, parallel/comm_model.py; profiles/bench_r3_v5_final.json,
+# profiles/es_projection_r3.jsonl)
+T1_MS = 0.3064
+ES_MS = {2: 0.285, 4: 0.2714, 8: 0.2621}
 METRIC = "activations/sec (ensemble train) + FVU@L0, Pythia-70m resid SAE at 1/2/4/8 GPU"
 
 
@@ -69,14 +74,16 @@ def parse(argv=None):
     ap.add_argument("--quality-steps", type=int, default=3000,
                     help="after the timed region, keep training (untimed) until this many steps in total "
                          "before the FVU@L0 evaluation (the timed K steps alone are far from converged)")
-    ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--grad-dtype", choices=["fp32", "bf16"], default=None,
+                    help="gradient transport of the data-parallel modes (default: dp fp32 all-reduce; zero1 bf16 "
+                         "all-to-all with fp32 accumulation on the row owner, parallel/zero.py)")
     ap.add_argument("--parallelism", choices=["auto", "es", "dp", "zero1"], default="auto",
                     help="N>1: 'es' = ensemble-axis sharding (each GPU owns models/N models and trains "
                          "them on the all-gathered global batch: identical updates to data parallel on the "
                          "global batch, but only the 2 MB batch crosses xGMI instead of 67 MB of gradients); "
                          "'dp' = data parallel with chunk-pipelined RCCL gradient all-reduce; 'zero1' = data "
                          "parallel with reduce-scatter, row-sharded Adam and a bf16 shadow all-gather; "
-                         "auto = es when models %% N == 0")
+                         "auto = the mode parallel/comm_model.py predicts fastest at this N")
     ap.add_argument("--dp-chunks", type=int, default=None,
                     help="dp / zero1: split the ensemble into this many model chunks whose gradient all-reduce "
                          "overlaps the next chunk's compute (1 = one reduction per step; default 2, or 1 on "
@@ -89,6 +96,11 @@ def parse(argv=None):
                     help="create the process group even at N=1 and run the N>1 code path (rehearses the "
                          "sharded step with real RCCL collectives on a one-GPU box)")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--graph-group", type=int, default=None,
+                    help="steps per graph replay (default: engine/graph_plan.tile's choice, <= 8)")
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="untimed non-training GPU load before the warmup so the timed steps run at the "
+                         "steady-state clock (settle_clocks; reported as 'settle' in the JSON; 0 = off)")
     ap.add_argument("--compare-parallelism", type=int, default=1,
                     help="N>1: after the headline run, also time the other strategy (es <-> dp) and report it "
                          "under alt_parallelism")
@@ -177,7 +189,7 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
         # under the previous group's replay) and ONE HIP graph replay of the s steps
         return Runner(lambda: es.run_groups([1], sample_steps, pattern), dicts, close=es.flush,
                       run=lambda groups: es.run_groups(groups, sample_steps, pattern),
-                      setup=lambda tiling: es.prime_groups(tiling.sizes, pattern))
+                      setup=lambda tiling: (ring.ensure_permutation(), es.prime_groups(tiling.sizes, pattern)))
     if args.engine == "fused" and distributed:
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
@@ -247,7 +259,7 @@ def comm_bytes(mode, args, world):
     params = args.models * (2 * n * args.d + n)
     gbytes = 2 if args.grad_dtype == "bf16" else 4
     return comm_bytes_per_step(mode, world, params * gbytes, shadow_bytes=args.models * 2 * n * args.d * 2,
-                               batch_bytes=args.batch * args.d * 2)
+                               batch_bytes=world * args.batch * args.d * 2)  # gathered global batch
 
 
 def timed(runner, groups, info, B):
@@ -266,13 +278,42 @@ def timed(runner, groups, info, B):
     return 1e3 * elapsed / steps, B * info.world_size * steps / elapsed
 
 
+def settle_clocks(device, ms: float):
+    """Untimed, NON-training GPU load before the warmup: the grouped bf16 MFMA GEMM (the step's own
+    kernel, plain epilogue) on scratch random operands for ``ms`` milliseconds.  MI355X raises its
+    clock over the first ~100 ms of sustained load (profiles/settle_r4.jsonl: a run started from an
+    idle GPU takes 351 us per step over its first 20 steps, 328 us by 20 ms, 324-325 us from 100 ms
+    on), so a 20-step timed region that starts on a cold GPU measures the ramp, not the step.
+    Touches no training state.  Returns what ran (reported in the JSON)."""
+    if ms <= 0:
+        return None
+    from sparse_coding__amd.ops import gemm as gemm_ops
+
+    g = torch.Generator(device=device).manual_seed(7)
+    a = torch.randn(2048, 512, device=device, generator=g).to(torch.bfloat16)
+    b = torch.randn(8, 2048, 512, device=device, generator=g).to(torch.bfloat16)
+    out = torch.empty(8, 2048, 2048, device=device, dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    launches = 0
+    while 1e3 * (time.perf_counter() - t0) < ms:
+        for _ in range(25):
+            gemm_ops.matmul_nt(a, b, out)
+        launches += 25
+        torch.cuda.synchronize()
+    return {"what": "grouped bf16 MFMA GEMM 8 x 2048x2048x512 on scratch buffers (no training state)",
+            "ms": round(1e3 * (time.perf_counter() - t0), 1), "launches": launches}
+
+
 def warm_and_time(runner, args, info, B):
-    """Capture every graph first, run the warmup through those same graphs (the last warmup replay
-    is a timed-size group), then time exactly ``args.steps`` steps (engine/graph_plan.py)."""
+    """Capture every graph first, settle the clocks (untimed, non-training, reported), run the
+    warmup through the timed region's own graphs (the last warmup replay is a timed-size group),
+    then time exactly ``args.steps`` steps (engine/graph_plan.py)."""
     from sparse_coding__amd.engine.graph_plan import tile
 
-    tiling = tile(args.steps, args.warmup, GRAPH_STEPS)
+    tiling = tile(args.steps, args.warmup, args.graph_group or GRAPH_STEPS, exact=bool(args.graph_group))
     runner.setup(tiling)
+    runner.settle = settle_clocks(info.device, args.settle_ms)
     runner.run(list(tiling.warm))
     runner.finish()  # no warmup work may spill into the timed region
     ms, value = timed(runner, list(tiling.timed), info, B)
@@ -299,17 +340,23 @@ def main(argv=None):
     ring, held_out = build_ring(args, device)
     B = args.batch
 
-    grad_dtype = torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32
     distributed = info.world_size > 1 or args.force_dist
     if args.dp_chunks is None:
         args.dp_chunks = 2 if info.world_size > 1 else 1
+    from sparse_coding__amd.parallel import comm_model
+
+    shape = comm_model.StepShape(models=args.models, n=n, d=args.d, batch=B, t1_ms=T1_MS,
+                                 untied=args.kind == "untied", es_ms=dict(ES_MS))
     par = args.parallelism
     if par == "auto":
-        # N > 1: ensemble-axis sharding (per model identical to data parallel on the global batch;
-        # moves the 2 MB batch instead of 67 MB of gradients per step)
-        par = "es" if (distributed and args.models % info.world_size == 0) else "dp"
+        # N > 1: the mode the per-N comm/compute model predicts fastest (ensemble-axis sharding at
+        # the headline config: it moves the batch, not 67 MB of gradients per step)
+        par = comm_model.best_mode(info.world_size, shape, args.dp_chunks) if distributed else "dp"
     if not distributed:
         par = "dp"  # one GPU: the plain fused step (no collectives)
+    if args.grad_dtype is None:
+        args.grad_dtype = "bf16" if par == "zero1" else "fp32"
+    grad_dtype = torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32
     if par == "es" and args.models % info.world_size:
         raise SystemExit(f"--parallelism es needs models % N == 0 ({args.models} models, N={info.world_size})")
 
@@ -342,6 +389,7 @@ def main(argv=None):
         a_ms, a_value, _ = warm_and_time(alt_runner, args, info, B)
         alt_runner.close()
         alt = {"parallelism": f"{other}{info.world_size}", "value": round(a_value, 1), "ms_per_step": round(a_ms, 4),
+               "predicted_ms_per_step": comm_model.predict(other, info.world_size, shape, args.dp_chunks),
                "dp_chunks": args.dp_chunks if other == "dp" else None,
                "comm_bytes_per_gpu_per_step": comm_bytes(other, args, info.world_size)}
 
@@ -373,6 +421,10 @@ def main(argv=None):
             },
             # ring-collective bytes each GPU sends per step in this mode (analytic; 0 on one GPU)
             "comm_bytes_per_gpu_per_step": comm_bytes(par, args, info.world_size) if distributed else 0,
+            # parallel/comm_model.py: predicted per-GPU step of every mode at this N (link model +
+            # overlap model; the measured ms_per_step above is the check on it)
+            "predicted_ms_per_step": {m: comm_model.predict(m, info.world_size, shape, args.dp_chunks)["ms_per_step"]
+                                      for m in ("dp", "zero1", "es")} if distributed else None,
             "comm_bytes_other_modes": {m: comm_bytes(m, args, max(info.world_size, 8)) for m in ("dp", "zero1", "es")},
             "model_activations_per_s": round(value * args.models, 1),
             "baseline_note": "vs_baseline divides by BASELINE.md row 12 (reference math, same shapes, "
@@ -381,6 +433,7 @@ def main(argv=None):
                              "engine on the same MI355X (profiles/bench_eager_r2.json)",
             # how the steps were cut into HIP graph replays: all graphs captured + uploaded before
             # warmup; the warmup replays every graph the timed region replays (engine/graph_plan.py)
+            "settle": getattr(runner, "settle", None),
             "graph_replays": {"timed": list(tiling.timed), "warmup": list(tiling.warm),
                               "warm_covered": tiling.covered} if par == "dp" and not distributed
             and not args.no_graph and args.engine == "fused" else None,

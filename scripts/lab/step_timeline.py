@@ -3,7 +3,8 @@
 A step starts at its ring-gather kernel.  Prints per step: wall from its gather to the next
 step's gather, busy time (sum of kernel durations), idle gaps, and per-kernel durations, so a
 short timed region (--steps 20) can be compared with the steady state kernel by kernel.
-Usage: python step_timeline.py TRACE_DIR [N_STEPS]
+Usage: python step_timeline.py TRACE_DIR [N_STEPS]   (N_STEPS 0: every step; also prints the busy time
+averaged over consecutive windows of 20 steps, with the window's start time in ms)
 """
 import collections
 import csv
@@ -25,7 +26,7 @@ def main():
     rows = [r for r in csv.DictReader(open(f)) if "scamd" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if "gather_rows_perm" in r["Kernel_Name"]]
-    sel = starts[-nsteps:]
+    sel = starts[-nsteps:] if nsteps > 0 else starts
     out = []
     for k, i0 in enumerate(sel):
         i1 = sel[k + 1] if k + 1 < len(sel) else len(rows)
@@ -38,8 +39,16 @@ def main():
             kern[short(r["Kernel_Name"])] = round((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000, 1)
         out.append({"step": k, "wall_us": round((t1 - t0) / 1000, 1), "busy_us": round(busy / 1000, 1),
                     "kernels": kern})
-    for o in out:
-        print(json.dumps(o))
+    if nsteps > 0:
+        for o in out:
+            print(json.dumps(o))
+    else:
+        t_first = int(rows[sel[0]]["Start_Timestamp"])
+        for w in range(0, len(out), 20):
+            win = out[w:w + 20]
+            t = (int(rows[sel[w]]["Start_Timestamp"]) - t_first) / 1e6
+            print(json.dumps({"from_step": w, "t_ms": round(t, 2), "busy_us": round(sum(o["busy_us"] for o in win) / len(win), 1),
+                              "wall_us": round(sum(o["wall_us"] for o in win) / len(win), 1)}))
     walls = [o["wall_us"] for o in out[:-1]]
     print(json.dumps({"mean_wall_us": round(sum(walls) / max(1, len(walls)), 1),
                       "mean_busy_us": round(sum(o["busy_us"] for o in out) / len(out), 1)}))

@@ -83,6 +83,12 @@ class DeviceRing:
         self._cursor = 0
         self.epoch += 1
 
+    def ensure_permutation(self):
+        """Draw the current epoch's permutation now if none exists (setup time, not first use)."""
+        if self._perm is None and self.size:
+            self._new_epoch()
+        return self
+
     def sample(self, batch_size: int, out: Optional[torch.Tensor] = None, return_index: bool = False):
         """Random batch (without replacement within an epoch), gathered on device.
         With ``return_index`` also returns the ring row indices ``[batch_size]``."""

@@ -592,6 +592,10 @@ class FusedSAEEnsemble:
                 self._source_graph((count,))
         for p in patterns:
             self._source_graph(tuple(bool(c) for c in p))
+        # the source's first permutation too (a 2M-row device randperm costs milliseconds of host
+        # time: drawn here, it cannot idle the GPU between a clock settle and the timed steps)
+        if hasattr(self._source, "prepare"):
+            self._source.prepare(self.step_count, max([1] + [len(p) for p in patterns]))
 
     def _counting_at(self, t: int) -> bool:
         return self.track_feature_counts and (t % self.count_every == 0)

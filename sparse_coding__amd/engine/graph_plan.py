@@ -29,12 +29,14 @@ class Tiling:
         return sorted(set(self.timed) | set(self.warm))
 
 
-def tile(steps: int, warmup: int, max_group: int = 8) -> Tiling:
+def tile(steps: int, warmup: int, max_group: int = 8, exact: bool = False) -> Tiling:
+    """``exact``: use group size ``max_group`` (capped at ``steps``) whatever the warmup covers."""
     steps, warmup = int(steps), int(warmup)
     if steps < 1 or warmup < 0:
         raise ValueError(f"need steps >= 1 and warmup >= 0 (got {steps}, {warmup})")
     best = None
-    for s in range(min(max_group, steps), 0, -1):
+    lo = min(max_group, steps) if exact else 1
+    for s in range(min(max_group, steps), lo - 1, -1):
         r = steps % s
         need = s + r  # one replay of each timed graph; the S-group last
         replays = steps // s + (1 if r else 0)

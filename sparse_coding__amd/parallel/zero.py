@@ -46,7 +46,7 @@ def shard_range(total: int, rank: int, world: int):
 def comm_bytes_per_step(mode: str, world: int, grad_bytes: int, shadow_bytes: int = 0, batch_bytes: int = 0) -> int:
     """Bytes each GPU sends per step (ring collectives) for the data-parallel modes: ``dp``
     all-reduce 2 (N-1)/N g; ``zero1`` reduce-scatter + all-gather (N-1)/N (g + s); ``es``
-    (ensemble sharding) all-gather of the batch (N-1)/N b."""
+    (ensemble sharding) all-gather of the global batch (N-1)/N b (b = the gathered N B rows)."""
     f = (world - 1) / world
     if mode == "dp":
         return int(2 * f * grad_bytes)
@@ -72,6 +72,29 @@ def reduce_scatter_async(out, inp):
         out.copy_(tmp.view(dist.get_world_size(), -1)[r])
         return None
     return dist.reduce_scatter_tensor(out, inp, async_op=True)
+
+
+def reduce_scatter_lowp(out, inp, send, recv):
+    """out (fp32) = this rank's 1/N slice of sum_ranks(inp), moving ``send.dtype`` (bf16) over the
+    links but accumulating in fp32 on the owner: every rank sends rank j's slice of its (rounded)
+    gradient to j (all-to-all), and the owner sums the N received slices in fp32.  Same bytes per
+    GPU as a bf16 reduce-scatter, (N-1)/N x g/2, without the ring's N-1 bf16 re-roundings of the
+    partial sums.  Synchronous on the host only for gloo (CPU transport); returns a work handle or
+    None, and a finisher that does the fp32 sum once the transfer completed."""
+    world = dist.get_world_size()
+    send.copy_(inp.view(-1))
+    if send.is_cuda and dist.get_backend() == "gloo":  # gloo moves CPU tensors only for all-to-all
+        s_cpu, r_cpu = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
+        dist.all_to_all_single(r_cpu, s_cpu)
+        recv.copy_(r_cpu)
+        work = None
+    else:
+        work = dist.all_to_all_single(recv, send, async_op=True)
+
+    def finish():
+        torch.sum(recv.view(world, -1), dim=0, dtype=torch.float32, out=out.view(-1))
+
+    return work, finish
 
 
 def all_gather_async(flat, lo, hi):
@@ -156,9 +179,9 @@ class ZeroFusedChunk:
             self.g_dec_shard = torch.empty(rows, d, device=dev)
             self.g_enc_shard = torch.empty(rows, d, device=dev) if kind == "untied" else None
         self._lowp = grad_dtype != torch.float32 and not self._solo
-        if self._lowp:  # reduce in bf16, widen the owned shard afterwards
+        if self._lowp:  # bf16 transport (all-to-all), fp32 accumulation on the row owner
             self._rs_in = [torch.empty(G * n * d, device=dev, dtype=grad_dtype) for _ in range(2 if kind == "untied" else 1)]
-            self._rs_out = [torch.empty(rows * d, device=dev, dtype=grad_dtype) for _ in self._rs_in]
+            self._rs_out = [torch.empty(info.world_size * rows * d, device=dev, dtype=grad_dtype) for _ in self._rs_in]
         self.graph = graph
         self.x_static = x_static
         self._graphs = {}
@@ -213,9 +236,7 @@ class ZeroFusedChunk:
         dsts = [self.g_dec_shard] + ([self.g_enc_shard] if e.kind == "untied" else [])
         for i, (src, dst) in enumerate(zip(srcs, dsts)):
             if self._lowp:
-                self._rs_in[i].copy_(src.view(-1))
-                w = reduce_scatter_async(self._rs_out[i], self._rs_in[i])
-                pend.add(w, (lambda i=i, dst=dst: dst.view(-1).copy_(self._rs_out[i])))
+                pend.add(*reduce_scatter_lowp(dst, src, self._rs_in[i], self._rs_out[i]))
             else:
                 pend.add(reduce_scatter_async(dst.view(-1), src.reshape(-1)))
         # untied: _g_flat = [g_enc | g_bias]; tied: [g_dict | g_bias | extras] -- the tail is small
@@ -290,9 +311,10 @@ class ZeroEagerChunk:
     all-gathers the updated parameters.  Elementwise Adam (torchopt semantics, the ensemble's
     own lr / betas / eps), so it equals the single-process optimizer on the global batch."""
 
-    def __init__(self, ensemble, info: DistInfo):
+    def __init__(self, ensemble, info: DistInfo, grad_dtype: torch.dtype = torch.float32):
         self.ens = ensemble
         self.info = info
+        self.grad_dtype = grad_dtype
         self.scale = 1.0
         self.last = None
         leaves, self._spec = pytree.tree_flatten(ensemble.params)
@@ -313,6 +335,9 @@ class ZeroEagerChunk:
         self.count = 0
         self._gshard = torch.empty_like(self.m)
         self._pad_grad = torch.zeros(self._padded, device=dev)
+        if grad_dtype != torch.float32:  # bf16 transport, fp32 owner accumulation
+            self._send = torch.empty(self._padded, device=dev, dtype=grad_dtype)
+            self._recv = torch.empty(self._padded, device=dev, dtype=grad_dtype)
 
     def set_grad_scale(self, s: float):
         self.scale = s
@@ -332,7 +357,9 @@ class ZeroEagerChunk:
 
     def reduce_async(self):
         pend = _Pending()
-        if dist.is_initialized():  # (gloo with CUDA tensors: through an all-reduce)
+        if dist.is_initialized() and self.grad_dtype != torch.float32:
+            pend.add(*reduce_scatter_lowp(self._gshard, self._pad_grad, self._send, self._recv))
+        elif dist.is_initialized():  # (gloo with CUDA tensors: through an all-reduce)
             pend.add(reduce_scatter_async(self._gshard, self._pad_grad))
         else:
             self._gshard.copy_(self._pad_grad[self.lo:self.hi])
