@@ -185,6 +185,11 @@ class RingGraphSource:
             self._ep0_host = int(step)
             self.ring.epoch += 1
 
+    def tail_gather(self, out: torch.Tensor):
+        """(ring buffer, permutation, epoch start, out): what a fused step tail needs to fetch the NEXT
+        step's rows into ``out`` (csrc/adam.hip step_tail_kernel, row ``(t + 1 - ep0) * B + r``)."""
+        return (self.ring.buf, self.perm, self.ep0, out)
+
     def gather(self, out: torch.Tensor, step_dev: torch.Tensor):
         """The capturable fetch: ``out`` [B, ...] <- this step's rows."""
         from ..ops.rows import gather_rows_perm

@@ -222,6 +222,15 @@ class FusedSAEEnsemble:
         self.feature_counts = torch.zeros(G, n, device=dev) if track_feature_counts else None
         self.rows_seen = 0
         self.out = torch.zeros(G, 6, device=dev)
+        # fused step tail (csrc/adam.hip step_tail_kernel: row Adam + loss terms + bias Adam + the next
+        # step's batch gather in ONE launch) for the plain untied / tied single-device step; it keeps
+        # per-32-column b^2 partial sums (parity-double-buffered by the step counter) for |b|
+        self._tail_ok = (self.kind in ("untied", "tied") and self.act == gemm_ops.ACT_RELU and not self.learned_center
+                         and self.nactive is None and self.wsplit == 1 and n % 32 == 0 and d <= 1024
+                         and os.environ.get("SC_FUSED_TAIL", "1") not in ("", "0"))
+        self._bsq = torch.zeros(2, G, n // 32, device=dev) if self._tail_ok else None
+        self._ticket = torch.zeros(1, device=dev, dtype=torch.int32) if self._tail_ok else None
+        self._bsq_dirty = True
         # threshold SAEs: per-feature partial sums of the code gradient on the activation's ramp
         # (the scale gradient's source, written by the code-gradient epilogue)
         self.dotpart = torch.zeros(G, tm, n, device=dev) if self.kind == "threshold" else None
@@ -238,8 +247,19 @@ class FusedSAEEnsemble:
         self.rcol = torch.zeros(G, tm, d, device=dev) if self.learned_center else None
 
     # ------------------------------------------------------------------ helpers
+    def _refresh_bsq(self):
+        """The fused tail's b^2 partials of the current bias (after any update outside the tail)."""
+        if self._bsq is not None:
+            adam_ops.bias_sq_parts(self.params[self._bkey], self._bsq, self.step_count & 1)
+        self._bsq_dirty = False
+
+    def _tail_ready(self):
+        if getattr(self, "_bsq_dirty", False) and self._bsq is not None:
+            self._refresh_bsq()
+
     def refresh_shadows(self):
         """Rebuild the bf16 shadows from the fp32 masters (after any out-of-band edit)."""
+        self._bsq_dirty = True
         if self.kind == "untied":
             adam_ops.shadow_rows(self.params["encoder"], self.enc_shadow, normalize=False)
             adam_ops.shadow_rows(self.params["decoder"], self.dec_shadow, self.norms, normalize=True)
@@ -405,10 +425,21 @@ class FusedSAEEnsemble:
 
     def apply_update(self):
         """Kernels 5-6: fused Adam on the weights, then bias Adam + loss reduction."""
+        self._tail_ready()
         self._apply_update_kernels()
         self._host_step()
 
-    def _apply_update_kernels(self):
+    def _apply_update_kernels(self, gather=None):
+        if self._tail_ok:
+            # one launch: row Adam + loss terms + bias Adam (+ the next step's batch gather), the
+            # device step counter advanced by its last block
+            adam_ops.step_tail(self._adam_sets(), self.lr, *self.betas, self.eps, self.step_dev,
+                               self.params[self._bkey], self.m[self._bkey], self.v[self._bkey], self.colpart,
+                               self.enc_part, self.dec_part, self.l1, self.bias_decay, self.out, self.batch_size,
+                               self._alpha, self._bsq, self._ticket,
+                               cnt_part=self.cnt_part if self._counted else None,
+                               feat_count=self.feature_counts if self._counted else None, gather=gather)
+            return
         # scale / centering first: their gradients read the pre-update dictionary (adam_first)
         if self.kind == "threshold" or self.learned_center:
             self._threshold_extra_adam()
@@ -475,6 +506,8 @@ class FusedSAEEnsemble:
 
     def _bias_loss(self, update, reduced, defer_step=False):
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
+        if update:
+            self._bsq_dirty = True  # (a bias update outside the fused tail)
         b1, b2 = self.betas
         if reduced:  # bias gradient already summed (and possibly all-reduced) into g_bias
             colpart, tm, gscale = self.g_bias, 1, 1.0
@@ -492,6 +525,7 @@ class FusedSAEEnsemble:
     def step_batch(self, batch, expand_dims=True):
         """One Adam step of every model on ``batch [B, d]``; returns a device tensor [G, 6]:
         (loss, l_reconstruction, l_l1, l_bias_decay, mean L0, |b|).  Never synchronises."""
+        self._tail_ready()
         if self.use_graph:
             for i, t in enumerate(self._static_inputs):
                 if batch is t:
@@ -513,7 +547,7 @@ class FusedSAEEnsemble:
             self._graph = None
         return self
 
-    def _step_kernels(self, x, count=None):
+    def _step_kernels(self, x, count=None, gather=None):
         """All kernels of one step (captured as one HIP graph when enabled).  Side-stream
         variants of this sequence -- decoder Adam beside the encoder weight gradient, the loss /
         bias-Adam tail beside the weight gradient, Adam fused into the weight-gradient epilogue,
@@ -523,7 +557,7 @@ class FusedSAEEnsemble:
         x = self.prepare(x)
         self.forward(x, count, target)
         self.backward_weights(x)
-        self._apply_update_kernels()
+        self._apply_update_kernels(gather if self._tail_ok else None)
 
     def add_static_input(self, t: torch.Tensor) -> int:
         """Register another persistent input buffer [B, d] bf16: ``step_batch(t)`` then replays
@@ -574,9 +608,13 @@ class FusedSAEEnsemble:
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                for count in pattern:
-                    self._source.gather(self.x_static, self.step_dev)  # the step's first kernel
-                    self._step_kernels(self.x_static, count)
+                # each step's batch: the first step's own gather kernel; later steps' rows are fetched by
+                # the previous step's fused tail (one launch fewer per step) when the source allows it
+                nxt = self._source.tail_gather(self.x_static) if (self._tail_ok and hasattr(self._source, "tail_gather")) else None
+                for i, count in enumerate(pattern):
+                    if i == 0 or nxt is None:
+                        self._source.gather(self.x_static, self.step_dev)
+                    self._step_kernels(self.x_static, count, gather=nxt if i + 1 < len(pattern) else None)
             _upload(g, self.device)
             self._graph[key] = g
         return g
@@ -608,6 +646,7 @@ class FusedSAEEnsemble:
         feature-counting steps: by default step t counts when ``t % count_every == 0``;
         ``pattern`` (one bool per step) fixes it per replay instead, e.g. count on the first step
         of every group, so one graph serves every group whatever step it starts at."""
+        self._tail_ready()
         t = self.step_count
         if pattern is None:
             pattern = tuple(self._counting_at(t + s) for s in range(int(steps)))
@@ -648,6 +687,7 @@ class FusedSAEEnsemble:
         """``len(xs)`` optimizer steps as ONE graph replay, step s on the persistent batch buffer
         ``xs[s]`` (e.g. the all-gathered global batches of a multi-step group under ensemble
         sharding); ``pattern`` = feature counting per step (default: the first step only)."""
+        self._tail_ready()
         xs = list(xs)
         if pattern is None:
             pattern = [i == 0 for i in range(len(xs))]
@@ -663,6 +703,7 @@ class FusedSAEEnsemble:
     def step_static(self, which: int = 0):
         """Replay the captured step on whatever is in ``x_static`` (fill it first, e.g. with
         ``torch.index_select(..., out=engine.x_static)``), or on static input ``which``."""
+        self._tail_ready()
         if self._graph is None:
             self._capture()
         count = self._counting()

@@ -89,6 +89,13 @@ def signatures():
         "sc_stream_create_cumask": [c_void_p, c_int, C.POINTER(c_void_p)],
         "sc_stream_destroy": [c_void_p],
         "sc_graph_upload": [c_void_p, c_void_p],
+        "sc_step_tail": [c_int, C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
+                         C.POINTER(c_void_p), C.POINTER(c_void_p), C.POINTER(c_void_p),
+                         C.POINTER(c_int), C.POINTER(c_int), c_int, c_int, c_void_p, c_float, c_float, c_float,
+                         c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
+                         c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
+                         c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long,
+                         c_void_p],
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
         "sc_basis_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int,
                            c_void_p],

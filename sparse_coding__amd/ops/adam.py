@@ -96,3 +96,64 @@ def bias_loss(b, m, v, colpart, tm, enc_part, enc_tiles, dec_part, dec_tiles, l1
         bc1, bc2, int(update), _lib.ptr(step_dev), _lib.stream_handle(), int(bool(defer_step)),
     )
     _lib.check(rc, "sc_bias_loss")
+
+
+def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, enc_part, dec_part, l1, bias_decay,
+              out, B, gscale, bsq, ticket, cnt_part=None, feat_count=None, gather=None):
+    """The end of a single-device step as ONE launch (csrc/adam.hip ``step_tail_kernel``): row Adam over
+    ``sets`` (as ``adam_rows``), the loss terms into ``out`` [G, 6], bias Adam (gradient = ``gscale``
+    x the column sums of ``colpart`` [G, tm, n]), feature on-counts when ``cnt_part`` /
+    ``feat_count`` are given, and -- with ``gather`` = (ring buffer [N, d], perm int64, ep0 int32 [1],
+    out [rows, d]) -- the NEXT step's batch fetch.  The device step counter ``step_dev`` is read by
+    every block and advanced by the last one.  ``bsq`` [2, G, n/32] fp32 holds the b^2 partial sums
+    of the current bias at index ``step & 1`` (``bias_sq_parts``); the tail writes the other half.
+    ``ticket``: one zero-initialised int32 (reset by the kernel)."""
+    shp = tuple(sets[0]["p"].shape)
+    d = shp[-1]
+    nrows = sets[0]["p"].numel() // d
+    G, n = bias.shape
+    gbf16 = sets[0]["g"].dtype == torch.bfloat16
+    for s in sets:
+        for k in ("p", "g", "m", "v"):
+            t = s[k]
+            want = torch.bfloat16 if (k == "g" and gbf16) else torch.float32
+            if t.dtype != want or tuple(t.shape) != shp or not t.is_contiguous():
+                raise ValueError(f"step_tail set tensor {k} must be contiguous {want} {shp}")
+    if len(shp) != 3 or shp[0] != G or shp[1] != n or n % 32 or d % 256 or d > 1024:
+        raise ValueError(f"step_tail needs [G, n, d] sets with n % 32 == 0, d in 256..1024 (got {shp}, bias {G}x{n})")
+    if tuple(bsq.shape) != (2, G, n // 32) or bsq.dtype != torch.float32 or not bsq.is_contiguous():
+        raise ValueError("bsq must be contiguous fp32 [2, G, n/32]")
+    if ticket.dtype != torch.int32 or ticket.numel() < 1 or step_dev is None:
+        raise ValueError("ticket must be int32 and step_dev a device counter")
+    tm = colpart.shape[1]
+    if tuple(colpart.shape) != (G, tm, n) or (cnt_part is not None and tuple(cnt_part.shape) != (G, tm, n)):
+        raise ValueError("colpart / cnt_part must be [G, tm, n]")
+    gbuf = perm = ep0 = gout = None
+    grows = row_bytes = nbuf = nperm = 0
+    if gather is not None:
+        gbuf, perm, ep0, gout = gather
+        row_bytes = gbuf.shape[-1] * gbuf.element_size()
+        if (row_bytes % 16 or gout.dtype != gbuf.dtype or gout.shape[-1] != gbuf.shape[-1] or not gout.is_contiguous()
+                or perm.dtype != torch.int64 or ep0.dtype != torch.int32):
+            raise ValueError("gather: contiguous rows of 16-byte multiples, int64 perm, int32 ep0")
+        grows, nbuf, nperm = gout.shape[0], gbuf.shape[0], perm.numel()
+    rows = (C.c_int * len(sets))(*[nrows for _ in sets])
+    norm = (C.c_int * len(sets))(*[int(bool(s["norm"])) for s in sets])
+    rc = _lib.lib().sc_step_tail(
+        len(sets), _vp([s["p"] for s in sets]), _vp([s["g"] for s in sets]),
+        _vp([s["m"] for s in sets]), _vp([s["v"] for s in sets]),
+        _vp([s.get("shadow") for s in sets]), _vp([s.get("norms") for s in sets]),
+        rows, norm, d, n, _lib.ptr(lr), b1, b2, eps, _lib.ptr(step_dev), int(gbf16),
+        G, _lib.ptr(bias), _lib.ptr(bias_m), _lib.ptr(bias_v), _lib.ptr(colpart), tm, _lib.ptr(enc_part),
+        enc_part.shape[1], _lib.ptr(dec_part), dec_part.shape[1], _lib.ptr(cnt_part), _lib.ptr(feat_count),
+        _lib.ptr(l1), _lib.ptr(bias_decay), _lib.ptr(out), n, B, float(gscale), _lib.ptr(bsq), _lib.ptr(ticket),
+        _lib.ptr(gbuf), nbuf, _lib.ptr(perm), nperm, _lib.ptr(ep0), _lib.ptr(gout), grows, row_bytes,
+        _lib.stream_handle(),
+    )
+    _lib.check(rc, "sc_step_tail")
+
+
+def bias_sq_parts(bias, bsq, parity: int):
+    """bsq[parity] = per-32-column sums of bias^2 (what the step tail reads as |b|^2)."""
+    G, n = bias.shape
+    torch.sum(bias.view(G, n // 32, 32).square(), dim=-1, out=bsq[parity])

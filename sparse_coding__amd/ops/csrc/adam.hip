@@ -52,9 +52,8 @@ __device__ __forceinline__ void bias_corrections(float b1, float b2, int t, floa
 // kernel's HBM bytes less to read and half the GEMM's output stores; the moments, the master
 // and the update arithmetic stay fp32.
 template <int NV, bool GBF = false>
-__global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
+__device__ __forceinline__ void adam_row(const AdamArgs& a, long wave) {
   const int lane = threadIdx.x & 63;
-  const long wave = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   long row = wave;
   int s = 0;
   if (row >= a.set[0].rows) {
@@ -172,6 +171,11 @@ __global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
   }
 }
 
+template <int NV, bool GBF = false>
+__global__ __launch_bounds__(256) void adam_rows_kernel(AdamArgs a) {
+  adam_row<NV, GBF>(a, (long)blockIdx.x * 4 + (threadIdx.x >> 6));
+}
+
 // Writes a bf16 (optionally row-normalised) shadow of fp32 rows; used at init
 // and after any out-of-band parameter change (e.g. FISTA basis update).
 __global__ __launch_bounds__(256) void shadow_rows_kernel(const float* p, uint16_t* shadow, float* norms,
@@ -218,6 +222,7 @@ struct BiasArgs {
   const float* lr;                 // [G]
   float* out;                      // [G][6]: loss, l_rec, l_l1, l_bias_decay, mean L0, |b|
   int n, B, d;
+  int nmodels;                     // G (the fused step tail indexes its b^2 partials by model)
   float gscale;                    // converts colpart sums to dL/db (2/(B d) for raw dpre_s)
   float b1, b2, eps, bc1, bc2;
   int update;                      // 0: only losses (eval)
@@ -325,6 +330,150 @@ __global__ __launch_bounds__(256) void bias_adam_kernel(BiasArgs a) {
   a.b[idx] = bj - (a.lr[g] / bc1) * mj / (sqrtf(vj / bc2) + a.eps);
 }
 
+
+// ------------------------------------------------------------------ fused step tail
+// The end of a single-device training step as ONE launch (it replaces adam_rows + loss_reduce +
+// bias_adam and the next step's batch-gather launch; three ~5 us latency-bound kernels and their
+// launch gaps).  Block roles by index (the small latency-bound roles first, so they are not a
+// tail behind the HBM-bound Adam rows):
+//   [0, G)                      loss terms of model g (reduces the GEMM-epilogue partials)
+//   [G, G + G n/32)             bias Adam, 32 columns of one model (+ feature on-counts)
+//   [.., + ngather)             the NEXT step's batch gather from the ring permutation
+//   [.., + rows/4)              row Adam (norm Jacobian, update, bf16 shadow, row norms)
+// Cross-block dependencies are removed instead of ordered:
+//   * |b| (loss term and bias-decay gradient, both of the pre-update bias) comes from per-32-
+//     column partial sums of b^2 written by the PREVIOUS step's bias blocks (double-buffered by
+//     step parity: this step reads bsq[t & 1] and writes bsq[(t + 1) & 1]);
+//   * every block reads the device step counter t at its start; the last block to finish
+//     (atomic ticket) advances it -- after every other block has taken its ticket, i.e. after
+//     every read of t.
+struct TailArgs {
+  float* bsq;                 // [2][G][n/32] partial sums of b^2 (parity-double-buffered)
+  int* ticket;                // zero-initialised block counter (reset by the last block)
+  // next-step gather (ngather blocks; 0 = none): out[r] = buf[perm[(t + 1 - ep0) * rows + r]]
+  const u32x4_t* gbuf; long nbuf; const long* perm; long nperm; const int* ep0; u32x4_t* gout; long grows;
+  int row_vec;
+  int nloss, nbias, ngather;  // block counts of the roles
+};
+
+__device__ __forceinline__ void tail_loss(const BiasArgs& a, const TailArgs& t, int g, int par) {
+  __shared__ float red[8];
+  const int tid = threadIdx.x, nb = a.n / 32;
+  float bs = 0.f;
+  for (int j = tid; j < nb; j += 256) bs += t.bsq[((long)par * a.nmodels + g) * nb + j];
+  bs = block_sum_256(bs, red);
+  float l1 = 0.f, l0 = 0.f, se = 0.f;
+  const float2* ep = reinterpret_cast<const float2*>(a.enc_part) + (long)g * a.enc_tiles;
+#pragma unroll 4
+  for (int k = tid; k < a.enc_tiles; k += 256) {
+    const float2 v = ep[k];
+    l1 += v.x;
+    l0 += v.y;
+  }
+#pragma unroll 4
+  for (int k = tid; k < a.dec_tiles; k += 256) se += a.dec_part[(long)g * a.dec_tiles + k];
+  l1 = block_sum_256(l1, red);
+  l0 = block_sum_256(l0, red);
+  se = block_sum_256(se, red);
+  if (tid == 0) {
+    const float bnorm = sqrtf(bs);
+    const float l_rec = se / ((float)a.B * a.d);
+    const float l_l1 = a.l1[g] * l1 / a.B;
+    const float l_bd = a.bias_decay[g] * bnorm;
+    float* o = a.out + g * 6;
+    o[0] = l_rec + l_l1 + l_bd;
+    o[1] = l_rec;
+    o[2] = l_l1;
+    o[3] = l_bd;
+    o[4] = l0 / a.B;
+    o[5] = bnorm;
+  }
+}
+
+__device__ __forceinline__ void tail_bias(const BiasArgs& a, const TailArgs& t, int bx, int g, int step, int par) {
+  __shared__ float gred[8][33], cred[8][33], sred[8];
+  const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const int n = a.n, nb = n / 32;
+  const int j = bx * 32 + col;
+  const bool counting = a.cnt_part && a.feat_count;
+  // |b| of the pre-update bias from the previous step's partials (every block of the model alike)
+  float bs = 0.f;
+  for (int k = threadIdx.x; k < nb; k += 256) bs += t.bsq[((long)par * a.nmodels + g) * nb + k];
+  bs = block_sum_256(bs, sred);
+  float gs = 0.f, cs = 0.f;
+  for (int k = grp; k < a.tm; k += 8) {
+    const long o = ((long)g * a.tm + k) * n + j;
+    gs += a.colpart[o];
+    if (counting) cs += a.cnt_part[o];
+  }
+  gred[grp][col] = gs;
+  cred[grp][col] = cs;
+  __syncthreads();
+  if (grp != 0) return;
+  float gsum = 0.f, csum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    gsum += gred[r][col];
+    csum += cred[r][col];
+  }
+  const long idx = (long)g * n + j;
+  if (counting) a.feat_count[idx] += csum;
+  const float bnorm = sqrtf(bs);
+  const float beta = a.bias_decay[g];
+  const float bd = (beta != 0.f && bnorm > 0.f) ? beta / bnorm : 0.f;
+  float bc1, bc2;
+  bias_corrections(a.b1, a.b2, step + 1, bc1, bc2);
+  const float bj = a.b[idx];
+  const float gj = gsum * a.gscale + bd * bj;
+  const float mj = a.b1 * a.m[idx] + (1.f - a.b1) * gj;
+  const float vj = a.b2 * a.v[idx] + (1.f - a.b2) * gj * gj;
+  a.m[idx] = mj;
+  a.v[idx] = vj;
+  const float bn = bj - (a.lr[g] / bc1) * mj / (sqrtf(vj / bc2) + a.eps);
+  a.b[idx] = bn;
+  // this block's 32 columns of |b_new|^2 for the next step (lanes 0-31 of wave 0)
+  float sq = bn * bn;
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 32);
+  if (col == 0) t.bsq[((long)(par ^ 1) * a.nmodels + g) * nb + bx] = sq;
+}
+
+template <int NV, bool GBF>
+__global__ __launch_bounds__(256) void step_tail_kernel(AdamArgs a, BiasArgs b, TailArgs t) {
+  const int bid = blockIdx.x;
+  const int step = *a.step;          // completed steps before this one (t); read by every block
+  const int par = step & 1;
+  if (bid < t.nloss) {
+    tail_loss(b, t, bid, par);
+  } else if (bid < t.nloss + t.nbias) {
+    const int k = bid - t.nloss, nb = b.n / 32;
+    tail_bias(b, t, k % nb, k / nb, step, par);
+  } else if (bid < t.nloss + t.nbias + t.ngather) {
+    const long r = (long)(bid - t.nloss - t.nbias) * 4 + (threadIdx.x >> 6);
+    if (r < t.grows) {
+      const int lane = threadIdx.x & 63;
+      const long jj = (long)(step + 1 - t.ep0[0]) * t.grows + r;
+      long src = (jj >= 0 && jj < t.nperm) ? t.perm[jj] : 0;
+      src = (src >= 0 && src < t.nbuf) ? src : 0;
+      const u32x4_t* sp = t.gbuf + src * t.row_vec;
+      u32x4_t* op = t.gout + r * t.row_vec;
+      for (int v = lane; v < t.row_vec; v += 64) op[v] = sp[v];
+    }
+  } else {
+    adam_row<NV, GBF>(a, (long)(bid - t.nloss - t.nbias - t.ngather) * 4 + (threadIdx.x >> 6));
+  }
+  // the last block to finish advances the step counter (all reads of it happened before)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const int done = atomicAdd(t.ticket, 1);
+    if (done == (int)gridDim.x - 1) {
+      atomicExch(t.ticket, 0);
+      atomicAdd(b.step, 1);
+    }
+  }
+}
+
 }  // namespace scamd
 
 using namespace scamd;
@@ -380,12 +529,63 @@ int sc_bias_loss(int G, float* b, float* m, float* v, const float* colpart, int 
   a.enc_part = enc_part; a.enc_tiles = enc_tiles; a.dec_part = dec_part; a.dec_tiles = dec_tiles;
   a.cnt_part = cnt_part; a.feat_count = feat_count;
   a.l1 = l1; a.bias_decay = bias_decay; a.lr = lr; a.out = out;
-  a.n = n; a.B = B; a.d = d; a.gscale = gscale;
+  a.n = n; a.B = B; a.d = d; a.nmodels = G; a.gscale = gscale;
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.update = update; a.step = step;
   a.defer_step = defer_step ? 1 : 0;
   hipLaunchKernelGGL(loss_reduce_kernel, dim3(G), dim3(256), 0, stream, a);
   if (update || (cnt_part && feat_count))
     hipLaunchKernelGGL(bias_adam_kernel, dim3((n + 31) / 32, G), dim3(256), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// Fused step tail (see step_tail_kernel): row Adam over the sets + loss terms + bias Adam, the next
+// step's batch gather when gbuf != nullptr, and the device step counter advanced by the last block.
+// bsq: [2][G][n/32] b^2 partials (parity of *step current); ticket: one zero-initialised int.
+int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* m, float* const* v,
+                 void* const* shadow, float* const* norms, const int* rows, const int* norm, int d,
+                 int rows_per_model, const float* lr, float b1, float b2, float eps, int* step, int gbf16,
+                 int G, float* b, float* bm, float* bv, const float* colpart, int tm, const float* enc_part,
+                 int enc_tiles, const float* dec_part, int dec_tiles, const float* cnt_part, float* feat_count,
+                 const float* l1, const float* bias_decay, float* out, int n, int B, float gscale,
+                 float* bsq, int* ticket, const void* gbuf, long nbuf, const long* perm, long nperm,
+                 const int* ep0, void* gout, long grows, long row_bytes, hipStream_t stream) {
+  if (d % 256 || d > 4096 || nset < 1 || nset > 2 || n % 32 || !step || !ticket || !bsq) return 1;
+  if (gbuf && (row_bytes % 16 || nbuf < 1)) return 1;
+  AdamArgs a;
+  long total = 0;
+  for (int i = 0; i < nset; ++i) {
+    a.set[i] = {p[i], g[i], m[i], v[i], reinterpret_cast<uint16_t*>(shadow[i]), norms[i], rows[i], norm[i]};
+    total += rows[i];
+  }
+  if (nset == 1) a.set[1] = a.set[0], a.set[1].rows = 0;
+  a.nset = nset; a.d = d; a.rows_per_model = rows_per_model; a.lr = lr;
+  a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = 1.f; a.bc2 = 1.f; a.step = step;
+  a.nsplit = 1; a.gstride = 0; a.row0 = 0; a.live = nullptr;
+  BiasArgs ba;
+  ba.b = b; ba.m = bm; ba.v = bv; ba.colpart = colpart; ba.tm = tm;
+  ba.enc_part = enc_part; ba.enc_tiles = enc_tiles; ba.dec_part = dec_part; ba.dec_tiles = dec_tiles;
+  ba.cnt_part = cnt_part; ba.feat_count = feat_count;
+  ba.l1 = l1; ba.bias_decay = bias_decay; ba.lr = lr; ba.out = out;
+  ba.n = n; ba.B = B; ba.d = d; ba.nmodels = G; ba.gscale = gscale;
+  ba.b1 = b1; ba.b2 = b2; ba.eps = eps; ba.bc1 = 1.f; ba.bc2 = 1.f; ba.update = 1; ba.step = step;
+  ba.defer_step = 0;
+  TailArgs t;
+  t.bsq = bsq; t.ticket = ticket;
+  t.gbuf = reinterpret_cast<const u32x4_t*>(gbuf); t.nbuf = nbuf; t.perm = perm; t.nperm = nperm; t.ep0 = ep0;
+  t.gout = reinterpret_cast<u32x4_t*>(gout); t.grows = gbuf ? grows : 0;
+  t.row_vec = (int)(row_bytes / 16);
+  t.nloss = G; t.nbias = G * (n / 32); t.ngather = gbuf ? (int)((grows + 3) / 4) : 0;
+  const long blocks = t.nloss + t.nbias + t.ngather + (total + 3) / 4;
+#define SC_TAIL(NVV)                                                                                   \
+  case NVV:                                                                                            \
+    if (gbf16) hipLaunchKernelGGL((step_tail_kernel<NVV, true>), dim3(blocks), dim3(256), 0, stream, a, ba, t); \
+    else hipLaunchKernelGGL((step_tail_kernel<NVV, false>), dim3(blocks), dim3(256), 0, stream, a, ba, t);      \
+    break;
+  switch (d / 256) {
+    SC_TAIL(1) SC_TAIL(2) SC_TAIL(3) SC_TAIL(4)
+    default: return 1;
+  }
+#undef SC_TAIL
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -112,3 +112,41 @@ def test_prime_source_captures_without_running():
     e.step_source(1)
     torch.cuda.synchronize()
     assert len(e._graph) == n_graphs and e.step_count == 11 and int(e.step_dev.item()) == 11
+
+
+@pytest.mark.parametrize("kind", ["untied", "tied"])
+def test_fused_step_tail_matches_separate_kernels(kind, monkeypatch):
+    """The fused step tail (row Adam + loss terms + bias Adam + step counter in one launch, |b| from
+    parity-double-buffered b^2 partials) against the separate adam_rows / loss_reduce / bias_adam
+    kernels: parameters, moments, losses, feature counts and the device step counter, over eager steps
+    (counting and non-counting) with a non-zero bias decay, and after an out-of-band bias edit."""
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE, FunctionalTiedSAE
+
+    torch.manual_seed(21)
+    sig = FunctionalSAE if kind == "untied" else FunctionalTiedSAE
+    d, n, B = 512, 1024, 256
+    models = [sig.init(d, n, l1, bias_decay=bd, device=DEV) for l1, bd in ((1e-4, 0.0), (1e-3, 1e-3), (1e-2, 3e-2))]
+    for p, _ in models:
+        p["encoder_bias"].normal_(0.0, 0.1)
+    a = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=DEV, count_every=2)
+    monkeypatch.setenv("SC_FUSED_TAIL", "0")
+    b = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=DEV, count_every=2)
+    assert a._tail_ok and not b._tail_ok
+    feats = torch.nn.functional.normalize(torch.randn(2048, d, device=DEV), dim=-1)
+    for i in range(6):
+        if i == 3:  # an out-of-band edit of the bias (refresh_shadows marks the b^2 partials stale)
+            for e in (a, b):
+                e.params["encoder_bias"].mul_(0.5)
+                e.refresh_shadows()
+        x = (torch.relu(torch.randn(B, 2048, device=DEV) - 2.0) @ feats).to(torch.bfloat16)
+        oa = a.step_batch(x).clone()
+        ob = b.step_batch(x).clone()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(oa, ob, rtol=1e-5, atol=1e-6)
+    assert int(a.step_dev.item()) == int(b.step_dev.item()) == 6 and int(a._ticket.item()) == 0
+    for k in a.params:
+        torch.testing.assert_close(a.params[k], b.params[k], rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(a.m[k], b.m[k], rtol=1e-6, atol=1e-9)
+        torch.testing.assert_close(a.v[k], b.v[k], rtol=1e-6, atol=1e-12)
+    torch.testing.assert_close(a.feature_counts, b.feature_counts, rtol=0, atol=0)
