@@ -105,6 +105,10 @@ def parse(argv=None):
                     help="N>1: after the headline run, also time the other strategy (es <-> dp) and report it "
                          "under alt_parallelism")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of HIP graphs")
+    ap.add_argument("--dp-graph", type=int, default=1,
+                    help="dp / zero1: 1 = multi-step HIP graphs with the RCCL collectives captured inside them "
+                         "(parallel/graphed.py, native communicator); 0 = host-issued collectives between "
+                         "per-chunk graph replays (parallel/data_parallel.py, parallel/zero.py)")
     return ap.parse_args(argv)
 
 
@@ -190,6 +194,27 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
         return Runner(lambda: es.run_groups([1], sample_steps, pattern), dicts, close=es.flush,
                       run=lambda groups: es.run_groups(groups, sample_steps, pattern),
                       setup=lambda tiling: (ring.ensure_permutation(), es.prime_groups(tiling.sizes, pattern)))
+    if args.engine == "fused" and distributed and not args.no_graph and args.dp_graph:
+        # data parallel / ZeRO-1 with the collectives INSIDE multi-step HIP graphs (native RCCL
+        # communicator on its own stream, parallel/rccl.py + parallel/graphed.py)
+        from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+        from sparse_coding__amd.engine.graph_plan import count_pattern
+        from sparse_coding__amd.parallel.data_parallel import split_models
+        from sparse_coding__amd.parallel.graphed import GraphedDataParallel
+        from sparse_coding__amd.parallel.rccl import RcclComm
+
+        engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device)
+                   for m in split_models(models, args.dp_chunks)]
+        comm = RcclComm(info)
+        gdp = GraphedDataParallel(engines, info, comm, ring.graph_source(B, info.rank, info.world_size), mode=par,
+                                  grad_dtype=grad_dtype)
+
+        def run(groups):
+            for s in groups:
+                gdp.run(s, count_pattern(s, GRAPH_STEPS))
+
+        return Runner(lambda: run([1]), lambda: gdp.to_learned_dicts(device), close=comm.close, run=run,
+                      setup=lambda tiling: gdp.prime([count_pattern(s, GRAPH_STEPS) for s in tiling.sizes]))
     if args.engine == "fused" and distributed:
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
@@ -385,9 +410,13 @@ def main(argv=None):
     if distributed and args.compare_parallelism and args.models % info.world_size == 0:
         other = "dp" if par in ("es", "zero1") else "es"
         alt_models = [sig.init(args.d, n, float(l1), device=device) for l1 in l1s]
-        alt_runner = make_runner(other, args, info, sig, alt_models, ring, device, grad_dtype)
-        a_ms, a_value, _ = warm_and_time(alt_runner, args, info, B)
-        alt_runner.close()
+        try:
+            alt_runner = make_runner(other, args, info, sig, alt_models, ring, device, grad_dtype)
+            a_ms, a_value, _ = warm_and_time(alt_runner, args, info, B)
+            alt_runner.close()
+        except Exception as exc:  # the headline run above stands on its own
+            print(f"[bench] alt parallelism {other} failed: {exc!r}", file=sys.stderr)
+            a_ms = a_value = float("nan")
         alt = {"parallelism": f"{other}{info.world_size}", "value": round(a_value, 1), "ms_per_step": round(a_ms, 4),
                "predicted_ms_per_step": comm_model.predict(other, info.world_size, shape, args.dp_chunks),
                "dp_chunks": args.dp_chunks if other == "dp" else None,

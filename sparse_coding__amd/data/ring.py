@@ -141,10 +141,11 @@ class DeviceRing:
         self._cursor += need
         return out
 
-    def graph_source(self, batch_size: int) -> "RingGraphSource":
+    def graph_source(self, batch_size: int, rank: int = 0, world: int = 1) -> "RingGraphSource":
         """A batch source whose fetch can run INSIDE a training engine's HIP graph (see
-        ``RingGraphSource``); it walks this ring's permutations like ``sample``."""
-        return RingGraphSource(self, batch_size)
+        ``RingGraphSource``); it walks this ring's permutations like ``sample`` (``sample_shard``
+        for a data-parallel rank)."""
+        return RingGraphSource(self, batch_size, rank, world)
 
     def batches_per_epoch(self, batch_size: int) -> int:
         return self.size // batch_size
@@ -161,12 +162,17 @@ class RingGraphSource:
     captured step), ep0 a device scalar.  Between replays ``prepare(t)`` rolls a fresh permutation
     into the same buffer (and sets ep0 = t) when the epoch is exhausted -- the same
     without-replacement epochs as ``DeviceRing.sample``.  The fetch itself is one gather kernel
-    that is part of the step's graph, so no plain launch sits between graph replays."""
+    that is part of the step's graph, so no plain launch sits between graph replays.
 
-    def __init__(self, ring: DeviceRing, batch_size: int):
-        if ring.size < batch_size:
-            raise ValueError("ring holds fewer rows than one batch")
+    Data parallel (``rank`` of ``world``): every rank walks the same permutation (same ring seed) and
+    step t of rank r reads the block ``perm[((t - ep0) N + r) B, +B)`` -- its shard of the global batch
+    of N B rows, the ``DeviceRing.sample_shard`` (DistributedSampler) semantics."""
+
+    def __init__(self, ring: DeviceRing, batch_size: int, rank: int = 0, world: int = 1):
+        if ring.size < batch_size * world:
+            raise ValueError("ring holds fewer rows than one global batch")
         self.ring, self.B = ring, int(batch_size)
+        self.rank, self.world = int(rank), int(world)
         dev = ring.device
         # the permutation covers the rows valid at attach time (the captured gather reads this
         # buffer, so its size is fixed); rows appended later are walked after ``resize()``
@@ -179,7 +185,7 @@ class RingGraphSource:
         """Host bookkeeping before replaying steps ``step .. step + steps - 1``: a new permutation
         when they would run past the current one (a multi-step replay may start the next epoch
         up to ``steps - 1`` batches early: every epoch is still a without-replacement pass)."""
-        if self._ep0_host is None or (step - self._ep0_host + steps) * self.B > self.perm.numel():
+        if self._ep0_host is None or (step - self._ep0_host + steps) * self.B * self.world > self.perm.numel():
             self.perm.copy_(torch.randperm(self.rows, device=self.ring.device, generator=self.ring.gen))
             self.ep0.fill_(int(step))
             self._ep0_host = int(step)
@@ -187,14 +193,18 @@ class RingGraphSource:
 
     def tail_gather(self, out: torch.Tensor):
         """(ring buffer, permutation, epoch start, out): what a fused step tail needs to fetch the NEXT
-        step's rows into ``out`` (csrc/adam.hip step_tail_kernel, row ``(t + 1 - ep0) * B + r``)."""
+        step's rows into ``out`` (csrc/adam.hip step_tail_kernel, row ``(t + 1 - ep0) * B + r``);
+        None for a data-parallel shard (the tail's fetch has no rank offset)."""
+        if self.world != 1:
+            return None
         return (self.ring.buf, self.perm, self.ep0, out)
 
     def gather(self, out: torch.Tensor, step_dev: torch.Tensor):
         """The capturable fetch: ``out`` [B, ...] <- this step's rows."""
         from ..ops.rows import gather_rows_perm
 
-        return gather_rows_perm(self.ring.buf, self.perm, step_dev, self.ep0, out)
+        return gather_rows_perm(self.ring.buf, self.perm, step_dev, self.ep0, out, stride=self.B * self.world,
+                                offset=self.rank * self.B)
 
 
 def _kernels_available() -> bool:

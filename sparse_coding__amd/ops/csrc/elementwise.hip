@@ -136,11 +136,13 @@ __global__ __launch_bounds__(256) void gather_rows_perm_kernel(const u32x4_t* __
                                                                const long* __restrict__ perm, long nperm,
                                                                const int* __restrict__ step,
                                                                const int* __restrict__ ep0,
-                                                               u32x4_t* __restrict__ out, long rows, int row_vec) {
+                                                               u32x4_t* __restrict__ out, long rows, int row_vec,
+                                                               long stride, long offset) {
   const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int lane = threadIdx.x & 63;
-  const long j = (long)(step[0] - ep0[0]) * rows + r;
+  // (data parallel: stride = N B, offset = rank B -- this rank's shard of each global batch)
+  const long j = (long)(step[0] - ep0[0]) * stride + offset + r;
   long src = (j >= 0 && j < nperm) ? perm[j] : 0;
   src = (src >= 0 && src < nbuf) ? src : 0;
   const u32x4_t* s = buf + src * row_vec;
@@ -213,12 +215,12 @@ int sc_gather_rows(const void* buf, const long* idx, void* out, long rows, long 
 }
 
 int sc_gather_rows_perm(const void* buf, long nbuf, const long* perm, long nperm, const int* step, const int* ep0,
-                        void* out, long rows, long row_bytes, hipStream_t stream) {
-  if (row_bytes % 16 || rows < 0 || nbuf < 1) return 1;
+                        void* out, long rows, long row_bytes, long stride, long offset, hipStream_t stream) {
+  if (row_bytes % 16 || rows < 0 || nbuf < 1 || stride < rows || offset < 0) return 1;
   if (rows == 0) return 0;
   hipLaunchKernelGGL(gather_rows_perm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
                      reinterpret_cast<const u32x4_t*>(buf), nbuf, perm, nperm, step, ep0,
-                     reinterpret_cast<u32x4_t*>(out), rows, (int)(row_bytes / 16));
+                     reinterpret_cast<u32x4_t*>(out), rows, (int)(row_bytes / 16), stride, offset);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

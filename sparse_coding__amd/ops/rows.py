@@ -30,10 +30,11 @@ def gather_rows(buf: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None =
 
 
 def gather_rows_perm(buf: torch.Tensor, perm: torch.Tensor, step: torch.Tensor, ep0: torch.Tensor,
-                     out: torch.Tensor) -> torch.Tensor:
-    """out[i] = buf[perm[(step - ep0) * rows + i]] with ``step`` / ``ep0`` int32 [1] DEVICE scalars, so
-    the fetch can be captured in a HIP graph and still walk the permutation (rows = out.shape[0]).
-    Positions past ``perm`` (a host bookkeeping error) read row 0 instead of faulting."""
+                     out: torch.Tensor, stride: int | None = None, offset: int = 0) -> torch.Tensor:
+    """out[i] = buf[perm[(step - ep0) * stride + offset + i]] with ``step`` / ``ep0`` int32 [1] DEVICE
+    scalars, so the fetch can be captured in a HIP graph and still walk the permutation (default
+    stride = rows = out.shape[0]; data parallel: stride = N B, offset = rank B).  Positions past
+    ``perm`` (a host bookkeeping error) read row 0 instead of faulting."""
     if not (buf.is_cuda and buf.is_contiguous() and out.is_contiguous()):
         raise ValueError("gather_rows_perm needs contiguous GPU buffers")
     row_bytes = buf[0].numel() * buf.element_size()
@@ -44,8 +45,10 @@ def gather_rows_perm(buf: torch.Tensor, perm: torch.Tensor, step: torch.Tensor, 
     for t in (step, ep0):
         if t.dtype != torch.int32 or t.numel() < 1 or t.device != buf.device:
             raise ValueError("step / ep0 must be int32 device scalars")
+    stride = out.shape[0] if stride is None else int(stride)
     rc = _lib.lib().sc_gather_rows_perm(_lib.ptr(buf), buf.shape[0], _lib.ptr(perm), perm.numel(), _lib.ptr(step),
-                                        _lib.ptr(ep0), _lib.ptr(out), out.shape[0], row_bytes, _lib.stream_handle())
+                                        _lib.ptr(ep0), _lib.ptr(out), out.shape[0], row_bytes, stride, int(offset),
+                                        _lib.stream_handle())
     _lib.check(rc, "sc_gather_rows_perm")
     return out
 

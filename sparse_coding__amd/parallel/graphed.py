@@ -1,0 +1,236 @@
+"""Data-parallel (DP / ZeRO-1) fused training with the collectives INSIDE multi-step HIP graphs.
+
+The host-issued data-parallel paths (``parallel/data_parallel.py``, ``parallel/zero.py``) replay a
+"grads" and an "update" graph per model chunk and issue the collectives between them through
+ProcessGroupNCCL -- four graph replays and their idle gaps per step at two chunks, plus an eager
+batch gather.  Here a group of S optimizer steps is ONE graph: per step the rank's batch shard is
+fetched from the HBM ring inside the graph (``RingGraphSource`` rank shard, device step counter),
+every chunk computes its gradients, its reduction runs on the communicator's own stream
+(``parallel/rccl.py``: RCCL enqueued on our stream, captured as graph nodes) while the next chunk
+computes, and the chunk's update joins on exactly that reduction's event::
+
+    step s:  fetch x_s | chunk 0 fwd+bwd -> reduce(0) ....................... (comm stream)
+                       | update(K-1 of step s-1)     <- waits reduce(K-1, s-1)   (cross-step)
+                       | chunk 1 fwd+bwd -> reduce(1) ...
+                       | update(0)                   <- waits reduce(0)
+    end of group: update(K-1)
+
+``mode="dp"``: all-reduce of each chunk's flat fp32 gradient (pre-scaled by 1/N in the GEMM
+epilogues, so the SUM is the global-batch mean).  ``mode="zero1"``: each chunk's dictionary rows
+are sharded over ranks -- reduce-scatter of the weight gradients (fp32; or bf16 transport by
+all-to-all with fp32 accumulation on the owner), all-reduce of the small bias / extras tail, Adam on
+the owned rows only, all-gather of the updated bf16 shadows and row norms (waited on by the chunk's
+next compute).  Per model the update is exactly data-parallel Adam on the global batch of N B rows
+(reference DDP semantics, ``experiments/huge_batch_size.py:259-345``).
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from .dist import DistInfo
+from .zero import shard_range
+
+
+class _Chunk:
+    def __init__(self, engine, mode: str, info: DistInfo, grad_dtype):
+        e = self.engine = engine
+        kind = getattr(e, "kind", None)
+        if kind not in ("untied", "tied") or e.learned_center or e.nactive is not None:
+            raise NotImplementedError(f"graphed data parallel of engine kind {kind} (masked / learned centre)")
+        if e.wsplit != 1 or e.g_bf is not None:
+            raise NotImplementedError("graphed data parallel needs the engine's flat fp32 gradients (wgrad_split=1)")
+        self.mode = mode
+        G, n, d = e.n_models, e.n, e.d
+        N = max(1, info.world_size)
+        self.world = N
+        if mode == "zero1":
+            self.lo, self.hi = shard_range(G * n, info.rank, N)
+            rows = self.hi - self.lo
+            dev = e.device
+            self.srcs = [e.g_dec] + ([e.g_enc] if kind == "untied" else [])
+            self.shards = [torch.empty(rows, d, device=dev) for _ in self.srcs]
+            self.lowp = grad_dtype != torch.float32 and N > 1
+            if self.lowp:
+                self.send = [torch.empty(G * n * d, device=dev, dtype=grad_dtype) for _ in self.srcs]
+                self.recv = [torch.empty(N * rows * d, device=dev, dtype=grad_dtype) for _ in self.srcs]
+            self.tail = e._g_flat[G * n * d:]  # [g_bias | extras]: all-reduced whole
+        self.red_ev = None    # completion of this chunk's gradient reduction (current step)
+        self.gath_ev = None   # completion of this chunk's shadow all-gather (ZeRO-1)
+
+
+class GraphedDataParallel:
+    def __init__(self, engines: Sequence, info: DistInfo, comm, source, mode: str = "dp",
+                 grad_dtype: torch.dtype = torch.float32, count_every: int = 8, sync_params: bool = True):
+        if mode not in ("dp", "zero1"):
+            raise ValueError(f"mode must be 'dp' or 'zero1', got {mode!r}")
+        self.info, self.comm, self.source, self.mode = info, comm, source, mode
+        self.chunks = [_Chunk(e, mode, info, grad_dtype) for e in engines]
+        e0 = engines[0]
+        self.B, self.d, self.device = e0.batch_size, e0.d, e0.device
+        for e in engines:
+            if e.batch_size != self.B or e.d != self.d:
+                raise ValueError("every chunk engine must take the same [B, d] batch")
+            e.grad_scale = 1.0 / max(1, info.world_size)
+        self.x = torch.empty(self.B, self.d, device=self.device, dtype=torch.bfloat16)
+        self.count_every = count_every
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        if sync_params and info.world_size > 1:  # identical initial parameters: rank 0's
+            for e in engines:
+                for t in e.params.values():
+                    comm.broadcast(t)
+                e.refresh_shadows()
+            torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ one step (captured)
+    def _compute(self, c: _Chunk, count: bool):
+        e = c.engine
+        e._counted = count
+        xp = e.prepare(self.x)
+        e.forward(xp, count)
+        e.wgrad_first(xp)
+        e.wgrad_second(xp, reduce_bias=True)
+
+    def _reduce(self, c: _Chunk):
+        e = c.engine
+        if self.mode == "dp":
+            c.red_ev = self.comm.all_reduce(e.grad_all, overlap=True)
+            return
+        evs = []
+        for i, (src, dst) in enumerate(zip(c.srcs, c.shards)):
+            if c.lowp:  # bf16 transport, fp32 accumulation on the row owner
+                c.send[i].copy_(src.view(-1))
+                evs.append(self.comm.all_to_all(c.recv[i], c.send[i], overlap=True))
+            elif c.world > 1:
+                evs.append(self.comm.reduce_scatter(dst.view(-1), src.view(-1), overlap=True))
+        evs.append(self.comm.all_reduce(c.tail, overlap=True))
+        c.red_ev = evs
+
+    def _wait(self, evs):
+        if evs is None:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        for ev in (evs if isinstance(evs, list) else [evs]):
+            if ev is not None:
+                cur.wait_event(ev)
+
+    def _update(self, c: _Chunk):
+        from ..ops import adam as adam_ops
+
+        e = c.engine
+        self._wait(c.red_ev)
+        c.red_ev = None
+        if self.mode == "dp":
+            e.adam_rows_all()
+            e._bias_loss(update=True, reduced=True)
+            return
+        G, n, d = e.n_models, e.n, e.d
+        lo, hi = c.lo, c.hi
+        if c.world == 1:  # one rank: the shard is the whole gradient
+            grads = c.srcs
+        else:
+            if c.lowp:
+                for i, dst in enumerate(c.shards):
+                    torch.sum(c.recv[i].view(c.world, -1), dim=0, dtype=torch.float32, out=dst.view(-1))
+            grads = c.shards
+        rows = lambda t: t.view(G * n, d)[lo:hi]  # noqa: E731
+        g = [gg.view(-1, d) if c.world == 1 else gg for gg in grads]
+        if e.kind == "untied":
+            sets = [dict(p=rows(e.params["decoder"]), g=rows(g[0]) if c.world == 1 else g[0], m=rows(e.m["decoder"]),
+                         v=rows(e.v["decoder"]), shadow=rows(e.dec_shadow), norms=e.norms.view(-1)[lo:hi], norm=True),
+                    dict(p=rows(e.params["encoder"]), g=rows(g[1]) if c.world == 1 else g[1], m=rows(e.m["encoder"]),
+                         v=rows(e.v["encoder"]), shadow=rows(e.enc_shadow), norms=None, norm=False)]
+        else:
+            sets = [dict(p=rows(e.params["encoder"]), g=rows(g[0]) if c.world == 1 else g[0], m=rows(e.m["encoder"]),
+                         v=rows(e.v["encoder"]), shadow=rows(e.enc_shadow), norms=e.norms.view(-1)[lo:hi], norm=True)]
+        adam_ops.adam_rows(sets, e.lr, e.step_count + 1, *e.betas, e.eps, rows_per_model=n, step_dev=e.step_dev,
+                           row0=lo)
+        e._bias_loss(update=True, reduced=True)
+        if c.world > 1:  # every rank's updated shadows (and norms) for the chunk's next compute
+            evs = []
+            for sh in ([e.dec_shadow] if e.kind == "untied" else []) + [e.enc_shadow]:
+                flat = sh.view(-1)
+                evs.append(self.comm.all_gather(flat, flat[lo * d:hi * d], overlap=True))
+            evs.append(self.comm.all_gather(e.norms.view(-1), e.norms.view(-1)[lo:hi], overlap=True))
+            c.gath_ev = evs
+
+    def _steps(self, pattern: Sequence[bool]):
+        """The kernels (and collectives) of ``len(pattern)`` steps; capture target."""
+        e0 = self.chunks[0].engine
+        K = len(self.chunks)
+        prev: Optional[_Chunk] = None
+        for count in pattern:
+            if prev is not None and K == 1:  # one chunk: its update precedes its next compute (and the fetch)
+                self._update(prev)
+                prev = None
+            self.source.gather(self.x, e0.step_dev)
+            for c in self.chunks:
+                if c.gath_ev is not None:  # ZeRO-1: this chunk's shadows from the last update
+                    self._wait(c.gath_ev)
+                    c.gath_ev = None
+                self._compute(c, count)
+                self._reduce(c)
+                if prev is not None:
+                    self._update(prev)
+                prev = c
+        self._update(prev)
+        for c in self.chunks:  # every side-stream op joins the capture before it ends
+            self._wait(c.gath_ev)
+            c.gath_ev = None
+        self.comm.join()
+
+    def _graph(self, pattern):
+        key = tuple(bool(c) for c in pattern)
+        g = self._graphs.get(key)
+        if g is None:
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._steps(key)
+            from ..ops import _lib
+
+            _lib.upload_graph(g, self.device)
+            self._graphs[key] = g
+        return g
+
+    # ------------------------------------------------------------------ API
+    def prime(self, patterns: Sequence[Sequence[bool]]):
+        """Capture + upload (nothing runs) every group graph later replays use."""
+        for p in patterns:
+            self._graph(p)
+        e0 = self.chunks[0].engine
+        self.source.prepare(e0.step_count, max([1] + [len(p) for p in patterns]))
+
+    def run(self, steps: int, pattern: Optional[Sequence[bool]] = None):
+        """``steps`` data-parallel optimizer steps as ONE graph replay."""
+        e0 = self.chunks[0].engine
+        if pattern is None:
+            pattern = [i % self.count_every == 0 for i in range(int(steps))]
+        pattern = tuple(bool(c) and e0.track_feature_counts for c in pattern)
+        self.source.prepare(e0.step_count, len(pattern))
+        self._graph(pattern).replay()
+        for c in self.chunks:
+            for count in pattern:
+                c.engine._counted = count
+                c.engine._host_step()
+        return [c.engine.out for c in self.chunks]
+
+    def gather_masters(self):
+        """ZeRO-1: every rank's fp32 masters and moments complete (exports / checkpoints)."""
+        if self.mode != "zero1" or self.info.world_size <= 1:
+            return
+        for c in self.chunks:
+            e = c.engine
+            d = e.d
+            keys = ["decoder", "encoder"] if e.kind == "untied" else ["encoder"]
+            for store in (e.params, e.m, e.v):
+                for k in keys:
+                    flat = store[k].view(-1)
+                    self.comm.all_gather(flat, flat[c.lo * d:c.hi * d])
+        torch.cuda.synchronize(self.device)
+
+    def to_learned_dicts(self, device="cpu") -> List:
+        self.gather_masters()
+        return [ld for c in self.chunks for ld in c.engine.to_learned_dicts(device)]

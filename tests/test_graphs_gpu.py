@@ -150,3 +150,45 @@ def test_fused_step_tail_matches_separate_kernels(kind, monkeypatch):
         torch.testing.assert_close(a.m[k], b.m[k], rtol=1e-6, atol=1e-9)
         torch.testing.assert_close(a.v[k], b.v[k], rtol=1e-6, atol=1e-12)
     torch.testing.assert_close(a.feature_counts, b.feature_counts, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("mode,chunks", [("dp", 1), ("dp", 2), ("zero1", 2)])
+def test_graphed_data_parallel_one_rank_matches_single_engine(mode, chunks):
+    """Data parallel with the collectives captured in multi-step graphs (native RCCL communicator on
+    its own stream, one rank) == the single-engine multi-step graph on the same ring batches:
+    parameters, losses and feature counts (model chunks, cross-step update order, ZeRO-1 shards)."""
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.engine.graph_plan import count_pattern
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+    from sparse_coding__amd.parallel.data_parallel import split_models
+    from sparse_coding__amd.parallel.dist import DistInfo
+    from sparse_coding__amd.parallel.graphed import GraphedDataParallel
+    from sparse_coding__amd.parallel.rccl import RcclComm
+
+    torch.manual_seed(17)
+    d, n, B = 512, 1024, 256
+    rows = (torch.randn(B * 40, d, device=DEV) * 2).to(torch.bfloat16)
+    rings = []
+    for _ in range(2):
+        r = DeviceRing(rows.shape[0], d, device=DEV, seed=6)
+        r.push(rows)
+        rings.append(r)
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3, 3e-3, 1e-2)]
+    info = DistInfo(device=torch.device(DEV))
+    comm = RcclComm(info)
+    engines = [FusedSAEEnsemble(m, FunctionalSAE, lr=1e-3, batch_size=B, device=DEV) for m in split_models(models, chunks)]
+    gdp = GraphedDataParallel(engines, info, comm, rings[0].graph_source(B), mode=mode)
+    single = FusedSAEEnsemble(models, FunctionalSAE, lr=1e-3, batch_size=B, device=DEV).enable_graph()
+    single.attach_source(rings[1].graph_source(B))
+    for s in (3, 5, 3):
+        gdp.run(s, count_pattern(s))
+        single.step_source(s, count_pattern(s))
+    torch.cuda.synchronize()
+    comm.close()
+    for k in single.params:
+        got = torch.cat([e.params[k] for e in engines])
+        torch.testing.assert_close(got, single.params[k], rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(torch.cat([e.feature_counts for e in engines]), single.feature_counts, rtol=0, atol=0)
+    torch.testing.assert_close(torch.cat([e.out for e in engines])[:, :3], single.out[:, :3], rtol=1e-4, atol=1e-6)
+    assert all(int(e.step_dev.item()) == 11 for e in engines)
