@@ -15,7 +15,7 @@ for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursiv
     for r in csv.DictReader(open(f)):
         name = r.get("Kernel_Name", "?")
         short = name.split("(")[0].replace("void ", "").replace("scamd::", "")
-        if any(t in name for t in ("sae_gemm_kernel", "adam", "topk", "bias_loss", "rowblock")):
+        if any(t in name for t in ("sae_gemm_kernel", "adam", "topk", "bias_loss", "step_tail", "fista")):
             key = name[:160] + (f" grid={r.get('Grid_Size')}" if "rowblock" in name else "")
             vals[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
             meta[key] = (r.get("VGPR_Count"), r.get("Accum_VGPR_Count"), r.get("LDS_Block_Size"), r.get("Grid_Size"),

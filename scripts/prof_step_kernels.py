@@ -1,5 +1,7 @@
-"""Runs each kernel of the fused SAE step (config 2 shapes) a few times, plus the top-k
-select of config 4, for rocprofv3 counter collection (scripts/gpu.sh pmc)."""
+"""Runs each kernel of the fused SAE step (config 2 shapes, as the engine launches them: the
+code gradient from the encoder's activity mask, the fused step tail) a few times, plus the top-k
+select of config 4 and a config-5 FISTA solve (d = n = 1024, 8 models, 20 iterations), for
+rocprofv3 counter collection (scripts/gpu.sh pmc)."""
 import os
 import sys
 
@@ -21,16 +23,25 @@ for _ in range(3):
     e.step_batch(x)
 torch.cuda.synchronize()
 for _ in range(5):
-    gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c, e.enc_part, None, None)
+    gemm.encode_relu(x, e.enc_shadow, e.params["encoder_bias"], e.c, e.enc_part, None, None, mask_out=e.cmask)
     gemm.decode_residual(e.c, e.dec_shadow, x, e.r, e.dec_part)
-    gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart)
+    gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart, mask=e.cmask)
     gemm.weight_grads([[(e.c, e.r)], [(e.dpre, x)]], [e.g_dec, e.g_enc], 1e-6)
-    adam_ops.adam_rows(e._adam_sets(), e.lr, 5, step_dev=None)
+    e._apply_update_kernels()  # the fused step tail (row Adam + losses + bias Adam)
 torch.cuda.synchronize()
 # config 4 top-k select: 8 models, B=2048, n=6144
 scores = torch.randn(8, 2048, 6144, device=dev)
 k = torch.tensor([8, 16, 24, 32, 48, 64, 96, 128], dtype=torch.int32, device=dev)
 for _ in range(3):
     topk_ops.topk_select(scores, k, 128)
+torch.cuda.synchronize()
+# config 5 FISTA: Gram-form persistent solve, 8 models, d = n = 1024, B = 2048
+from sparse_coding__amd.ops import fista as F  # noqa: E402
+
+D = torch.nn.functional.normalize(torch.randn(8, 1024, 1024, device=dev), dim=-1)
+X = torch.randn(2048, 1024, device=dev) * 0.1
+lam = torch.full((8,), 1e-3, device=dev)
+for _ in range(2):
+    F.fista(X, D, lam, iters=20, backend="hip")
 torch.cuda.synchronize()
 print("done")

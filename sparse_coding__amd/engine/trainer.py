@@ -65,14 +65,22 @@ class EnsembleTrainer:
         self.n_models = len(models)
         self.meta = [dict(b) for _, b in models]
         self.es = None
+        self.dp = None
         self.local = slice(0, len(models))
-        if parallel == "es":
+        if parallel in ("dp", "zero1"):
+            # data parallel over the ranks (each rank passes its own rows to `step`): on MI355X the
+            # fused engine with the RCCL collectives captured in its step graph (parallel/graphed.py,
+            # native communicator); elsewhere the eager ensemble with gloo / ProcessGroup collectives
+            if objective != "loss" or sig is FunctionalFista:
+                raise ValueError("parallel='dp'/'zero1' trains the SAE objectives (no FISTA hooks)")
+            self._init_dp(models, sig, lr, batch_size, device, engine, dist, parallel)
+        elif parallel == "es":
             # ensemble-axis sharding (parallel/ensemble_shard.py): this rank trains its block
             # of the models on the all-gathered global batch; `step` takes this rank's rows
             self._init_sharded(models, sig, lr, batch_size, device, engine, dist, use_graph)
             models = list(models[self.local])
         elif parallel != "none":
-            raise ValueError(f"parallel must be 'none' or 'es', got {parallel!r}")
+            raise ValueError(f"parallel must be 'none', 'es', 'dp' or 'zero1', got {parallel!r}")
         if objective not in ("loss", "fista_loss"):
             raise ValueError(f"objective must be 'loss' or 'fista_loss', got {objective!r}")
         if objective == "fista_loss" and (sig is not FunctionalFista or parallel != "none"):
@@ -85,7 +93,9 @@ class EnsembleTrainer:
             raise ValueError(f"fused engine requested but unavailable: {why}")
         self.engine_reason = why
         self.kind = "eager"
-        if self.es is not None:
+        if self.dp is not None:
+            self.kind = self._dp_kind
+        elif self.es is not None:
             self.impl = self.es.engine
             self.kind = self._es_kind
         elif objective == "fista_loss":
@@ -135,6 +145,33 @@ class EnsembleTrainer:
         self.last_losses: Dict[str, torch.Tensor] = {}
         self.steps = 0
 
+    def _init_dp(self, models, sig, lr, batch_size, device, engine, dist, mode):
+        from ..parallel.dist import DistInfo
+
+        info = dist if dist is not None else DistInfo(device=torch.device(device))
+        fused, _ = _fused_ok(models, sig, batch_size, device) if engine in ("auto", "fused") else (False, "")
+        if fused and sig is not TopKEncoder and getattr(sig, "fused_kind", None) in ("untied", "tied"):
+            from ..parallel.graphed import GraphedDataParallel
+            from ..parallel.rccl import RcclComm
+            from .fused import FusedSAEEnsemble
+
+            eng = FusedSAEEnsemble(models, sig, lr=lr, batch_size=batch_size, device=device)
+            self._comm = RcclComm(info)
+            self.dp = GraphedDataParallel([eng], info, self._comm, None, mode=mode)
+            self.impl = eng
+            self._dp_kind = f"{mode}-graphed"
+            return
+        from ..parallel.data_parallel import ChunkedDataParallel, DataParallelEnsemble, EagerChunk
+        from ..parallel.zero import ZeroEagerChunk
+
+        ens = FunctionalEnsemble(models, sig, adam, {"lr": lr}, device=device)
+        self.impl = ens
+        if mode == "zero1":
+            self.dp = ChunkedDataParallel([ZeroEagerChunk(ens, info)], info)
+        else:
+            self.dp = DataParallelEnsemble(ens, info)
+        self._dp_kind = f"{mode}-eager"
+
     def _init_sharded(self, models, sig, lr, batch_size, device, engine, dist, use_graph):
         from ..parallel.dist import DistInfo
         from ..parallel.ensemble_shard import EnsembleSharded, shard_range
@@ -167,6 +204,18 @@ class EnsembleTrainer:
     def step(self, batch: torch.Tensor) -> torch.Tensor:
         """One optimizer step of every model; returns per-model total loss [G] on device
         (with ensemble sharding: of this rank's models, on the gathered global batch)."""
+        if self.dp is not None:  # data parallel: `batch` is this rank's rows
+            if self.kind.endswith("graphed"):
+                out = self.dp.step_batch(batch)[0]
+                self.last_losses = {"loss": out[:, 0], "l_reconstruction": out[:, 1], "l_l1": out[:, 2],
+                                    "l_bias_decay": out[:, 3], "l0": out[:, 4]}
+            else:
+                res = self.dp.step_batch(batch.to(self.device, torch.float32))
+                loss = res[0]  # (loss, aux) of the eager DP wrapper / the chunk losses of ZeRO-1
+                self.last_losses = dict(loss) if isinstance(loss, dict) else {"loss": loss}
+            self.steps += 1
+            self.last_loss = self.last_losses["loss"]
+            return self.last_loss
         if self.es is not None:
             x = batch.to(self.device, self.es.gbuf[0].dtype)
             out = self.es.step_batch(x)
@@ -243,6 +292,9 @@ class EnsembleTrainer:
         if self.es is not None:
             lds = self.es.to_learned_dicts(self.meta, self.sig, device)
             return list(zip(lds, self.hyperparams(ensemble_hyperparams, buffer_hyperparams)))
+        if self.dp is not None and self.kind.endswith("graphed"):
+            lds = self.dp.to_learned_dicts(device)
+            return list(zip(lds, self.hyperparams(ensemble_hyperparams, buffer_hyperparams)))
         lds = self.impl.to_learned_dicts(device)
         return list(zip(lds, self.hyperparams(ensemble_hyperparams, buffer_hyperparams)))
 
@@ -255,7 +307,12 @@ class EnsembleTrainer:
 
     def state_dict(self) -> Dict[str, Any]:
         st = {"kind": self.kind, "steps": self.steps, "name": self.name, "args": self.args}
-        if self.kind == "fused-sae":
+        if self.kind == "zero1-eager":
+            raise NotImplementedError("checkpoint of the eager ZeRO-1 trainer (its moments are sharded)")
+        if self.kind.endswith("-graphed"):
+            self.dp.gather_masters()  # ZeRO-1: every rank's masters / moments complete
+            st["impl"] = self.impl.state_dict()
+        elif self.kind == "fused-sae":
             st["impl"] = self.impl.state_dict()
         elif self.kind == "fused-topk":
             st["impl"] = {"params": self.impl.params, "m": self.impl.m, "v": self.impl.v,
@@ -273,7 +330,8 @@ class EnsembleTrainer:
             raise ValueError(f"checkpoint engine {st['kind']} != {self.kind}")
         self.steps = int(st["steps"])
         imp = st["impl"]
-        if self.kind in ("fused-sae", "analytic", "fista-loss", "fista-loss-fused", "unrolled"):
+        if self.kind in ("fused-sae", "analytic", "fista-loss", "fista-loss-fused", "unrolled", "dp-graphed",
+                         "zero1-graphed"):
             self.impl.load_state_dict(imp)
         elif self.kind == "fused-topk":
             for d_ in ("params", "m", "v"):

@@ -51,7 +51,7 @@ def signatures():
         "sc_bias_loss": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int,
                          c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_int, c_int, c_int, c_float, c_float, c_float, c_float,
-                         c_float, c_float, c_int, c_void_p, c_void_p, c_int],
+                         c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_int],
     }
     optional = {
         "sc_topk_select": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -215,7 +215,8 @@ struct BiasArgs {
   int enc_tiles;
   const float* dec_part;           // [G][dec_tiles] (sum R^2)
   int dec_tiles;
-  const float* cnt_part;           // optional [G][tm][n] feature on-counts
+  const float* cnt_part;           // optional [G][cnt_tm][n] feature on-counts
+  int cnt_tm;                      // row-tile slots of cnt_part (the bias gradient may arrive reduced: tm = 1)
   float* feat_count;               // optional [G][n] accumulated counts
   const float* l1;                 // [G]
   const float* bias_decay;         // [G]
@@ -297,11 +298,10 @@ __global__ __launch_bounds__(256) void bias_adam_kernel(BiasArgs a) {
   const bool counting = a.cnt_part && a.feat_count;
   float gs = 0.f, cs = 0.f;
   if (ok) {
-    for (int t = grp; t < a.tm; t += 8) {
-      const long o = ((long)g * a.tm + t) * n + j;
-      if (a.update) gs += a.colpart[o];
-      if (counting) cs += a.cnt_part[o];
-    }
+    if (a.update)
+      for (int t = grp; t < a.tm; t += 8) gs += a.colpart[((long)g * a.tm + t) * n + j];
+    if (counting)
+      for (int t = grp; t < a.cnt_tm; t += 8) cs += a.cnt_part[((long)g * a.cnt_tm + t) * n + j];
   }
   gred[grp][col] = gs;
   cred[grp][col] = cs;
@@ -523,11 +523,11 @@ int sc_bias_loss(int G, float* b, float* m, float* v, const float* colpart, int 
                  const float* enc_part, int enc_tiles, const float* dec_part, int dec_tiles,
                  const float* cnt_part, float* feat_count, const float* l1, const float* bias_decay,
                  const float* lr, float* out, int n, int B, int d, float gscale, float b1, float b2, float eps,
-                 float bc1, float bc2, int update, int* step, hipStream_t stream, int defer_step) {
+                 float bc1, float bc2, int update, int* step, hipStream_t stream, int defer_step, int cnt_tm) {
   BiasArgs a;
   a.b = b; a.m = m; a.v = v; a.colpart = colpart; a.tm = tm;
   a.enc_part = enc_part; a.enc_tiles = enc_tiles; a.dec_part = dec_part; a.dec_tiles = dec_tiles;
-  a.cnt_part = cnt_part; a.feat_count = feat_count;
+  a.cnt_part = cnt_part; a.feat_count = feat_count; a.cnt_tm = cnt_tm > 0 ? cnt_tm : tm;
   a.l1 = l1; a.bias_decay = bias_decay; a.lr = lr; a.out = out;
   a.n = n; a.B = B; a.d = d; a.nmodels = G; a.gscale = gscale;
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = bc1; a.bc2 = bc2; a.update = update; a.step = step;
@@ -564,7 +564,7 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
   BiasArgs ba;
   ba.b = b; ba.m = bm; ba.v = bv; ba.colpart = colpart; ba.tm = tm;
   ba.enc_part = enc_part; ba.enc_tiles = enc_tiles; ba.dec_part = dec_part; ba.dec_tiles = dec_tiles;
-  ba.cnt_part = cnt_part; ba.feat_count = feat_count;
+  ba.cnt_part = cnt_part; ba.feat_count = feat_count; ba.cnt_tm = tm;
   ba.l1 = l1; ba.bias_decay = bias_decay; ba.lr = lr; ba.out = out;
   ba.n = n; ba.B = B; ba.d = d; ba.nmodels = G; ba.gscale = gscale;
   ba.b1 = b1; ba.b2 = b2; ba.eps = eps; ba.bc1 = 1.f; ba.bc2 = 1.f; ba.update = 1; ba.step = step;

@@ -165,7 +165,8 @@ class GraphedDataParallel:
             if prev is not None and K == 1:  # one chunk: its update precedes its next compute (and the fetch)
                 self._update(prev)
                 prev = None
-            self.source.gather(self.x, e0.step_dev)
+            if self.source is not None:  # else the caller filled self.x (one step per replay)
+                self.source.gather(self.x, e0.step_dev)
             for c in self.chunks:
                 if c.gath_ev is not None:  # ZeRO-1: this chunk's shadows from the last update
                     self._wait(c.gath_ev)
@@ -201,7 +202,8 @@ class GraphedDataParallel:
         for p in patterns:
             self._graph(p)
         e0 = self.chunks[0].engine
-        self.source.prepare(e0.step_count, max([1] + [len(p) for p in patterns]))
+        if self.source is not None:
+            self.source.prepare(e0.step_count, max([1] + [len(p) for p in patterns]))
 
     def run(self, steps: int, pattern: Optional[Sequence[bool]] = None):
         """``steps`` data-parallel optimizer steps as ONE graph replay."""
@@ -209,13 +211,24 @@ class GraphedDataParallel:
         if pattern is None:
             pattern = [i % self.count_every == 0 for i in range(int(steps))]
         pattern = tuple(bool(c) and e0.track_feature_counts for c in pattern)
-        self.source.prepare(e0.step_count, len(pattern))
+        if self.source is None and len(pattern) != 1:
+            raise ValueError("without a batch source every replay is one step on self.x (step_batch)")
+        if self.source is not None:
+            self.source.prepare(e0.step_count, len(pattern))
         self._graph(pattern).replay()
         for c in self.chunks:
             for count in pattern:
                 c.engine._counted = count
                 c.engine._host_step()
         return [c.engine.out for c in self.chunks]
+
+    def step_batch(self, x_local: torch.Tensor, count: Optional[bool] = None):
+        """One step on this rank's rows ``x_local`` [B, d] (no in-graph source: EnsembleTrainer)."""
+        self.x.copy_(x_local.to(self.device, torch.bfloat16))
+        e0 = self.chunks[0].engine
+        if count is None:
+            count = e0._counting()
+        return self.run(1, [count])
 
     def gather_masters(self):
         """ZeRO-1: every rank's fp32 masters and moments complete (exports / checkpoints)."""

@@ -145,10 +145,12 @@ def test_fused_step_tail_matches_separate_kernels(kind, monkeypatch):
         torch.cuda.synchronize()
         torch.testing.assert_close(oa, ob, rtol=1e-5, atol=1e-6)
     assert int(a.step_dev.item()) == int(b.step_dev.item()) == 6 and int(a._ticket.item()) == 0
+    # (|b| is summed in another order -- per-32-column partials -- so the bias-decay gradient, and
+    # through the codes everything downstream, may differ in the last bits)
     for k in a.params:
-        torch.testing.assert_close(a.params[k], b.params[k], rtol=1e-6, atol=1e-7)
-        torch.testing.assert_close(a.m[k], b.m[k], rtol=1e-6, atol=1e-9)
-        torch.testing.assert_close(a.v[k], b.v[k], rtol=1e-6, atol=1e-12)
+        torch.testing.assert_close(a.params[k], b.params[k], rtol=1e-4, atol=2e-6)
+        torch.testing.assert_close(a.m[k], b.m[k], rtol=1e-3, atol=1e-8)
+        torch.testing.assert_close(a.v[k], b.v[k], rtol=1e-3, atol=1e-11)
     torch.testing.assert_close(a.feature_counts, b.feature_counts, rtol=0, atol=0)
 
 
@@ -186,9 +188,50 @@ def test_graphed_data_parallel_one_rank_matches_single_engine(mode, chunks):
         single.step_source(s, count_pattern(s))
     torch.cuda.synchronize()
     comm.close()
+    # (the two paths sum the gradients in different orders -- one- vs two-problem weight-gradient
+    # launches, bias sums in torch vs in the fused tail -- and Adam amplifies last-bit differences of
+    # near-zero gradients, so compare the parameter CHANGES in norm)
     for k in single.params:
         got = torch.cat([e.params[k] for e in engines])
-        torch.testing.assert_close(got, single.params[k], rtol=2e-5, atol=2e-6)
-    torch.testing.assert_close(torch.cat([e.feature_counts for e in engines]), single.feature_counts, rtol=0, atol=0)
-    torch.testing.assert_close(torch.cat([e.out for e in engines])[:, :3], single.out[:, :3], rtol=1e-4, atol=1e-6)
+        p0 = torch.stack([m[0][k] for m in models])
+        rel = float((got - single.params[k]).norm() / (single.params[k] - p0).norm())
+        assert rel < 1e-2, (k, rel)
+    # feature on-counts: every counting step's rows (a handful of codes near zero may flip with the
+    # last-bit parameter differences)
+    dc = (torch.cat([e.feature_counts for e in engines]) - single.feature_counts).abs()
+    assert float(dc.max()) <= 2 and float((dc > 0).float().mean()) < 0.01, (float(dc.max()), float((dc > 0).float().mean()))
+    assert float(single.feature_counts.sum()) > 0
+    torch.testing.assert_close(torch.cat([e.out for e in engines])[:, :3], single.out[:, :3], rtol=1e-3, atol=1e-6)
     assert all(int(e.step_dev.item()) == 11 for e in engines)
+
+
+@pytest.mark.parametrize("mode", ["dp", "zero1"])
+def test_trainer_graphed_data_parallel_one_rank(mode):
+    """EnsembleTrainer(parallel='dp' / 'zero1') on a GPU: the fused engine with in-graph RCCL
+    collectives (one rank, caller-provided batches) trains like the plain fused trainer."""
+    from sparse_coding__amd.engine.trainer import EnsembleTrainer
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+    from sparse_coding__amd.parallel.dist import DistInfo
+
+    torch.manual_seed(19)
+    d, n, B = 512, 1024, 256
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3, 1e-2)]
+    tr = EnsembleTrainer(models, FunctionalSAE, lr=1e-3, batch_size=B, device=DEV, parallel=mode,
+                         dist=DistInfo(device=torch.device(DEV)), args={"dict_size": n})
+    ref = EnsembleTrainer(models, FunctionalSAE, lr=1e-3, batch_size=B, device=DEV, args={"dict_size": n})
+    assert tr.kind == f"{mode}-graphed" and ref.kind == "fused-sae"
+    feats = torch.nn.functional.normalize(torch.randn(2048, d, device=DEV), dim=-1)
+    for _ in range(6):
+        x = (torch.relu(torch.randn(B, 2048, device=DEV) - 2.0) @ feats).to(torch.bfloat16)
+        a = tr.step(x).clone()
+        b = ref.step(x).clone()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-6)
+    for k in ref.impl.params:
+        p0 = torch.stack([m[0][k] for m in models])
+        rel = float((tr.impl.params[k] - ref.impl.params[k]).norm() / (ref.impl.params[k] - p0).norm())
+        assert rel < 1e-2, (k, rel)
+    lds = tr.to_learned_dicts(["dict_size"], ["l1_alpha"])
+    assert len(lds) == 3 and lds[2][1]["dict_size"] == n
+    st = tr.state_dict()
+    assert st["kind"] == f"{mode}-graphed" and st["impl"]["step"] == 6

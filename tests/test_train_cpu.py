@@ -639,3 +639,45 @@ def test_trainer_ensemble_sharded_gloo():
     for g in range(4):
         np.testing.assert_array_equal(encs[g], res[1][0][g])
         np.testing.assert_allclose(encs[g], single.params["encoder"][g].numpy(), atol=2e-5, rtol=1e-4)
+
+
+def _trainer_dp_worker(rank, world, port, xs, init, mode, out_q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
+
+    info = init_distributed("gloo")
+    tr = EnsembleTrainer(init, FunctionalSAE, lr=1e-2, batch_size=xs[0].shape[0] // world, device="cpu",
+                         dist=info, parallel=mode, args={"dict_size": 32})
+    assert tr.kind == f"{mode}-eager"
+    for x in xs:
+        tr.step(x.chunk(world)[rank])
+    lds = tr.to_learned_dicts(["dict_size"], ["l1_alpha"])
+    out_q.put((rank, [ld.encoder.numpy().copy() for ld, _ in lds]))
+    shutdown(info)
+
+
+@pytest.mark.parametrize("mode", ["dp", "zero1"])
+def test_trainer_data_parallel_gloo(mode):
+    """EnsembleTrainer(parallel='dp' / 'zero1') over two gloo ranks == one process training every
+    model on the global batch."""
+    torch.manual_seed(4)
+    init = [FunctionalSAE.init(16, 32, l1) for l1 in (1e-4, 1e-3, 3e-3)]
+    xs = [torch.randn(64, 16) for _ in range(3)]
+    single = EnsembleTrainer(init, FunctionalSAE, lr=1e-2, batch_size=64, device="cpu", engine="eager")
+    for x in xs:
+        single.step(x)
+    ref = [single.impl.params["encoder"][i].detach().numpy() for i in range(3)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_dp_worker, args=(r, 2, port, xs, init, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i in range(3):
+        np.testing.assert_array_equal(res[0][i], res[1][i])
+        np.testing.assert_allclose(res[0][i], ref[i], atol=2e-5, rtol=1e-4)
