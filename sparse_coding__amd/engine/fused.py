@@ -764,9 +764,16 @@ class FusedSAEEnsemble:
         return [self.sig.to_learned_dict(p, b) for p, b in self.unstack(device)]
 
     def state_dict(self):
+        # the bf16 shadows and row norms the kernels read are saved too: rebuilding them from the
+        # masters (refresh_shadows) reduces the norms in another order than the Adam kernel that
+        # wrote them, so an exact (bit-identical) resume needs the stored ones
+        sh = {"enc": self.enc_shadow}
+        if self.dec_shadow is not self.enc_shadow:
+            sh["dec"] = self.dec_shadow
         return {"kind": self.kind, "params": self.params, "m": self.m, "v": self.v, "lr": self.lr,
                 "l1": self.l1, "bias_decay": self.bias_decay, "step": self.step_count,
-                "nactive": self.nactive, "feature_counts": self.feature_counts, "rows_seen": self.rows_seen}
+                "nactive": self.nactive, "feature_counts": self.feature_counts, "rows_seen": self.rows_seen,
+                "shadows": sh, "norms": self.norms, "bsq": self._bsq if not self._bsq_dirty else None}
 
     def load_state_dict(self, sd):
         for k in self.params:
@@ -779,4 +786,15 @@ class FusedSAEEnsemble:
         if sd.get("feature_counts") is not None and self.feature_counts is not None:
             self.feature_counts.copy_(sd["feature_counts"])
         self.rows_seen = int(sd.get("rows_seen", 0))
-        self.refresh_shadows()
+        sh = sd.get("shadows")
+        if sh is not None and sd.get("norms") is not None:
+            self.enc_shadow.copy_(sh["enc"])
+            if "dec" in sh and self.dec_shadow is not self.enc_shadow:
+                self.dec_shadow.copy_(sh["dec"])
+            self.norms.copy_(sd["norms"])
+            self._bsq_dirty = True
+            if sd.get("bsq") is not None and self._bsq is not None:
+                self._bsq.copy_(sd["bsq"])  # the fused tail's |b|^2 partials, as the kernel summed them
+                self._bsq_dirty = False
+        else:  # (older checkpoints: rebuilt from the masters)
+            self.refresh_shadows()

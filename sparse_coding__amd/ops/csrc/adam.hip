@@ -462,14 +462,16 @@ __global__ __launch_bounds__(256) void step_tail_kernel(AdamArgs a, BiasArgs b, 
   } else {
     adam_row<NV, GBF>(a, (long)(bid - t.nloss - t.nbias - t.ngather) * 4 + (threadIdx.x >> 6));
   }
-  // the last block to finish advances the step counter (all reads of it happened before)
+  // The last block to finish advances the step counter.  Every block's read of *step was consumed
+  // (bias corrections, parity) before its ticket, so no fence is needed -- and none is wanted: an
+  // agent-scope release writes back the XCD's L2 (one per block: ~2.4x the whole step, measured).
+  // Relaxed agent-scope RMWs are coherent across the XCDs.
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
-    const int done = atomicAdd(t.ticket, 1);
+    const int done = __hip_atomic_fetch_add(t.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (done == (int)gridDim.x - 1) {
-      atomicExch(t.ticket, 0);
-      atomicAdd(b.step, 1);
+      __hip_atomic_store(t.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(b.step, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
