@@ -1,0 +1,46 @@
+"""Host-side planning: how a run of steps is cut into HIP graph replays (engine/graph_plan.py) and the
+per-N communication model the bench uses to choose the multi-GPU mode (parallel/comm_model.py)."""
+import pytest
+
+from sparse_coding__amd.engine.graph_plan import chunks, count_pattern, tile
+from sparse_coding__amd.parallel import comm_model
+
+
+@pytest.mark.parametrize("steps,warmup", [(20, 5), (200, 20), (192, 32), (7, 5), (1, 1), (50, 10), (3, 20),
+                                          (20, 0), (97, 13)])
+def test_tile_covers_and_counts(steps, warmup):
+    t = tile(steps, warmup)
+    assert sum(t.timed) == steps and sum(t.warm) == warmup
+    assert max(t.timed) <= 8 and len(set(t.timed)) <= 2  # one group size + at most one remainder
+    if t.covered:  # every timed graph replayed in the warmup, a timed-size group last
+        assert set(t.timed) <= set(t.warm) and t.warm[-1] == t.group
+    else:
+        assert warmup < t.group + steps % t.group
+
+
+def test_tile_driver_command_and_long_run():
+    assert tile(20, 5).timed == (5, 5, 5, 5) and tile(20, 5).warm == (5,)
+    assert tile(200, 20).timed == (8,) * 25 and tile(200, 20).warm == (4, 8, 8)
+    assert tile(20, 5, 8, exact=True).timed == (8, 8, 4)
+    assert chunks(19, 8) == [8, 8, 3] and count_pattern(5) == (True, False, False, False, False)
+    assert count_pattern(17, 8) == tuple(i in (0, 8, 16) for i in range(17))
+
+
+def test_comm_model_headline():
+    shape = comm_model.StepShape(models=8, n=2048, d=512, batch=2048, t1_ms=0.31, es_ms={2: 0.285, 4: 0.271, 8: 0.262})
+    # bytes: dp all-reduces 2 (N-1)/N of the fp32 gradients; zero1 moves bf16 gradients + shadows once
+    g = shape.params * 4
+    assert comm_model.bytes_per_gpu("dp", 8, shape) == int(2 * 7 / 8 * g)
+    assert comm_model.bytes_per_gpu("zero1", 8, shape, 2) == int(7 / 8 * (shape.params * 2 + shape.shadow_bytes))
+    assert comm_model.bytes_per_gpu("es", 8, shape) == int(7 / 8 * 8 * 2048 * 512 * 2)
+    for n in (2, 4, 8):
+        p = {m: comm_model.predict(m, n, shape) for m in ("dp", "zero1", "es")}
+        assert p["dp"]["ms_per_step"] > p["zero1"]["ms_per_step"] > p["es"]["ms_per_step"]
+        assert p["es"]["exposed_comm_ms"] == 0.0
+        assert comm_model.best_mode(n, shape) == "es"
+    # more links at larger N: the dp all-reduce gets cheaper per GPU
+    assert comm_model.predict("dp", 8, shape)["comm_ms"] < comm_model.predict("dp", 2, shape)["comm_ms"]
+    # a model count that does not split over N leaves es out
+    odd = comm_model.StepShape(models=6, n=2048, d=512, batch=2048, t1_ms=0.25)
+    assert comm_model.best_mode(4, odd) in ("dp", "zero1")
+    assert comm_model.predict("dp", 1, shape)["comm_ms"] == 0.0
