@@ -96,6 +96,9 @@ def parse(argv=None):
                     help="create the process group even at N=1 and run the N>1 code path (rehearses the "
                          "sharded step with real RCCL collectives on a one-GPU box)")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--wgrad-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="single GPU: storage of the weight gradients between the wgrad GEMM and Adam (the "
+                         "moments, masters and the update stay fp32)")
     ap.add_argument("--graph-group", type=int, default=None,
                     help="steps per graph replay (default: engine/graph_plan.tile's choice, <= 8)")
     ap.add_argument("--settle-ms", type=float, default=150.0,
@@ -245,7 +248,7 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
 
         from sparse_coding__amd.engine.graph_plan import count_pattern
 
-        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device)
+        eng = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=device, grad_dtype=args.wgrad_dtype)
         if args.no_graph:
             def step():
                 ring.sample_shard(B, 0, 1, out=eng.x_static)
