@@ -108,7 +108,7 @@ def parse(argv=None):
                     help="N>1: after the headline run, also time the other strategy (es <-> dp) and report it "
                          "under alt_parallelism")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of HIP graphs")
-    ap.add_argument("--dp-graph", type=int, default=1,
+    ap.add_argument("--dp-graph", type=int, default=0,
                     help="dp / zero1: 1 = multi-step HIP graphs with the RCCL collectives captured inside them "
                          "(parallel/graphed.py, native communicator); 0 = host-issued collectives between "
                          "per-chunk graph replays (parallel/data_parallel.py, parallel/zero.py)")
