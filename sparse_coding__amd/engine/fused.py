@@ -226,7 +226,7 @@ class FusedSAEEnsemble:
         # step's batch gather in ONE launch) for the plain untied / tied single-device step; it keeps
         # per-32-column b^2 partial sums (parity-double-buffered by the step counter) for |b|
         self._tail_ok = (self.kind in ("untied", "tied") and self.act == gemm_ops.ACT_RELU and not self.learned_center
-                         and self.nactive is None and self.wsplit == 1 and n % 32 == 0 and d <= 1024
+                         and self.nactive is None and n % 32 == 0 and d <= 1024
                          and os.environ.get("SC_FUSED_TAIL", "1") not in ("", "0"))
         self._bsq = torch.zeros(2, G, n // 32, device=dev) if self._tail_ok else None
         self._ticket = torch.zeros(1, device=dev, dtype=torch.int32) if self._tail_ok else None
@@ -438,7 +438,8 @@ class FusedSAEEnsemble:
                                self.enc_part, self.dec_part, self.l1, self.bias_decay, self.out, self.batch_size,
                                self._alpha, self._bsq, self._ticket,
                                cnt_part=self.cnt_part if self._counted else None,
-                               feat_count=self.feature_counts if self._counted else None, gather=gather)
+                               feat_count=self.feature_counts if self._counted else None, gather=gather,
+                               **self._adam_split_kw())
             return
         # scale / centering first: their gradients read the pre-update dictionary (adam_first)
         if self.kind == "threshold" or self.learned_center:

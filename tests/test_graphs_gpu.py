@@ -114,8 +114,8 @@ def test_prime_source_captures_without_running():
     assert len(e._graph) == n_graphs and e.step_count == 11 and int(e.step_dev.item()) == 11
 
 
-@pytest.mark.parametrize("kind", ["untied", "tied"])
-def test_fused_step_tail_matches_separate_kernels(kind, monkeypatch):
+@pytest.mark.parametrize("kind,G,B", [("untied", 3, 256), ("tied", 3, 256), ("untied", 1, 4096)])
+def test_fused_step_tail_matches_separate_kernels(kind, G, B, monkeypatch):
     """The fused step tail (row Adam + loss terms + bias Adam + step counter in one launch, |b| from
     parity-double-buffered b^2 partials) against the separate adam_rows / loss_reduce / bias_adam
     kernels: parameters, moments, losses, feature counts and the device step counter, over eager steps
@@ -125,14 +125,16 @@ def test_fused_step_tail_matches_separate_kernels(kind, monkeypatch):
 
     torch.manual_seed(21)
     sig = FunctionalSAE if kind == "untied" else FunctionalTiedSAE
-    d, n, B = 512, 1024, 256
-    models = [sig.init(d, n, l1, bias_decay=bd, device=DEV) for l1, bd in ((1e-4, 0.0), (1e-3, 1e-3), (1e-2, 3e-2))]
+    d, n = 512, 1024
+    hp = ((1e-3, 1e-3), (1e-4, 0.0), (1e-2, 3e-2))[:G]
+    models = [sig.init(d, n, l1, bias_decay=bd, device=DEV) for l1, bd in hp]
     for p, _ in models:
         p["encoder_bias"].normal_(0.0, 0.1)
     a = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=DEV, count_every=2)
     monkeypatch.setenv("SC_FUSED_TAIL", "0")
     b = FusedSAEEnsemble(models, sig, lr=1e-3, batch_size=B, device=DEV, count_every=2)
     assert a._tail_ok and not b._tail_ok
+    assert (a.wsplit > 1) == (G == 1)  # one model on a large batch: split-K gradient slabs into the tail
     feats = torch.nn.functional.normalize(torch.randn(2048, d, device=DEV), dim=-1)
     for i in range(6):
         if i == 3:  # an out-of-band edit of the bias (refresh_shadows marks the b^2 partials stale)
