@@ -229,7 +229,7 @@ class FusedSAEEnsemble:
                          and self.nactive is None and n % 32 == 0 and d <= 1024
                          and os.environ.get("SC_FUSED_TAIL", "1") not in ("", "0"))
         self._bsq = torch.zeros(2, G, n // 32, device=dev) if self._tail_ok else None
-        self._ticket = torch.zeros(1, device=dev, dtype=torch.int32) if self._tail_ok else None
+        self._ticket = torch.zeros(adam_ops.TICKET_INTS, device=dev, dtype=torch.int32) if self._tail_ok else None
         self._bsq_dirty = True
         # threshold SAEs: per-feature partial sums of the code gradient on the activation's ramp
         # (the scale gradient's source, written by the code-gradient epilogue)

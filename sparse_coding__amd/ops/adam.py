@@ -99,6 +99,9 @@ def bias_loss(b, m, v, colpart, tm, enc_part, enc_tiles, dec_part, dec_tiles, l1
     _lib.check(rc, "sc_bias_loss")
 
 
+TICKET_INTS = (1 + 64) * 32  # csrc/adam.hip: top + TK_SUB sub-counters, one 128-byte line each
+
+
 def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, enc_part, dec_part, l1, bias_decay,
               out, B, gscale, bsq, ticket, cnt_part=None, feat_count=None, gather=None, nsplit=1, gstride=0):
     """The end of a single-device step as ONE launch (csrc/adam.hip ``step_tail_kernel``): row Adam over
@@ -108,7 +111,7 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
     out [rows, d]) -- the NEXT step's batch fetch.  The device step counter ``step_dev`` is read by
     every block and advanced by the last one.  ``bsq`` [2, G, n/32] fp32 holds the b^2 partial sums
     of the current bias at index ``step & 1`` (``bias_sq_parts``); the tail writes the other half.
-    ``ticket``: one zero-initialised int32 (reset by the kernel).  ``nsplit`` / ``gstride``: each set's
+    ``ticket``: ``TICKET_INTS`` zero-initialised int32 (completion counters; reset by the kernel).  ``nsplit`` / ``gstride``: each set's
     gradient is the first of ``nsplit`` split-K partial slabs (as ``adam_rows``)."""
     shp = tuple(sets[0]["p"].shape)
     d = shp[-1]
@@ -125,7 +128,7 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
         raise ValueError(f"step_tail needs [G, n, d] sets with n % 32 == 0, d in 256..1024 (got {shp}, bias {G}x{n})")
     if tuple(bsq.shape) != (2, G, n // 32) or bsq.dtype != torch.float32 or not bsq.is_contiguous():
         raise ValueError("bsq must be contiguous fp32 [2, G, n/32]")
-    if ticket.dtype != torch.int32 or ticket.numel() < 1 or step_dev is None:
+    if ticket.dtype != torch.int32 or ticket.numel() < TICKET_INTS or step_dev is None:
         raise ValueError("ticket must be int32 and step_dev a device counter")
     tm = colpart.shape[1]
     if tuple(colpart.shape) != (G, tm, n) or (cnt_part is not None and tuple(cnt_part.shape) != (G, tm, n)):
