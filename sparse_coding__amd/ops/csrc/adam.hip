@@ -338,8 +338,9 @@ __global__ __launch_bounds__(256) void bias_adam_kernel(BiasArgs a) {
 // tail behind the HBM-bound Adam rows):
 //   [0, G)                      loss terms of model g (reduces the GEMM-epilogue partials)
 //   [G, G + G n/32)             bias Adam, 32 columns of one model (+ feature on-counts)
-//   [.., + ngather)             the NEXT step's batch gather from the ring permutation
 //   [.., + rows/4)              row Adam (norm Jacobian, update, bf16 shadow, row norms)
+//   [.., + ngather)             the NEXT step's batch gather from the ring permutation (last:
+//                               its rows stay L2-hot for the next encoder)
 // Cross-block dependencies are removed instead of ordered:
 //   * |b| (loss term and bias-decay gradient, both of the pre-update bias) comes from per-32-
 //     column partial sums of b^2 written by the PREVIOUS step's bias blocks (double-buffered by
@@ -450,8 +451,11 @@ __global__ __launch_bounds__(256) void step_tail_kernel(AdamArgs a, BiasArgs b, 
   } else if (bid < t.nloss + t.nbias) {
     const int k = bid - t.nloss, nb = b.n / 32;
     tail_bias(b, t, k % nb, k / nb, step, par);
-  } else if (bid < t.nloss + t.nbias + t.ngather) {
-    const long r = (long)(bid - t.nloss - t.nbias) * 4 + (threadIdx.x >> 6);
+  } else if (bid >= (int)gridDim.x - t.ngather) {
+    // the next step's batch: the LAST blocks dispatched, so the rows are written at the end of the
+    // launch and still sit in L2 when the next step's encoder reads them (written first, the Adam
+    // stream evicted them: encoder 67 vs 57 us, measured)
+    const long r = (long)(bid - ((int)gridDim.x - t.ngather)) * 4 + (threadIdx.x >> 6);
     if (r < t.grows) {
       const int lane = threadIdx.x & 63;
       const long jj = (long)(step + 1 - t.ep0[0]) * t.grows + r;
@@ -462,7 +466,7 @@ __global__ __launch_bounds__(256) void step_tail_kernel(AdamArgs a, BiasArgs b, 
       for (int v = lane; v < t.row_vec; v += 64) op[v] = sp[v];
     }
   } else {
-    adam_row<NV, GBF>(a, (long)(bid - t.nloss - t.nbias - t.ngather) * 4 + (threadIdx.x >> 6));
+    adam_row<NV, GBF>(a, (long)(bid - t.nloss - t.nbias) * 4 + (threadIdx.x >> 6));
   }
   // The last block to finish advances the step counter.  Every block's read of *step was consumed
   // (bias corrections, parity) before its ticket, so no fence is needed -- and none is wanted: an
