@@ -1,6 +1,6 @@
 """Per-step timeline of the last N training steps in a rocprofv3 kernel trace.
 
-A step starts at its ring-gather kernel.  Prints per step: wall from its gather to the next
+A step starts at its encoder GEMM.  Prints per step: wall from its gather to the next
 step's gather, busy time (sum of kernel durations), idle gaps, and per-kernel durations, so a
 short timed region (--steps 20) can be compared with the steady state kernel by kernel.
 Usage: python step_timeline.py TRACE_DIR [N_STEPS]   (N_STEPS 0: every step; also prints the busy time
@@ -20,12 +20,23 @@ def short(name):
     return n.split("::")[-1][-30:]
 
 
+def _epi(name):
+    if "sae_gemm_kernel" not in name or "Shape<" not in name:
+        return None
+    try:
+        return int(name.split("Shape<")[1].split(">, ")[1].split(",")[2])
+    except (IndexError, ValueError):
+        return None
+
+
 def main():
     f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
     nsteps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     rows = [r for r in csv.DictReader(open(f)) if "scamd" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "gather_rows_perm" in r["Kernel_Name"]]
+    # a step starts at its encoder GEMM (EPI_ENC 0 / EPI_ENC_CNT 6); the batch gather of a graph's
+    # first step (the others run inside the previous step's fused tail) counts to the step before
+    starts = [i for i, r in enumerate(rows) if _epi(r["Kernel_Name"]) in (0, 6)]
     sel = starts[-nsteps:] if nsteps > 0 else starts
     out = []
     for k, i0 in enumerate(sel):

@@ -194,7 +194,13 @@ class FusedSAEEnsemble:
         # Adam kernel sums the partial slabs.  (Data-parallel paths use the flat buffers.)
         nprob = 2 if self.kind == "untied" else 1
         kdim = B if self.kind == "untied" else 2 * B
-        self.wsplit = (gemm_ops.wgrad_split(G, n, d, kdim, nprob, live=self._live) if wgrad_split == "auto"
+        # untied ReLU step with the code gradient fused into the encoder weight gradient
+        # (csrc/sae_dcw.hip: dpre never reaches HBM, one launch less); SC_FUSED_DCW=0 turns it off
+        self._dcw = (self.kind == "untied" and self.act == gemm_ops.ACT_RELU and self.nactive is None
+                     and gemm_ops.dcw_supported(G, B, n, d) and (grad_dtype or "fp32") == "fp32"
+                     and wgrad_split in ("auto", 1) and os.environ.get("SC_FUSED_DCW", "1") not in ("", "0"))
+        self.wsplit = (1 if self._dcw else
+                       gemm_ops.wgrad_split(G, n, d, kdim, nprob, live=self._live) if wgrad_split == "auto"
                        else int(wgrad_split))
         self.g_parts = (alloc(nprob, self.wsplit, G, n, d, device=dev, dtype=torch.float32)
                         if self.wsplit > 1 else None)
@@ -327,6 +333,8 @@ class FusedSAEEnsemble:
                                act=self.act, ascale=ascale, mask2=self.cmask2, nactive=self.nactive,
                                live_host=self._live)
             return
+        if self._dcw:  # the code gradient runs inside the encoder weight gradient (_enc_wgrad)
+            return
         gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                            mask=self.cmask, nactive=self.nactive, live_host=self._live)
 
@@ -348,10 +356,19 @@ class FusedSAEEnsemble:
     def wgrad_second(self, x, reduce_bias=True):
         """Untied: dW_e = dpre^T x (encoder) + bias grad.  Tied: nothing."""
         if self.kind == "untied":
-            gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha, nactive=self.nactive,
-                                  live_host=self._live)
+            self._enc_wgrad(x)
             if reduce_bias:
                 self._reduce_bias_grad()
+
+    def _enc_wgrad(self, x):
+        """g_enc = alpha dpre^T x: fused with the code gradient (and its bias-gradient column
+        sums) when ``_dcw``, else from the dpre the code-gradient GEMM wrote."""
+        if self._dcw:
+            gemm_ops.code_grad_wgrad(self.r, self.dec_shadow, x, self.cmask, self.l1, self.g_enc, self.colpart,
+                                     self._alpha)
+        else:
+            gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha, nactive=self.nactive,
+                                  live_host=self._live)
 
     def _reduce_bias_grad(self):
         torch.sum(self.colpart, dim=1, keepdim=True, out=self.g_bias)
@@ -372,6 +389,10 @@ class FusedSAEEnsemble:
         split = self.g_parts is not None
         self._g_from_parts = split
         self._g_from_bf = gbf = self.g_bf is not None
+        if self._dcw:  # decoder gradient, then the fused code / encoder gradient
+            gemm_ops.weight_grads([[(self.c, self.r)]], [self.g_dec], self._alpha)
+            self._enc_wgrad(x)
+            return
         if self.kind == "untied":
             outs = ([self.g_parts[0], self.g_parts[1]] if split else
                     [self.g_bf[0], self.g_bf[1]] if gbf else [self.g_dec, self.g_enc])
