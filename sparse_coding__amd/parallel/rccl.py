@@ -71,6 +71,19 @@ def library():
     return _lib
 
 
+def uid_bytes(uid: _UniqueId) -> bytes:
+    """All 128 bytes of a unique id (NULs included) for the bootstrap broadcast."""
+    return C.string_at(C.addressof(uid), C.sizeof(uid))
+
+
+def uid_from_bytes(data: bytes) -> _UniqueId:
+    if len(data) != C.sizeof(_UniqueId):
+        raise RcclError(f"RCCL unique id has {len(data)} bytes, expected {C.sizeof(_UniqueId)}")
+    uid = _UniqueId()
+    C.memmove(C.addressof(uid), data, len(data))
+    return uid
+
+
 def _check(rc: int, what: str):
     if rc != 0:
         msg = library().ncclGetErrorString(rc)
@@ -101,10 +114,12 @@ class RcclComm:
         if self.rank == 0:
             _check(library().ncclGetUniqueId(C.byref(uid)), "ncclGetUniqueId")
         if self.world > 1 or dist.is_initialized():
-            # the unique id travels over the bootstrap (the default group's store / collectives)
-            obj = [bytes(uid.internal) if self.rank == 0 else None]
+            # the unique id travels over the bootstrap (the default group's store / collectives).
+            # Raw 128 bytes through the struct's address: the ``internal`` field reads back as a
+            # bytes COPY cut at the first NUL (and writing through that copy corrupted the heap)
+            obj = [uid_bytes(uid) if self.rank == 0 else None]
             dist.broadcast_object_list(obj, src=0, device=self.device if info.backend == "nccl" else None)
-            C.memmove(uid.internal, obj[0], 128)
+            uid = uid_from_bytes(obj[0])
         self._comm = C.c_void_p()
         with torch.cuda.device(self.device):
             _check(library().ncclCommInitRank(C.byref(self._comm), self.world, uid, self.rank), "ncclCommInitRank")

@@ -44,3 +44,23 @@ def test_comm_model_headline():
     odd = comm_model.StepShape(models=6, n=2048, d=512, batch=2048, t1_ms=0.25)
     assert comm_model.best_mode(4, odd) in ("dp", "zero1")
     assert comm_model.predict("dp", 1, shape)["comm_ms"] == 0.0
+
+
+def test_rccl_unique_id_roundtrip_keeps_every_byte():
+    """The RCCL unique id crosses the bootstrap as raw bytes: NULs inside it must survive (the
+    struct's c_char field reads back cut at the first NUL), and decoding writes a fresh struct."""
+    import ctypes as C
+
+    from sparse_coding__amd.parallel.rccl import RcclError, _UniqueId, uid_bytes, uid_from_bytes
+
+    uid = _UniqueId()
+    raw = bytes((i * 37) % 256 for i in range(128))  # NULs at several offsets
+    C.memmove(C.addressof(uid), raw, 128)
+    b = uid_bytes(uid)
+    assert b == raw and len(b) == 128
+    back = uid_from_bytes(b)
+    assert uid_bytes(back) == raw
+    import pytest
+
+    with pytest.raises(RcclError):
+        uid_from_bytes(raw[:100])
