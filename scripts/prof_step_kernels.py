@@ -27,6 +27,7 @@ for _ in range(5):
     gemm.decode_residual(e.c, e.dec_shadow, x, e.r, e.dec_part)
     gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart, mask=e.cmask)
     gemm.weight_grads([[(e.c, e.r)], [(e.dpre, x)]], [e.g_dec, e.g_enc], 1e-6)
+    gemm.code_grad_wgrad(e.r, e.dec_shadow, x, e.cmask, e.l1, e.g_enc, e.colpart, 1e-6)  # fused dc + enc wgrad
     e._apply_update_kernels()  # the fused step tail (row Adam + losses + bias Adam)
 torch.cuda.synchronize()
 # config 4 top-k select: 8 models, B=2048, n=6144

@@ -26,7 +26,7 @@
 //                       GEMM2 (32 MFMA)
 //
 // LDS: R slabs 4 x 8 KB, x slabs 4 x 2 x 8 KB, S exchange 32 KB, P image 8 KB, the activity
-// words of a 2048-row batch segment 16 KB = 152 KB.
+// words of a 2048-row batch segment 16 KB, 1 KB junk for the L2 warm-up touches = 153 KB.
 #include "gemm_tiles.h"
 
 namespace scamd {
@@ -46,6 +46,20 @@ struct DcwArgs {
 };
 
 constexpr int DCW_JN = 64, DCW_BT = 32, DCW_SEG = 2048;
+constexpr int DCW_PF = 4;  // chunks ahead of the L2 warm-up touches
+
+// L2 warm-up: one dword per lane from 64 distinct 128-byte lines, LDS-DMA'd into a junk LDS
+// word (no VGPR is written, so nothing has to stay reserved while it is in flight).  Counted
+// by vmcnt like every other transfer (the explicit waits below include it).
+__device__ __forceinline__ void touch_lines(const i32x4_t& rs, uint32_t voff, uint32_t soff, char* junk) {
+  asm volatile(
+      "s_mov_b32 m0, %0\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %1, %2, %3 offen lds"
+      :
+      : "s"((uint32_t)reinterpret_cast<uintptr_t>(junk)), "v"(voff), "s"(rs), "s"(soff)
+      : "memory", "m0");
+}
 
 template <int D>
 __global__ __launch_bounds__(256, 1) void sae_dcw_kernel(DcwArgs a) {
@@ -60,7 +74,8 @@ __global__ __launch_bounds__(256, 1) void sae_dcw_kernel(DcwArgs a) {
   constexpr int S_OFF = X_OFF + 8 * SLAB;           // [4 w][4 t][2 i][64] f32x4
   constexpr int P_OFF = S_OFF + 4 * 4 * 2 * 64 * 16;  // [32 b][256 B] image (64 j used)
   constexpr int M_OFF = P_OFF + DCW_BT * 256;       // [32 blocks][64] u64
-  __shared__ __attribute__((aligned(16))) char smem[M_OFF + (DCW_SEG / 64) * 512];
+  constexpr int J_OFF = M_OFF + (DCW_SEG / 64) * 512;  // [4 waves][256 B] junk (L2 touches)
+  __shared__ __attribute__((aligned(16))) char smem[J_OFF + 4 * 256];
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -108,6 +123,17 @@ __global__ __launch_bounds__(256, 1) void sae_dcw_kernel(DcwArgs a) {
     for (int ct = 0; ct < CT; ++ct) acc[it][ct] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float cs[4] = {0.f, 0.f, 0.f, 0.f};
 
+  // L2 warm-up of chunk c + DCW_PF: the XCD's 32 workgroups stream the same R[g] and x rows in near
+  // lockstep, so without it every chunk starts with the full MALL / HBM latency; waves 0-1 touch
+  // the R chunk, 2-3 the x chunk (256 lines each), lanes spread over the lines by feature block
+  const int tq = (((j0 / DCW_JN) * 2 + (w & 1)) * 64 + lane) & 255;
+  const uint32_t vt = (uint32_t)((tq >> 3) * D * 2 + (tq & 7) * 128);
+  char* const junk = smem + J_OFF + w * 256;
+  auto touch = [&](int c) {
+    const int cc = min(c, nc - 1);  // always issued: the vmcnt bookkeeping counts it
+    touch_lines(w < 2 ? rsR : rsX, vt, (uint32_t)(cc * DCW_BT * D * 2), junk);
+  };
+
   auto issue_r = [&](int c) { issue_pieces<PPW>(rsR, vr, (uint32_t)(c * DCW_BT * D * 2), rslab, w); };
   auto issue_x = [&](int c) {
     issue_pieces<PPW>(rsX, vx, (uint32_t)(c * DCW_BT * D * 2), xs0 + (c & 1) * 4 * SLAB, w);
@@ -131,11 +157,12 @@ __global__ __launch_bounds__(256, 1) void sae_dcw_kernel(DcwArgs a) {
       if (c == 0) {
         issue_r(0);
         issue_x(0);
+        for (int t = 1; t <= DCW_PF; ++t) touch(t);
       }
       __syncthreads();  // (drains this wave's DMAs as well)
     }
-    // ---- R(c) landed (the only younger transfer: x(c), issued after it)
-    wait_vmcnt<PPW>();
+    // ---- R(c) landed (younger: x(c) and one L2 touch, issued after it)
+    wait_vmcnt<PPW + 1>();
     // ---- GEMM1: S partial over this wave's K slice; lane gets S[b = 16 i + (l&15)][j = 16 t + 4(l>>4) + r]
     f32x4_t sacc[4][2];
 #pragma unroll
@@ -160,6 +187,7 @@ __global__ __launch_bounds__(256, 1) void sae_dcw_kernel(DcwArgs a) {
     if (c + 1 < nc) {
       issue_r(c + 1);
       issue_x(c + 1);
+      touch(c + 1 + DCW_PF);
     }
     // ---- exchange the K partials: wave w sums the 16-column tile t = w of all four
 #pragma unroll
@@ -188,8 +216,8 @@ __global__ __launch_bounds__(256, 1) void sae_dcw_kernel(DcwArgs a) {
       *reinterpret_cast<ushort4*>(pimg + mmaj_off(b, j >> 3) + (j & 7) * 2) = h;
     }
     lds_barrier();
-    // ---- x(c) landed (younger: R(c+1), x(c+1))
-    if (c + 1 < nc) wait_vmcnt<2 * PPW>();
+    // ---- x(c) landed (younger: R(c+1), x(c+1), the touch)
+    if (c + 1 < nc) wait_vmcnt<2 * PPW + 1>();
     else wait_vmcnt<0>();
     // ---- GEMM2: g_enc[j][col] += P^T x; lane gets [j = 16 it + (l&15)][col = 16 ct + 4(l>>4) + r]
     bf16x8_t fp[4];
