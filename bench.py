@@ -101,6 +101,9 @@ def parse(argv=None):
                          "moments, masters and the update stay fp32)")
     ap.add_argument("--graph-group", type=int, default=None,
                     help="steps per graph replay (default: engine/graph_plan.tile's choice, <= 8)")
+    ap.add_argument("--settle-mode", choices=["gemm", "step"], default="gemm",
+                    help="settle load: 'gemm' = the grouped GEMM on scratch operands; 'step' = the same fused "
+                         "step on a scratch ensemble of the benchmark's shapes (discarded, shares no state)")
     ap.add_argument("--settle-ms", type=float, default=150.0,
                     help="untimed non-training GPU load before the warmup so the timed steps run at the "
                          "steady-state clock (settle_clocks; reported as 'settle' in the JSON; 0 = off)")
@@ -306,6 +309,38 @@ def timed(runner, groups, info, B):
     return 1e3 * elapsed / steps, B * info.world_size * steps / elapsed
 
 
+def settle_step(device, ms: float, args):
+    """Untimed settle load with the step's own kernel mix: a SCRATCH ensemble of the benchmark's
+    shapes (fresh random weights, its own buffers and graph, a fixed random batch) replays its
+    training step for ``ms`` milliseconds and is then discarded.  Nothing of the measured models is
+    read or written."""
+    if ms <= 0:
+        return None
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.models.signatures import FunctionalSAE, FunctionalTiedSAE
+
+    sig = FunctionalSAE if args.kind == "untied" else FunctionalTiedSAE
+    n = args.d * args.ratio
+    gen = torch.Generator(device=device).manual_seed(11)
+    scratch = [sig.init(args.d, n, 1e-3, device=device) for _ in range(args.models)]
+    eng = FusedSAEEnsemble(scratch, sig, lr=1e-3, batch_size=args.batch, device=device).enable_graph()
+    eng.x_static.copy_(torch.randn(args.batch, args.d, device=device, generator=gen).to(torch.bfloat16))
+    eng.step_batch(eng.x_static)  # capture
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    steps = 0
+    while 1e3 * (time.perf_counter() - t0) < ms:
+        for _ in range(16):
+            eng.step_batch(eng.x_static)
+        steps += 16
+        torch.cuda.synchronize()
+    out = {"what": "the fused training step on a scratch ensemble of the same shapes (discarded; no state "
+                   "shared with the measured models)", "ms": round(1e3 * (time.perf_counter() - t0), 1),
+           "steps": steps}
+    del eng, scratch
+    return out
+
+
 def settle_clocks(device, ms: float):
     """Untimed, NON-training GPU load before the warmup: the grouped bf16 MFMA GEMM (the step's own
     kernel, plain epilogue) on scratch random operands for ``ms`` milliseconds.  MI355X raises its
@@ -341,7 +376,8 @@ def warm_and_time(runner, args, info, B):
 
     tiling = tile(args.steps, args.warmup, args.graph_group or GRAPH_STEPS, exact=bool(args.graph_group))
     runner.setup(tiling)
-    runner.settle = settle_clocks(info.device, args.settle_ms)
+    runner.settle = (settle_step(info.device, args.settle_ms, args) if args.settle_mode == "step"
+                     else settle_clocks(info.device, args.settle_ms))
     runner.run(list(tiling.warm))
     runner.finish()  # no warmup work may spill into the timed region
     ms, value = timed(runner, list(tiling.timed), info, B)

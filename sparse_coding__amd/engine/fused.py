@@ -194,11 +194,13 @@ class FusedSAEEnsemble:
         # Adam kernel sums the partial slabs.  (Data-parallel paths use the flat buffers.)
         nprob = 2 if self.kind == "untied" else 1
         kdim = B if self.kind == "untied" else 2 * B
-        # untied ReLU step with the code gradient fused into the encoder weight gradient
-        # (csrc/sae_dcw.hip: dpre never reaches HBM, one launch less); SC_FUSED_DCW=0 turns it off
+        # opt-in (SC_FUSED_DCW=1): the code gradient fused into the encoder weight gradient
+        # (csrc/sae_dcw.hip, dpre never reaches HBM).  Correct, but slower on MI355X at d = 512:
+        # 127 us against 49 + ~33 us for the two GEMMs it replaces -- each workgroup must stream
+        # R and x (4 MB) through one CU at <= ~80 GB/s with its 4 waves (profiles/r4/dcw/README.md)
         self._dcw = (self.kind == "untied" and self.act == gemm_ops.ACT_RELU and self.nactive is None
                      and gemm_ops.dcw_supported(G, B, n, d) and (grad_dtype or "fp32") == "fp32"
-                     and wgrad_split in ("auto", 1) and os.environ.get("SC_FUSED_DCW", "1") not in ("", "0"))
+                     and wgrad_split in ("auto", 1) and os.environ.get("SC_FUSED_DCW", "0") not in ("", "0"))
         self.wsplit = (1 if self._dcw else
                        gemm_ops.wgrad_split(G, n, d, kdim, nprob, live=self._live) if wgrad_split == "auto"
                        else int(wgrad_split))
@@ -232,7 +234,7 @@ class FusedSAEEnsemble:
         # step's batch gather in ONE launch) for the plain untied / tied single-device step; it keeps
         # per-32-column b^2 partial sums (parity-double-buffered by the step counter) for |b|
         self._tail_ok = (self.kind in ("untied", "tied") and self.act == gemm_ops.ACT_RELU and not self.learned_center
-                         and self.nactive is None and n % 32 == 0 and d <= 1024
+                         and n % 32 == 0 and d <= 1024
                          and os.environ.get("SC_FUSED_TAIL", "1") not in ("", "0"))
         self._bsq = torch.zeros(2, G, n // 32, device=dev) if self._tail_ok else None
         self._ticket = torch.zeros(adam_ops.TICKET_INTS, device=dev, dtype=torch.int32) if self._tail_ok else None
@@ -460,7 +462,7 @@ class FusedSAEEnsemble:
                                self._alpha, self._bsq, self._ticket,
                                cnt_part=self.cnt_part if self._counted else None,
                                feat_count=self.feature_counts if self._counted else None, gather=gather,
-                               **self._adam_split_kw())
+                               live=self.nactive, **self._adam_split_kw())
             return
         # scale / centering first: their gradients read the pre-update dictionary (adam_first)
         if self.kind == "threshold" or self.learned_center:

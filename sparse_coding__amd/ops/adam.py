@@ -103,7 +103,8 @@ TICKET_INTS = (1 + 64) * 32  # csrc/adam.hip: top + TK_SUB sub-counters, one 128
 
 
 def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, enc_part, dec_part, l1, bias_decay,
-              out, B, gscale, bsq, ticket, cnt_part=None, feat_count=None, gather=None, nsplit=1, gstride=0):
+              out, B, gscale, bsq, ticket, cnt_part=None, feat_count=None, gather=None, nsplit=1, gstride=0,
+              live=None):
     """The end of a single-device step as ONE launch (csrc/adam.hip ``step_tail_kernel``): row Adam over
     ``sets`` (as ``adam_rows``), the loss terms into ``out`` [G, 6], bias Adam (gradient = ``gscale``
     x the column sums of ``colpart`` [G, tm, n]), feature on-counts when ``cnt_part`` /
@@ -112,7 +113,8 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
     every block and advanced by the last one.  ``bsq`` [2, G, n/32] fp32 holds the b^2 partial sums
     of the current bias at index ``step & 1`` (``bias_sq_parts``); the tail writes the other half.
     ``ticket``: ``TICKET_INTS`` zero-initialised int32 (completion counters; reset by the kernel).  ``nsplit`` / ``gstride``: each set's
-    gradient is the first of ``nsplit`` split-K partial slabs (as ``adam_rows``)."""
+    gradient is the first of ``nsplit`` split-K partial slabs (as ``adam_rows``).  ``live``: int32 [G] live
+    row counts of a masked ensemble (rows past them are skipped, as ``adam_rows``)."""
     shp = tuple(sets[0]["p"].shape)
     d = shp[-1]
     nrows = sets[0]["p"].numel() // d
@@ -153,7 +155,7 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
         enc_part.shape[1], _lib.ptr(dec_part), dec_part.shape[1], _lib.ptr(cnt_part), _lib.ptr(feat_count),
         _lib.ptr(l1), _lib.ptr(bias_decay), _lib.ptr(out), n, B, float(gscale), _lib.ptr(bsq), _lib.ptr(ticket),
         _lib.ptr(gbuf), nbuf, _lib.ptr(perm), nperm, _lib.ptr(ep0), _lib.ptr(gout), grows, row_bytes,
-        int(nsplit), int(gstride), _lib.stream_handle(),
+        int(nsplit), int(gstride), _lib.ptr(live), _lib.stream_handle(),
     )
     _lib.check(rc, "sc_step_tail")
 
