@@ -101,7 +101,7 @@ def parse(argv=None):
                          "moments, masters and the update stay fp32)")
     ap.add_argument("--graph-group", type=int, default=None,
                     help="steps per graph replay (default: engine/graph_plan.tile's choice, <= 8)")
-    ap.add_argument("--settle-mode", choices=["gemm", "step"], default="gemm",
+    ap.add_argument("--settle-mode", choices=["gemm", "step"], default="step",
                     help="settle load: 'gemm' = the grouped GEMM on scratch operands; 'step' = the same fused "
                          "step on a scratch ensemble of the benchmark's shapes (discarded, shares no state)")
     ap.add_argument("--settle-ms", type=float, default=150.0,
