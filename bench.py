@@ -111,10 +111,11 @@ def parse(argv=None):
                     help="N>1: after the headline run, also time the other strategy (es <-> dp) and report it "
                          "under alt_parallelism")
     ap.add_argument("--no-graph", action="store_true", help="launch kernels eagerly instead of HIP graphs")
-    ap.add_argument("--dp-graph", type=int, default=0,
-                    help="dp / zero1: 1 = multi-step HIP graphs with the RCCL collectives captured inside them "
-                         "(parallel/graphed.py, native communicator); 0 = host-issued collectives between "
-                         "per-chunk graph replays (parallel/data_parallel.py, parallel/zero.py)")
+    ap.add_argument("--dist-graph", "--dp-graph", dest="dist_graph", type=int, default=1,
+                    help="N>1 / --force-dist: 1 = multi-step HIP graphs with the RCCL collectives captured inside "
+                         "them (parallel/graphed.py, native communicator on its own stream: es all-gathers, dp "
+                         "all-reduce, zero1 reduce-scatter / all-gather); 0 = host-issued collectives through "
+                         "ProcessGroupNCCL between graph replays (parallel/ensemble_shard.py, data_parallel.py, zero.py)")
     return ap.parse_args(argv)
 
 
@@ -188,6 +189,20 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
 
         if args.no_graph:
             return Runner(lambda: es.step_sampled(sample), dicts, close=es.flush)
+        if args.dist_graph and distributed:
+            # the group's batch fetch and in-place all-gathers captured in its graph (parallel/graphed.py)
+            from sparse_coding__amd.parallel.graphed import GraphedEnsembleSharded
+            from sparse_coding__amd.parallel.rccl import RcclComm
+
+            comm = RcclComm(info)
+            ges = GraphedEnsembleSharded(es, comm, ring.graph_source(B, info.rank, info.world_size))
+
+            def run_g(groups):
+                for s in groups:
+                    ges.run(s, count_pattern(s, GRAPH_STEPS))
+
+            return Runner(lambda: run_g([1]), dicts, close=comm.close, run=run_g,
+                          setup=lambda tiling: ges.prime([count_pattern(s, GRAPH_STEPS) for s in tiling.sizes]))
 
         def sample_steps(out, s):  # this rank's rows of the next s steps, one gather kernel
             return ring.sample_shard_steps(B, info.rank, info.world_size, s, out)
@@ -200,7 +215,7 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
         return Runner(lambda: es.run_groups([1], sample_steps, pattern), dicts, close=es.flush,
                       run=lambda groups: es.run_groups(groups, sample_steps, pattern),
                       setup=lambda tiling: (ring.ensure_permutation(), es.prime_groups(tiling.sizes, pattern)))
-    if args.engine == "fused" and distributed and not args.no_graph and args.dp_graph:
+    if args.engine == "fused" and distributed and not args.no_graph and args.dist_graph:
         # data parallel / ZeRO-1 with the collectives INSIDE multi-step HIP graphs (native RCCL
         # communicator on its own stream, parallel/rccl.py + parallel/graphed.py)
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble

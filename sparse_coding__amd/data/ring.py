@@ -206,6 +206,21 @@ class RingGraphSource:
         return gather_rows_perm(self.ring.buf, self.perm, step_dev, self.ep0, out, stride=self.B * self.world,
                                 offset=self.rank * self.B)
 
+    def gather_into_global(self, glob: torch.Tensor, step_dev: torch.Tensor):
+        """The capturable fetch of a multi-step group for an in-place all-gather: ``glob`` [s, N B, ...]
+        (one global batch per step); this rank's rows of steps t .. t+s-1 go straight into its slots
+        ``glob[k, rank B : (rank + 1) B]`` in ONE launch (no send buffer, no copy)."""
+        from ..ops.rows import gather_rows_perm
+
+        s, NB = glob.shape[0], glob.shape[1]
+        if NB != self.B * self.world or not glob.is_contiguous():
+            raise ValueError(f"glob must be contiguous [s, {self.B * self.world}, ...]")
+        flat = glob.view(s * NB, *glob.shape[2:])
+        lo = self.rank * self.B
+        out = flat[lo: (s - 1) * NB + lo + self.B]
+        return gather_rows_perm(self.ring.buf, self.perm, step_dev, self.ep0, out, stride=NB, offset=lo,
+                                inner=self.B, ostride=NB)
+
 
 def _kernels_available() -> bool:
     from ..ops import _lib

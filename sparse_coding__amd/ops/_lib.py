@@ -70,7 +70,7 @@ def signatures():
         "sc_center_rows": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
         "sc_gather_rows": [c_void_p, c_void_p, c_void_p, c_long, c_long, c_void_p],
         "sc_gather_rows_perm": [c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_long, c_long,
-                                c_long, c_long, c_void_p],
+                                c_long, c_long, c_long, c_long, c_void_p],
         "sc_gather_rows_blocks": [c_void_p, c_long, c_void_p, c_long, c_long, c_long, c_long, c_long, c_void_p,
                                   c_long, c_void_p],
         "sc_lista_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,

@@ -137,16 +137,19 @@ __global__ __launch_bounds__(256) void gather_rows_perm_kernel(const u32x4_t* __
                                                                const int* __restrict__ step,
                                                                const int* __restrict__ ep0,
                                                                u32x4_t* __restrict__ out, long rows, int row_vec,
-                                                               long stride, long offset) {
+                                                               long stride, long offset, long inner, long ostride) {
   const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= rows) return;
   const int lane = threadIdx.x & 63;
-  // (data parallel: stride = N B, offset = rank B -- this rank's shard of each global batch)
-  const long j = (long)(step[0] - ep0[0]) * stride + offset + r;
+  // (data parallel: stride = N B, offset = rank B -- this rank's shard of each global batch;
+  // several steps at once: `inner` rows per step, step k of the group at perm block +k stride and
+  // at output row k ostride -- e.g. straight into this rank's slot of each step's global batch)
+  const long k = r / inner, i = r - k * inner;
+  const long j = (long)(step[0] - ep0[0]) * stride + offset + k * stride + i;
   long src = (j >= 0 && j < nperm) ? perm[j] : 0;
   src = (src >= 0 && src < nbuf) ? src : 0;
   const u32x4_t* s = buf + src * row_vec;
-  u32x4_t* o = out + r * row_vec;
+  u32x4_t* o = out + (k * ostride + i) * row_vec;
   for (int v = lane; v < row_vec; v += 64) o[v] = s[v];
 }
 
@@ -215,12 +218,16 @@ int sc_gather_rows(const void* buf, const long* idx, void* out, long rows, long 
 }
 
 int sc_gather_rows_perm(const void* buf, long nbuf, const long* perm, long nperm, const int* step, const int* ep0,
-                        void* out, long rows, long row_bytes, long stride, long offset, hipStream_t stream) {
-  if (row_bytes % 16 || rows < 0 || nbuf < 1 || stride < rows || offset < 0) return 1;
+                        void* out, long rows, long row_bytes, long stride, long offset, long inner, long ostride,
+                        hipStream_t stream) {
+  if (inner <= 0) inner = rows;
+  if (ostride <= 0) ostride = inner;
+  if (row_bytes % 16 || rows < 0 || nbuf < 1 || stride < inner || offset < 0 || rows % inner || ostride < inner)
+    return 1;
   if (rows == 0) return 0;
   hipLaunchKernelGGL(gather_rows_perm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
                      reinterpret_cast<const u32x4_t*>(buf), nbuf, perm, nperm, step, ep0,
-                     reinterpret_cast<u32x4_t*>(out), rows, (int)(row_bytes / 16), stride, offset);
+                     reinterpret_cast<u32x4_t*>(out), rows, (int)(row_bytes / 16), stride, offset, inner, ostride);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

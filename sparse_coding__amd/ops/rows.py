@@ -30,10 +30,13 @@ def gather_rows(buf: torch.Tensor, idx: torch.Tensor, out: torch.Tensor | None =
 
 
 def gather_rows_perm(buf: torch.Tensor, perm: torch.Tensor, step: torch.Tensor, ep0: torch.Tensor,
-                     out: torch.Tensor, stride: int | None = None, offset: int = 0) -> torch.Tensor:
+                     out: torch.Tensor, stride: int | None = None, offset: int = 0, inner: int | None = None,
+                     ostride: int | None = None) -> torch.Tensor:
     """out[i] = buf[perm[(step - ep0) * stride + offset + i]] with ``step`` / ``ep0`` int32 [1] DEVICE
     scalars, so the fetch can be captured in a HIP graph and still walk the permutation (default
-    stride = rows = out.shape[0]; data parallel: stride = N B, offset = rank B).  Positions past
+    stride = rows = out.shape[0]; data parallel: stride = N B, offset = rank B).  Several steps in one
+    launch: ``inner`` rows per step, step k's rows from perm block + k ``stride`` written at output
+    row k ``ostride`` (default ``inner``): out rows [k ostride, k ostride + inner).  Positions past
     ``perm`` (a host bookkeeping error) read row 0 instead of faulting."""
     if not (buf.is_cuda and buf.is_contiguous() and out.is_contiguous()):
         raise ValueError("gather_rows_perm needs contiguous GPU buffers")
@@ -45,10 +48,15 @@ def gather_rows_perm(buf: torch.Tensor, perm: torch.Tensor, step: torch.Tensor, 
     for t in (step, ep0):
         if t.dtype != torch.int32 or t.numel() < 1 or t.device != buf.device:
             raise ValueError("step / ep0 must be int32 device scalars")
-    stride = out.shape[0] if stride is None else int(stride)
+    inner = int(inner) if inner else None
+    ostride = int(ostride) if ostride else (inner or 0)
+    rows = out.shape[0] if inner is None else ((out.shape[0] - inner) // ostride + 1) * inner
+    if inner is not None and ((out.shape[0] - inner) % ostride or out.shape[0] < inner):
+        raise ValueError("out must hold whole strided step blocks: (k - 1) ostride + inner rows")
+    stride = (out.shape[0] if inner is None else inner) if stride is None else int(stride)
     rc = _lib.lib().sc_gather_rows_perm(_lib.ptr(buf), buf.shape[0], _lib.ptr(perm), perm.numel(), _lib.ptr(step),
-                                        _lib.ptr(ep0), _lib.ptr(out), out.shape[0], row_bytes, stride, int(offset),
-                                        _lib.stream_handle())
+                                        _lib.ptr(ep0), _lib.ptr(out), rows, row_bytes, stride, int(offset),
+                                        int(inner or 0), int(ostride or 0), _lib.stream_handle())
     _lib.check(rc, "sc_gather_rows_perm")
     return out
 

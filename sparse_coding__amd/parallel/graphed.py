@@ -247,3 +247,90 @@ class GraphedDataParallel:
     def to_learned_dicts(self, device="cpu") -> List:
         self.gather_masters()
         return [ld for c in self.chunks for ld in c.engine.to_learned_dicts(device)]
+
+
+class GraphedEnsembleSharded:
+    """Ensemble-axis sharding (``parallel/ensemble_shard.py``) with the batch all-gathers INSIDE the
+    multi-step HIP graph.
+
+    Per group of s steps, one graph holds: ONE gather kernel writing this rank's rows of all s steps
+    straight into its slots of the s global batches (``RingGraphSource.gather_into_global``, device
+    step counter), s in-place all-gathers on the communicator's stream (``parallel/rccl.py``), and the
+    s steps of the rank's models, step k waiting on exactly gather k's event -- so gather k+1.. run
+    under step k's GEMMs and no collective is issued from the host.  Per model the update is the
+    data-parallel one on the N B global rows, as in ``EnsembleSharded``.  Reference: the sweep
+    sharding of ``cluster_runs.py:100-157`` / DDP of ``experiments/huge_batch_size.py:259-345``.
+    """
+
+    def __init__(self, es, comm, source):
+        e = es.engine
+        if not hasattr(e, "_step_kernels") or not hasattr(e, "step_dev"):
+            raise NotImplementedError("graphed ensemble sharding needs the fused engine")
+        if getattr(source, "world", 1) != es.info.world_size or getattr(source, "rank", 0) != es.info.rank:
+            raise ValueError("the source must be this rank's shard (ring.graph_source(B, rank, world))")
+        self.es, self.comm, self.source, self.engine = es, comm, source, e
+        self.B, self.N = es.B, max(1, es.info.world_size)
+        self.device = e.device
+        self._glob = None
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+
+    def _buffers(self, s: int):
+        if self._glob is None or self._glob.shape[0] < s:
+            self._glob = torch.empty(s, self.N * self.B, self.es.d, device=self.device, dtype=torch.bfloat16)
+            self._graphs = {}  # captured on the old buffer
+        return self._glob
+
+    def _steps(self, pattern):
+        e = self.engine
+        s = len(pattern)
+        glob = self._buffers(s)[:s]
+        self.source.gather_into_global(glob, e.step_dev)
+        B, r = self.B, self.es.info.rank
+        evs = [self.comm.all_gather(glob[k], glob[k][r * B:(r + 1) * B], overlap=True) for k in range(s)]
+        cur = torch.cuda.current_stream(self.device)
+        for k, count in enumerate(pattern):
+            if evs[k] is not None:
+                cur.wait_event(evs[k])
+            e._counted = count
+            e._step_kernels(glob[k], count)
+        self.comm.join()
+
+    def _graph(self, pattern):
+        key = tuple(bool(c) for c in pattern)
+        self._buffers(len(key))
+        g = self._graphs.get(key)
+        if g is None:
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._steps(key)
+            from ..ops import _lib
+
+            _lib.upload_graph(g, self.device)
+            self._graphs[key] = g
+        return g
+
+    def prime(self, patterns):
+        """Capture + upload (nothing runs) every group graph later replays use."""
+        e = self.engine
+        self._buffers(max([1] + [len(p) for p in patterns]))
+        e._tail_ready()
+        for p in patterns:
+            self._graph(tuple(bool(c) and e.track_feature_counts for c in p))
+        self.source.prepare(e.step_count, max([1] + [len(p) for p in patterns]))
+
+    def run(self, steps: int, pattern=None):
+        """``steps`` ensemble-sharded optimizer steps as ONE graph replay."""
+        e = self.engine
+        if pattern is None:
+            pattern = [i == 0 for i in range(int(steps))]
+        pattern = tuple(bool(c) and e.track_feature_counts for c in pattern)
+        if len(pattern) != int(steps):
+            raise ValueError("one counting flag per step")
+        e._tail_ready()
+        self.source.prepare(e.step_count, len(pattern))
+        self._graph(pattern).replay()
+        for count in pattern:
+            e._counted = count
+            e._host_step()
+        return e.out

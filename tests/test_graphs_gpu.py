@@ -207,6 +207,48 @@ def test_graphed_data_parallel_one_rank_matches_single_engine(mode, chunks):
     assert all(int(e.step_dev.item()) == 11 for e in engines)
 
 
+def test_graphed_ensemble_sharded_one_rank_matches_single_engine():
+    """Ensemble sharding with the batch fetch and the in-place all-gathers captured in the group graph
+    (native RCCL communicator, one rank) == the single-engine multi-step graph on the same ring
+    batches: the same kernels on the same rows, so parameters and losses agree exactly."""
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+    from sparse_coding__amd.engine.graph_plan import count_pattern
+    from sparse_coding__amd.models.signatures import FunctionalSAE
+    from sparse_coding__amd.parallel.dist import DistInfo
+    from sparse_coding__amd.parallel.ensemble_shard import EnsembleSharded
+    from sparse_coding__amd.parallel.graphed import GraphedEnsembleSharded
+    from sparse_coding__amd.parallel.rccl import RcclComm
+
+    torch.manual_seed(23)
+    d, n, B = 512, 1024, 256
+    rows = (torch.randn(B * 40, d, device=DEV) * 2).to(torch.bfloat16)
+    rings = []
+    for _ in range(2):
+        r = DeviceRing(rows.shape[0], d, device=DEV, seed=8)
+        r.push(rows)
+        rings.append(r)
+    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3, 3e-3, 1e-2)]
+    info = DistInfo(device=torch.device(DEV))
+    comm = RcclComm(info)
+    es = EnsembleSharded(models, lambda m, bs: FusedSAEEnsemble(m, FunctionalSAE, lr=1e-3, batch_size=bs, device=DEV),
+                         info, batch_per_rank=B, d=d)
+    ges = GraphedEnsembleSharded(es, comm, rings[0].graph_source(B, 0, 1))
+    ges.prime([count_pattern(s) for s in (3, 5)])
+    single = FusedSAEEnsemble(models, FunctionalSAE, lr=1e-3, batch_size=B, device=DEV).enable_graph()
+    single.attach_source(rings[1].graph_source(B))
+    for s in (3, 5, 3, 5):
+        ges.run(s, count_pattern(s))
+        single.step_source(s, count_pattern(s))
+    torch.cuda.synchronize()
+    comm.close()
+    for k in single.params:
+        torch.testing.assert_close(es.engine.params[k], single.params[k], rtol=0, atol=0)
+    torch.testing.assert_close(es.engine.out, single.out, rtol=0, atol=0)
+    torch.testing.assert_close(es.engine.feature_counts, single.feature_counts, rtol=0, atol=0)
+    assert int(es.engine.step_dev.item()) == 16
+
+
 @pytest.mark.parametrize("mode", ["dp", "zero1"])
 def test_trainer_graphed_data_parallel_one_rank(mode):
     """EnsembleTrainer(parallel='dp' / 'zero1') on a GPU: the fused engine with in-graph RCCL
@@ -237,3 +279,25 @@ def test_trainer_graphed_data_parallel_one_rank(mode):
     assert len(lds) == 3 and lds[2][1]["dict_size"] == n
     st = tr.state_dict()
     assert st["kind"] == f"{mode}-graphed" and st["impl"]["step"] == 6
+
+
+def test_ring_gather_into_global_matches_indexing():
+    """One launch fills rank r's slots of s consecutive global batches from the ring permutation
+    (the in-place all-gather layout of graphed ensemble sharding); other ranks' slots untouched."""
+    from sparse_coding__amd.data.ring import DeviceRing
+
+    torch.manual_seed(29)
+    d, B, N, r, s = 256, 64, 3, 1, 4
+    rows = (torch.randn(B * N * 12, d, device=DEV)).to(torch.bfloat16)
+    ring = DeviceRing(rows.shape[0], d, device=DEV, seed=3)
+    ring.push(rows)
+    src = ring.graph_source(B, r, N)
+    src.prepare(2, s)
+    step = torch.tensor([4], device=DEV, dtype=torch.int32)
+    glob = torch.zeros(s, N * B, d, device=DEV, dtype=torch.bfloat16)
+    src.gather_into_global(glob, step)
+    t0 = (4 - int(src.ep0.item())) * N * B
+    for k in range(s):
+        idx = src.perm[t0 + k * N * B + r * B: t0 + k * N * B + (r + 1) * B]
+        assert torch.equal(glob[k, r * B:(r + 1) * B], ring.buf[idx])
+        assert not glob[k, :r * B].any() and not glob[k, (r + 1) * B:].any()
