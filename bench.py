@@ -31,6 +31,7 @@ from __future__ import annotations
 import argparse
 import json
 import math
+import os
 import sys
 import time
 
@@ -531,10 +532,32 @@ def main(argv=None):
                                 for l, (a, b) in zip(l1s, quality)]
             rec["fvu_eval"] = {"train_steps": trained, "held_out_rows": int(held_out.shape[0]),
                                "act_norm": args.act_norm}
-        print(json.dumps(rec), flush=True)
+        _emit(json.dumps(rec))
     shutdown(info)
     return 0
 
 
+_JSON_FD = None
+
+
+def _keep_stdout_for_json():
+    """The driver reads ONE JSON line from rank 0's stdout, but native libraries print there too (RCCL's
+    version banner when a communicator is created): point fd 1 at stderr for everything else and
+    keep a private copy of the original stdout for the result line."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def _emit(line: str):
+    if _JSON_FD is None:
+        print(line, flush=True)
+        return
+    os.write(_JSON_FD, (line + "\n").encode())
+
+
 if __name__ == "__main__":
+    _keep_stdout_for_json()
     sys.exit(main())

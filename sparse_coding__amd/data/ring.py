@@ -206,6 +206,17 @@ class RingGraphSource:
         return gather_rows_perm(self.ring.buf, self.perm, step_dev, self.ep0, out, stride=self.B * self.world,
                                 offset=self.rank * self.B)
 
+    def gather_steps(self, out: torch.Tensor, step_dev: torch.Tensor):
+        """The capturable fetch of a multi-step group: ``out`` [s, B, ...] <- this rank's rows of steps
+        t .. t+s-1 (one launch)."""
+        from ..ops.rows import gather_rows_perm
+
+        s = out.shape[0]
+        if out.shape[1] != self.B or not out.is_contiguous():
+            raise ValueError(f"out must be contiguous [s, {self.B}, ...]")
+        return gather_rows_perm(self.ring.buf, self.perm, step_dev, self.ep0, out.view(s * self.B, *out.shape[2:]),
+                                stride=self.B * self.world, offset=self.rank * self.B, inner=self.B, ostride=self.B)
+
     def gather_into_global(self, glob: torch.Tensor, step_dev: torch.Tensor):
         """The capturable fetch of a multi-step group for an in-place all-gather: ``glob`` [s, N B, ...]
         (one global batch per step); this rank's rows of steps t .. t+s-1 go straight into its slots

@@ -108,7 +108,8 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
     """The end of a single-device step as ONE launch (csrc/adam.hip ``step_tail_kernel``): row Adam over
     ``sets`` (as ``adam_rows``), the loss terms into ``out`` [G, 6], bias Adam (gradient = ``gscale``
     x the column sums of ``colpart`` [G, tm, n]), feature on-counts when ``cnt_part`` /
-    ``feat_count`` are given, and -- with ``gather`` = (ring buffer [N, d], perm int64, ep0 int32 [1],
+    ``feat_count`` are given (``cnt_part`` [G, cnt_tm, n] may have its own slot count: a data-parallel
+    bias gradient arrives already reduced, ``colpart`` = g_bias [G, 1, n] with ``gscale`` 1), and -- with ``gather`` = (ring buffer [N, d], perm int64, ep0 int32 [1],
     out [rows, d]) -- the NEXT step's batch fetch.  The device step counter ``step_dev`` is read by
     every block and advanced by the last one.  ``bsq`` [2, G, n/32] fp32 holds the b^2 partial sums
     of the current bias at index ``step & 1`` (``bias_sq_parts``); the tail writes the other half.
@@ -133,8 +134,9 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
     if ticket.dtype != torch.int32 or ticket.numel() < TICKET_INTS or step_dev is None:
         raise ValueError("ticket must be int32 and step_dev a device counter")
     tm = colpart.shape[1]
-    if tuple(colpart.shape) != (G, tm, n) or (cnt_part is not None and tuple(cnt_part.shape) != (G, tm, n)):
-        raise ValueError("colpart / cnt_part must be [G, tm, n]")
+    cnt_tm = cnt_part.shape[1] if cnt_part is not None else tm
+    if tuple(colpart.shape) != (G, tm, n) or (cnt_part is not None and tuple(cnt_part.shape) != (G, cnt_tm, n)):
+        raise ValueError("colpart must be [G, tm, n] and cnt_part [G, cnt_tm, n]")
     gbuf = perm = ep0 = gout = None
     grows = row_bytes = nbuf = nperm = 0
     if gather is not None:
@@ -155,7 +157,7 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
         enc_part.shape[1], _lib.ptr(dec_part), dec_part.shape[1], _lib.ptr(cnt_part), _lib.ptr(feat_count),
         _lib.ptr(l1), _lib.ptr(bias_decay), _lib.ptr(out), n, B, float(gscale), _lib.ptr(bsq), _lib.ptr(ticket),
         _lib.ptr(gbuf), nbuf, _lib.ptr(perm), nperm, _lib.ptr(ep0), _lib.ptr(gout), grows, row_bytes,
-        int(nsplit), int(gstride), _lib.ptr(live), _lib.stream_handle(),
+        int(nsplit), int(gstride), _lib.ptr(live), int(cnt_tm), _lib.stream_handle(),
     )
     _lib.check(rc, "sc_step_tail")
 

@@ -566,7 +566,7 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
                  const float* l1, const float* bias_decay, float* out, int n, int B, float gscale,
                  float* bsq, int* ticket, const void* gbuf, long nbuf, const long* perm, long nperm,
                  const int* ep0, void* gout, long grows, long row_bytes, int nsplit, long gstride,
-                 const int* live, hipStream_t stream) {
+                 const int* live, int cnt_tm, hipStream_t stream) {
   if (d % 256 || d > 4096 || nset < 1 || nset > 2 || n % 32 || !step || !ticket || !bsq || nsplit < 1) return 1;
   if (gbuf && (row_bytes % 16 || nbuf < 1)) return 1;
   AdamArgs a;
@@ -582,7 +582,9 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
   BiasArgs ba;
   ba.b = b; ba.m = bm; ba.v = bv; ba.colpart = colpart; ba.tm = tm;
   ba.enc_part = enc_part; ba.enc_tiles = enc_tiles; ba.dec_part = dec_part; ba.dec_tiles = dec_tiles;
-  ba.cnt_part = cnt_part; ba.feat_count = feat_count; ba.cnt_tm = tm;
+  // (the bias gradient may arrive reduced -- data parallel: tm = 1 -- while the on-counts keep the
+  // encoder's per-128-row slots)
+  ba.cnt_part = cnt_part; ba.feat_count = feat_count; ba.cnt_tm = cnt_tm > 0 ? cnt_tm : tm;
   ba.l1 = l1; ba.bias_decay = bias_decay; ba.lr = lr; ba.out = out;
   ba.n = n; ba.B = B; ba.d = d; ba.nmodels = G; ba.gscale = gscale;
   ba.b1 = b1; ba.b2 = b2; ba.eps = eps; ba.bc1 = 1.f; ba.bc2 = 1.f; ba.update = 1; ba.step = step;

@@ -30,6 +30,8 @@ from typing import Dict, List, Optional, Sequence
 
 import torch
 
+from ..ops import adam as adam_ops
+
 from .dist import DistInfo
 from .zero import shard_range
 
@@ -75,6 +77,7 @@ class GraphedDataParallel:
                 raise ValueError("every chunk engine must take the same [B, d] batch")
             e.grad_scale = 1.0 / max(1, info.world_size)
         self.x = torch.empty(self.B, self.d, device=self.device, dtype=torch.bfloat16)
+        self._xs = None  # [s, B, d]: a group's batches, fetched in one launch at the group's start
         self.count_every = count_every
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         if sync_params and info.world_size > 1:  # identical initial parameters: rank 0's
@@ -85,13 +88,15 @@ class GraphedDataParallel:
             torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ one step (captured)
-    def _compute(self, c: _Chunk, count: bool):
+    def _compute(self, c: _Chunk, count: bool, x: torch.Tensor):
         e = c.engine
         e._counted = count
-        xp = e.prepare(self.x)
+        xp = e.prepare(x)
         e.forward(xp, count)
-        e.wgrad_first(xp)
-        e.wgrad_second(xp, reduce_bias=True)
+        # both weight gradients in ONE grouped launch (the chunk's reduction waits for all of them
+        # anyway), then the bias gradient into the flat buffer
+        e.backward_weights(xp)
+        e._reduce_bias_grad()
 
     def _reduce(self, c: _Chunk):
         e = c.engine
@@ -117,14 +122,21 @@ class GraphedDataParallel:
                 cur.wait_event(ev)
 
     def _update(self, c: _Chunk):
-        from ..ops import adam as adam_ops
-
         e = c.engine
         self._wait(c.red_ev)
         c.red_ev = None
         if self.mode == "dp":
-            e.adam_rows_all()
-            e._bias_loss(update=True, reduced=True)
+            if e._tail_ok:
+                # the fused step tail (row Adam + losses + bias Adam, one launch) on the all-reduced
+                # gradients: the bias gradient arrives reduced and scaled ([G, 1, n], gscale 1)
+                adam_ops.step_tail(e._adam_sets(), e.lr, *e.betas, e.eps, e.step_dev, e.params[e._bkey],
+                                   e.m[e._bkey], e.v[e._bkey], e.g_bias, e.enc_part, e.dec_part, e.l1,
+                                   e.bias_decay, e.out, e.batch_size, 1.0, e._bsq, e._ticket,
+                                   cnt_part=e.cnt_part if e._counted else None,
+                                   feat_count=e.feature_counts if e._counted else None, live=e.nactive)
+            else:
+                e.adam_rows_all()
+                e._bias_loss(update=True, reduced=True)
             return
         G, n, d = e.n_models, e.n, e.d
         lo, hi = c.lo, c.hi
@@ -161,17 +173,19 @@ class GraphedDataParallel:
         e0 = self.chunks[0].engine
         K = len(self.chunks)
         prev: Optional[_Chunk] = None
-        for count in pattern:
-            if prev is not None and K == 1:  # one chunk: its update precedes its next compute (and the fetch)
+        if self.source is not None:  # this rank's rows of every step of the group: ONE launch
+            xs = self._xs_buffer(len(pattern))[: len(pattern)]
+            self.source.gather_steps(xs, e0.step_dev)
+        for i, count in enumerate(pattern):
+            if prev is not None and K == 1:  # one chunk: its update precedes its next compute
                 self._update(prev)
                 prev = None
-            if self.source is not None:  # else the caller filled self.x (one step per replay)
-                self.source.gather(self.x, e0.step_dev)
+            x = xs[i] if self.source is not None else self.x  # (no source: the caller filled self.x)
             for c in self.chunks:
                 if c.gath_ev is not None:  # ZeRO-1: this chunk's shadows from the last update
                     self._wait(c.gath_ev)
                     c.gath_ev = None
-                self._compute(c, count)
+                self._compute(c, count, x)
                 self._reduce(c)
                 if prev is not None:
                     self._update(prev)
@@ -182,8 +196,16 @@ class GraphedDataParallel:
             c.gath_ev = None
         self.comm.join()
 
+    def _xs_buffer(self, s: int):
+        if self._xs is None or self._xs.shape[0] < s:
+            self._xs = torch.empty(s, self.B, self.d, device=self.device, dtype=torch.bfloat16)
+            self._graphs = {}  # captured on the old buffer
+        return self._xs
+
     def _graph(self, pattern):
         key = tuple(bool(c) for c in pattern)
+        if self.source is not None:
+            self._xs_buffer(len(key))
         g = self._graphs.get(key)
         if g is None:
             torch.cuda.synchronize(self.device)
@@ -199,6 +221,10 @@ class GraphedDataParallel:
     # ------------------------------------------------------------------ API
     def prime(self, patterns: Sequence[Sequence[bool]]):
         """Capture + upload (nothing runs) every group graph later replays use."""
+        if self.source is not None:
+            self._xs_buffer(max([1] + [len(p) for p in patterns]))
+        for c in self.chunks:
+            c.engine._tail_ready()
         for p in patterns:
             self._graph(p)
         e0 = self.chunks[0].engine
@@ -215,6 +241,8 @@ class GraphedDataParallel:
             raise ValueError("without a batch source every replay is one step on self.x (step_batch)")
         if self.source is not None:
             self.source.prepare(e0.step_count, len(pattern))
+        for c in self.chunks:
+            c.engine._tail_ready()
         self._graph(pattern).replay()
         for c in self.chunks:
             for count in pattern:
