@@ -404,11 +404,10 @@ __device__ __forceinline__ void tail_bias(const BiasArgs& a, const TailArgs& t, 
   for (int k = threadIdx.x; k < nb; k += 256) bs += t.bsq[((long)par * a.nmodels + g) * nb + k];
   bs = block_sum_256(bs, sred);
   float gs = 0.f, cs = 0.f;
-  for (int k = grp; k < a.tm; k += 8) {
-    const long o = ((long)g * a.tm + k) * n + j;
-    gs += a.colpart[o];
-    if (counting) cs += a.cnt_part[o];
-  }
+  for (int k = grp; k < a.tm; k += 8) gs += a.colpart[((long)g * a.tm + k) * n + j];
+  // (on-counts keep the encoder's 128-row slots even when the bias gradient arrives reduced, tm = 1)
+  if (counting)
+    for (int k = grp; k < a.cnt_tm; k += 8) cs += a.cnt_part[((long)g * a.cnt_tm + k) * n + j];
   gred[grp][col] = gs;
   cred[grp][col] = cs;
   __syncthreads();
