@@ -41,7 +41,7 @@ def adam_rows(sets, lr, step, b1=0.9, b2=0.999, eps=1e-8, rows_per_model=None, s
         for k in ("p", "g", "m", "v"):
             t = s[k]
             want = torch.bfloat16 if (k == "g" and gbf16) else torch.float32
-            if t.dtype != want or tuple(t.shape) != shp or not t.is_contiguous():
+            if t.dtype != want or tuple(t.shape) != tuple(sets[0]["p"].shape) or not t.is_contiguous():
                 raise ValueError(f"adam set tensor {k} must be contiguous {want} {shp} (bf16 gradients: all sets)")
         if s.get("shadow") is not None and (s["shadow"].dtype != torch.bfloat16 or s["shadow"].numel() != nrows * d):
             raise ValueError("shadow must be bf16 of the parameter's size")
@@ -104,7 +104,7 @@ TICKET_INTS = (1 + 64) * 32  # csrc/adam.hip: top + TK_SUB sub-counters, one 128
 
 def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, enc_part, dec_part, l1, bias_decay,
               out, B, gscale, bsq, ticket, cnt_part=None, feat_count=None, gather=None, nsplit=1, gstride=0,
-              live=None):
+              live=None, row0=None):
     """The end of a single-device step as ONE launch (csrc/adam.hip ``step_tail_kernel``): row Adam over
     ``sets`` (as ``adam_rows``), the loss terms into ``out`` [G, 6], bias Adam (gradient = ``gscale``
     x the column sums of ``colpart`` [G, tm, n]), feature on-counts when ``cnt_part`` /
@@ -115,17 +115,22 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
     of the current bias at index ``step & 1`` (``bias_sq_parts``); the tail writes the other half.
     ``ticket``: ``TICKET_INTS`` zero-initialised int32 (completion counters; reset by the kernel).  ``nsplit`` / ``gstride``: each set's
     gradient is the first of ``nsplit`` split-K partial slabs (as ``adam_rows``).  ``live``: int32 [G] live
-    row counts of a masked ensemble (rows past them are skipped, as ``adam_rows``)."""
+    row counts of a masked ensemble (rows past them are skipped, as ``adam_rows``).  ``row0``: the sets are
+    [rows, d] views of rows [row0, row0 + rows) of the [G n, d] stacks (a ZeRO-1 shard)."""
     shp = tuple(sets[0]["p"].shape)
     d = shp[-1]
     nrows = sets[0]["p"].numel() // d
     G, n = bias.shape
+    if row0 is not None:  # a row shard: check it, then treat it like the full stack below
+        if len(shp) != 2 or row0 < 0 or row0 + shp[0] > G * n:
+            raise ValueError(f"row shard [{shp}] at row {row0} is outside the [{G} x {n}] stack")
+        shp = (G, n, d)
     gbf16 = sets[0]["g"].dtype == torch.bfloat16
     for s in sets:
         for k in ("p", "g", "m", "v"):
             t = s[k]
             want = torch.bfloat16 if (k == "g" and gbf16) else torch.float32
-            if t.dtype != want or tuple(t.shape) != shp or not t.is_contiguous():
+            if t.dtype != want or tuple(t.shape) != tuple(sets[0]["p"].shape) or not t.is_contiguous():
                 raise ValueError(f"step_tail set tensor {k} must be contiguous {want} {shp}")
     if len(shp) != 3 or shp[0] != G or shp[1] != n or n % 32 or d % 256 or d > 1024:
         raise ValueError(f"step_tail needs [G, n, d] sets with n % 32 == 0, d in 256..1024 (got {shp}, bias {G}x{n})")
@@ -157,7 +162,7 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
         enc_part.shape[1], _lib.ptr(dec_part), dec_part.shape[1], _lib.ptr(cnt_part), _lib.ptr(feat_count),
         _lib.ptr(l1), _lib.ptr(bias_decay), _lib.ptr(out), n, B, float(gscale), _lib.ptr(bsq), _lib.ptr(ticket),
         _lib.ptr(gbuf), nbuf, _lib.ptr(perm), nperm, _lib.ptr(ep0), _lib.ptr(gout), grows, row_bytes,
-        int(nsplit), int(gstride), _lib.ptr(live), int(cnt_tm), _lib.stream_handle(),
+        int(nsplit), int(gstride), _lib.ptr(live), int(cnt_tm), int(row0 or 0), _lib.stream_handle(),
     )
     _lib.check(rc, "sc_step_tail")
 

@@ -565,7 +565,7 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
                  const float* l1, const float* bias_decay, float* out, int n, int B, float gscale,
                  float* bsq, int* ticket, const void* gbuf, long nbuf, const long* perm, long nperm,
                  const int* ep0, void* gout, long grows, long row_bytes, int nsplit, long gstride,
-                 const int* live, int cnt_tm, hipStream_t stream) {
+                 const int* live, int cnt_tm, long row0, hipStream_t stream) {
   if (d % 256 || d > 4096 || nset < 1 || nset > 2 || n % 32 || !step || !ticket || !bsq || nsplit < 1) return 1;
   if (gbuf && (row_bytes % 16 || nbuf < 1)) return 1;
   AdamArgs a;
@@ -577,7 +577,9 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
   if (nset == 1) a.set[1] = a.set[0], a.set[1].rows = 0;
   a.nset = nset; a.d = d; a.rows_per_model = rows_per_model; a.lr = lr;
   a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = 1.f; a.bc2 = 1.f; a.step = step;
-  a.nsplit = nsplit; a.gstride = gstride; a.row0 = 0; a.live = live;  // live: masked ensembles (may be null)
+  // live: masked ensembles (may be null); row0: the sets are rows [row0, row0 + rows) of the
+  // [G n] stack (a ZeRO-1 shard; the loss and bias roles still cover every model)
+  a.nsplit = nsplit; a.gstride = gstride; a.row0 = row0; a.live = live;
   BiasArgs ba;
   ba.b = b; ba.m = bm; ba.v = bv; ba.colpart = colpart; ba.tm = tm;
   ba.enc_part = enc_part; ba.enc_tiles = enc_tiles; ba.dec_part = dec_part; ba.dec_tiles = dec_tiles;

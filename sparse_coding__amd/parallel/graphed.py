@@ -157,9 +157,17 @@ class GraphedDataParallel:
         else:
             sets = [dict(p=rows(e.params["encoder"]), g=rows(g[0]) if c.world == 1 else g[0], m=rows(e.m["encoder"]),
                          v=rows(e.v["encoder"]), shadow=rows(e.enc_shadow), norms=e.norms.view(-1)[lo:hi], norm=True)]
-        adam_ops.adam_rows(sets, e.lr, e.step_count + 1, *e.betas, e.eps, rows_per_model=n, step_dev=e.step_dev,
-                           row0=lo)
-        e._bias_loss(update=True, reduced=True)
+        if e._tail_ok:
+            # the fused step tail on the owned rows (row Adam) + every model's losses and bias Adam
+            # (the bias gradient arrives all-reduced and scaled)
+            adam_ops.step_tail(sets, e.lr, *e.betas, e.eps, e.step_dev, e.params[e._bkey], e.m[e._bkey],
+                               e.v[e._bkey], e.g_bias, e.enc_part, e.dec_part, e.l1, e.bias_decay, e.out,
+                               e.batch_size, 1.0, e._bsq, e._ticket, cnt_part=e.cnt_part if e._counted else None,
+                               feat_count=e.feature_counts if e._counted else None, row0=lo)
+        else:
+            adam_ops.adam_rows(sets, e.lr, e.step_count + 1, *e.betas, e.eps, rows_per_model=n,
+                               step_dev=e.step_dev, row0=lo)
+            e._bias_loss(update=True, reduced=True)
         if c.world > 1:  # every rank's updated shadows (and norms) for the chunk's next compute
             evs = []
             for sh in ([e.dec_shadow] if e.kind == "untied" else []) + [e.enc_shadow]:
