@@ -121,7 +121,9 @@ class GraphedDataParallel:
             if ev is not None:
                 cur.wait_event(ev)
 
-    def _update(self, c: _Chunk):
+    def _update(self, c: _Chunk, gather=None):
+        """The chunk's update after its reduction; ``gather`` (fused tail only): also copy the NEXT
+        step's batch into the engines' input (see ``_steps``)."""
         e = c.engine
         self._wait(c.red_ev)
         c.red_ev = None
@@ -133,7 +135,8 @@ class GraphedDataParallel:
                                    e.m[e._bkey], e.v[e._bkey], e.g_bias, e.enc_part, e.dec_part, e.l1,
                                    e.bias_decay, e.out, e.batch_size, 1.0, e._bsq, e._ticket,
                                    cnt_part=e.cnt_part if e._counted else None,
-                                   feat_count=e.feature_counts if e._counted else None, live=e.nactive)
+                                   feat_count=e.feature_counts if e._counted else None, live=e.nactive,
+                                   gather=gather)
             else:
                 e.adam_rows_all()
                 e._bias_loss(update=True, reduced=True)
@@ -163,7 +166,7 @@ class GraphedDataParallel:
             adam_ops.step_tail(sets, e.lr, *e.betas, e.eps, e.step_dev, e.params[e._bkey], e.m[e._bkey],
                                e.v[e._bkey], e.g_bias, e.enc_part, e.dec_part, e.l1, e.bias_decay, e.out,
                                e.batch_size, 1.0, e._bsq, e._ticket, cnt_part=e.cnt_part if e._counted else None,
-                               feat_count=e.feature_counts if e._counted else None, row0=lo)
+                               feat_count=e.feature_counts if e._counted else None, row0=lo, gather=gather)
         else:
             adam_ops.adam_rows(sets, e.lr, e.step_count + 1, *e.betas, e.eps, rows_per_model=n,
                                step_dev=e.step_dev, row0=lo)
@@ -180,23 +183,37 @@ class GraphedDataParallel:
         """The kernels (and collectives) of ``len(pattern)`` steps; capture target."""
         e0 = self.chunks[0].engine
         K = len(self.chunks)
+        s = len(pattern)
         prev: Optional[_Chunk] = None
-        if self.source is not None:  # this rank's rows of every step of the group: ONE launch
-            xs = self._xs_buffer(len(pattern))[: len(pattern)]
+        # The engines read every step's batch from self.x.  With a source, this rank's rows of all the
+        # group's steps are fetched at its start in ONE launch (xs); step 0's batch is copied into x,
+        # and the fused tail of the update that runs right before step i's first compute copies xs[i]
+        # (through an identity index from the group's first step), so each encoder reads a batch
+        # written just before it (L2 / MALL-hot, as in the single-GPU step).
+        feed = None
+        if self.source is not None:
+            xs = self._xs_buffer(s)[:s]
             self.source.gather_steps(xs, e0.step_dev)
+            if all(c.engine._tail_ok for c in self.chunks):
+                self._ep0.copy_(e0.step_dev)
+                feed = (self._xs.view(-1, self.d), self._ident, self._ep0, self.x)
+            self.x.copy_(xs[0])
         for i, count in enumerate(pattern):
             if prev is not None and K == 1:  # one chunk: its update precedes its next compute
-                self._update(prev)
+                self._update(prev, gather=feed)
                 prev = None
-            x = xs[i] if self.source is not None else self.x  # (no source: the caller filled self.x)
-            for c in self.chunks:
+            if self.source is not None and feed is None and i > 0:
+                self.x.copy_(xs[i])
+            for ci, c in enumerate(self.chunks):
                 if c.gath_ev is not None:  # ZeRO-1: this chunk's shadows from the last update
                     self._wait(c.gath_ev)
                     c.gath_ev = None
-                self._compute(c, count, x)
+                self._compute(c, count, self.x)
                 self._reduce(c)
                 if prev is not None:
-                    self._update(prev)
+                    # (K > 1: the update in the last chunk's slot is the one right before step i+1)
+                    last = K > 1 and ci == K - 1 and i + 1 < s
+                    self._update(prev, gather=feed if last else None)
                 prev = c
         self._update(prev)
         for c in self.chunks:  # every side-stream op joins the capture before it ends
@@ -207,6 +224,8 @@ class GraphedDataParallel:
     def _xs_buffer(self, s: int):
         if self._xs is None or self._xs.shape[0] < s:
             self._xs = torch.empty(s, self.B, self.d, device=self.device, dtype=torch.bfloat16)
+            self._ident = torch.arange(s * self.B, device=self.device, dtype=torch.int64)
+            self._ep0 = torch.zeros(1, device=self.device, dtype=torch.int32)
             self._graphs = {}  # captured on the old buffer
         return self._xs
 
@@ -312,8 +331,15 @@ class GraphedEnsembleSharded:
 
     def _buffers(self, s: int):
         if self._glob is None or self._glob.shape[0] < s:
-            self._glob = torch.empty(s, self.N * self.B, self.es.d, device=self.device, dtype=torch.bfloat16)
-            self._graphs = {}  # captured on the old buffer
+            NB = self.N * self.B
+            self._glob = torch.empty(s, NB, self.es.d, device=self.device, dtype=torch.bfloat16)
+            # the engine's input and the tail-gather plumbing: step k's fused tail copies global batch
+            # k+1 into it (rows (t + 1 - ep0) NB + r of the group buffer through an identity index),
+            # so each step's encoder reads a batch written just before it -- as the single-GPU step
+            self._x = torch.empty(NB, self.es.d, device=self.device, dtype=torch.bfloat16)
+            self._ident = torch.arange(s * NB, device=self.device, dtype=torch.int64)
+            self._ep0 = torch.zeros(1, device=self.device, dtype=torch.int32)
+            self._graphs = {}  # captured on the old buffers
         return self._glob
 
     def _steps(self, pattern):
@@ -324,11 +350,20 @@ class GraphedEnsembleSharded:
         B, r = self.B, self.es.info.rank
         evs = [self.comm.all_gather(glob[k], glob[k][r * B:(r + 1) * B], overlap=True) for k in range(s)]
         cur = torch.cuda.current_stream(self.device)
+        tail = bool(e._tail_ok)
+        if tail:
+            self._ep0.copy_(e.step_dev)  # the group's first step: the tail's index base
+            flat = self._glob.view(-1, self.es.d)
         for k, count in enumerate(pattern):
-            if evs[k] is not None:
-                cur.wait_event(evs[k])
+            if k == 0 or not tail:
+                if evs[k] is not None:
+                    cur.wait_event(evs[k])
+                self._x.copy_(glob[k])
+            if tail and k + 1 < s and evs[k + 1] is not None:
+                cur.wait_event(evs[k + 1])  # the tail of step k reads global batch k+1
             e._counted = count
-            e._step_kernels(glob[k], count)
+            e._step_kernels(self._x, count, gather=(flat, self._ident, self._ep0, self._x) if tail and k + 1 < s
+                            else None)
         self.comm.join()
 
     def _graph(self, pattern):
