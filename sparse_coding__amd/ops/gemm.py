@@ -37,6 +37,20 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 _CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 1,
                 EPI_DC_MASK: 1, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
 _CFG_OVERRIDE = None
+
+
+def _env_cfgs():
+    """``SC_GEMM_CFG="epi:cfg,..."`` (e.g. ``0:13,6:13,7:13``) overrides per-epilogue defaults -- for
+    same-box A/B runs of whole steps (scripts/gemm_lab.py times the kernels in isolation)."""
+    import os
+
+    spec = os.environ.get("SC_GEMM_CFG", "").strip()
+    for item in filter(None, spec.split(",")):
+        epi, cfg = item.split(":")
+        _CFG_DEFAULT[int(epi)] = int(cfg)
+
+
+_env_cfgs()
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 # cfg bits 2-3 select the K pipeline: 0 BK64 x 2-stage LDS ring (default), 1 BK32 x 4,
 # 2 BK32 x 2 (smallest LDS footprint: most co-resident blocks), 3 BK32 x 3 (the
