@@ -34,8 +34,12 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 # picks that.  A persistent 128x128 tile loop with a continuous LDS-DMA stream across tiles
 # (bit-identical, not faster: two co-resident workgroups per CU already hide the same
 # latencies) and Adam fused into the weight-gradient epilogue were measured and removed.
-_CFG_DEFAULT = {EPI_ENC: 1, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 1,
-                EPI_DC_MASK: 1, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
+# Round 4, in-step A/B on one box (profiles/r4/cfg_ab/): the encoder and code-gradient epilogues on
+# 128x128 blocks with the BK32 x 3-stage ring (cfg 13: 48 KB of LDS instead of 64, so one more
+# workgroup co-resides per CU) -- 0.2932 / 0.2947 vs 0.3100 / 0.3088 ms per step with BK64 x 2
+# (isolated kernel timings showed only ~1 us: the gain is in-step co-residency)
+_CFG_DEFAULT = {EPI_ENC: 13, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 13,
+                EPI_DC_MASK: 13, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
 _CFG_OVERRIDE = None
 
 
