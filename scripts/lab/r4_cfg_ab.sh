@@ -3,8 +3,8 @@
 # epi 0 encoder, 6 encoder + counts, 7 code gradient, 1 decoder, 3 weight gradients.
 set -e
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
-O="$GRAFT_REPO_ROOT/gpurun_out/r4cfg"; mkdir -p "$O"
-V=("new:" "old:0:1,6:1,7:1" "dec13:1:13" "dec9:1:9" "encdc9:0:9,6:9,7:9" "encdc15:0:15,6:15,7:15" "wg11:3:11" "wg9:3:9")
+O="$GRAFT_REPO_ROOT/gpurun_out/${CFG_OUT:-r4cfg}"; mkdir -p "$O"
+V=(${CFG_VARIANTS:-"new:" "old:0:1,6:1,7:1" "dec13:1:13" "dec9:1:9" "encdc9:0:9,6:9,7:9" "encdc15:0:15,6:15,7:15" "wg11:3:11" "wg9:3:9"})
 for r in 1 2; do
   for spec in "${V[@]}"; do
     name=${spec%%:*}; cfg=${spec#*:}
