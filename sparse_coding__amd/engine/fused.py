@@ -571,7 +571,7 @@ class FusedSAEEnsemble:
             self._graph = None
         return self
 
-    def _step_kernels(self, x, count=None, gather=None):
+    def _step_kernels(self, x, count=None, gather=None, before_update=None):
         """All kernels of one step (captured as one HIP graph when enabled).  Side-stream
         variants of this sequence -- decoder Adam beside the encoder weight gradient, the loss /
         bias-Adam tail beside the weight gradient, Adam fused into the weight-gradient epilogue,
@@ -581,6 +581,8 @@ class FusedSAEEnsemble:
         x = self.prepare(x)
         self.forward(x, count, target)
         self.backward_weights(x)
+        if before_update is not None:  # e.g. a stream wait the update (its next-batch fetch) needs
+            before_update()
         self._apply_update_kernels(gather if self._tail_ok else None)
 
     def add_static_input(self, t: torch.Tensor) -> int:

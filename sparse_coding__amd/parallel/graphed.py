@@ -359,11 +359,12 @@ class GraphedEnsembleSharded:
                 if evs[k] is not None:
                     cur.wait_event(evs[k])
                 self._x.copy_(glob[k])
-            if tail and k + 1 < s and evs[k + 1] is not None:
-                cur.wait_event(evs[k + 1])  # the tail of step k reads global batch k+1
+            nxt = tail and k + 1 < s
+            # the tail of step k reads global batch k+1: only the update waits for that gather
+            wait = (lambda ev=evs[k + 1]: cur.wait_event(ev)) if nxt and evs[k + 1] is not None else None
             e._counted = count
-            e._step_kernels(self._x, count, gather=(flat, self._ident, self._ep0, self._x) if tail and k + 1 < s
-                            else None)
+            e._step_kernels(self._x, count, gather=(flat, self._ident, self._ep0, self._x) if nxt else None,
+                            before_update=wait)
         self.comm.join()
 
     def _graph(self, pattern):
