@@ -462,7 +462,7 @@ class FusedSAEEnsemble:
                                self._alpha, self._bsq, self._ticket,
                                cnt_part=self.cnt_part if self._counted else None,
                                feat_count=self.feature_counts if self._counted else None, gather=gather,
-                               live=self.nactive, **self._adam_split_kw())
+                               live=self.nactive, live_host=self._live, **self._adam_split_kw())
             return
         # scale / centering first: their gradients read the pre-update dictionary (adam_first)
         if self.kind == "threshold" or self.learned_center:

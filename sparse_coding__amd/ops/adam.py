@@ -104,7 +104,7 @@ TICKET_INTS = (1 + 64) * 32  # csrc/adam.hip: top + TK_SUB sub-counters, one 128
 
 def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, enc_part, dec_part, l1, bias_decay,
               out, B, gscale, bsq, ticket, cnt_part=None, feat_count=None, gather=None, nsplit=1, gstride=0,
-              live=None, row0=None):
+              live=None, row0=None, live_host=None):
     """The end of a single-device step as ONE launch (csrc/adam.hip ``step_tail_kernel``): row Adam over
     ``sets`` (as ``adam_rows``), the loss terms into ``out`` [G, 6], bias Adam (gradient = ``gscale``
     x the column sums of ``colpart`` [G, tm, n]), feature on-counts when ``cnt_part`` /
@@ -115,7 +115,8 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
     of the current bias at index ``step & 1`` (``bias_sq_parts``); the tail writes the other half.
     ``ticket``: ``TICKET_INTS`` zero-initialised int32 (completion counters; reset by the kernel).  ``nsplit`` / ``gstride``: each set's
     gradient is the first of ``nsplit`` split-K partial slabs (as ``adam_rows``).  ``live``: int32 [G] live
-    row counts of a masked ensemble (rows past them are skipped, as ``adam_rows``).  ``row0``: the sets are
+    row counts of a masked ensemble (rows past them are skipped, as ``adam_rows``; with ``live_host``, the
+    same sizes as host ints, the row blocks cover only live rows).  ``row0``: the sets are
     [rows, d] views of rows [row0, row0 + rows) of the [G n, d] stacks (a ZeRO-1 shard)."""
     shp = tuple(sets[0]["p"].shape)
     d = shp[-1]
@@ -162,7 +163,9 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
         enc_part.shape[1], _lib.ptr(dec_part), dec_part.shape[1], _lib.ptr(cnt_part), _lib.ptr(feat_count),
         _lib.ptr(l1), _lib.ptr(bias_decay), _lib.ptr(out), n, B, float(gscale), _lib.ptr(bsq), _lib.ptr(ticket),
         _lib.ptr(gbuf), nbuf, _lib.ptr(perm), nperm, _lib.ptr(ep0), _lib.ptr(gout), grows, row_bytes,
-        int(nsplit), int(gstride), _lib.ptr(live), int(cnt_tm), int(row0 or 0), _lib.stream_handle(),
+        int(nsplit), int(gstride), _lib.ptr(live), int(cnt_tm), int(row0 or 0),
+        C.cast((C.c_int * len(live_host))(*[int(v) for v in live_host]), C.c_void_p)
+        if (live_host is not None and live is not None) else None, _lib.stream_handle(),
     )
     _lib.check(rc, "sc_step_tail")
 

@@ -12,6 +12,8 @@
 // also reduces the deterministic per-tile partials written by the GEMM
 // epilogues (no float atomics anywhere in the step).
 #include "common.h"
+
+#include <algorithm>
 #include <stdlib.h>
 
 namespace scamd {
@@ -357,6 +359,9 @@ struct TailArgs {
   const u32x4_t* gbuf; long nbuf; const long* perm; long nperm; const int* ep0; u32x4_t* gout; long grows;
   int row_vec;
   int nloss, nbias, ngather;  // block counts of the roles
+  // masked ensembles: the row-Adam blocks cover only live rows (lcomp: live-row prefix lpre[g] over
+  // the models, the same for every set; compact row rc of set s -> row g n + rc - lpre[g] of model g)
+  int lcomp, lG, lpre[17];
 };
 
 __device__ __forceinline__ void tail_loss(const BiasArgs& a, const TailArgs& t, int g, int par) {
@@ -465,7 +470,18 @@ __global__ __launch_bounds__(256) void step_tail_kernel(AdamArgs a, BiasArgs b, 
       for (int v = lane; v < t.row_vec; v += 64) op[v] = sp[v];
     }
   } else {
-    adam_row<NV, GBF>(a, (long)(bid - t.nloss - t.nbias) * 4 + (threadIdx.x >> 6));
+    long r = (long)(bid - t.nloss - t.nbias) * 4 + (threadIdx.x >> 6);
+    if (t.lcomp) {  // compacted masked grid: skip the dead rows' blocks altogether
+      const long per = t.lpre[t.lG];
+      const int s = (int)(r / per);
+      long rc = r - s * per;
+      int g = 0;
+#pragma unroll
+      for (int k = 1; k < 16; ++k)
+        if (k < t.lG && rc >= t.lpre[k]) g = k;
+      r = s < a.nset ? (long)s * a.set[0].rows + (long)g * a.rows_per_model + (rc - t.lpre[g]) : a.set[0].rows * 2;
+    }
+    adam_row<NV, GBF>(a, r);
   }
   // The last block to finish advances the step counter.  Every block's read of *step was consumed
   // (bias corrections, parity) before its ticket, so no fence is needed -- and none is wanted: an
@@ -565,7 +581,7 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
                  const float* l1, const float* bias_decay, float* out, int n, int B, float gscale,
                  float* bsq, int* ticket, const void* gbuf, long nbuf, const long* perm, long nperm,
                  const int* ep0, void* gout, long grows, long row_bytes, int nsplit, long gstride,
-                 const int* live, int cnt_tm, long row0, hipStream_t stream) {
+                 const int* live, int cnt_tm, long row0, const int* live_h, hipStream_t stream) {
   if (d % 256 || d > 4096 || nset < 1 || nset > 2 || n % 32 || !step || !ticket || !bsq || nsplit < 1) return 1;
   if (gbuf && (row_bytes % 16 || nbuf < 1)) return 1;
   AdamArgs a;
@@ -596,7 +612,21 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
   t.gout = reinterpret_cast<u32x4_t*>(gout); t.grows = gbuf ? grows : 0;
   t.row_vec = (int)(row_bytes / 16);
   t.nloss = G; t.nbias = G * (n / 32); t.ngather = gbuf ? (int)((grows + 3) / 4) : 0;
-  const long blocks = t.nloss + t.nbias + t.ngather + (total + 3) / 4;
+  t.lcomp = 0; t.lG = G;
+  long arows = total;
+  // host copy of a masked ensemble's live sizes (full-stack sets only, G <= 16): launch live rows only
+  if (live_h && live && row0 == 0 && G <= 16 && rows_per_model > 0 && rows[0] == (long)G * rows_per_model &&
+      (nset == 1 || rows[1] == rows[0])) {
+    t.lpre[0] = 0;
+    for (int g = 0; g < G; ++g)
+      t.lpre[g + 1] = t.lpre[g] + std::min(rows_per_model, std::max(0, live_h[g]));
+    for (int g = G + 1; g < 17; ++g) t.lpre[g] = t.lpre[G];
+    if (t.lpre[G] > 0) {
+      t.lcomp = 1;
+      arows = (long)nset * t.lpre[G];
+    }
+  }
+  const long blocks = t.nloss + t.nbias + t.ngather + (arows + 3) / 4;
 #define SC_TAIL(NVV)                                                                                   \
   case NVV:                                                                                            \
     if (gbf16) hipLaunchKernelGGL((step_tail_kernel<NVV, true>), dim3(blocks), dim3(256), 0, stream, a, ba, t); \
