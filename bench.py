@@ -47,10 +47,10 @@ BASELINE_ACT_PER_S = 1.86e3
 # ``bench.py --engine eager`` (profiles/bench_eager_r2.json: 2.63 ms/step).
 EAGER_SAME_BOX_ACT_PER_S = 779054.6
 # single-GPU step and per-rank ensemble-sharded steps measured on one MI355X (inputs of the
-# comm model's prediction, parallel/comm_model.py; profiles/bench_r3_v5_final.json,
-# profiles/es_projection_r3.jsonl)
-T1_MS = 0.3064
-ES_MS = {2: 0.285, 4: 0.2714, 8: 0.2621}
+# comm model's prediction, parallel/comm_model.py; round 4: profiles/r4/final_defaults/long_*.json,
+# profiles/r4/es_projection/es_projection_r4.jsonl -- G/N models on N B rows, single-step graphs)
+T1_MS = 0.300
+ES_MS = {2: 0.2657, 4: 0.246, 8: 0.2374}
 METRIC = "activations/sec (ensemble train) + FVU@L0, Pythia-70m resid SAE at 1/2/4/8 GPU"
 
 
