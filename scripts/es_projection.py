@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--models", type=int, default=8)
     ap.add_argument("--d", type=int, default=512)
     ap.add_argument("--ratio", type=int, default=4)
+    ap.add_argument("--ns", default="1,2,4,8", help="the N-GPU layouts to measure")
+    ap.add_argument("--wsplit", default="auto", help="weight-gradient split-K of the per-rank engine")
     a = ap.parse_args()
     from sparse_coding__amd.engine.fused import FusedSAEEnsemble
     from sparse_coding__amd.models.signatures import FunctionalSAE
@@ -39,11 +41,13 @@ def main():
     l1s = np.logspace(-4, -2, a.models)
     models = [FunctionalSAE.init(a.d, n, float(l), device=dev) for l in l1s]
     t1 = None
-    for N in (1, 2, 4, 8):
+    for N in [int(v) for v in a.ns.split(",")]:
         if a.models % N:
             continue
         gb = N * a.batch
-        eng = FusedSAEEnsemble(models[: a.models // N], FunctionalSAE, lr=1e-3, batch_size=gb, device=dev)
+        ws = a.wsplit if a.wsplit == "auto" else int(a.wsplit)
+        eng = FusedSAEEnsemble(models[: a.models // N], FunctionalSAE, lr=1e-3, batch_size=gb, device=dev,
+                               wgrad_split=ws)
         eng.enable_graph()
         x = torch.randn(gb, a.d, device=dev).to(torch.bfloat16)
         eng.x_static.copy_(x)
