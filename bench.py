@@ -169,6 +169,18 @@ class Runner:
             self.step()
 
 
+def _native_comm(info):
+    """The native RCCL communicator for the in-graph collectives, or None (then the runner falls
+    back to host-issued ProcessGroupNCCL collectives) if it cannot be created here."""
+    from sparse_coding__amd.parallel.rccl import RcclComm
+
+    try:
+        return RcclComm(info)
+    except Exception as exc:  # e.g. no librccl symbols / ncclCommInitRank error
+        print(f"[bench] native RCCL communicator unavailable ({exc!r}); host-issued collectives", file=sys.stderr)
+        return None
+
+
 def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
     B = args.batch
     distributed = info.world_size > 1 or args.force_dist
@@ -190,12 +202,11 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
 
         if args.no_graph:
             return Runner(lambda: es.step_sampled(sample), dicts, close=es.flush)
-        if args.dist_graph and distributed:
+        comm = _native_comm(info) if args.dist_graph and distributed else None
+        if comm is not None:
             # the group's batch fetch and in-place all-gathers captured in its graph (parallel/graphed.py)
             from sparse_coding__amd.parallel.graphed import GraphedEnsembleSharded
-            from sparse_coding__amd.parallel.rccl import RcclComm
 
-            comm = RcclComm(info)
             ges = GraphedEnsembleSharded(es, comm, ring.graph_source(B, info.rank, info.world_size))
 
             def run_g(groups):
@@ -216,18 +227,18 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
         return Runner(lambda: es.run_groups([1], sample_steps, pattern), dicts, close=es.flush,
                       run=lambda groups: es.run_groups(groups, sample_steps, pattern),
                       setup=lambda tiling: (ring.ensure_permutation(), es.prime_groups(tiling.sizes, pattern)))
-    if args.engine == "fused" and distributed and not args.no_graph and args.dist_graph:
+    comm = (_native_comm(info) if args.engine == "fused" and distributed and not args.no_graph and args.dist_graph
+            else None)
+    if comm is not None:
         # data parallel / ZeRO-1 with the collectives INSIDE multi-step HIP graphs (native RCCL
         # communicator on its own stream, parallel/rccl.py + parallel/graphed.py)
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.engine.graph_plan import count_pattern
         from sparse_coding__amd.parallel.data_parallel import split_models
         from sparse_coding__amd.parallel.graphed import GraphedDataParallel
-        from sparse_coding__amd.parallel.rccl import RcclComm
 
         engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device)
                    for m in split_models(models, args.dp_chunks)]
-        comm = RcclComm(info)
         gdp = GraphedDataParallel(engines, info, comm, ring.graph_source(B, info.rank, info.world_size), mode=par,
                                   grad_dtype=grad_dtype)
 
