@@ -72,11 +72,17 @@ def main():
     torch.manual_seed(0)
     l1s = np.logspace(-4, -2, 8)
     models = [FunctionalSAE.init(512, 2048, float(l), device=dev) for l in l1s]
+    from sparse_coding__amd.engine.graph_plan import chunks, count_pattern
+
+    # the bench's step: multi-step HIP graphs with the ring gather inside (the fused tail fetches
+    # each next batch)
     eng = FusedSAEEnsemble(models, FunctionalSAE, lr=1e-3, batch_size=a.batch, device=dev).enable_graph()
+    eng.attach_source(ring.graph_source(a.batch))
+    groups = list(chunks(a.steps, 8))
+    eng.prime_source(patterns=[count_pattern(s, 8) for s in sorted(set(groups))])
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        ring.sample(a.batch, out=eng.x_static)
-        eng.step_static()
+    for s in groups:
+        eng.step_source(s, count_pattern(s, 8))
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     rec.update(train_steps=a.steps, train_s=round(el, 2), train_act_per_s=round(a.steps * a.batch / el, 1))
