@@ -79,11 +79,18 @@ def cfg_topk(a):
     eng = FusedTopKEnsemble(models, lr=1e-3, batch_size=B, device=dev, sparse_k=sk)
     eng.enable_graph(not a.eager)
     ring = _ring(d, dev)
-    el = _timed(lambda: eng.step_batch(ring.sample(B, out=eng.x_static)), a.steps, a.warmup, torch.cuda.synchronize)
+    gs = max(1, int(a.graph_steps)) if not a.eager else 1
+    if gs > 1:  # multi-step graphs with the batch gather inside (engine/topk.py run_source)
+        src = ring.graph_source(B)
+        steps = max(1, a.steps // gs) * gs
+        el = _timed(lambda: eng.run_source(src, gs), steps // gs, max(1, a.warmup // gs), torch.cuda.synchronize)
+    else:
+        steps = a.steps
+        el = _timed(lambda: eng.step_batch(ring.sample(B, out=eng.x_static)), steps, a.warmup, torch.cuda.synchronize)
     return {"config": f"4: GPT-2-small residual d={d}, ratio {ratio} (n={n}), fused top-k, k={ks}",
-            "value": round(B * a.steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / a.steps, 3),
-            "batch": B, "models": len(ks), "sparse_wgrad_models": eng.sparse_g, "graph": not a.eager,
-            "dtype": "bf16", "data": "synthetic"}
+            "value": round(B * steps / el, 1), "unit": "activations/s", "ms_per_step": round(1e3 * el / steps, 3),
+            "steps": steps, "batch": B, "models": len(ks), "sparse_wgrad_models": eng.sparse_g, "graph": not a.eager,
+            "graph_steps": gs, "dtype": "bf16", "data": "synthetic"}
 
 
 def cfg_fista(a):
@@ -397,6 +404,8 @@ def main():
     ap.add_argument("--ratio", type=float, default=1.0)
     ap.add_argument("--sparse-k", default="auto", help="topk: models with k <= this take the slot-list wgrad")
     ap.add_argument("--eager", action="store_true", help="topk: no HIP graph")
+    ap.add_argument("--graph-steps", type=int, default=8,
+                    help="topk: steps per graph replay with the batch gather in the graph (1: host sampling)")
     ap.add_argument("--variant", default="both", choices=["both", "masked", "unmasked"], help="masked: which run")
     ap.add_argument("--ring-gb", type=float, default=0.0,
                     help="fista: ring size in GB of HBM (0: 512k rows); config5: 0 = free memory - reserve")

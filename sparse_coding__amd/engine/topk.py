@@ -103,6 +103,7 @@ class FusedTopKEnsemble:
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)
         self.use_graph = False
         self._graphs = None
+        self._src_graphs = None
 
     # ------------------------------------------------------------------ the step
     def _step_kernels(self, x, cur: int):
@@ -156,6 +157,39 @@ class FusedTopKEnsemble:
         self.idx = self.idx_buf[self._cur]
         self._cur ^= 1
         self.step_count += 1
+        return self.mse
+
+    def _capture_source(self, source, steps: int, cur0: int):
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            for i in range(steps):
+                source.gather(self.x_static, self.step_dev)
+                self._step_kernels(self.x_static, cur0 ^ (i & 1))
+        return g
+
+    def run_source(self, source, steps: int):
+        """``steps`` optimizer steps as ONE graph replay with every batch fetched INSIDE the graph
+        (``data.ring.RingGraphSource``: one gather kernel per step on the device step counter), so
+        no host sampling or replay boundary sits between steps.  The pick-buffer parity follows the
+        step index; graphs are cached per (steps, starting parity)."""
+        steps = int(steps)
+        if steps < 1:
+            raise ValueError("steps must be >= 1")
+        if getattr(source, "B", self.batch_size) != self.batch_size:
+            raise ValueError("the source's batch size differs from the engine's")
+        if self._src_graphs is None or self._src_graphs[0] is not source:
+            self._src_graphs = (source, {})
+        key = (steps, self._cur)
+        graphs = self._src_graphs[1]
+        source.prepare(self.step_count, steps)
+        if key not in graphs:
+            graphs[key] = self._capture_source(source, steps, self._cur)
+        graphs[key].replay()
+        last = self._cur ^ ((steps - 1) & 1)
+        self.idx = self.idx_buf[last]
+        self._cur = last ^ 1
+        self.step_count += steps
         return self.mse
 
     # ------------------------------------------------------------------ inference / export

@@ -301,3 +301,36 @@ def test_ring_gather_into_global_matches_indexing():
         idx = src.perm[t0 + k * N * B + r * B: t0 + k * N * B + (r + 1) * B]
         assert torch.equal(glob[k, r * B:(r + 1) * B], ring.buf[idx])
         assert not glob[k, :r * B].any() and not glob[k, (r + 1) * B:].any()
+
+
+def test_topk_multistep_source_graph_matches_eager_steps():
+    """Top-k engine: odd / even multi-step graphs with the batch gather inside (run_source) are
+    bit-identical to eager steps on the same permutation's batches."""
+    from sparse_coding__amd.data.ring import DeviceRing
+    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
+    from sparse_coding__amd.models.topk import TopKEncoder
+
+    torch.manual_seed(31)
+    d, n, B, ks = 256, 1024, 256, [4, 8, 32]
+    models = [TopKEncoder.init(d, n, k, device=DEV) for k in ks]
+    a = FusedTopKEnsemble(models, lr=1e-3, batch_size=B, device=DEV)
+    b = FusedTopKEnsemble(models, lr=1e-3, batch_size=B, device=DEV)
+    rows = torch.randn(B * 16, d, device=DEV).to(torch.bfloat16)
+    ring = DeviceRing(rows.shape[0], d, device=DEV, seed=5)
+    ring.push(rows)
+    src = ring.graph_source(B)
+    losses_a = []
+    for s in (3, 2, 3):
+        a.run_source(src, s)
+        losses_a.append(a.mse.clone())
+    assert a.step_count == 8 and int(src.ep0.item()) == 0
+    losses_b = []
+    for t in range(8):
+        b.step_batch(ring.buf[src.perm[t * B:(t + 1) * B]])
+        if t in (2, 4, 7):
+            losses_b.append(b.mse.clone())
+    torch.cuda.synchronize()
+    for la, lb in zip(losses_a, losses_b):
+        assert torch.equal(la, lb)
+    assert torch.equal(a.params["dict"], b.params["dict"])
+    assert torch.equal(a.idx, b.idx)
