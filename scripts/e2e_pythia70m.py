@@ -19,6 +19,7 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -35,6 +36,7 @@ def main():
     ap.add_argument("--act-norm", type=float, default=9.0,
                     help="rescale rows to this mean norm (a trained Pythia-70m layer-2 residual's); 0 = keep")
     ap.add_argument("--out", default="gpurun_out/e2e")
+    ap.add_argument("--keep-ckpt", action="store_true", help="write learned_dicts.pt into --out (64 MB)")
     a = ap.parse_args()
     from sparse_coding__amd.data.harvest import ActivationHarvester, build_model, harvest_to_ring, synthetic_token_batches
     from sparse_coding__amd.data.ring import DeviceRing
@@ -94,7 +96,9 @@ def main():
                          "fvu_kernel": round(float(f), 4), "l0_kernel": round(float(z), 2)}
                         for l, s, f, z in zip(l1s, scores, fvu_k.cpu(), l0_k.cpu())]
     # 4. checkpoint round trip (reference layout, safe loader)
-    path = os.path.join(a.out, "learned_dicts.pt")
+    # (64 MB of fp32 dictionaries: kept out of --out unless --keep-ckpt, so a results directory
+    # stays small enough to copy back)
+    path = os.path.join(a.out if a.keep_ckpt else tempfile.mkdtemp(), "learned_dicts.pt")
     ckpt.save_learned_dicts([(ld, {"dict_size": 2048, "l1_alpha": float(l)})
                              for ld, l in zip(eng.to_learned_dicts("cpu"), l1s)], path)
     back = ckpt.load_learned_dicts(path)
