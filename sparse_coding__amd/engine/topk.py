@@ -91,6 +91,9 @@ class FusedTopKEnsemble:
         while gs < G and ks[gs] <= int(sparse_k) and d <= 1024:
             gs += 1
         self.sparse_g = gs
+        # the decode scatters codes / code gradients only for the dense-wgrad models (config 4:
+        # 1.054 vs 1.059 ms/step scattering for all, profiles/r4/topk_scatter/)
+        self._dense_from = gs
         self.lists = topk_ops.SlotLists(gs, B, n, ks, kmax, dev) if gs else None
         self.dscv = torch.zeros(G, B, kmax, device=dev) if gs else None
         # bf16 dictionary gradient by default: the dense GEMM's bf16 epilogue + Adam's bf16 loads
@@ -112,7 +115,7 @@ class FusedTopKEnsemble:
         gemm_ops.matmul_nt(x, self.shadow, self.scores)
         topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val))
         topk_ops.decode_grad(idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
-                             self.dscbuf, dscv=self.dscv, prev_idx=prev)
+                             self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from)
         torch.sum(self.row_se, dim=1, out=self._se)
         torch.mul(self._se, 1.0 / (B * d), out=self.mse)
         alpha = 2.0 / (B * d)

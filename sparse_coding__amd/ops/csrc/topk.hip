@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
     const int* __restrict__ idx, const float* __restrict__ val, const int* __restrict__ kv,
     const uint16_t* __restrict__ D, const uint16_t* __restrict__ X, long sx, uint16_t* __restrict__ R,
     float* __restrict__ row_se, uint16_t* __restrict__ codebuf, uint16_t* __restrict__ dscbuf, int G, int B,
-    int n, int d, int kmax, float* __restrict__ dscv, const int* __restrict__ prev_idx) {
+    int n, int d, int kmax, float* __restrict__ dscv, const int* __restrict__ prev_idx, int g_dense0) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)G * B) return;
@@ -689,10 +689,13 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
   se = wave_sum(se);
   if (lane == 0) row_se[row] = se;
   if (!codebuf) return;
+  // models below g_dense0 take the slot-list weight gradient: their dots still feed dscv, but the
+  // dense code / code-gradient buffers are never read, so nothing is scattered (or cleared) there
+  const bool dense = g >= g_dense0;
   // code gradients (units of R): dscore_j = 1[v_j > 0] <R, D[idx_j]>; scatter code and dscore
   uint16_t* Cb = codebuf + row * (long)n;
   uint16_t* Sb = dscbuf + row * (long)n;
-  if (prev_idx) {
+  if (prev_idx && dense) {
     // the previous step's picks of this row go back to zero here (replaces a separate clear
     // launch after the weight gradient); the wait keeps them ordered before the new picks'
     // stores, which may hit the same columns from other lanes of this wave
@@ -738,7 +741,7 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
     const int j = j0 + (lane & (DOTS - 1));
     if (lane < DOTS && j < k) {
       const float w = V[j];
-      if (w > 0.f) {
+      if (w > 0.f && dense) {
         const int c = I[j];
         Cb[c] = f2bf(w);
         Sb[c] = f2bf(dot);
@@ -1026,14 +1029,15 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
 
 int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const void* D, const void* X, long sx,
                         void* R, float* row_se, void* codebuf, void* dscbuf, int G, int B, int n, int d, int kmax,
-                        hipStream_t stream, float* dscv, const int* prev_idx) {
+                        hipStream_t stream, float* dscv, const int* prev_idx, int g_dense0) {
   if (d % 4) return 1;
   const int nv = (d + 255) / 256;
   dim3 grid(((long)G * B + 3) / 4);
 #define SC_D(V) \
   if (nv <= V) { hipLaunchKernelGGL((topk_decode_grad_kernel<V>), grid, dim3(256), 0, stream, idx, val, k, \
       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx, reinterpret_cast<uint16_t*>(R), \
-      row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx); \
+      row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx, \
+      g_dense0); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   SC_D(1) SC_D(2) SC_D(3) SC_D(4) SC_D(8) SC_D(16)
 #undef SC_D

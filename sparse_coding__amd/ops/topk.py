@@ -34,12 +34,15 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
     return idx, val
 
 
-def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dscv=None, prev_idx=None):
+def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dscv=None, prev_idx=None,
+                dense_from: int = 0):
     """Sparse decode + residual (bf16 r_out [G, B, d]) + per-row squared error; with the dense
     buffers, also scatter codes and code gradients <R, D[idx]> (units of R) for the wgrad GEMM;
     with ``dscv`` ([G, B, kmax] fp32) also the per-slot code gradients for ``sparse_wgrad``.
     ``prev_idx``: the previous step's picks ([G, B, kmax]), zeroed in the dense buffers first
-    (instead of a ``clear`` after the previous weight gradient)."""
+    (instead of a ``clear`` after the previous weight gradient).  ``dense_from``: models below it
+    (slot-list weight gradient) get their per-slot ``dscv`` only -- nothing is scattered into (or
+    cleared from) their dense buffers, which stay zero."""
     if prev_idx is not None and (prev_idx.shape != idx.shape or prev_idx.dtype != torch.int32
                                  or not prev_idx.is_contiguous()):
         raise ValueError("prev_idx must be contiguous int32 of idx's shape")
@@ -48,7 +51,8 @@ def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dsc
     sx = 0 if x.dim() == 2 else B * d
     rc = _lib.lib().sc_topk_decode_grad(_lib.ptr(idx), _lib.ptr(val), _lib.ptr(k), _lib.ptr(D), _lib.ptr(x), sx,
                                         _lib.ptr(r_out), _lib.ptr(row_se), _lib.ptr(codebuf), _lib.ptr(dscbuf),
-                                        G, B, n, d, kmax, _lib.stream_handle(), _lib.ptr(dscv), _lib.ptr(prev_idx))
+                                        G, B, n, d, kmax, _lib.stream_handle(), _lib.ptr(dscv), _lib.ptr(prev_idx),
+                                        int(dense_from))
     _lib.check(rc, "sc_topk_decode_grad")
 
 

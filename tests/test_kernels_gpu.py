@@ -1224,7 +1224,14 @@ def test_topk_sparse_wgrad_matches_dense(out_dtype):
     sparse2 = torch.empty(G, n, d, device=DEV, dtype=out_dtype)
     T.slot_lists(idx, k, lists)
     T.sparse_wgrad(lists, val, dscv, r, x, sparse2, 1e-2)
+    # models below dense_from: the same dscv / residual, nothing scattered into the dense buffers
+    cb2, db2, dscv2 = torch.zeros_like(cb), torch.zeros_like(db), torch.zeros_like(dscv)
+    r2, se2 = torch.empty_like(r), torch.empty_like(se)
+    T.decode_grad(idx, val, k, D, x, r2, se2, cb2, db2, dscv=dscv2, dense_from=2)
     torch.cuda.synchronize()
+    assert torch.equal(dscv2, dscv) and torch.equal(r2, r) and torch.equal(se2, se)
+    assert not cb2[:2].any() and not db2[:2].any()
+    assert torch.equal(cb2[2:], cb[2:]) and torch.equal(db2[2:], db[2:])
     assert torch.equal(sparse, sparse2)  # deterministic
     for g in range(G):
         rel = ((sparse[g].float() - dense[g]).norm() / dense[g].norm()).item()
