@@ -157,6 +157,8 @@ class Runner:
 
     def __init__(self, step, dicts, finish=None, close=None, run=None, setup=None):
         self.step, self.dicts = step, dicts
+        self.path, self.comm, self.consistency = "single", None, None
+        self.fallback = None  # why the in-graph path was abandoned for host-issued collectives
         self.finish = finish or (lambda: None)
         self.close = close or (lambda: None)
         self._run = run
@@ -169,21 +171,41 @@ class Runner:
             self.step()
 
 
-def _native_comm(info):
-    """The native RCCL communicator for the in-graph collectives, or None (then the runner falls
-    back to host-issued ProcessGroupNCCL collectives) if it cannot be created here."""
+def _graph_comm(info, args):
+    """The communicator the in-graph (graphed) multi-GPU paths run on, and what it is:
+    ``("rccl", RcclComm)`` -- the native RCCL communicator whose collectives are captured in the step
+    graphs; ``("gloo", HostComm)`` -- gloo rehearsals (e.g. ranks sharing one GPU): the same graphed
+    step sequence, run uncaptured with host-staged collectives; ``(reason, None)`` -- no native
+    communicator here: the runner uses host-issued ProcessGroupNCCL collectives."""
+    if info.backend == "gloo":
+        from sparse_coding__amd.parallel.host_comm import HostComm
+
+        return "gloo", HostComm(info)
     from sparse_coding__amd.parallel.rccl import RcclComm
 
     try:
-        return RcclComm(info)
+        return "rccl", RcclComm(info)
     except Exception as exc:  # e.g. no librccl symbols / ncclCommInitRank error
         print(f"[bench] native RCCL communicator unavailable ({exc!r}); host-issued collectives", file=sys.stderr)
-        return None
+        return f"native RCCL communicator unavailable: {exc!r}", None
 
 
-def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
+PATH_NAMES = {
+    "single": "none (one GPU, no collectives)",
+    "rccl": "in-graph RCCL (native communicator, collectives captured in the multi-step HIP graphs)",
+    "gloo": "graphed step sequence uncaptured, gloo host-staged collectives (rehearsal)",
+    "host": "host-issued ProcessGroup collectives between HIP graph replays",
+    "eager": "eager engine, host-issued ProcessGroup collectives",
+}
+
+
+def make_runner(par, args, info, sig, models, ring, device, grad_dtype, dist_graph=None):
+    """The runner of one training configuration.  ``runner.path`` names the collective path
+    (PATH_NAMES); ``runner.comm`` is the graphed paths' communicator; ``runner.consistency()``
+    (collective, every rank) checks the ranks agree after the run."""
     B = args.batch
     distributed = info.world_size > 1 or args.force_dist
+    dist_graph = args.dist_graph if dist_graph is None else dist_graph
     if args.engine == "fused" and par == "es":
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.parallel.ensemble_shard import EnsembleSharded
@@ -201,8 +223,10 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
             return es.to_learned_dicts(metas, sig, device)
 
         if args.no_graph:
-            return Runner(lambda: es.step_sampled(sample), dicts, close=es.flush)
-        comm = _native_comm(info) if args.dist_graph and distributed else None
+            r = Runner(lambda: es.step_sampled(sample), dicts, close=es.flush)
+            r.path, r.consistency = "host", lambda: _batch_spread(es.gbuf, info)
+            return r
+        kind, comm = _graph_comm(info, args) if dist_graph and distributed else ("host", None)
         if comm is not None:
             # the group's batch fetch and in-place all-gathers captured in its graph (parallel/graphed.py)
             from sparse_coding__amd.parallel.graphed import GraphedEnsembleSharded
@@ -213,8 +237,11 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
                 for s in groups:
                     ges.run(s, count_pattern(s, GRAPH_STEPS))
 
-            return Runner(lambda: run_g([1]), dicts, close=comm.close, run=run_g,
-                          setup=lambda tiling: ges.prime([count_pattern(s, GRAPH_STEPS) for s in tiling.sizes]))
+            r = Runner(lambda: run_g([1]), dicts, close=comm.close, run=run_g,
+                       setup=lambda tiling: ges.prime([count_pattern(s, GRAPH_STEPS) for s in tiling.sizes]))
+            r.path, r.comm = kind, comm
+            r.consistency = lambda: _batch_spread([ges._glob], info)
+            return r
 
         def sample_steps(out, s):  # this rank's rows of the next s steps, one gather kernel
             return ring.sample_shard_steps(B, info.rank, info.world_size, s, out)
@@ -224,11 +251,14 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
 
         # multi-step groups: per group one local-row gather, s batch all-gathers (RCCL stream, issued
         # under the previous group's replay) and ONE HIP graph replay of the s steps
-        return Runner(lambda: es.run_groups([1], sample_steps, pattern), dicts, close=es.flush,
-                      run=lambda groups: es.run_groups(groups, sample_steps, pattern),
-                      setup=lambda tiling: (ring.ensure_permutation(), es.prime_groups(tiling.sizes, pattern)))
-    comm = (_native_comm(info) if args.engine == "fused" and distributed and not args.no_graph and args.dist_graph
-            else None)
+        r = Runner(lambda: es.run_groups([1], sample_steps, pattern), dicts, close=es.flush,
+                   run=lambda groups: es.run_groups(groups, sample_steps, pattern),
+                   setup=lambda tiling: (ring.ensure_permutation(), es.prime_groups(tiling.sizes, pattern)))
+        r.path = "host"
+        r.consistency = lambda: _batch_spread(getattr(es, "_gglob", es.gbuf), info)
+        return r
+    kind, comm = (_graph_comm(info, args) if args.engine == "fused" and distributed and not args.no_graph and dist_graph
+                  else ("host", None))
     if comm is not None:
         # data parallel / ZeRO-1 with the collectives INSIDE multi-step HIP graphs (native RCCL
         # communicator on its own stream, parallel/rccl.py + parallel/graphed.py)
@@ -237,7 +267,8 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
         from sparse_coding__amd.parallel.data_parallel import split_models
         from sparse_coding__amd.parallel.graphed import GraphedDataParallel
 
-        engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device)
+        # flat fp32 gradients (no split-K slabs): the reductions read the engines' grad_all
+        engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device, wgrad_split=1)
                    for m in split_models(models, args.dp_chunks)]
         gdp = GraphedDataParallel(engines, info, comm, ring.graph_source(B, info.rank, info.world_size), mode=par,
                                   grad_dtype=grad_dtype)
@@ -246,14 +277,21 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
             for s in groups:
                 gdp.run(s, count_pattern(s, GRAPH_STEPS))
 
-        return Runner(lambda: run([1]), lambda: gdp.to_learned_dicts(device), close=comm.close, run=run,
-                      setup=lambda tiling: gdp.prime([count_pattern(s, GRAPH_STEPS) for s in tiling.sizes]))
+        def masters():
+            gdp.gather_masters()
+            return [t for e in engines for k in sorted(e.params) for t in (e.params[k],)]
+
+        r = Runner(lambda: run([1]), lambda: gdp.to_learned_dicts(device), close=comm.close, run=run,
+                   setup=lambda tiling: gdp.prime([count_pattern(s, GRAPH_STEPS) for s in tiling.sizes]))
+        r.path, r.comm = kind, comm
+        r.consistency = lambda: _replica_delta(masters(), info)
+        return r
     if args.engine == "fused" and distributed:
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
         from sparse_coding__amd.parallel.data_parallel import ChunkedDataParallel, FusedChunk, split_models
         from sparse_coding__amd.parallel.zero import ZeroFusedChunk
 
-        engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device)
+        engines = [FusedSAEEnsemble(m, sig, lr=1e-3, batch_size=B, device=device, wgrad_split=1)
                    for m in split_models(models, args.dp_chunks)]
         xbuf = torch.empty(B, args.d, device=device, dtype=torch.bfloat16)
         graph = not args.no_graph  # each chunk's compute and update replay from HIP graphs
@@ -264,15 +302,24 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
         # cross-step: the last chunk's collectives overlap the next step's first (encoder) GEMMs
         trainer = ChunkedDataParallel(chunks, info, grad_dtype, cross_step=True)
 
-        def dicts():
+        def gather():
             trainer.flush()
             for c in chunks:  # ZeRO-1: every rank gathers the current masters before exporting
                 if hasattr(c, "gather_masters"):
                     c.gather_masters()
+
+        def dicts():
+            gather()
             return [ld for e in engines for ld in e.to_learned_dicts(device)]
 
-        return Runner(lambda: trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf)),
-                      dicts, finish=trainer.flush, close=trainer.flush)
+        def masters():
+            gather()
+            return [t for e in engines for k in sorted(e.params) for t in (e.params[k],)]
+
+        r = Runner(lambda: trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size, out=xbuf)),
+                   dicts, finish=trainer.flush, close=trainer.flush)
+        r.path, r.consistency = "host", lambda: _replica_delta(masters(), info)
+        return r
     if args.engine == "fused":
         from sparse_coding__amd.engine.fused import FusedSAEEnsemble
 
@@ -303,8 +350,49 @@ def make_runner(par, args, info, sig, models, ring, device, grad_dtype):
 
     ens = FunctionalEnsemble(models, sig, adam, {"lr": 1e-3}, device=device)
     trainer = DataParallelEnsemble(ens, info)
-    return Runner(lambda: trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size).float()),
-                  lambda: ens.to_learned_dicts(device))
+    r = Runner(lambda: trainer.step_batch(ring.sample_shard(B, info.rank, info.world_size).float()),
+               lambda: ens.to_learned_dicts(device))
+    r.path = "eager" if distributed else "single"
+    r.consistency = lambda: _replica_delta([ens.params[k] for k in sorted(ens.params)], info)
+    return r
+
+
+def _replica_delta(tensors, info):
+    """Data parallel: max |p - p_rank0| over every master and rank (0.0 = replicas identical).
+    Collective."""
+    import torch.distributed as tdist
+
+    worst = 0.0
+    for t in tensors:
+        mine = t.detach().contiguous()
+        if info.backend == "gloo":
+            mine = mine.cpu()
+        ref = mine.clone()
+        tdist.broadcast(ref, src=0)
+        worst = max(worst, float((mine.float() - ref.float()).abs().max()))
+    from sparse_coding__amd.parallel.dist import all_reduce_max
+
+    return {"what": "max |master - rank 0's master| over all parameters and ranks (after the ZeRO-1 gather)",
+            "max_abs_delta": all_reduce_max(worst, info)}
+
+
+def _batch_spread(bufs, info):
+    """Ensemble sharding: every rank must have trained on the same global batches.  Checksums of the
+    gathered global-batch buffers (sum and an index-weighted sum in fp64) compared across ranks."""
+    import torch.distributed as tdist
+
+    sums = []
+    for b in bufs:
+        if b is None:
+            continue
+        x = b.detach().double().reshape(-1)
+        w = torch.arange(x.numel(), device=x.device, dtype=torch.float64).remainder_(9973).add_(1)
+        sums += [float(x.sum()), float((x * w).sum())]
+    everyone = [None] * info.world_size
+    tdist.all_gather_object(everyone, sums)
+    spread = max((abs(a - b) for other in everyone for a, b in zip(other, everyone[0])), default=0.0)
+    return {"what": "spread over ranks of fp64 checksums of the last gathered global batches (0.0 = identical)",
+            "checksums_rank0": everyone[0], "max_abs_spread": spread}
 
 
 def comm_bytes(mode, args, world):
@@ -395,24 +483,160 @@ def settle_clocks(device, ms: float):
             "ms": round(1e3 * (time.perf_counter() - t0), 1), "launches": launches}
 
 
-def warm_and_time(runner, args, info, B):
-    """Capture every graph first, settle the clocks (untimed, non-training, reported), run the
-    warmup through the timed region's own graphs (the last warmup replay is a timed-size group),
-    then time exactly ``args.steps`` steps (engine/graph_plan.py)."""
+def _agree(err, info):
+    """Every rank's error (or None) -> the first one any rank reported (collective; the ranks must
+    all take the same path afterwards or the next collective deadlocks)."""
+    if info.world_size <= 1:
+        return err
+    import torch.distributed as tdist
+
+    everyone = [None] * info.world_size
+    tdist.all_gather_object(everyone, err)
+    return next((f"rank {r}: {e}" for r, e in enumerate(everyone) if e is not None), None)
+
+
+def ready_runner(par, args, info, sig, models, ring, device, grad_dtype):
+    """``make_runner`` + capture of every graph (+ the first warmup group for the in-graph RCCL path).
+    If capturing or first replaying the in-graph collectives fails on ANY rank, every rank drops that
+    runner and rebuilds the same configuration (fresh from ``models``) on host-issued collectives
+    (``--dist-graph 0``) in this process; the JSON reports it (``collectives.fallback``).
+    Returns (runner, tiling, warmup groups still to run)."""
     from sparse_coding__amd.engine.graph_plan import tile
 
     tiling = tile(args.steps, args.warmup, args.graph_group or GRAPH_STEPS, exact=bool(args.graph_group))
+    warm = list(tiling.warm)
+    runner = make_runner(par, args, info, sig, models, ring, device, grad_dtype)
+    if runner.path != "rccl":
+        runner.setup(tiling)
+        return runner, tiling, warm
+    err = None
+    try:
+        runner.setup(tiling)
+    except Exception as exc:
+        err = f"capture of the in-graph collectives failed: {exc!r}"
+    err = _agree(err, info)
+    if err is None and warm:
+        try:
+            runner.run(warm[:1])
+            runner.finish()
+            torch.cuda.synchronize()
+        except Exception as exc:
+            err = f"first replay of the in-graph collectives failed: {exc!r}"
+        err = _agree(err, info)
+        if err is None:
+            warm = warm[1:]
+    if err is None:
+        return runner, tiling, warm
+    print(f"[bench] {err}; falling back to host-issued collectives (--dist-graph 0)", file=sys.stderr)
+    try:
+        runner.close()
+    except Exception as exc:  # the communicator may be unusable; the fallback does not need it
+        print(f"[bench] closing the failed communicator: {exc!r}", file=sys.stderr)
+    runner = make_runner(par, args, info, sig, models, ring, device, grad_dtype, dist_graph=0)
+    runner.fallback = err
     runner.setup(tiling)
+    return runner, tiling, list(tiling.warm)
+
+
+def warm_and_time(runner, tiling, warm, args, info, B):
+    """Graphs are captured (``ready_runner``); settle the clocks (untimed, non-training, reported), run
+    the warmup through the timed region's own graphs (the last warmup replay is a timed-size group),
+    then time exactly ``args.steps`` steps (engine/graph_plan.py)."""
     runner.settle = (settle_step(info.device, args.settle_ms, args) if args.settle_mode == "step"
                      else settle_clocks(info.device, args.settle_ms))
-    runner.run(list(tiling.warm))
+    runner.run(warm)
     runner.finish()  # no warmup work may spill into the timed region
     ms, value = timed(runner, list(tiling.timed), info, B)
-    return ms, value, tiling
+    return ms, value
+
+
+def _in_torchrun() -> bool:
+    return "WORLD_SIZE" in os.environ and "RANK" in os.environ
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(gpus: int, argv, script: str | None = None) -> int:
+    """``--gpus N > 1`` outside torchrun: start N rank processes (``torch.distributed.run``, one per GPU,
+    rendezvous on 127.0.0.1) and forward rank 0's JSON line.  This process does no GPU work (it only
+    counted devices, which does not initialise HIP) and exits with the launcher's return code
+    (non-zero when any rank failed).  Reference: ``experiments/huge_batch_size.py:358-363``
+    (``mp.spawn(..., nprocs=torch.cuda.device_count())``)."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           script or os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"[bench] launching {gpus} ranks: {' '.join(cmd)}", file=sys.stderr)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    emitted = 0
+    for line in proc.stdout:
+        if line.startswith("{") and '"metric"' in line:
+            _emit(line.strip())
+            emitted += 1
+        else:
+            sys.stderr.write(line)
+    rc = proc.wait()
+    if rc == 0 and emitted != 1:
+        print(f"[bench] the ranks exited 0 but printed {emitted} result lines", file=sys.stderr)
+        return 4
+    return rc
+
+
+def check_world(args) -> str | None:
+    """Errors that must stop the run before any GPU work (None = go)."""
+    if args.gpus < 1:
+        return f"--gpus must be >= 1 (got {args.gpus})"
+    if _in_torchrun():
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            return f"torchrun started WORLD_SIZE={world} ranks but --gpus {args.gpus}"
+    if not args.shared_gpu and args.gpus > 1:
+        have = torch.cuda.device_count()  # counts devices without initialising HIP
+        if args.gpus > have:
+            return f"--gpus {args.gpus} but this node has {have} GPU(s) (use --shared-gpu for a one-GPU rehearsal)"
+    return None
+
+
+def rank_devices(info, comm=None):
+    """Per rank: its device index and name, RCCL's own device / rank / count of the communicator, and
+    HIP_VISIBLE_DEVICES -- gathered to rank 0 (collective)."""
+    mine = {"rank": info.rank, "device": str(info.device),
+            "visible": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")}
+    if info.device.type == "cuda":
+        props = torch.cuda.get_device_properties(info.device)
+        mine["name"] = props.name
+        mine["uuid"] = str(getattr(props, "uuid", ""))[:36] or None
+    if comm is not None and hasattr(comm, "device_index"):
+        mine.update(rccl_device=comm.device_index(), rccl_rank=comm.user_rank())
+    if info.world_size <= 1:
+        return [mine]
+    import torch.distributed as tdist
+
+    everyone = [None] * info.world_size
+    tdist.all_gather_object(everyone, mine)
+    return everyone
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
+    bad = check_world(args)
+    if bad:
+        print(f"[bench] {bad}", file=sys.stderr)
+        return 3
+    if args.gpus > 1 and not _in_torchrun():
+        return launch_ranks(args.gpus, argv)  # before anything touches the GPU in this process
     from sparse_coding__amd.parallel.dist import init_distributed, shutdown
 
     info = init_distributed(None if args.dist_backend == "auto" else args.dist_backend,
@@ -449,10 +673,12 @@ def main(argv=None):
         args.grad_dtype = "bf16" if par == "zero1" else "fp32"
     grad_dtype = torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32
     if par == "es" and args.models % info.world_size:
-        raise SystemExit(f"--parallelism es needs models % N == 0 ({args.models} models, N={info.world_size})")
+        print(f"[bench] --parallelism es needs models % N == 0 ({args.models} models, N={info.world_size})",
+              file=sys.stderr)
+        return 3
 
-    runner = make_runner(par, args, info, sig, models, ring, device, grad_dtype)
-    ms, value, tiling = warm_and_time(runner, args, info, B)
+    runner, tiling, warm = ready_runner(par, args, info, sig, models, ring, device, grad_dtype)
+    ms, value = warm_and_time(runner, tiling, warm, args, info, B)
 
     quality = None
     trained = args.warmup + args.steps
@@ -467,6 +693,13 @@ def main(argv=None):
         lds = runner.dicts()  # collective in the sharded mode: every rank takes part
         if info.is_main:
             quality = fvu_l0(lds, held_out.float())
+    runner.finish()
+    torch.cuda.synchronize()
+    # cross-rank check of the run just timed (collective): replicas identical (dp / zero1) or the same
+    # global batches on every rank (es)
+    consistency = runner.consistency() if distributed and runner.consistency is not None else None
+    devices = rank_devices(info, runner.comm)
+    rccl_ranks = runner.comm.count() if runner.comm is not None and hasattr(runner.comm, "count") else None
     runner.close()
 
     # N > 1: also time the other multi-GPU strategy on the same models (untimed for the
@@ -476,17 +709,23 @@ def main(argv=None):
     if distributed and args.compare_parallelism and args.models % info.world_size == 0:
         other = "dp" if par in ("es", "zero1") else "es"
         alt_models = [sig.init(args.d, n, float(l1), device=device) for l1 in l1s]
-        try:
-            alt_runner = make_runner(other, args, info, sig, alt_models, ring, device, grad_dtype)
-            a_ms, a_value, _ = warm_and_time(alt_runner, args, info, B)
-            alt_runner.close()
-        except Exception as exc:  # the headline run above stands on its own
-            print(f"[bench] alt parallelism {other} failed: {exc!r}", file=sys.stderr)
-            a_ms = a_value = float("nan")
-        alt = {"parallelism": f"{other}{info.world_size}", "value": round(a_value, 1), "ms_per_step": round(a_ms, 4),
+        alt = {"parallelism": f"{other}{info.world_size}",
                "predicted_ms_per_step": comm_model.predict(other, info.world_size, shape, args.dp_chunks),
                "dp_chunks": args.dp_chunks if other == "dp" else None,
                "comm_bytes_per_gpu_per_step": comm_bytes(other, args, info.world_size)}
+        try:
+            alt_runner, a_tiling, a_warm = ready_runner(other, args, info, sig, alt_models, ring, device, grad_dtype)
+            a_ms, a_value = warm_and_time(alt_runner, a_tiling, a_warm, args, info, B)
+            alt_runner.finish()
+            torch.cuda.synchronize()
+            alt.update(value=round(a_value, 1), ms_per_step=round(a_ms, 4),
+                       collective_path=PATH_NAMES.get(alt_runner.path, alt_runner.path),
+                       fallback=alt_runner.fallback,
+                       consistency=alt_runner.consistency() if alt_runner.consistency is not None else None)
+            alt_runner.close()
+        except Exception as exc:  # the headline run above stands on its own; the failure is on record
+            print(f"[bench] alt parallelism {other} failed: {exc!r}", file=sys.stderr)
+            alt.update(value=None, ms_per_step=None, error=repr(exc))
 
     if info.is_main:
         rec = {
@@ -535,6 +774,15 @@ def main(argv=None):
             "vs_eager_same_box": round(value / (EAGER_SAME_BOX_ACT_PER_S * info.world_size), 2)
             if EAGER_SAME_BOX_ACT_PER_S and args.engine == "fused" and args.d == 512 and args.ratio == 4
             and args.models == 8 and B == 2048 else None,
+        }
+        rec["collectives"] = {
+            "path": PATH_NAMES.get(runner.path, runner.path) if distributed else PATH_NAMES["single"],
+            "fallback": runner.fallback,
+            "process_group": {"backend": info.backend, "ranks": info.world_size},
+            # the native communicator's own count (ncclCommCount), None when no native comm ran
+            "rccl_ranks": rccl_ranks,
+            "rank_devices": devices,
+            "consistency": consistency,
         }
         if alt is not None:
             rec["alt_parallelism"] = alt

@@ -194,15 +194,10 @@ class FusedSAEEnsemble:
         # Adam kernel sums the partial slabs.  (Data-parallel paths use the flat buffers.)
         nprob = 2 if self.kind == "untied" else 1
         kdim = B if self.kind == "untied" else 2 * B
-        # opt-in (SC_FUSED_DCW=1): the code gradient fused into the encoder weight gradient
-        # (csrc/sae_dcw.hip, dpre never reaches HBM).  Correct, but slower on MI355X at d = 512:
-        # 127 us against 49 + ~33 us for the two GEMMs it replaces -- each workgroup must stream
-        # R and x (4 MB) through one CU at <= ~80 GB/s with its 4 waves (profiles/r4/dcw/README.md)
-        self._dcw = (self.kind == "untied" and self.act == gemm_ops.ACT_RELU and self.nactive is None
-                     and gemm_ops.dcw_supported(G, B, n, d) and (grad_dtype or "fp32") == "fp32"
-                     and wgrad_split in ("auto", 1) and os.environ.get("SC_FUSED_DCW", "0") not in ("", "0"))
-        self.wsplit = (1 if self._dcw else
-                       gemm_ops.wgrad_split(G, n, d, kdim, nprob, live=self._live) if wgrad_split == "auto"
+        # (a code gradient fused into the encoder weight gradient, so dpre never reaches HBM, was
+        # measured slower at d = 512 -- 127 vs 49 + ~33 us, per-CU operand feed -- and lives in
+        # scripts/lab/sae_dcw.hip with its numbers in profiles/r4/dcw/README.md)
+        self.wsplit = (gemm_ops.wgrad_split(G, n, d, kdim, nprob, live=self._live) if wgrad_split == "auto"
                        else int(wgrad_split))
         self.g_parts = (alloc(nprob, self.wsplit, G, n, d, device=dev, dtype=torch.float32)
                         if self.wsplit > 1 else None)
@@ -253,6 +248,17 @@ class FusedSAEEnsemble:
         # learned centering: fp32 column sums of the residual from the decoder epilogue (the
         # center gradient's direct term, taken before the bf16 rounding of R)
         self.rcol = torch.zeros(G, tm, d, device=dev) if self.learned_center else None
+
+    def use_flat_grads(self):
+        """Write the weight gradients straight into the fp32 flat buffer (``grad_all``): no split-K
+        slabs, no bf16 gradient copy.  Data-parallel paths reduce that buffer, so they call this on
+        every engine they wrap (an engine built with ``wgrad_split='auto'`` may have picked a split
+        for its shape, e.g. 4 models on 2048 rows)."""
+        self.wsplit = 1
+        self.g_parts = None
+        self.g_bf = None
+        self._g_from_parts = self._g_from_bf = False
+        return self
 
     # ------------------------------------------------------------------ helpers
     def _refresh_bsq(self):
@@ -335,8 +341,6 @@ class FusedSAEEnsemble:
                                act=self.act, ascale=ascale, mask2=self.cmask2, nactive=self.nactive,
                                live_host=self._live)
             return
-        if self._dcw:  # the code gradient runs inside the encoder weight gradient (_enc_wgrad)
-            return
         gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                            mask=self.cmask, nactive=self.nactive, live_host=self._live)
 
@@ -363,14 +367,9 @@ class FusedSAEEnsemble:
                 self._reduce_bias_grad()
 
     def _enc_wgrad(self, x):
-        """g_enc = alpha dpre^T x: fused with the code gradient (and its bias-gradient column
-        sums) when ``_dcw``, else from the dpre the code-gradient GEMM wrote."""
-        if self._dcw:
-            gemm_ops.code_grad_wgrad(self.r, self.dec_shadow, x, self.cmask, self.l1, self.g_enc, self.colpart,
-                                     self._alpha)
-        else:
-            gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha, nactive=self.nactive,
-                                  live_host=self._live)
+        """g_enc = alpha dpre^T x from the dpre the code-gradient GEMM wrote."""
+        gemm_ops.weight_grads([[(self.dpre, x)]], [self.g_enc], self._alpha, nactive=self.nactive,
+                              live_host=self._live)
 
     def _reduce_bias_grad(self):
         torch.sum(self.colpart, dim=1, keepdim=True, out=self.g_bias)
@@ -391,10 +390,6 @@ class FusedSAEEnsemble:
         split = self.g_parts is not None
         self._g_from_parts = split
         self._g_from_bf = gbf = self.g_bf is not None
-        if self._dcw:  # decoder gradient, then the fused code / encoder gradient
-            gemm_ops.weight_grads([[(self.c, self.r)]], [self.g_dec], self._alpha)
-            self._enc_wgrad(x)
-            return
         if self.kind == "untied":
             outs = ([self.g_parts[0], self.g_parts[1]] if split else
                     [self.g_bf[0], self.g_bf[1]] if gbf else [self.g_dec, self.g_enc])

@@ -155,8 +155,14 @@ class EnsembleTrainer:
             from ..parallel.rccl import RcclComm
             from .fused import FusedSAEEnsemble
 
-            eng = FusedSAEEnsemble(models, sig, lr=lr, batch_size=batch_size, device=device)
-            self._comm = RcclComm(info)
+            # flat fp32 gradients: the reductions read grad_all (no split-K slabs for this shape)
+            eng = FusedSAEEnsemble(models, sig, lr=lr, batch_size=batch_size, device=device, wgrad_split=1)
+            if info.world_size > 1 and info.backend == "gloo":
+                from ..parallel.host_comm import HostComm
+
+                self._comm = HostComm(info)  # gloo ranks (e.g. sharing one GPU): host-staged, eager steps
+            else:
+                self._comm = RcclComm(info)
             self.dp = GraphedDataParallel([eng], info, self._comm, None, mode=mode)
             self.impl = eng
             self._dp_kind = f"{mode}-graphed"
@@ -304,6 +310,19 @@ class EnsembleTrainer:
         host = {k: v.detach().float().cpu() for k, v in self.last_losses.items() if torch.is_tensor(v)}
         count = (self.local.stop - self.local.start) if self.es is not None else self.n_models
         return [{k: float(v[i]) for k, v in host.items()} for i in range(count)]
+
+    def close(self):
+        """Release the data-parallel communicator: synchronise, drop the captured graphs that hold its
+        collectives, then destroy it (idempotent; the GC never has to)."""
+        comm = getattr(self, "_comm", None)
+        if comm is None:
+            return
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        if self.dp is not None and hasattr(self.dp, "_graphs"):
+            self.dp._graphs = {}
+        comm.close()
+        self._comm = None
 
     def state_dict(self) -> Dict[str, Any]:
         st = {"kind": self.kind, "steps": self.steps, "name": self.name, "args": self.args}

@@ -274,38 +274,6 @@ def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, 
             dotpart=dotpart, dc_tied=tied_bias is not None, bias=tied_bias, sbias=n)
 
 
-def dcw_supported(G, B, n, d) -> bool:
-    """Shapes ``code_grad_wgrad`` runs (d = 512; one 64-feature workgroup per CU or more)."""
-    return d == 512 and n % 64 == 0 and B % 128 == 0 and G * (n // 64) >= 256
-
-
-def code_grad_wgrad(r, w_hat, x, mask, l1, g_enc, colpart, alpha):
-    """Fused code gradient + encoder weight gradient of the untied ReLU SAE (csrc/sae_dcw.hip):
-
-        dpre_s = 1[c > 0] * (r @ w_hat^T + l1 d / 2)      (never stored)
-        g_enc  = alpha * dpre_s^T @ x                     fp32 [G, n, d]
-        colpart[g, t, j] = sum over rows 128 t .. 128 t + 127 of dpre_s[., j]
-
-    i.e. ``code_grad(..., mask=mask)`` followed by ``weight_grads([[(dpre, x)]], [g_enc], alpha)``
-    without the [G, B, n] round trip.  ``mask``: the encoder's activity bitmask."""
-    G, B, d = r.shape
-    n = w_hat.shape[1]
-    _bf16(r, "r"); _bf16(w_hat, "w_hat"); _bf16(x, "x")
-    _need(dcw_supported(G, B, n, d), f"fused code/encoder gradient does not support G={G}, B={B}, n={n}, d={d}")
-    _need(tuple(w_hat.shape) == (G, n, d), "w_hat shape")
-    sx = _x_stride(x, B, d, G)
-    _need(mask.dtype == torch.int64 and tuple(mask.shape) == code_mask_shape(G, B, n) and mask.is_contiguous(),
-          "mask must be the encoder's activity bitmask")
-    _need(l1.dtype == torch.float32 and l1.numel() == G, "l1 must be fp32[G]")
-    _need(g_enc.dtype == torch.float32 and tuple(g_enc.shape) == (G, n, d) and g_enc.is_contiguous(), "g_enc fp32 [G, n, d]")
-    _need(colpart.dtype == torch.float32 and colpart.is_contiguous() and colpart.numel() >= G * (B // 128) * n,
-          "colpart too small")
-    rc = _lib.lib().sc_sae_dcw(_lib.ptr(r), _lib.ptr(w_hat), _lib.ptr(x), sx, _lib.ptr(mask), _lib.ptr(l1),
-                               d / 2.0, float(alpha), _lib.ptr(g_enc), _lib.ptr(colpart), G, B, n, d,
-                               _lib.stream_handle())
-    _lib.check(rc, "sc_sae_dcw")
-
-
 def wgrad_split(G, n, d, K, nprob, live=None):
     """Split-K factor for the weight-gradient GEMM: 1 while the 256x256 grid already fills
     the 256 CUs; otherwise the smallest power of two that reaches 256 blocks and keeps

@@ -132,7 +132,7 @@ class EnsembleSharded:
         if have is None or have[0].shape[0] < s * self.B:
             dev, dt = self.gbuf[0].device, self.gbuf[0].dtype
             self._gsend = [torch.empty(s * self.B, self.d, device=dev, dtype=dt) for _ in range(2)]
-            self._gglob = [torch.empty(s, self.global_batch, self.d, device=dev, dtype=dt) for _ in range(2)]
+            self._gglob = [torch.zeros(s, self.global_batch, self.d, device=dev, dtype=dt) for _ in range(2)]
         return self._gsend, self._gglob
 
     def _issue_group(self, par: int, s: int, sample_steps):

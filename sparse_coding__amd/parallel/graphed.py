@@ -42,8 +42,9 @@ class _Chunk:
         kind = getattr(e, "kind", None)
         if kind not in ("untied", "tied") or e.learned_center or e.nactive is not None:
             raise NotImplementedError(f"graphed data parallel of engine kind {kind} (masked / learned centre)")
-        if e.wsplit != 1 or e.g_bf is not None:
-            raise NotImplementedError("graphed data parallel needs the engine's flat fp32 gradients (wgrad_split=1)")
+        # the reductions read the flat fp32 gradient buffer: drop any split-K slabs / bf16 copy the
+        # engine picked for its own shape (FusedSAEEnsemble(wgrad_split='auto'))
+        e.use_flat_grads()
         self.mode = mode
         G, n, d = e.n_models, e.n, e.d
         N = max(1, info.world_size)
@@ -65,10 +66,14 @@ class _Chunk:
 
 class GraphedDataParallel:
     def __init__(self, engines: Sequence, info: DistInfo, comm, source, mode: str = "dp",
-                 grad_dtype: torch.dtype = torch.float32, count_every: int = 8, sync_params: bool = True):
+                 grad_dtype: torch.dtype = torch.float32, count_every: int = 8, sync_params: bool = True,
+                 capture: Optional[bool] = None):
         if mode not in ("dp", "zero1"):
             raise ValueError(f"mode must be 'dp' or 'zero1', got {mode!r}")
         self.info, self.comm, self.source, self.mode = info, comm, source, mode
+        # capture=False: run the group's kernels and collectives eagerly (the same _steps sequence);
+        # the default follows the communicator (a host-staged gloo comm cannot be captured)
+        self.capture = getattr(comm, "capturable", True) if capture is None else bool(capture)
         self.chunks = [_Chunk(e, mode, info, grad_dtype) for e in engines]
         e0 = engines[0]
         self.B, self.d, self.device = e0.batch_size, e0.d, e0.device
@@ -229,6 +234,15 @@ class GraphedDataParallel:
             self._graphs = {}  # captured on the old buffer
         return self._xs
 
+    def _exec(self, pattern):
+        """Replay the group's graph (captured on first use), or run its steps eagerly."""
+        if self.capture:
+            self._graph(pattern).replay()
+            return
+        if self.source is not None:
+            self._xs_buffer(len(pattern))
+        self._steps(tuple(bool(c) for c in pattern))
+
     def _graph(self, pattern):
         key = tuple(bool(c) for c in pattern)
         if self.source is not None:
@@ -253,7 +267,8 @@ class GraphedDataParallel:
         for c in self.chunks:
             c.engine._tail_ready()
         for p in patterns:
-            self._graph(p)
+            if self.capture:
+                self._graph(p)
         e0 = self.chunks[0].engine
         if self.source is not None:
             self.source.prepare(e0.step_count, max([1] + [len(p) for p in patterns]))
@@ -270,7 +285,7 @@ class GraphedDataParallel:
             self.source.prepare(e0.step_count, len(pattern))
         for c in self.chunks:
             c.engine._tail_ready()
-        self._graph(pattern).replay()
+        self._exec(pattern)
         for c in self.chunks:
             for count in pattern:
                 c.engine._counted = count
@@ -317,13 +332,15 @@ class GraphedEnsembleSharded:
     sharding of ``cluster_runs.py:100-157`` / DDP of ``experiments/huge_batch_size.py:259-345``.
     """
 
-    def __init__(self, es, comm, source):
+    def __init__(self, es, comm, source, capture: Optional[bool] = None):
         e = es.engine
         if not hasattr(e, "_step_kernels") or not hasattr(e, "step_dev"):
             raise NotImplementedError("graphed ensemble sharding needs the fused engine")
         if getattr(source, "world", 1) != es.info.world_size or getattr(source, "rank", 0) != es.info.rank:
             raise ValueError("the source must be this rank's shard (ring.graph_source(B, rank, world))")
         self.es, self.comm, self.source, self.engine = es, comm, source, e
+        # capture=False: the same _steps sequence run eagerly (host-staged gloo comm: not capturable)
+        self.capture = getattr(comm, "capturable", True) if capture is None else bool(capture)
         self.B, self.N = es.B, max(1, es.info.world_size)
         self.device = e.device
         self._glob = None
@@ -332,7 +349,7 @@ class GraphedEnsembleSharded:
     def _buffers(self, s: int):
         if self._glob is None or self._glob.shape[0] < s:
             NB = self.N * self.B
-            self._glob = torch.empty(s, NB, self.es.d, device=self.device, dtype=torch.bfloat16)
+            self._glob = torch.zeros(s, NB, self.es.d, device=self.device, dtype=torch.bfloat16)
             # the engine's input and the tail-gather plumbing: step k's fused tail copies global batch
             # k+1 into it (rows (t + 1 - ep0) NB + r of the group buffer through an identity index),
             # so each step's encoder reads a batch written just before it -- as the single-GPU step
@@ -388,7 +405,8 @@ class GraphedEnsembleSharded:
         self._buffers(max([1] + [len(p) for p in patterns]))
         e._tail_ready()
         for p in patterns:
-            self._graph(tuple(bool(c) and e.track_feature_counts for c in p))
+            if self.capture:
+                self._graph(tuple(bool(c) and e.track_feature_counts for c in p))
         self.source.prepare(e.step_count, max([1] + [len(p) for p in patterns]))
 
     def run(self, steps: int, pattern=None):
@@ -401,7 +419,11 @@ class GraphedEnsembleSharded:
             raise ValueError("one counting flag per step")
         e._tail_ready()
         self.source.prepare(e.step_count, len(pattern))
-        self._graph(pattern).replay()
+        if self.capture:
+            self._graph(pattern).replay()
+        else:
+            self._buffers(len(pattern))
+            self._steps(pattern)
         for count in pattern:
             e._counted = count
             e._host_step()

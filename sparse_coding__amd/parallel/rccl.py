@@ -60,6 +60,9 @@ def library():
             "ncclGroupStart": [],
             "ncclGroupEnd": [],
             "ncclGetVersion": [C.POINTER(i)],
+            "ncclCommCount": [vp, C.POINTER(i)],
+            "ncclCommCuDevice": [vp, C.POINTER(i)],
+            "ncclCommUserRank": [vp, C.POINTER(i)],
         }
         for name, args in sig.items():
             fn = getattr(lib, name)
@@ -193,7 +196,26 @@ class RcclComm:
         return self._run(lambda s: _check(library().ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), dt, int(root),
                                                            self._comm, s), "ncclBroadcast"), overlap)
 
+    # ------------------------------------------------------------------ introspection
+    def _query(self, fn: str) -> int:
+        v = C.c_int()
+        _check(getattr(library(), fn)(self._comm, C.byref(v)), fn)
+        return v.value
+
+    def count(self) -> int:
+        """Ranks in the communicator, as RCCL itself reports them (ncclCommCount)."""
+        return self._query("ncclCommCount")
+
+    def device_index(self) -> int:
+        """The HIP device this rank's communicator runs on (ncclCommCuDevice)."""
+        return self._query("ncclCommCuDevice")
+
+    def user_rank(self) -> int:
+        return self._query("ncclCommUserRank")
+
     def close(self):
+        """Synchronise the device (no captured or enqueued collective may still reference the
+        communicator), then destroy it.  Idempotent.  Owners of captured graphs drop them first."""
         if self._comm:
             torch.cuda.synchronize(self.device)
             _check(library().ncclCommDestroy(self._comm), "ncclCommDestroy")
@@ -202,6 +224,7 @@ class RcclComm:
     def __del__(self):  # pragma: no cover - best effort at interpreter exit
         try:
             if self._comm and os.environ.get("SC_RCCL_NO_DESTROY") is None:
+                torch.cuda.synchronize(self.device)
                 library().ncclCommDestroy(self._comm)
                 self._comm = C.c_void_p()
         except Exception:

@@ -1,0 +1,73 @@
+"""bench.py's launcher contract on the CPU: ``--gpus N`` runs N ranks or fails fast, never silently one."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_check_world_rejects_mismatches(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("RANK", raising=False)
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)
+    assert bench.check_world(bench.parse(["--gpus", "1"])) is None
+    assert "has 1 GPU" in bench.check_world(bench.parse(["--gpus", "2"]))
+    assert bench.check_world(bench.parse(["--gpus", "2", "--shared-gpu"])) is None
+    assert "--gpus must be" in bench.check_world(bench.parse(["--gpus", "0"]))
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 8)
+    assert "WORLD_SIZE=4" in bench.check_world(bench.parse(["--gpus", "2"]))
+    assert bench.check_world(bench.parse(["--gpus", "4"])) is None
+
+
+def test_main_fails_fast_without_enough_gpus(monkeypatch):
+    """More GPUs asked for than the node has: non-zero before any GPU work or launch."""
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("RANK", raising=False)
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)
+    launched = []
+    monkeypatch.setattr(bench, "launch_ranks", lambda *a, **k: launched.append(a) or 0)
+    assert bench.main(["--gpus", "2"]) == 3
+    assert not launched
+    # enough devices: the parent hands over to the launcher instead of running one GPU
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 8)
+    assert bench.main(["--gpus", "8", "--steps", "3"]) == 0
+    assert launched and launched[0][0] == 8 and "--steps" in launched[0][1]
+
+
+PROBE = r'''
+import json, os, sys
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+print("noise on stdout from rank", rank, flush=True)
+if rank == 0:
+    print(json.dumps({"metric": "probe", "n_gpus": world, "argv": sys.argv[1:]}), flush=True)
+sys.exit(int(os.environ.get("PROBE_RC", "0")) if rank == world - 1 else 0)
+'''
+
+
+@pytest.mark.parametrize("rc", [0, 5])
+def test_launch_ranks_forwards_rank0_json_and_worst_rc(tmp_path, rc, capfd, monkeypatch):
+    """The launcher starts N torch.distributed.run ranks, forwards exactly rank 0's JSON line to stdout
+    (other stdout goes to stderr) and returns non-zero when any rank fails."""
+    script = tmp_path / "probe.py"
+    script.write_text(PROBE)
+    monkeypatch.setenv("PROBE_RC", str(rc))
+    got = bench.launch_ranks(3, ["--gpus", "3", "--steps", "2"], script=str(script))
+    out, err = capfd.readouterr()
+    if rc == 0:
+        assert got == 0
+        lines = [ln for ln in out.splitlines() if ln.strip()]
+        assert len(lines) == 1, out
+        rec = json.loads(lines[0])
+        assert rec["n_gpus"] == 3 and rec["argv"] == ["--gpus", "3", "--steps", "2"]
+        assert "noise on stdout" in err
+    else:
+        assert got != 0
