@@ -33,6 +33,8 @@ static Stat stat(std::vector<double> v) {
   return {q(0.5), q(0.1), q(0.9)};
 }
 
+static const char* g_raw_dir = nullptr;  // argv[1]: per-block raw stamps as CSV (one file per kernel)
+
 template <class F>
 static void run(const char* name, long nblocks, F launch) {
   long long* st;
@@ -72,6 +74,20 @@ static void run(const char* name, long nblocks, F launch) {
     epi.push_back((s[3] - s[2]) / ghz / 1e3);
     life.push_back((s[3] - s[0]) / ghz / 1e3);
   }
+  if (g_raw_dir) {
+    char path[512];
+    snprintf(path, sizeof path, "%s/%s.csv", g_raw_dir, name);
+    FILE* fo = fopen(path, "w");
+    if (fo) {
+      fprintf(fo, "block,start_us,fill_us,kloop_us,epi_us,hw_id,xcc_id\n");
+      for (long b = 0; b < nblocks; ++b) {
+        const long long* s = &h[b * 8];
+        fprintf(fo, "%ld,%.3f,%.3f,%.3f,%.3f,%lld,%lld\n", b, (s[0] - t0) / ghz / 1e3, (s[1] - s[0]) / ghz / 1e3,
+                (s[2] - s[1]) / ghz / 1e3, (s[3] - s[2]) / ghz / 1e3, s[6], s[7]);
+      }
+      fclose(fo);
+    }
+  }
   Stat a = stat(start), f = stat(fill), k = stat(kloop), e = stat(epi), l = stat(life);
   printf("{\"kernel\": \"%s\", \"blocks\": %ld, \"us_per_launch\": %.2f, \"stamped_span_us\": %.2f, \"clock_ghz\": %.3f, "
          "\"start_us\": [%.2f, %.2f, %.2f], \"fill_us\": [%.2f, %.2f, %.2f], \"kloop_us\": [%.2f, %.2f, %.2f], "
@@ -82,7 +98,8 @@ static void run(const char* name, long nblocks, F launch) {
   (void)hipFree(st);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) g_raw_dir = argv[1];
   const int G = 8, B = 2048, d = 512, n = 2048;
   uint16_t *x, *we, *wd, *c, *r;
   float *bias, *part, *g;
@@ -111,6 +128,7 @@ int main() {
     p.M = B; p.N = n; p.K1 = d; p.K2 = 0; p.G = G; p.ldc = n; p.sc = (long)B * n;
     p.bias = bias; p.sbias = n; p.part = part; p.cmask = cmask; p.ksplit = 1;
 #ifndef LAB_BIG
+    run("enc_128_bk32x3", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 32, 3, false>(EPI_ENC, true, true, p, 1, 0); });
     run("enc_128", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 64, 2>(EPI_ENC, true, true, p, 1, 0); });
 #else
     run("enc_256", n_blocks<S256>(B, n, G, 1), [&] { launch<S256, 64, 2>(EPI_ENC, true, true, p, 1, 0); });
@@ -125,6 +143,22 @@ int main() {
     p.aux = x; p.ldaux = d; p.saux = 0; p.part = part; p.ksplit = 1;
 #ifndef LAB_BIG
     run("dec_128", n_blocks<S128>(B, d, G, 1), [&] { launch<S128, 64, 2>(EPI_DEC, true, false, p, 1, 0); });
+#endif
+  }
+  {  // code gradient: dpre = 1[c > 0] (R Wd^T + l d / 2), activity from the bitmask, 128x128 BK32x3
+    GemmParams p{};
+    float* l1;
+    float* colpart;
+    (void)hipMalloc(&l1, G * 4);
+    (void)hipMalloc(&colpart, (long)G * (B / 128) * n * 4);
+    (void)hipMemset(l1, 0, G * 4);
+    p.prob[0].a[0] = p.prob[0].a[1] = {r, d, (long)B * d};
+    p.prob[0].b[0] = p.prob[0].b[1] = {wd, d, (long)n * d};
+    p.prob[0].c = c; p.prob[0].alpha = 1.f; p.nprob = 1;
+    p.M = B; p.N = n; p.K1 = d; p.K2 = 0; p.G = G; p.ldc = n; p.sc = (long)B * n;
+    p.colpart = colpart; p.l1 = l1; p.l1_add_scale = d / 2.0f; p.cmask = cmask; p.ksplit = 1;
+#ifndef LAB_BIG
+    run("dc_128_bk32x3", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 32, 3, false>(EPI_DC_MASK, true, true, p, 1, 0); });
 #endif
   }
   {  // weight gradients: dWd = c^T R, dWe = c^T x (stand-in for dpre), 256x256, two problems

@@ -152,57 +152,6 @@ def _sae_epilogues(G, B, d, n):
     _close(gt, gd + ge, rtol=1e-3, atol=1e-6)
 
 
-def test_fused_code_grad_wgrad_matches_two_kernels(G, B, n, shared_x):
-    """csrc/sae_dcw.hip (code gradient fused into the encoder weight gradient) against the
-    code-gradient GEMM + weight-gradient GEMM it replaces and against fp32 torch; B = 4096 crosses
-    the kernel's 2048-row activity-word segments."""
-    from sparse_coding__amd.ops import gemm
-
-    torch.manual_seed(7)
-    d = 512
-    gen = torch.Generator(device=DEV).manual_seed(7)
-    x = _bf(B, d, gen=gen) if shared_x else _bf(G, B, d, gen=gen)
-    we = _bf(G, n, d, scale=0.05, gen=gen)
-    wd = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV, generator=gen), dim=-1).to(torch.bfloat16)
-    bias = torch.randn(G, n, device=DEV, generator=gen) * 0.1 - 0.05
-    c = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
-    part = torch.zeros(G, (B // 128) * (n // 128), 2, device=DEV)
-    cmask = torch.zeros(gemm.code_mask_shape(G, B, n), device=DEV, dtype=torch.int64)
-    gemm.encode_relu(x, we, bias, c, part, mask_out=cmask)
-    r = _bf(G, B, d, scale=0.5, gen=gen)
-    l1 = torch.logspace(-4, -2, G, device=DEV)
-    alpha = 2.0 / (B * d)
-    dpre = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
-    col_a = torch.zeros(G, B // 128, n, device=DEV)
-    gemm.code_grad(r, wd, c, l1, dpre, col_a, mask=cmask)
-    g_a = torch.empty(G, n, d, device=DEV)
-    gemm.weight_grads([[(dpre, x)]], [g_a], alpha)
-    assert gemm.dcw_supported(G, B, n, d)
-    g_b = torch.full((G, n, d), float("nan"), device=DEV)
-    col_b = torch.full((G, B // 128, n), float("nan"), device=DEV)
-    gemm.code_grad_wgrad(r, wd, x, cmask, l1, g_b, col_b, alpha)
-    torch.cuda.synchronize()
-    assert torch.isfinite(g_b).all() and torch.isfinite(col_b).all()
-    # same bf16 dpre up to the K-split summation order of R W_hat^T (rare 1-ulp bf16 flips)
-    rel = ((g_b - g_a).norm() / g_a.norm()).item()
-    assert rel < 2e-3, rel
-    torch.testing.assert_close(col_b, col_a, rtol=1e-4, atol=1e-3)
-    # fp32 reference of the op
-    on = (c.float() > 0).float()
-    dref = (r.float() @ wd.float().transpose(1, 2) + (l1 * d / 2)[:, None, None]) * on
-    xf = x.float() if not shared_x else x.float().expand(G, B, d)
-    gref = alpha * dref.transpose(1, 2) @ xf
-    for gi in range(G):
-        err = ((g_b[gi] - gref[gi]).norm() / gref[gi].norm()).item()
-        assert err < 1e-2, (gi, err)
-    torch.testing.assert_close(col_b.sum(1), dref.sum(1), rtol=1e-3, atol=1e-2)
-    # deterministic: a second launch is bit-identical
-    g_c = torch.empty_like(g_b)
-    col_c = torch.empty_like(col_b)
-    gemm.code_grad_wgrad(r, wd, x, cmask, l1, g_c, col_c, alpha)
-    assert torch.equal(g_b, g_c) and torch.equal(col_b, col_c)
-
-
 def test_adam_rows_matches_autograd():
     from sparse_coding__amd.ops import adam as adam_ops
 
