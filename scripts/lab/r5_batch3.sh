@@ -1,0 +1,36 @@
+#!/bin/bash
+# round 5, GPU batch 3: split-tail test, GEMM phase stamps (fixed), split-tail A/B on the headline bench
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/r5b3
+mkdir -p $O/phases
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "[batch] $name: $*" >&2
+  timeout -k 10 "$t" "$@"
+  local rc=$?
+  echo "[batch] $name rc=$rc" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[batch] stopping after $name (rc=$rc)" >&2; exit $rc; fi
+  return 0
+}
+step test 300 python -u -m pytest tests/test_graphs_gpu.py -q -k "split_tail or multi_step or fused_step_tail" --timeout 120 --timeout-method thread > $O/test.log 2>&1
+tail -3 $O/test.log
+step phases 120 scripts/lab/gemm_phases_128 $O/phases > $O/phases.jsonl
+cat $O/phases.jsonl
+for r in 1 2 3; do
+  for v in 0 1; do
+    SC_SPLIT_TAIL=$v step ab_$v 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/ab_$v.jsonl
+  done
+done
+for r in 1 2; do
+  for v in 0 1; do
+    SC_SPLIT_TAIL=$v step drv_$v 120 python bench.py --steps 20 --warmup 5 --no-eval >> $O/drv_$v.jsonl
+  done
+done
+python3 - <<'PY'
+import json
+for v in (0, 1):
+    for f in ("ab", "drv"):
+        ms = [json.loads(l)["ms_per_step"] for l in open(f"gpurun_out/r5b3/{f}_{v}.jsonl") if l.startswith("{")]
+        print(f"split={v} {f}: {ms}")
+PY

@@ -84,17 +84,28 @@ __device__ __forceinline__ long mask_word(const GemmParams& p, int g, int row0, 
 // builds compile these to nothing.
 #ifdef SC_PHASE_STAMPS
 __device__ long long* sc_stamp_buf;
+// volatile asm: the builtins are free to be scheduled (and merged) anywhere in the kernel
+__device__ __forceinline__ long long sc_memtime() {
+  long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  return t;
+}
+__device__ __forceinline__ long long sc_memrealtime() {
+  long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  return t;
+}
 #define SC_STAMP(k)                                                                      \
   do {                                                                                   \
     if (threadIdx.x == 0 && sc_stamp_buf) {                                              \
       long long* st_ = sc_stamp_buf + (long)blockIdx.x * 8;                              \
-      st_[k] = (long long)__builtin_amdgcn_s_memtime();                                  \
+      st_[k] = sc_memtime();                                                             \
       if ((k) == 0) {                                                                    \
-        st_[4] = (long long)__builtin_amdgcn_s_memrealtime();                            \
+        st_[4] = sc_memrealtime();                                                       \
         st_[6] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);                   \
         st_[7] = (long long)__builtin_amdgcn_s_getreg((15 << 11) | 20);                  \
       }                                                                                  \
-      if ((k) == 3) st_[5] = (long long)__builtin_amdgcn_s_memrealtime();                \
+      if ((k) == 3) st_[5] = sc_memrealtime();                                           \
     }                                                                                    \
   } while (0)
 #else
