@@ -13,8 +13,21 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[batch] stopping after $name (rc=$rc)" >&2; exit $rc; fi
   return 0
 }
-step test 300 python -u -m pytest tests/test_graphs_gpu.py -q -k "split_tail or multi_step or fused_step_tail" --timeout 120 --timeout-method thread > $O/test.log 2>&1
-tail -3 $O/test.log
+step test 400 python -u -m pytest tests/test_graphs_gpu.py tests/test_kernels_gpu.py -q -k "split_tail or multi_step or fused_step_tail or topk" --timeout 120 --timeout-method thread > $O/test.log 2>&1
+tail -30 $O/test.log
+for r in 1 2; do
+  for v in dense cand; do
+    SC_TOPK_SELECT=$v step topk_$v 200 python scripts/bench_configs.py topk --steps 80 --warmup 16 >> $O/topk_$v.jsonl
+  done
+done
+cat $O/topk_*.jsonl
+(cd /tmp && SC_TOPK_SELECT=cand step prof_topk 300 rocprofv3 --kernel-trace --stats -d $O/prof_topk -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/bench_configs.py topk --steps 40 --warmup 8 > $O/prof_topk.log 2>&1)
+python3 - <<'PY'
+import csv, glob
+f = glob.glob("gpurun_out/r5b3/prof_topk/**/*kernel_stats.csv", recursive=True)[0]
+for r in list(csv.DictReader(open(f)))[:14]:
+    print(f"{r['Name'][:110]:110s} {r['Calls']:>5} {float(r['AverageNs'])/1e3:9.2f}us {float(r['Percentage']):6.2f}%")
+PY
 step phases 120 scripts/lab/gemm_phases_128 $O/phases > $O/phases.jsonl
 cat $O/phases.jsonl
 for r in 1 2 3; do
