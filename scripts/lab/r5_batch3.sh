@@ -13,7 +13,7 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[batch] stopping after $name (rc=$rc)" >&2; exit $rc; fi
   return 0
 }
-step test 400 python -u -m pytest tests/test_graphs_gpu.py tests/test_kernels_gpu.py -q -k "split_tail or multi_step or fused_step_tail or topk" --timeout 120 --timeout-method thread > $O/test.log 2>&1
+step test 400 python -u -m pytest tests/test_graphs_gpu.py tests/test_kernels_gpu.py -q -k "split_tail or multi_step or fused_step_tail or topk or sae_epilogues or fused_step_matches" --timeout 120 --timeout-method thread > $O/test.log 2>&1
 tail -30 $O/test.log
 for r in 1 2; do
   for v in dense cand; do
@@ -34,7 +34,16 @@ for r in 1 2 3; do
   for v in 0 1; do
     SC_SPLIT_TAIL=$v step ab_$v 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/ab_$v.jsonl
   done
+  SC_GEMM_CFG="0:14,7:14" step cfg14 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/cfg14.jsonl
+  SC_GEMM_CFG="0:14,6:14,7:14" step cfg14c 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/cfg14c.jsonl
+  SC_GEMM_CFG="0:14,7:14" SC_SPLIT_TAIL=1 step cfg14s 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/cfg14s.jsonl
 done
+python3 - <<'PY'
+import json
+for f in ("cfg14", "cfg14c", "cfg14s"):
+    ms = [json.loads(l)["ms_per_step"] for l in open(f"gpurun_out/r5b3/{f}.jsonl") if l.startswith("{")]
+    print(f, ms)
+PY
 for r in 1 2; do
   for v in 0 1; do
     SC_SPLIT_TAIL=$v step drv_$v 120 python bench.py --steps 20 --warmup 5 --no-eval >> $O/drv_$v.jsonl

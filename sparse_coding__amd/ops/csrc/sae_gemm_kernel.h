@@ -130,12 +130,14 @@ constexpr int epi_scratch_floats() { return 2 * S::WGM * S::BN + S::NW; }
 // 32 banks -- a group is 16 rows at one column, and the chunk XOR alone gives only 8 distinct
 // bank pairs (2-way, measured: 64 extra cycles per wave); the half swap makes them 16.
 // ds_read_b128 serves 16-lane groups on 64 banks: 2 rows x 8 chunks, distinct with the XOR.
-constexpr int STAGE_OFF = 4096, STAGE_ROW = 128, STAGE_WAVE = 64 * STAGE_ROW;
+constexpr int STAGE_OFF = 4096, STAGE_ROW = 128;
+template <class S>
+constexpr int stage_wave() { return S::WI * 16 * STAGE_ROW; }  // a wave's (16 WI) x 64 bf16 sub-tile
 __device__ __forceinline__ int stage_at(int row, int byte) {  // 8-byte granule of (row, byte)
   return row * STAGE_ROW + ((((byte >> 4) ^ (row >> 1)) & 7) << 4) + ((((byte >> 3) ^ row) & 1) << 3);
 }
 template <class S>
-constexpr int stage_bytes() { return STAGE_OFF + S::NW * STAGE_WAVE; }
+constexpr int stage_bytes() { return STAGE_OFF + S::NW * stage_wave<S>(); }
 
 template <class S, int EPI, bool AUX_EARLY, bool STAGE = false, bool FSTAGE = false>
 __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)[S::WI][S::WJ],
@@ -152,8 +154,8 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   const bool p1 = pi != 0;
   const int rowb = m0 + wr * (WI * 16) + (lane & 15);
   const int colb = n0 + wc * (WJ * 16) + 4 * (lane >> 4);
-  static_assert(!STAGE || (WI == 4 && WJ == 4 && 2 * S::WGM * BN + NW <= STAGE_OFF / 4), "stage layout");
-  char* stage = reinterpret_cast<char*>(red) + STAGE_OFF + wid * STAGE_WAVE;
+  static_assert(!STAGE || ((WI == 4 || WI == 8) && WJ == 4 && 2 * S::WGM * BN + NW <= STAGE_OFF / 4), "stage layout");
+  char* stage = reinterpret_cast<char*>(red) + STAGE_OFF + wid * stage_wave<S>();
   // one 4-wide bf16 output fragment (rows rowb + 16 i, columns colb + 16 j .. +3)
   auto put = [&](uint16_t* C, int i, int j, ushort4 h) {
     if constexpr (STAGE) {
@@ -167,7 +169,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
       uint16_t* Cw = C + (long)(m0 + wr * (WI * 16)) * p.ldc + n0 + wc * (WJ * 16);
       const int ch = lane & 7;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
+      for (int k = 0; k < 2 * WI; ++k) {
         const int row = 8 * k + (lane >> 3);
         uint4 v = *reinterpret_cast<const uint4*>(stage + row * STAGE_ROW + (((ch ^ (row >> 1)) & 7) << 4));
         if (row & 1) v = make_uint4(v.z, v.w, v.x, v.y);  // halves stored swapped on odd rows
@@ -651,7 +653,8 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
 }
 
 template <class S, bool AK, bool BKM, int EPI, int BKT, int NST>
-__global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
+// (256x128 blocks on the BK32 rings: two waves per SIMD, so two blocks co-reside per CU)
+__global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT == 32) ? 2 : 1) void sae_gemm_kernel(GemmParams p) {
   constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
   constexpr int TA = BM * BKT * 2, TBB = BN * BKT * 2;  // bytes per operand tile
   constexpr int PPWA = TA / 1024 / NW, PPWB = TBB / 1024 / NW;  // LDS-DMA pieces per wave
@@ -932,7 +935,7 @@ __global__ __launch_bounds__(S::NT) void sae_gemm_kernel(GemmParams p) {
 #undef SC_ISSUE
   SC_STAMP(2);
   lds_barrier();  // all reads of the ring done before smem is reused below
-  constexpr bool STAGE = S::WI == 4 && S::WJ == 4 && NST * STG >= stage_bytes<S>();
+  constexpr bool STAGE = (S::WI == 4 || S::WI == 8) && S::WJ == 4 && NST * STG >= stage_bytes<S>();
   constexpr bool FSTAGE = EPI == EPI_F32 && S::WJ == 4 && NST * STG >= S::NW * S::WI * 16 * STAGE_ROW;
   sae_epilogue<S, EPI, AUX_EARLY, STAGE, FSTAGE>(p, acc, auxv, biasv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn,
                                                  tiles_n, cptr, alpha, dead);
