@@ -190,6 +190,12 @@ class RingGraphSource:
             self.ep0.fill_(int(step))
             self._ep0_host = int(step)
             self.ring.epoch += 1
+        # every in-graph fetch of these steps -- the gather kernels and the fused tail's next-batch
+        # fetch (row (t + 1 - ep0) B N + r for t < step + steps - 1) -- indexes inside the permutation
+        # (the kernels clamp out-of-range indices to row 0 silently; this is the host-side check)
+        if (step - self._ep0_host + steps) * self.B * self.world > self.perm.numel() or step < self._ep0_host:
+            raise RuntimeError(f"steps {step}..{step + steps - 1} do not fit the ring permutation "
+                               f"({self.perm.numel()} rows from step {self._ep0_host}, {self.B * self.world} per step)")
 
     def tail_gather(self, out: torch.Tensor):
         """(ring buffer, permutation, epoch start, out): what a fused step tail needs to fetch the NEXT
