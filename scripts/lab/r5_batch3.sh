@@ -56,3 +56,10 @@ for v in (0, 1):
         ms = [json.loads(l)["ms_per_step"] for l in open(f"gpurun_out/r5b3/{f}_{v}.jsonl") if l.startswith("{")]
         print(f"split={v} {f}: {ms}")
 PY
+step masked_test 300 python -u -m pytest tests/test_masked_gpu.py -q --timeout 120 --timeout-method thread > $O/masked_test.log 2>&1
+tail -3 $O/masked_test.log
+for r in 1 2; do
+  step masked_base 200 python scripts/bench_configs.py masked --steps 80 --warmup 16 >> $O/masked_base.jsonl
+  SC_MASKED_DEC_CFG=5 step masked_lpt5 200 python scripts/bench_configs.py masked --steps 80 --warmup 16 --variant masked >> $O/masked_lpt5.jsonl
+done
+cat $O/masked_*.jsonl

@@ -130,9 +130,15 @@ class FusedSAEEnsemble:
         self.lr = torch.tensor([float(x) for x in lrs], device=dev, dtype=torch.float32)
         self.nactive = None
         self._live = None  # host copy of the live sizes: masked launches cover only live tiles
+        # masked decoder: block configuration (None = the per-epilogue default); with the host live
+        # sizes its blocks run longest-model-first, which pays once the grid needs more than one round
+        # of co-resident blocks (SC_MASKED_DEC_CFG, e.g. 5 = 128x128 on the BK64 x 3 ring, 1 block/CU)
+        self._dec_cfg = None
         if "dict_size" in b0:
             self._live = [int(m[1]["dict_size"]) for m in models]
             self.nactive = torch.tensor(self._live, device=dev, dtype=torch.int32)
+            env = os.environ.get("SC_MASKED_DEC_CFG", "").strip()
+            self._dec_cfg = int(env) if env else None
 
         # ----- bf16 shadows read by the GEMMs
         bf = torch.bfloat16
@@ -342,7 +348,7 @@ class FusedSAEEnsemble:
                              act=self.act, ascale=ascale, mask2_out=self.cmask2, live_host=self._live)
         self._join_side()  # the previous step's decoder Adam (split tail) before the decoder GEMM
         gemm_ops.decode_residual(self.c, self.dec_shadow, x if target is None else target, self.r, self.dec_part,
-                                 rcol=self.rcol, nactive=self.nactive)
+                                 rcol=self.rcol, nactive=self.nactive, live_host=self._live, cfg=self._dec_cfg)
         if self.act:
             gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                                dotpart=self.dotpart if self.kind == "threshold" else None, mask=self.cmask,

@@ -671,7 +671,7 @@ __global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT =
   const int ptm = p.M / PT, ptn = p.N / PT;  // partial-buffer grid (128 x 128 sub-tiles)
   const int per_split = p.ncomp ? p.ctotal : tiles_m * tiles_n * p.G;
   const int per_prob = per_split * p.ksplit;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = p.lpt ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int pi = (int)fdiv(bid, p.f_prob);
   int rem = bid - pi * per_prob;
   const int ksi = (int)fdiv(rem, p.f_split);
@@ -693,6 +693,13 @@ __global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT =
       tm = (int)fdiv(local, p.f_tn);
       tn = local - tm * tiles_n;
     }
+  } else if (p.lpt) {
+    const int tpm = tiles_m * tiles_n;
+    const int mr = rem / tpm;
+    g = p.lpt_order[mr < 16 ? mr : 15];
+    const int t = rem - mr * tpm;
+    tm = (int)fdiv(t, p.f_tn);
+    tn = t - tm * tiles_n;
   } else if (p.nactive || p.nact_m || p.nact_k) {
     // masked ensembles: models carry different live sizes, so the model index varies fastest --
     // with model-major order the XCD-aware remap hands each XCD one model's tiles and the XCD
@@ -993,9 +1000,27 @@ long compact_tiles(int epi, GemmParams& p) {
   return total;
 }
 
+// Host: longest-first model order for masked launches whose per-model K range differs (see
+// GemmParams::lpt); needs the host copy of the live sizes.
+inline void set_lpt(int epi, GemmParams& p) {
+  p.lpt = 0;
+  if (!(p.want_comp && p.nact_k && !p.nactive && !p.nact_m && p.ksplit == 1 && p.nprob == 1 && p.G <= 16 &&
+        (epi == EPI_DEC || epi == EPI_F32 || epi == EPI_BF16)))
+    return;
+  for (int g = 0; g < p.G; ++g) p.lpt_order[g] = g;
+  for (int a = 1; a < p.G; ++a)  // insertion sort by descending live size (stable)
+    for (int b = a; b > 0 && p.nact_h[p.lpt_order[b]] > p.nact_h[p.lpt_order[b - 1]]; --b) {
+      const int t = p.lpt_order[b];
+      p.lpt_order[b] = p.lpt_order[b - 1];
+      p.lpt_order[b - 1] = t;
+    }
+  p.lpt = 1;
+}
+
 template <class S, int BKT, int NST, bool FULL = true>
 int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t stream) {
   set_divisors<S>(p);
+  set_lpt(epi, p);
   const long comp = compact_tiles<S>(epi, p);
   if (comp) {
     p.f_split = make_fdiv((uint32_t)comp);
