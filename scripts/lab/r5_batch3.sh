@@ -37,10 +37,12 @@ for r in 1 2 3; do
   SC_GEMM_CFG="0:14,7:14" step cfg14 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/cfg14.jsonl
   SC_GEMM_CFG="0:14,6:14,7:14" step cfg14c 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/cfg14c.jsonl
   SC_GEMM_CFG="0:14,7:14" SC_SPLIT_TAIL=1 step cfg14s 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/cfg14s.jsonl
+  SC_GEMM_CFG="0:29,6:29,7:29" step cfg29 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/cfg29.jsonl
+  SC_GEMM_CFG="0:29,6:29,7:29" SC_SPLIT_TAIL=1 step cfg29s 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/cfg29s.jsonl
 done
 python3 - <<'PY'
 import json
-for f in ("cfg14", "cfg14c", "cfg14s"):
+for f in ("cfg14", "cfg14c", "cfg14s", "cfg29", "cfg29s"):
     ms = [json.loads(l)["ms_per_step"] for l in open(f"gpurun_out/r5b3/{f}.jsonl") if l.startswith("{")]
     print(f, ms)
 PY

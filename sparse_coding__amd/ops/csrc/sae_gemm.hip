@@ -33,7 +33,7 @@ int sc_gemm_shape(int M, int N, int G, int nprob) {
 // layout: bit0 = A is K-major, bit1 = B is K-major.
 // cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256;
 // bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4 (128x128 blocks: BK64 x 3),
-// 2: BK32 x 2, 3: BK32 x 3).
+// 2: BK32 x 2, 3: BK32 x 3); bit 4: 128x128 on the BK32 rings with the software-pipelined K loop.
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             const ScOperand* a /* [nprob][2] */, const ScOperand* b /* [nprob][2] */,
             void* const* c /* [nprob] */, const float* alpha /* [nprob] */, long ldc, long sc,
@@ -76,6 +76,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   const bool ak = layout & 1, bk = layout & 2;
   int shape = cfg & 3;
   const int pipe = (cfg >> 2) & 3;  // 0: BK64 x 2 stages, 1: BK32 x 4, 2: BK32 x 2, 3: BK32 x 3
+  const bool p32 = (cfg >> 4) & 1;  // 128x128 BK32 rings: the software-pipelined K loop
   if (shape == 0) shape = sc_gemm_shape(M, N, G, nprob);
   switch (shape) {
     case 3:
@@ -86,8 +87,10 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
       return launch_big(2, pipe, epi, ak, bk, p, nprob, stream);
     default:
       if (pipe == 1) return launch<S128, 64, 3, false>(epi, ak, bk, p, nprob, stream);  // 96 KB: 1 block/CU
-      if (pipe == 2) return launch<S128, 32, 2, false>(epi, ak, bk, p, nprob, stream);  // 32 KB: 4-5 blocks/CU
-      if (pipe == 3) return launch<S128, 32, 3, false>(epi, ak, bk, p, nprob, stream);
+      if (pipe == 2) return p32 ? launch<S128, 32, 2, false, true>(epi, ak, bk, p, nprob, stream)
+                                : launch<S128, 32, 2, false>(epi, ak, bk, p, nprob, stream);  // 32 KB: 4-5 blocks/CU
+      if (pipe == 3) return p32 ? launch<S128, 32, 3, false, true>(epi, ak, bk, p, nprob, stream)
+                                : launch<S128, 32, 3, false>(epi, ak, bk, p, nprob, stream);
       return launch<S128, 64, 2>(epi, ak, bk, p, nprob, stream);
   }
 }

@@ -652,9 +652,9 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   }
 }
 
-template <class S, bool AK, bool BKM, int EPI, int BKT, int NST>
 // (256x128 blocks on the BK32 rings: two waves per SIMD, so two blocks co-reside per CU)
-__global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT == 32) ? 2 : 1) void sae_gemm_kernel(GemmParams p) {
+template <class S, bool AK, bool BKM, int EPI, int BKT, int NST, bool P32 = false>
+__global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT == 32) ? 2 : (P32 && NST == 3) ? 3 : 1) void sae_gemm_kernel(GemmParams p) {
   constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
   constexpr int TA = BM * BKT * 2, TBB = BN * BKT * 2;  // bytes per operand tile
   constexpr int PPWA = TA / 1024 / NW, PPWB = TBB / 1024 / NW;  // LDS-DMA pieces per wave
@@ -801,7 +801,8 @@ __global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT =
   // The ReLU encoder epilogue's bias: loaded here, before the K-loop prologue issues its DMAs (so
   // the counted vmcnt waits below still see only tile DMAs as younger), its latency hidden.
   f32x4_t biasv[WJ];
-  if constexpr (EPI == EPI_ENC || EPI == EPI_ENC_CNT) {
+  // (the pipelined BK32 loop needs those 16 registers: it loads the bias after the loop)
+  if constexpr ((EPI == EPI_ENC || EPI == EPI_ENC_CNT) && !P32) {
     const float* bias = p.bias + (long)g * p.sbias;
 #pragma unroll
     for (int j = 0; j < WJ; ++j) biasv[j] = *reinterpret_cast<const f32x4_t*>(bias + colb + j * 16);
@@ -898,6 +899,75 @@ __global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT =
     }
     step(fa1, fb1, nk - 1, 1, fa0, fb0);
     last(fa1, fb1);
+  } else if constexpr (P32 && BKT == 32 && S::BM == 128 && S::BN == 128) {
+    // The same software pipeline for the BK32 rings (one 32-deep MFMA step per K-tile, 48 KB at
+    // three stages: three workgroups per CU): tile kt+1's fragments are read into the second
+    // register set while tile kt's MFMAs run.  At the barrier before those reads every wave holds
+    // tile kt in registers (lgkmcnt(0)), so tile kt's stage takes the DMA of tile kt+NST there.
+    // Unrolled by two for the register ping-pong; steady state (a DMA at both barriers), drain,
+    // last tile.
+    constexpr int RD = WI * (AK ? 1 : 2) + WJ * (BKM ? 1 : 2);
+    constexpr int MF = WI * WJ;
+    constexpr int MPR = MF / RD;
+    static_assert(MPR >= 1, "more LDS reads than MFMAs per step");
+    auto step = [&](bf16x8_t (&fan)[WI], bf16x8_t (&fbn)[WJ], int ktn, const bf16x8_t (&fa)[WI],
+                    const bf16x8_t (&fb)[WJ]) {
+      __builtin_amdgcn_sched_barrier(0);
+      frags(fan, fbn, ktn, 0);
+      mfmas(fa, fb);
+      sched_interleave<RD, MPR, MF - MPR * (RD - 1)>();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto last = [&](const bf16x8_t (&fa)[WI], const bf16x8_t (&fb)[WJ]) {
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(fa, fb);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto wait_tiles = [&](int younger) {
+      if (NST >= 4 && younger >= 3) wait_vmcnt<(NST >= 4 ? 3 : 0) * LPT>();
+      else if (NST >= 3 && younger >= 2) wait_vmcnt<(NST >= 3 ? 2 : 0) * LPT>();
+      else if (younger >= 1) wait_vmcnt<LPT>();
+      else wait_vmcnt<0>();
+    };
+    auto tile_barrier = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (kbeg + NST - 1 < nk) SC_ISSUE(kbeg + NST - 1);  // all NST stages in flight
+    bf16x8_t fa0[WI], fb0[WJ], fa1[WI], fb1[WJ];
+    wait_tiles(min(NST - 1, nk - 1 - kbeg));  // tile kbeg landed
+    tile_barrier();
+    SC_STAMP(1);
+    frags(fa0, fb0, kbeg, 0);
+    int kt = kbeg;  // invariant: fa0 / fb0 hold tile kt
+    for (; kt + 1 + NST < nk; kt += 2) {
+      wait_vmcnt<(NST - 2) * LPT>();  // tile kt+1 landed
+      tile_barrier();
+      SC_ISSUE(kt + NST);
+      step(fa1, fb1, kt + 1, fa0, fb0);
+      wait_vmcnt<(NST - 2) * LPT>();  // tile kt+2 landed
+      tile_barrier();
+      SC_ISSUE(kt + 1 + NST);
+      step(fa0, fb0, kt + 2, fa1, fb1);
+    }
+    for (; kt + 2 < nk; kt += 2) {
+      wait_tiles(min(NST - 2, nk - 2 - kt));
+      tile_barrier();
+      if (kt + NST < nk) SC_ISSUE(kt + NST);
+      step(fa1, fb1, kt + 1, fa0, fb0);
+      wait_tiles(min(NST - 2, nk - 3 - kt));
+      tile_barrier();
+      step(fa0, fb0, kt + 2, fa1, fb1);
+    }
+    if (kt + 1 < nk) {
+      wait_tiles(0);
+      tile_barrier();
+      step(fa1, fb1, kt + 1, fa0, fb0);
+      last(fa1, fb1);
+    } else {
+      last(fa0, fb0);
+    }
   } else for (int kt = kbeg; kt < nk; ++kt) {
     // Tile kt must have landed; tiles kt+1 .. kt+NST-2 may stay in flight.
     const int younger = min(NST - 2, nk - 1 - kt);
@@ -941,6 +1011,11 @@ __global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT =
   }  // !dead
 #undef SC_ISSUE
   SC_STAMP(2);
+  if constexpr ((EPI == EPI_ENC || EPI == EPI_ENC_CNT) && P32) {
+    const float* bias = p.bias + (long)g * p.sbias;
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) biasv[j] = *reinterpret_cast<const f32x4_t*>(bias + colb + j * 16);
+  }
   lds_barrier();  // all reads of the ring done before smem is reused below
   constexpr bool STAGE = (S::WI == 4 || S::WI == 8) && S::WJ == 4 && NST * STG >= stage_bytes<S>();
   constexpr bool FSTAGE = EPI == EPI_F32 && S::WJ == 4 && NST * STG >= S::NW * S::WI * 16 * STAGE_ROW;
@@ -1017,7 +1092,7 @@ inline void set_lpt(int epi, GemmParams& p) {
   p.lpt = 1;
 }
 
-template <class S, int BKT, int NST, bool FULL = true>
+template <class S, int BKT, int NST, bool FULL = true, bool P32 = false>
 int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t stream) {
   set_divisors<S>(p);
   set_lpt(epi, p);
@@ -1030,7 +1105,7 @@ int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t strea
   if constexpr (!FULL) {
     if (epi == EPI_BF16 || epi >= EPI_ENC_ACT || (epi == EPI_F32 && (ak || bk))) return 8;
   }
-#define SC_L(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_kernel<S, AKV, BKV, E, BKT, NST>), grid, block, 0, stream, p)
+#define SC_L(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_kernel<S, AKV, BKV, E, BKT, NST, P32>), grid, block, 0, stream, p)
   // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
   // epilogues; the plain F32 / BF16 epilogues exist for every layout.
   switch (epi) {
