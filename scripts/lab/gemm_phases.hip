@@ -79,11 +79,10 @@ static void run(const char* name, long nblocks, F launch) {
     snprintf(path, sizeof path, "%s/%s.csv", g_raw_dir, name);
     FILE* fo = fopen(path, "w");
     if (fo) {
-      fprintf(fo, "block,start_us,fill_us,kloop_us,epi_us,hw_id,xcc_id\n");
+      fprintf(fo, "block,t0,t1,t2,t3,rt0,rt3,hw_id,xcc_id\n");
       for (long b = 0; b < nblocks; ++b) {
         const long long* s = &h[b * 8];
-        fprintf(fo, "%ld,%.3f,%.3f,%.3f,%.3f,%lld,%lld\n", b, (s[0] - t0) / ghz / 1e3, (s[1] - s[0]) / ghz / 1e3,
-                (s[2] - s[1]) / ghz / 1e3, (s[3] - s[2]) / ghz / 1e3, s[6], s[7]);
+        fprintf(fo, "%ld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld\n", b, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]);
       }
       fclose(fo);
     }

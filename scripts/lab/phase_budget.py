@@ -16,10 +16,19 @@ for f in sorted(glob.glob(os.path.join(d, "*.csv"))):
     rows = list(csv.DictReader(open(f)))
     if not rows:
         continue
-    start = [float(r["start_us"]) for r in rows]
-    fill = [float(r["fill_us"]) for r in rows]
-    kl = [float(r["kloop_us"]) for r in rows]
-    ep = [float(r["epi_us"]) for r in rows]
+    t = [[int(r[k]) for k in ("t0", "t1", "t2", "t3")] for r in rows]
+    # shader clock from s_memtime vs s_memrealtime (100 MHz) over the launch; 2.0 GHz if unusable
+    r0, r1 = min(int(r["rt0"]) for r in rows), max(int(r["rt3"]) for r in rows)
+    m0, m1 = min(x[0] for x in t), max(x[3] for x in t)
+    ghz = (m1 - m0) / ((r1 - r0) * 10.0) if r1 > r0 else 0.0
+    if not 0.5 < ghz < 3.5:
+        print(f"  (clock from stamps {ghz:.3g} GHz unusable; assuming 2.0)")
+        ghz = 2.0
+    us = lambda ticks: ticks / ghz / 1e3  # noqa: E731
+    start = [us(x[0] - m0) for x in t]
+    fill = [us(x[1] - x[0]) for x in t]
+    kl = [us(x[2] - x[1]) for x in t]
+    ep = [us(x[3] - x[2]) for x in t]
     end = [s + a + b + c for s, a, b, c in zip(start, fill, kl, ep)]
     life = [e - s for s, e in zip(start, end)]
     span = max(end) - min(start)

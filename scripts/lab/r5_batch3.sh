@@ -13,6 +13,8 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[batch] stopping after $name (rc=$rc)" >&2; exit $rc; fi
   return 0
 }
+# the snapshot may be taken mid-edit: rebuild in-tree when the sources are newer than the library
+step build 600 python -c "from sparse_coding__amd.ops import build as b; b.build(force=False)"
 step test 400 python -u -m pytest tests/test_graphs_gpu.py tests/test_kernels_gpu.py -q -k "split_tail or multi_step or fused_step_tail or topk or sae_epilogues or fused_step_matches" --timeout 120 --timeout-method thread > $O/test.log 2>&1
 tail -30 $O/test.log
 for r in 1 2; do
@@ -28,8 +30,6 @@ f = glob.glob("gpurun_out/r5b3/prof_topk/**/*kernel_stats.csv", recursive=True)[
 for r in list(csv.DictReader(open(f)))[:14]:
     print(f"{r['Name'][:110]:110s} {r['Calls']:>5} {float(r['AverageNs'])/1e3:9.2f}us {float(r['Percentage']):6.2f}%")
 PY
-step phases 120 scripts/lab/gemm_phases_128 $O/phases > $O/phases.jsonl
-cat $O/phases.jsonl
 for r in 1 2 3; do
   for v in 0 1; do
     SC_SPLIT_TAIL=$v step ab_$v 120 python bench.py --steps 200 --warmup 20 --no-eval >> $O/ab_$v.jsonl
