@@ -130,15 +130,9 @@ class FusedSAEEnsemble:
         self.lr = torch.tensor([float(x) for x in lrs], device=dev, dtype=torch.float32)
         self.nactive = None
         self._live = None  # host copy of the live sizes: masked launches cover only live tiles
-        # masked decoder: block configuration (None = the per-epilogue default); with the host live
-        # sizes its blocks run longest-model-first, which pays once the grid needs more than one round
-        # of co-resident blocks (SC_MASKED_DEC_CFG, e.g. 5 = 128x128 on the BK64 x 3 ring, 1 block/CU)
-        self._dec_cfg = None
         if "dict_size" in b0:
             self._live = [int(m[1]["dict_size"]) for m in models]
             self.nactive = torch.tensor(self._live, device=dev, dtype=torch.int32)
-            env = os.environ.get("SC_MASKED_DEC_CFG", "").strip()
-            self._dec_cfg = int(env) if env else None
 
         # ----- bf16 shadows read by the GEMMs
         bf = torch.bfloat16
@@ -237,13 +231,6 @@ class FusedSAEEnsemble:
         self._tail_ok = (self.kind in ("untied", "tied") and self.act == gemm_ops.ACT_RELU and not self.learned_center
                          and n % 32 == 0 and d <= 1024
                          and os.environ.get("SC_FUSED_TAIL", "1") not in ("", "0"))
-        # split tail (untied, unmasked): the decoder's row Adam runs as a second launch on a side stream,
-        # beside the NEXT step's encoder GEMM (which does not read the decoder); the next decoder GEMM
-        # waits for it.  Both launches share the completion ticket (csrc/adam.hip, roles).
-        self._split_tail = (self._tail_ok and self.kind == "untied" and self.nactive is None
-                            and os.environ.get("SC_SPLIT_TAIL", "0") not in ("", "0"))
-        self._side = torch.cuda.Stream(dev) if self._split_tail else None
-        self._dec_ready = None  # event: the side-stream decoder Adam of the previous step
         self._bsq = torch.zeros(2, G, n // 32, device=dev) if self._tail_ok else None
         self._ticket = torch.zeros(adam_ops.TICKET_INTS, device=dev, dtype=torch.int32) if self._tail_ok else None
         self._bsq_dirty = True
@@ -346,9 +333,8 @@ class FusedSAEEnsemble:
         gemm_ops.encode_relu(x, self.enc_shadow, self.params[self._bkey], self.c, self.enc_part,
                              self.cnt_part if count else None, self.nactive, mask_out=self.cmask,
                              act=self.act, ascale=ascale, mask2_out=self.cmask2, live_host=self._live)
-        self._join_side()  # the previous step's decoder Adam (split tail) before the decoder GEMM
         gemm_ops.decode_residual(self.c, self.dec_shadow, x if target is None else target, self.r, self.dec_part,
-                                 rcol=self.rcol, nactive=self.nactive, live_host=self._live, cfg=self._dec_cfg)
+                                 rcol=self.rcol, nactive=self.nactive)
         if self.act:
             gemm_ops.code_grad(self.r, self.dec_shadow, self.c, self.l1, self.dpre, self.colpart,
                                dotpart=self.dotpart if self.kind == "threshold" else None, mask=self.cmask,
@@ -461,41 +447,7 @@ class FusedSAEEnsemble:
         self._apply_update_kernels()
         self._host_step()
 
-    def _join_side(self):
-        """Make the current stream wait for the split tail's side-stream decoder Adam, if pending."""
-        if self._dec_ready is not None:
-            torch.cuda.current_stream(self.device).wait_event(self._dec_ready)
-            self._dec_ready = None
-
-    def _split_tail_kernels(self, gather):
-        """The step tail as two launches sharing one completion ticket: the decoder rows' Adam on the
-        side stream (overlapping whatever the main stream runs next: the next step's encoder) and the
-        rest -- loss terms, bias Adam, encoder rows, next-batch gather -- on the main stream."""
-        G, n = self.n_models, self.n
-        dec, enc = self._adam_sets()
-        grows = gather[3].shape[0] if gather is not None else 0
-        n_main = adam_ops.tail_blocks(G, n, [G * n], grows, roles=3)
-        n_side = adam_ops.tail_blocks(G, n, [G * n], 0, roles=2)
-        common = dict(cnt_part=self.cnt_part if self._counted else None,
-                      feat_count=self.feature_counts if self._counted else None, blk_total=n_main + n_side,
-                      **self._adam_split_kw())
-        args = (self.lr, *self.betas, self.eps, self.step_dev, self.params[self._bkey], self.m[self._bkey],
-                self.v[self._bkey], self.colpart, self.enc_part, self.dec_part, self.l1, self.bias_decay, self.out,
-                self.batch_size, self._alpha, self._bsq, self._ticket)
-        cur = torch.cuda.current_stream(self.device)
-        self._join_side()
-        self._side.wait_stream(cur)
-        with torch.cuda.stream(self._side):
-            adam_ops.step_tail([dec], *args, roles=2, blk_base=n_main, **common)
-            ev = torch.cuda.Event()
-            ev.record(self._side)
-        adam_ops.step_tail([enc], *args, gather=gather, roles=3, blk_base=0, **common)
-        self._dec_ready = ev
-
     def _apply_update_kernels(self, gather=None):
-        if self._split_tail:
-            self._split_tail_kernels(gather)
-            return
         if self._tail_ok:
             # one launch: row Adam + loss terms + bias Adam (+ the next step's batch gather), the
             # device step counter advanced by its last block
@@ -614,7 +566,7 @@ class FusedSAEEnsemble:
             self._graph = None
         return self
 
-    def _step_kernels(self, x, count=None, gather=None, before_update=None, overlap_next=False):
+    def _step_kernels(self, x, count=None, gather=None, before_update=None):
         """All kernels of one step (captured as one HIP graph when enabled).  Side-stream
         variants of this sequence -- decoder Adam beside the encoder weight gradient, the loss /
         bias-Adam tail beside the weight gradient, Adam fused into the weight-gradient epilogue,
@@ -627,8 +579,6 @@ class FusedSAEEnsemble:
         if before_update is not None:  # e.g. a stream wait the update (its next-batch fetch) needs
             before_update()
         self._apply_update_kernels(gather if self._tail_ok else None)
-        if not overlap_next:  # (a split tail's side launch overlaps only a next step of the same graph)
-            self._join_side()
 
     def add_static_input(self, t: torch.Tensor) -> int:
         """Register another persistent input buffer [B, d] bf16: ``step_batch(t)`` then replays
@@ -685,8 +635,7 @@ class FusedSAEEnsemble:
                 for i, count in enumerate(pattern):
                     if i == 0 or nxt is None:
                         self._source.gather(self.x_static, self.step_dev)
-                    self._step_kernels(self.x_static, count, gather=nxt if i + 1 < len(pattern) else None,
-                                       overlap_next=i + 1 < len(pattern))
+                    self._step_kernels(self.x_static, count, gather=nxt if i + 1 < len(pattern) else None)
             _upload(g, self.device)
             self._graph[key] = g
         return g
@@ -745,8 +694,8 @@ class FusedSAEEnsemble:
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                for i, (x, count) in enumerate(zip(xs, pattern)):
-                    self._step_kernels(x, count, overlap_next=i + 1 < len(pattern))
+                for x, count in zip(xs, pattern):
+                    self._step_kernels(x, count)
             _upload(g, self.device)
             self._graph[key] = g
         return g

@@ -104,7 +104,7 @@ TICKET_INTS = (1 + 64) * 32  # csrc/adam.hip: top + TK_SUB sub-counters, one 128
 
 def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, enc_part, dec_part, l1, bias_decay,
               out, B, gscale, bsq, ticket, cnt_part=None, feat_count=None, gather=None, nsplit=1, gstride=0,
-              live=None, row0=None, live_host=None, roles=3, blk_base=0, blk_total=0):
+              live=None, row0=None, live_host=None):
     """The end of a single-device step as ONE launch (csrc/adam.hip ``step_tail_kernel``): row Adam over
     ``sets`` (as ``adam_rows``), the loss terms into ``out`` [G, 6], bias Adam (gradient = ``gscale``
     x the column sums of ``colpart`` [G, tm, n]), feature on-counts when ``cnt_part`` /
@@ -117,10 +117,7 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
     gradient is the first of ``nsplit`` split-K partial slabs (as ``adam_rows``).  ``live``: int32 [G] live
     row counts of a masked ensemble (rows past them are skipped, as ``adam_rows``; with ``live_host``, the
     same sizes as host ints, the row blocks cover only live rows).  ``row0``: the sets are
-    [rows, d] views of rows [row0, row0 + rows) of the [G n, d] stacks (a ZeRO-1 shard).
-    ``roles`` / ``blk_base`` / ``blk_total``: one step's tail split over two launches sharing the
-    completion ticket (``tail_blocks``): roles 1 = loss / bias / gather only, 2 = row Adam only,
-    3 = both; the launches number their blocks [blk_base, blk_base + blocks) of ``blk_total``."""
+    [rows, d] views of rows [row0, row0 + rows) of the [G n, d] stacks (a ZeRO-1 shard)."""
     shp = tuple(sets[0]["p"].shape)
     d = shp[-1]
     nrows = sets[0]["p"].numel() // d
@@ -168,17 +165,9 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
         _lib.ptr(gbuf), nbuf, _lib.ptr(perm), nperm, _lib.ptr(ep0), _lib.ptr(gout), grows, row_bytes,
         int(nsplit), int(gstride), _lib.ptr(live), int(cnt_tm), int(row0 or 0),
         C.cast((C.c_int * len(live_host))(*[int(v) for v in live_host]), C.c_void_p)
-        if (live_host is not None and live is not None) else None, int(roles), int(blk_base), int(blk_total),
-        _lib.stream_handle(),
+        if (live_host is not None and live is not None) else None, _lib.stream_handle(),
     )
     _lib.check(rc, "sc_step_tail")
-
-
-def tail_blocks(G: int, n: int, set_rows, gather_rows: int = 0, roles: int = 3) -> int:
-    """Blocks of one ``step_tail`` launch (unmasked sets): loss G + bias G n/32 + gather + rows/4."""
-    side = roles & 1
-    rows = sum(set_rows) if roles & 2 else 0
-    return (G + G * (n // 32) + (gather_rows + 3) // 4 if side else 0) + (rows + 3) // 4
 
 
 def bias_sq_parts(bias, bsq, parity: int):

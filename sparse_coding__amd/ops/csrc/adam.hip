@@ -362,10 +362,6 @@ struct TailArgs {
   // masked ensembles: the row-Adam blocks cover only live rows (lcomp: live-row prefix lpre[g] over
   // the models, the same for every set; compact row rc of set s -> row g n + rc - lpre[g] of model g)
   int lcomp, lG, lpre[17];
-  // one step's tail split over two launches that share the completion ticket (the decoder rows on a
-  // side stream beside the next step's encoder): this launch's first block in the shared numbering
-  // and the total number of blocks over both launches (blk_total == gridDim.x for a single launch)
-  long blk_base, blk_total;
 };
 
 __device__ __forceinline__ void tail_loss(const BiasArgs& a, const TailArgs& t, int g, int par) {
@@ -496,7 +492,7 @@ __global__ __launch_bounds__(256) void step_tail_kernel(AdamArgs a, BiasArgs b, 
   // and the block completing a sub-counter takes a ticket on the top counter.
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int nb = (int)t.blk_total, sub = (int)((t.blk_base + bid) % TK_SUB);
+    const int nb = (int)gridDim.x, sub = bid % TK_SUB;
     const int expect = nb / TK_SUB + (sub < nb % TK_SUB ? 1 : 0);
     int* sc = t.ticket + (1 + sub) * TK_LINE;
     if (__hip_atomic_fetch_add(sc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == expect - 1) {
@@ -585,13 +581,8 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
                  const float* l1, const float* bias_decay, float* out, int n, int B, float gscale,
                  float* bsq, int* ticket, const void* gbuf, long nbuf, const long* perm, long nperm,
                  const int* ep0, void* gout, long grows, long row_bytes, int nsplit, long gstride,
-                 const int* live, int cnt_tm, long row0, const int* live_h, int roles, long blk_base,
-                 long blk_total, hipStream_t stream) {
-  // roles: bit 0 = the loss / bias / gather roles, bit 1 = the row-Adam roles (the second launch of a
-  // split tail carries only its rows); blk_base / blk_total: the shared ticket's numbering (0 / 0 =
-  // this launch alone)
+                 const int* live, int cnt_tm, long row0, const int* live_h, hipStream_t stream) {
   if (d % 256 || d > 4096 || nset < 1 || nset > 2 || n % 32 || !step || !ticket || !bsq || nsplit < 1) return 1;
-  if (roles < 1 || roles > 3) return 1;
   if (gbuf && (row_bytes % 16 || nbuf < 1)) return 1;
   AdamArgs a;
   long total = 0;
@@ -620,8 +611,7 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
   t.gbuf = reinterpret_cast<const u32x4_t*>(gbuf); t.nbuf = nbuf; t.perm = perm; t.nperm = nperm; t.ep0 = ep0;
   t.gout = reinterpret_cast<u32x4_t*>(gout); t.grows = gbuf ? grows : 0;
   t.row_vec = (int)(row_bytes / 16);
-  const bool side = roles & 1;
-  t.nloss = side ? G : 0; t.nbias = side ? G * (n / 32) : 0; t.ngather = (side && gbuf) ? (int)((grows + 3) / 4) : 0;
+  t.nloss = G; t.nbias = G * (n / 32); t.ngather = gbuf ? (int)((grows + 3) / 4) : 0;
   t.lcomp = 0; t.lG = G;
   long arows = total;
   // host copy of a masked ensemble's live sizes (full-stack sets only, G <= 16): launch live rows only
@@ -636,11 +626,7 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
       arows = (long)nset * t.lpre[G];
     }
   }
-  if (!(roles & 2)) arows = 0;
   const long blocks = t.nloss + t.nbias + t.ngather + (arows + 3) / 4;
-  t.blk_base = blk_base;
-  t.blk_total = blk_total > 0 ? blk_total : blocks;
-  if (blk_base < 0 || blk_base + blocks > t.blk_total) return 1;
 #define SC_TAIL(NVV)                                                                                   \
   case NVV:                                                                                            \
     if (gbf16) hipLaunchKernelGGL((step_tail_kernel<NVV, true>), dim3(blocks), dim3(256), 0, stream, a, ba, t); \

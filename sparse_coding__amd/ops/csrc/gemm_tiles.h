@@ -108,12 +108,6 @@ struct GemmParams {
   int tpre[17];
   int tl[16];
   FDiv fl[16];
-  // --- masked launches whose K range shrinks per model (the decoder, nact_k): longest-first order.
-  // Block b runs a tile of model lpt_order[b / tiles-per-model] (models by descending live K), blocks
-  // go to the XCDs round-robin (no remap), so the longest blocks start first and the short ones fill
-  // the slots they free (a one-round grid is set by its largest model otherwise)
-  int lpt;
-  int lpt_order[16];
   // --- EPI_TOPK: top-k candidate compaction -- the scores never reach HBM densely.  Element
   // (row, col) with alpha * acc >= tk_lo[g M + row] (a lower bound of the row's k-th largest
   // score) is appended to its row's buffer tk_val / tk_col [G M][tk_cap] at slots reserved by one

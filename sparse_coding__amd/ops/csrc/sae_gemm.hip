@@ -68,7 +68,6 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.act = act; p.ascale = ascale;
   p.cmask2 = reinterpret_cast<uint64_t*>(cmask2); p.rcol = rcol;
   p.nact_m = nact_m; p.nact_k = nact_k;
-  p.lpt = 0;
   // masked launches with host copies of the live sizes launch only their live tiles
   p.want_comp = nact_host != nullptr && G <= 16;
   p.ncomp = 0;

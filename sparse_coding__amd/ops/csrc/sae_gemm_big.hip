@@ -12,10 +12,8 @@ int launch_big(int shape, int pipe, int epi, bool ak, bool bk, const GemmParams&
     if (pipe == 2) return launch<S256, 32, 2, false>(epi, ak, bk, p, nprob, stream);
     return launch<S256, 64, 2>(epi, ak, bk, p, nprob, stream);
   }
-  // 256x128 with the BK32 rings: 72 KB (3 stages) / 48 KB (2 stages) of LDS -> 2 / 3 blocks per CU;
-  // the step's K = 512 GEMMs then launch G B n / 32768 blocks (1024 at the headline: 2 full rounds)
-  if (pipe == 3) return launch<S256x128, 32, 3, false>(epi, ak, bk, p, nprob, stream);
-  if (pipe == 2) return launch<S256x128, 32, 2, false>(epi, ak, bk, p, nprob, stream);
+  // (256x128 on the BK32 rings, two blocks per CU, measured slower in the step: 0.302-0.307 vs
+  // 0.296-0.297 ms, profiles/r5/batch3/cfg14.jsonl)
   if (pipe) return 8;
   return launch<S256x128, 64, 2>(epi, ak, bk, p, nprob, stream);
 }

@@ -652,9 +652,9 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   }
 }
 
-// (256x128 blocks on the BK32 rings: two waves per SIMD, so two blocks co-reside per CU)
+// (the software-pipelined BK32 x 3 loop: three waves per SIMD, so three blocks co-reside per CU)
 template <class S, bool AK, bool BKM, int EPI, int BKT, int NST, bool P32 = false>
-__global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT == 32) ? 2 : (P32 && NST == 3) ? 3 : 1) void sae_gemm_kernel(GemmParams p) {
+__global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : 1) void sae_gemm_kernel(GemmParams p) {
   constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
   constexpr int TA = BM * BKT * 2, TBB = BN * BKT * 2;  // bytes per operand tile
   constexpr int PPWA = TA / 1024 / NW, PPWB = TBB / 1024 / NW;  // LDS-DMA pieces per wave
@@ -671,7 +671,7 @@ __global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT =
   const int ptm = p.M / PT, ptn = p.N / PT;  // partial-buffer grid (128 x 128 sub-tiles)
   const int per_split = p.ncomp ? p.ctotal : tiles_m * tiles_n * p.G;
   const int per_prob = per_split * p.ksplit;
-  const int bid = p.lpt ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int pi = (int)fdiv(bid, p.f_prob);
   int rem = bid - pi * per_prob;
   const int ksi = (int)fdiv(rem, p.f_split);
@@ -693,13 +693,6 @@ __global__ __launch_bounds__(S::NT, (S::WGM * S::WGN == 4 && S::WI == 8 && BKT =
       tm = (int)fdiv(local, p.f_tn);
       tn = local - tm * tiles_n;
     }
-  } else if (p.lpt) {
-    const int tpm = tiles_m * tiles_n;
-    const int mr = rem / tpm;
-    g = p.lpt_order[mr < 16 ? mr : 15];
-    const int t = rem - mr * tpm;
-    tm = (int)fdiv(t, p.f_tn);
-    tn = t - tm * tiles_n;
   } else if (p.nactive || p.nact_m || p.nact_k) {
     // masked ensembles: models carry different live sizes, so the model index varies fastest --
     // with model-major order the XCD-aware remap hands each XCD one model's tiles and the XCD
@@ -1075,27 +1068,9 @@ long compact_tiles(int epi, GemmParams& p) {
   return total;
 }
 
-// Host: longest-first model order for masked launches whose per-model K range differs (see
-// GemmParams::lpt); needs the host copy of the live sizes.
-inline void set_lpt(int epi, GemmParams& p) {
-  p.lpt = 0;
-  if (!(p.want_comp && p.nact_k && !p.nactive && !p.nact_m && p.ksplit == 1 && p.nprob == 1 && p.G <= 16 &&
-        (epi == EPI_DEC || epi == EPI_F32 || epi == EPI_BF16)))
-    return;
-  for (int g = 0; g < p.G; ++g) p.lpt_order[g] = g;
-  for (int a = 1; a < p.G; ++a)  // insertion sort by descending live size (stable)
-    for (int b = a; b > 0 && p.nact_h[p.lpt_order[b]] > p.nact_h[p.lpt_order[b - 1]]; --b) {
-      const int t = p.lpt_order[b];
-      p.lpt_order[b] = p.lpt_order[b - 1];
-      p.lpt_order[b - 1] = t;
-    }
-  p.lpt = 1;
-}
-
 template <class S, int BKT, int NST, bool FULL = true, bool P32 = false>
 int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t stream) {
   set_divisors<S>(p);
-  set_lpt(epi, p);
   const long comp = compact_tiles<S>(epi, p);
   if (comp) {
     p.f_split = make_fdiv((uint32_t)comp);

@@ -195,15 +195,13 @@ def encode_relu(x, w, bias, c_out, part, colpart=None, nactive=None, mask_out=No
             ascale=ascale, cmask2=mask2_out, nact_host=live_host if nactive is not None else None)
 
 
-def decode_residual(c, w_hat, x, r_out, part, rcol=None, nactive=None, live_host=None, cfg=None):
+def decode_residual(c, w_hat, x, r_out, part, rcol=None, nactive=None):
     """r[g] = c[g] @ w_hat[g] - x[g]  (bf16 out) with sum(r^2) partials.
 
     c: [G, B, n] bf16; w_hat: [G, n, d] bf16 (row-normalised dictionary);
     x: [B, d] or [G, B, d] bf16; r_out: [G, B, d] bf16; part: [G, (B/128)*(d/128)];
     rcol (optional): [G, B/128, d] fp32 column sums of the residual per 128-row tile, taken
-    before the bf16 rounding.  ``nactive`` / ``live_host`` (masked ensembles): the models' live
-    sizes on the device / host -- K tiles past them are skipped, and with the host copy the blocks
-    run longest-model-first (GemmParams::lpt).
+    before the bf16 rounding.
     """
     G, B, n = c.shape
     d = w_hat.shape[2]
@@ -218,8 +216,7 @@ def decode_residual(c, w_hat, x, r_out, part, rcol=None, nactive=None, live_host
     b = [_op(w_hat, d, n * d)] * 2  # stored [K=n][N=d] -> N-major
     # nactive (masked ensembles): codes past a model's live size are zero -- skip those K-tiles
     _launch(EPI_DEC, 1, B, d, n, 0, G, a, b, [r_out], [1.0], d, B * d, nact_k=nactive,
-            aux=x, ldaux=d, saux=sx, part=part, rcol=rcol,
-            nact_host=live_host if nactive is not None else None, cfg=cfg)
+            aux=x, ldaux=d, saux=sx, part=part, rcol=rcol)
 
 
 def code_grad(r, w_hat, c, l1, dpre_out, colpart, dotpart=None, tied_bias=None, mask=None, act=ACT_RELU,

@@ -335,43 +335,3 @@ def test_topk_multistep_source_graph_matches_eager_steps():
     assert torch.equal(a.params["dict"], b.params["dict"])
     assert torch.equal(a.idx, b.idx)
 
-
-@pytest.mark.parametrize("group", [5, 1])
-def test_split_tail_side_stream_matches_fused_tail(group, monkeypatch):
-    """SC_SPLIT_TAIL=1: the decoder rows' Adam as a second launch on a side stream (overlapping the next
-    step's encoder inside a multi-step graph, sharing the completion ticket) == the one-launch tail:
-    bit-identical parameters, losses, feature counts and device step counter."""
-    from sparse_coding__amd.data.ring import DeviceRing
-    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
-    from sparse_coding__amd.engine.graph_plan import count_pattern
-    from sparse_coding__amd.models.signatures import FunctionalSAE
-
-    torch.manual_seed(33)
-    d, n, B = 512, 1024, 256
-    rows = (torch.randn(B * 40, d, device=DEV) * 2).to(torch.bfloat16)
-    rings = []
-    for _ in range(2):
-        r = DeviceRing(rows.shape[0], d, device=DEV, seed=4)
-        r.push(rows)
-        rings.append(r)
-    models = [FunctionalSAE.init(d, n, l1, device=DEV) for l1 in (1e-4, 1e-3, 1e-2)]
-    monkeypatch.setenv("SC_SPLIT_TAIL", "1")
-    a = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
-    monkeypatch.setenv("SC_SPLIT_TAIL", "0")
-    b = FusedSAEEnsemble(models, FunctionalSAE, batch_size=B, device=DEV).enable_graph()
-    assert a._split_tail and not b._split_tail
-    a.attach_source(rings[0].graph_source(B))
-    b.attach_source(rings[1].graph_source(B))
-    for _ in range(3):
-        a.step_source(group, count_pattern(group))
-        b.step_source(group, count_pattern(group))
-    xa = a.step_batch(rows[:B])  # eager-captured single step too
-    xb = b.step_batch(rows[:B])
-    torch.cuda.synchronize()
-    assert int(a.step_dev.item()) == int(b.step_dev.item()) == 3 * group + 1
-    assert int(a._ticket.abs().sum().item()) == 0
-    for k in a.params:
-        assert torch.equal(a.params[k], b.params[k]), k
-        assert torch.equal(a.m[k], b.m[k]) and torch.equal(a.v[k], b.v[k]), k
-    assert torch.equal(a.dec_shadow, b.dec_shadow) and torch.equal(a.norms, b.norms)
-    assert torch.equal(xa, xb) and torch.equal(a.feature_counts, b.feature_counts)

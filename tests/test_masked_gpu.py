@@ -125,30 +125,3 @@ def test_compacted_split_k_weight_gradient():
     for g, s in enumerate(sizes):
         assert not parts[:, g, s:].any() and not ref[g, s:].any()
 
-
-@pytest.mark.parametrize("cfg", [1, 5])
-def test_masked_decoder_longest_first_matches_torch(cfg):
-    """The masked decoder with the host live sizes (longest-model-first block order, no XCD remap) on
-    the default one-round grid (cfg 1) and on the two-round BK64 x 3 grid (cfg 5): bit-identical to
-    the launch without them, and R = c W_hat - x against fp32 torch."""
-    from sparse_coding__amd.ops import gemm
-
-    torch.manual_seed(8)
-    G, B, d, n = 5, 512, 256, 1024
-    sizes = [1024, 128, 640, 384, 896]
-    live = torch.tensor(sizes, device=DEV, dtype=torch.int32)
-    x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
-    c = torch.relu(torch.randn(G, B, n, device=DEV)).to(torch.bfloat16)
-    for g, s in enumerate(sizes):
-        c[g, :, s:] = 0
-    wd = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1).to(torch.bfloat16)
-    r0 = torch.empty(G, B, d, device=DEV, dtype=torch.bfloat16)
-    r1 = torch.empty_like(r0)
-    p0 = torch.zeros(G, (B // 128) * (d // 128), device=DEV)
-    p1 = torch.zeros_like(p0)
-    gemm.decode_residual(c, wd, x, r0, p0, nactive=live, cfg=cfg)
-    gemm.decode_residual(c, wd, x, r1, p1, nactive=live, live_host=sizes, cfg=cfg)
-    torch.cuda.synchronize()
-    assert torch.equal(r0, r1) and torch.equal(p0, p1)
-    ref = c.float() @ wd.float() - x.float()
-    torch.testing.assert_close(r1.float(), ref, rtol=2e-2, atol=2e-2)
