@@ -1004,12 +1004,73 @@ __device__ __forceinline__ float key_float(uint32_t k) {  // inverse of order_ke
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
+
+// k-th largest of a wave's keys (PL per lane; key 0 = no key): 12 bisection steps over all keys
+// (DPP wave totals), then -- when the keys sharing t's top 12 bits fit one per lane, the usual case --
+// the last 20 bits by ballots over that compacted bucket (one v_cmp + popcount per bit); otherwise the
+// full scans continue.  Returns t; *gt = number of keys > t.  cbuf: 64 words of wave-private LDS.
+template <int PL>
+__device__ __forceinline__ uint32_t wave_kth_key(const uint32_t (&key)[PL], int k, int lane, uint32_t* cbuf,
+                                                 int* gt) {
+  constexpr int S1 = 12, LOW = 32 - S1;
+  uint32_t t = 0;
+#pragma unroll 1
+  for (int b = 31; b >= LOW; --b) {
+    const uint32_t cand = t | (1u << b);
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
+    if (wave_total(cnt) >= k) t = cand;
+  }
+  const uint32_t hi = t >> LOW;
+  int above = 0, inb = 0;
+#pragma unroll
+  for (int i = 0; i < PL; ++i) {
+    const uint32_t h = key[i] >> LOW;
+    above += h > hi ? 1 : 0;
+    inb += (h == hi && key[i] != 0u) ? 1 : 0;
+  }
+  const int n_above = wave_total(above), nb = wave_total(inb);
+  if (nb <= 64) {
+    int off = wave_incl_scan(inb, lane) - inb;
+#pragma unroll
+    for (int i = 0; i < PL; ++i)
+      if ((key[i] >> LOW) == hi && key[i] != 0u) cbuf[off++] = key[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool valid = lane < nb;
+    const uint32_t ck = valid ? cbuf[lane] : 0u;
+#pragma unroll 1
+    for (int b = LOW - 1; b >= 0; --b) {
+      const uint32_t cand = t | (1u << b);
+      if (n_above + (int)__popcll(__ballot(valid && ck >= cand)) >= k) t = cand;
+    }
+    *gt = n_above + (int)__popcll(__ballot(valid && ck > t));
+    return t;
+  }
+#pragma unroll 1
+  for (int b = LOW - 1; b >= 0; --b) {
+    const uint32_t cand = t | (1u << b);
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
+    if (wave_total(cnt) >= k) t = cand;
+  }
+  int c2 = 0;
+#pragma unroll
+  for (int i = 0; i < PL; ++i) c2 += key[i] > t ? 1 : 0;
+  *gt = wave_total(c2);
+  return t;
+}
+
 // lo[row] = the row's k-th largest sub-score lowered by 4 ulps of the orderable key (a guard against
 // any last-bit difference between the two GEMMs), -inf when k exceeds the subset.  One wave per row;
 // m <= 64 PL, m % 4 == 0.
 template <int PL>
 __global__ __launch_bounds__(256) void topk_row_bound_kernel(const float* __restrict__ sub, const int* __restrict__ kv,
                                                            float* __restrict__ lo, long rows, int B, int m) {
+  __shared__ uint32_t cbuf[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long row = (long)blockIdx.x * 4 + w;
   if (row >= rows) return;
@@ -1029,15 +1090,8 @@ __global__ __launch_bounds__(256) void topk_row_bound_kernel(const float* __rest
     if (lane == 0) lo[row] = -INFINITY;
     return;
   }
-  uint32_t t = 0;
-#pragma unroll 1
-  for (int b = 31; b >= 0; --b) {
-    const uint32_t cand = t | (1u << b);
-    int cnt = 0;
-#pragma unroll
-    for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
-    if (wave_total(cnt) >= k) t = cand;
-  }
+  int gt;
+  const uint32_t t = wave_kth_key<PL>(key, k, lane, cbuf[w], &gt);
   if (lane == 0) lo[row] = t > 4u ? key_float(t - 4u) : -INFINITY;
 }
 
@@ -1119,13 +1173,17 @@ __global__ __launch_bounds__(256) void topk_cand_select_kernel(const float* __re
   };
   uint32_t t = 0;
   int need = 0;
-  if (k > 0) {
+  if (k > 0 && inreg) {
+    int gt;
+    t = wave_kth_key<PL>(key, k, lane, reinterpret_cast<uint32_t*>(pfx[w]), &gt);
+    need = k - gt;  // ties at t to take, lowest columns first
+  } else if (k > 0) {
 #pragma unroll 1
     for (int b = 31; b >= 0; --b) {
       const uint32_t cand = t | (1u << b);
       if (count_ge(cand, false) >= k) t = cand;
     }
-    need = k - count_ge(t, true);  // ties at t to take, lowest columns first
+    need = k - count_ge(t, true);
   }
   for (int i = lane; i < nw; i += 64) tie[i] = pick[i] = 0ull;
   wave_lds_sync();
@@ -1228,7 +1286,8 @@ int sc_topk_cand_select(const float* cval, const int* ccol, int* ccnt, const int
                         int n, int cap, int kmax, int relu, hipStream_t stream) {
   if (n % 64 || n > 64 * CS_WORDS || cap < 1) return 1;
   const long rows = (long)G * B;
-  hipLaunchKernelGGL((topk_cand_select_kernel<16>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, cval, ccol,
+  // (32 candidates per lane in registers: a bound from every 8th feature leaves ~8 k per row)
+  hipLaunchKernelGGL((topk_cand_select_kernel<32>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, cval, ccol,
                      ccnt, k, idx, val, rows, B, n, cap, kmax, relu);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
