@@ -765,6 +765,18 @@ class FusedSAEEnsemble:
         var = s2 - s1.pow(2).sum(-1) / N  # total sum of squares about the mean
         return (se / var).float(), (l0 / N).float()
 
+    def feature_frequency(self) -> torch.Tensor:
+        """Per-feature firing frequency [G, n] = feature_counts / rows_seen.  The counts are SAMPLED:
+        the encoder epilogue accumulates them only on counting steps (every ``count_every``-th step, or
+        the first step of each multi-step graph replay), and ``rows_seen`` counts exactly those steps'
+        rows -- an unbiased estimate of the frequency, not an exact "ever fired" record.  A feature
+        that fires only on unsampled steps reads 0 here; consumers that need exact dead-feature
+        counts (dead-feature resampling, ``train/huge_batch.py``) build the engine with
+        ``count_every=1``."""
+        if self.feature_counts is None:
+            raise RuntimeError("feature counting is off (track_feature_counts=False)")
+        return self.feature_counts / max(1, self.rows_seen)
+
     def loss_dicts(self, out=None):
         out = (self.out if out is None else out).detach().cpu()
         keys = ["loss", "l_reconstruction", "l_l1", "l_bias_decay", "l0"]
