@@ -71,3 +71,48 @@ def test_launch_ranks_forwards_rank0_json_and_worst_rc(tmp_path, rc, capfd, monk
         assert "noise on stdout" in err
     else:
         assert got != 0
+
+
+def _consistency_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, ROOT)
+    import bench as b
+    from sparse_coding__amd.parallel.dist import DistInfo
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    info = DistInfo(rank, world, rank, torch.device("cpu"), "gloo")
+    same = [torch.arange(6, dtype=torch.float32)]
+    diff = [torch.arange(6, dtype=torch.float32) + (0.5 if rank == 1 else 0.0)]
+    out = {"same": b._replica_delta(same, info)["max_abs_delta"], "diff": b._replica_delta(diff, info)["max_abs_delta"],
+           "bsame": b._batch_spread([torch.ones(2, 3)], info)["max_abs_spread"],
+           "bdiff": b._batch_spread([torch.ones(2, 3) * (rank + 1)], info)["max_abs_spread"]}
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_cross_rank_consistency_checks_gloo():
+    """The bench's post-run checks: max |master - rank 0's| (dp / zero1) and the spread of global-batch
+    checksums (es) are 0 for identical ranks and non-zero otherwise, on every rank."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_consistency_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert res[r]["same"] == 0.0 and res[r]["diff"] == 0.5
+        assert res[r]["bsame"] == 0.0 and res[r]["bdiff"] > 0
