@@ -3,13 +3,11 @@
 Per step, for all models at once (reference runs a Python loop over models because
 k differs, ``autoencoders/ensemble.py:100-116``; math of ``autoencoders/topk_encoder.py:19-40``):
 
-1-2. (idx, val) = top-k(x D_hat^T), ReLU   candidate top-k: the scores are never stored densely --
-                                           a GEMM over every 8th feature bounds each row's k-th
-                                           largest score from below, the full scores GEMM appends
-                                           only the scores above that bound to per-row buffers
-                                           (EPI_TOPK epilogue) and an exact select picks the top-k
-                                           among them (column order, ties to the lowest column);
-                                           per-model k on device
+1. scores = x D_hat^T                     grouped MFMA GEMM (fp32 out)
+2. (idx, val) = top-k(scores), ReLU       exact select, per-model k on device (a select fused
+                                           into the scores GEMM -- candidate append above a
+                                           sampled bound -- measured 1.51 vs 1.01 ms/step at
+                                           config 4, profiles/r5/topk_candidates/)
 3. x_hat = sum val D_hat[idx]; R = x_hat - x; code gradients <R, D_hat[idx]>
                                            one wave per row (sparse gather from L2); the
                                            previous step's dense-buffer picks are cleared here
@@ -26,7 +24,6 @@ step t clears step t-1's picks).
 
 from __future__ import annotations
 
-import os
 from typing import Optional, Union
 
 import torch
@@ -79,22 +76,7 @@ class FusedTopKEnsemble:
         self.shadow = torch.empty(G, n, d, device=dev, dtype=bf)
         self.norms = torch.ones(G, n, device=dev)
         adam_ops.shadow_rows(self.params["dict"], self.shadow, self.norms, normalize=True)
-        # candidate top-k (ops/csrc/topk.hip, EPI_TOPK): the sub-score GEMM reads every s-th dictionary
-        # row; at least k of a row's full scores reach the k-th largest sub-score, so the full GEMM
-        # appends ~ k s candidates per row instead of storing n fp32 scores (SC_TOPK_SELECT=dense: the
-        # fp32 score matrix + dense select)
-        s = self._sub_stride = 8
-        self._cand = (os.environ.get("SC_TOPK_SELECT", "cand") != "dense" and n % (128 * s) == 0
-                      and kmax <= n // s and n <= 16384)
-        if self._cand:
-            self.sub = torch.empty(G, B, n // s, device=dev)
-            self.lo = torch.empty(G, B, device=dev)
-            self.cval = torch.empty(G, B, n, device=dev)
-            self.ccol = torch.empty(G, B, n, device=dev, dtype=torch.int32)
-            self.ccnt = torch.zeros(G, B, device=dev, dtype=torch.int32)  # re-zeroed by the select
-            self.scores = None
-        else:
-            self.scores = torch.empty(G, B, n, device=dev)
+        self.scores = torch.empty(G, B, n, device=dev)
         # pick buffers, alternating per step: the decode of step t zeroes step t-1's picks in the
         # dense code / dscore buffers (no separate clear launch)
         self.idx_buf = torch.zeros(2, G, B, kmax, device=dev, dtype=torch.int32)
@@ -133,7 +115,8 @@ class FusedTopKEnsemble:
     def _step_kernels(self, x, cur: int):
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
         idx, prev = self.idx_buf[cur], self.idx_buf[1 - cur]
-        self._select(x, idx)
+        gemm_ops.matmul_nt(x, self.shadow, self.scores)
+        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val))
         topk_ops.decode_grad(idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
                              self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from)
         torch.sum(self.row_se, dim=1, out=self._se)
@@ -149,17 +132,6 @@ class FusedTopKEnsemble:
                                  shadow=self.shadow, norms=self.norms, norm=True)],
                            self.lr, self.step_count + 1, *self.betas, self.eps, step_dev=self.step_dev)
         self.step_dev.add_(1)
-
-    def _select(self, x, idx):
-        """(idx, self.val) <- each row's top-k of x D_hat^T with ReLU on the kept values."""
-        if self._cand:
-            gemm_ops.matmul_nt_rows(x, self.shadow, self.sub, self._sub_stride)
-            topk_ops.row_bound(self.sub, self.k, self.lo)
-            gemm_ops.topk_candidates(x, self.shadow, self.lo, self.cval, self.ccol, self.ccnt)
-            topk_ops.cand_select(self.cval, self.ccol, self.ccnt, self.k, self.kmax, out=(idx, self.val))
-            return
-        gemm_ops.matmul_nt(x, self.shadow, self.scores)
-        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val))
 
     def enable_graph(self, enabled: bool = True):
         """Replay the whole step from a HIP graph (one per pick-buffer parity); the batch goes

@@ -54,11 +54,6 @@ def signatures():
                          c_float, c_float, c_int, c_void_p, c_void_p, c_int, c_int],
     }
     optional = {
-        "sc_topk_row_bound": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p],
-        "sc_topk_cand_select": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                                c_int, c_int, c_void_p],
-        "sc_gemm_topk": [c_void_p, c_long, c_long, c_void_p, c_long, c_long, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
         "sc_topk_select": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                            c_void_p],
         "sc_topk_decode_grad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,

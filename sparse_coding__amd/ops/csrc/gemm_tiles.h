@@ -23,7 +23,7 @@ constexpr int PT = 128;
 // (5 was EPI_ADAM, Adam fused into the weight-gradient epilogue: measured slower than the
 // separate streaming Adam kernel and removed)
 enum { EPI_ENC = 0, EPI_DEC = 1, EPI_DC = 2, EPI_F32 = 3, EPI_BF16 = 4, EPI_ENC_CNT = 6,
-       EPI_DC_MASK = 7, EPI_ENC_ACT = 8, EPI_DC_ACT = 9, EPI_ROWMAX = 10, EPI_TOPK = 11 };
+       EPI_DC_MASK = 7, EPI_ENC_ACT = 8, EPI_DC_ACT = 9, EPI_ROWMAX = 10 };
 
 // Activity bitmask of the codes: see mask_bit() in sae_gemm_kernel.h (one 64-bit word per lane
 // per 64x64 block, written by the encoder epilogue, read by the code-gradient epilogue instead
@@ -108,15 +108,6 @@ struct GemmParams {
   int tpre[17];
   int tl[16];
   FDiv fl[16];
-  // --- EPI_TOPK: top-k candidate compaction -- the scores never reach HBM densely.  Element
-  // (row, col) with alpha * acc >= tk_lo[g M + row] (a lower bound of the row's k-th largest
-  // score) is appended to its row's buffer tk_val / tk_col [G M][tk_cap] at slots reserved by one
-  // atomic add on tk_cnt[g M + row] per (row, wave); the consumer re-zeroes tk_cnt
-  const float* tk_lo;
-  float* tk_val;
-  int* tk_col;
-  int* tk_cnt;
-  int tk_cap;
 };
 
 // LDS image of a K-major tile [128 rows][BKT k] bf16.

@@ -94,33 +94,4 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   }
 }
 
-// Top-k candidate GEMM (EPI_TOPK): scores = x D^T per group, never stored; every score >= the row's
-// lower bound lo[g M + row] is appended to the row's candidate buffer (val / col [G M][cap], count
-// cnt [G M], zero on entry).  x: [M, K] bf16 shared by the groups (sx = 0) or per group; D: [G][N][K].
-int sc_gemm_topk(const void* x, long ldx, long sx, const void* D, long ldd, long sd, const float* lo, float* val,
-                 int* col, int* cnt, int cap, int M, int N, int K, int G, int cfg, hipStream_t stream) {
-  if (M % PT || N % PT || K % 64 || G < 1 || cap < 1 || !lo || !val || !col || !cnt) return 1;
-  GemmParams p{};
-  for (int s = 0; s < 2; ++s) {
-    p.prob[0].a[s] = {reinterpret_cast<const uint16_t*>(x), ldx, sx};
-    p.prob[0].b[s] = {reinterpret_cast<const uint16_t*>(D), ldd, sd};
-    p.prob[1].a[s] = p.prob[0].a[s];
-    p.prob[1].b[s] = p.prob[0].b[s];
-  }
-  p.prob[0].c = p.prob[1].c = val;  // (unused by the epilogue)
-  p.prob[0].alpha = p.prob[1].alpha = 1.f;
-  p.nprob = 1;
-  p.M = M; p.N = N; p.K1 = K; p.K2 = 0; p.G = G;
-  p.ldc = N; p.sc = (long)M * N;
-  p.ksplit = 1;
-  p.tk_lo = lo; p.tk_val = val; p.tk_col = col; p.tk_cnt = cnt; p.tk_cap = cap;
-  int shape = cfg & 3;
-  if (shape == 0) shape = sc_gemm_shape(M, N, G, 1);
-  if (shape == 3) {
-    if (!fits<S256>(M, N)) return 6;
-    return launch_big(3, 0, EPI_TOPK, true, true, p, 1, stream);
-  }
-  return launch<S128, 64, 2>(EPI_TOPK, true, true, p, 1, stream);
-}
-
 }  // extern "C"

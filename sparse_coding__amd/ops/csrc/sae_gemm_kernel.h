@@ -590,58 +590,6 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
     if (p.dotpart) colred_store(p.dotpart, 1);
     return;
   }
-  if constexpr (EPI == EPI_TOPK) {
-    // Candidates of the per-row top-k (engine/topk.py): every score >= the row's lower bound is
-    // appended to the row's buffer.  In the MFMA layout the four lanes (lane & 15) + 16 q hold one
-    // output row of this wave; one atomic add per (row, wave) reserves their slots (inclusive scan
-    // over q by two row shuffles).  The WI reservations are issued back to back (their round trips
-    // overlap) before any candidate is written.
-    const int q = lane >> 4;
-    float lo[WI];
-    int incl[WI], cnt[WI], base[WI];
-#pragma unroll
-    for (int i = 0; i < WI; ++i) lo[i] = p.tk_lo[(long)g * p.M + rowb + i * 16];
-#pragma unroll
-    for (int i = 0; i < WI; ++i) {
-      int c = 0;
-#pragma unroll
-      for (int j = 0; j < WJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) c += alpha * acc[i][j][r] >= lo[i] ? 1 : 0;
-      cnt[i] = c;
-      int v = c;
-      int up = __shfl_up(v, 16);
-      v += q >= 1 ? up : 0;
-      up = __shfl_up(v, 32);
-      v += q >= 2 ? up : 0;
-      incl[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < WI; ++i) {
-      const int tot = __shfl(incl[i], (lane & 15) + 48);
-      base[i] = (q == 0 && tot > 0) ? atomicAdd(p.tk_cnt + (long)g * p.M + rowb + i * 16, tot) : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < WI; ++i) {
-      const long row = (long)g * p.M + rowb + i * 16;
-      int pos = __shfl(base[i], lane & 15) + incl[i] - cnt[i];
-      const long rb = row * (long)p.tk_cap;
-#pragma unroll
-      for (int j = 0; j < WJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = alpha * acc[i][j][r];
-          if (v >= lo[i]) {
-            if (pos < p.tk_cap) {
-              p.tk_val[rb + pos] = v;
-              p.tk_col[rb + pos] = colb + j * 16 + r;
-            }
-            ++pos;
-          }
-        }
-    }
-    return;
-  }
   if constexpr (EPI == EPI_ROWMAX) {
     // max over this wave's columns of each output row, then over the four 16-lane groups
     // holding the same row; one partial per (row, wave column) -> C[g][row][tn * WGN + wc]
@@ -1107,9 +1055,6 @@ int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t strea
       break;
     case EPI_ROWMAX:
       if constexpr (FULL) { if (!(ak && bk)) return 5; SC_L(true, true, EPI_ROWMAX); }
-      break;
-    case EPI_TOPK:
-      if constexpr (FULL) { if (!(ak && bk)) return 5; SC_L(true, true, EPI_TOPK); }
       break;
     case EPI_F32:
       if constexpr (FULL) {

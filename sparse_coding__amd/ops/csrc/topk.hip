@@ -989,248 +989,6 @@ __global__ __launch_bounds__(256) void topk_scatter_kernel(const int* __restrict
 }
 
 
-// ---------------------------------------------------------------------------
-// Candidate top-k (the fp32 scores never make a dense HBM round trip).
-//   1. a GEMM over a strided subset of the dictionary (every s-th feature) gives m = n / s sub-scores
-//      per row; topk_row_bound_kernel takes the k-th largest of them: at least k of the row's full
-//      scores reach it, so it is a lower bound of the row's k-th largest score;
-//   2. the full scores GEMM (EPI_TOPK epilogue, sae_gemm_kernel.h) appends only the scores >= that
-//      bound to per-row candidate buffers (~ k n / m of them);
-//   3. topk_cand_select_kernel picks the exact top-k among a row's candidates: bisection on the
-//      orderable key, ties at the threshold resolved by column index, output in column order (an
-//      LDS bitmap over the row's columns ranks the picks), independent of the buffer's (atomic)
-//      append order -- deterministic.
-__device__ __forceinline__ float key_float(uint32_t k) {  // inverse of order_key
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
-
-
-// k-th largest of a wave's keys (PL per lane; key 0 = no key): 12 bisection steps over all keys
-// (DPP wave totals), then -- when the keys sharing t's top 12 bits fit one per lane, the usual case --
-// the last 20 bits by ballots over that compacted bucket (one v_cmp + popcount per bit); otherwise the
-// full scans continue.  Returns t; *gt = number of keys > t.  cbuf: 64 words of wave-private LDS.
-template <int PL>
-__device__ __forceinline__ uint32_t wave_kth_key(const uint32_t (&key)[PL], int k, int lane, uint32_t* cbuf,
-                                                 int* gt) {
-  constexpr int S1 = 12, LOW = 32 - S1;
-  uint32_t t = 0;
-#pragma unroll 1
-  for (int b = 31; b >= LOW; --b) {
-    const uint32_t cand = t | (1u << b);
-    int cnt = 0;
-#pragma unroll
-    for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
-    if (wave_total(cnt) >= k) t = cand;
-  }
-  const uint32_t hi = t >> LOW;
-  int above = 0, inb = 0;
-#pragma unroll
-  for (int i = 0; i < PL; ++i) {
-    const uint32_t h = key[i] >> LOW;
-    above += h > hi ? 1 : 0;
-    inb += (h == hi && key[i] != 0u) ? 1 : 0;
-  }
-  const int n_above = wave_total(above), nb = wave_total(inb);
-  if (nb <= 64) {
-    int off = wave_incl_scan(inb, lane) - inb;
-#pragma unroll
-    for (int i = 0; i < PL; ++i)
-      if ((key[i] >> LOW) == hi && key[i] != 0u) cbuf[off++] = key[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const bool valid = lane < nb;
-    const uint32_t ck = valid ? cbuf[lane] : 0u;
-#pragma unroll 1
-    for (int b = LOW - 1; b >= 0; --b) {
-      const uint32_t cand = t | (1u << b);
-      if (n_above + (int)__popcll(__ballot(valid && ck >= cand)) >= k) t = cand;
-    }
-    *gt = n_above + (int)__popcll(__ballot(valid && ck > t));
-    return t;
-  }
-#pragma unroll 1
-  for (int b = LOW - 1; b >= 0; --b) {
-    const uint32_t cand = t | (1u << b);
-    int cnt = 0;
-#pragma unroll
-    for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
-    if (wave_total(cnt) >= k) t = cand;
-  }
-  int c2 = 0;
-#pragma unroll
-  for (int i = 0; i < PL; ++i) c2 += key[i] > t ? 1 : 0;
-  *gt = wave_total(c2);
-  return t;
-}
-
-// lo[row] = the row's k-th largest sub-score lowered by 4 ulps of the orderable key (a guard against
-// any last-bit difference between the two GEMMs), -inf when k exceeds the subset.  One wave per row;
-// m <= 64 PL, m % 4 == 0.
-template <int PL>
-__global__ __launch_bounds__(256) void topk_row_bound_kernel(const float* __restrict__ sub, const int* __restrict__ kv,
-                                                           float* __restrict__ lo, long rows, int B, int m) {
-  __shared__ uint32_t cbuf[4][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long row = (long)blockIdx.x * 4 + w;
-  if (row >= rows) return;
-  const int k = kv[row / B];
-  const float* S = reinterpret_cast<const float*>(__builtin_assume_aligned(sub + row * m, 16));
-  uint32_t key[PL];
-#pragma unroll
-  for (int i = 0; i < PL / 4; ++i) {
-    const int c = (i * 64 + lane) * 4;
-    const float4 v = *reinterpret_cast<const float4*>(__builtin_assume_aligned(S + (min(c, m - 4) & ~3), 16));
-    const uint32_t live = 0u - (uint32_t)(c < m);
-    const float f[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) key[4 * i + j] = order_key(f[j]) & live;
-  }
-  if (k <= 0 || k > m) {
-    if (lane == 0) lo[row] = -INFINITY;
-    return;
-  }
-  int gt;
-  const uint32_t t = wave_kth_key<PL>(key, k, lane, cbuf[w], &gt);
-  if (lane == 0) lo[row] = t > 4u ? key_float(t - 4u) : -INFINITY;
-}
-
-constexpr int CS_WORDS = 256;  // columns per row <= 64 CS_WORDS (n <= 16384)
-
-// wave-exclusive prefix over the 64-bit column words of a per-wave LDS bitmap: pfx[w] = number of set
-// bits in words [0, w).  Lane l owns a contiguous run of ceil(nw / 64) words.
-__device__ __forceinline__ void bitmap_prefix(const uint64_t* bm, int* pfx, int nw, int lane) {
-  const int per = (nw + 63) >> 6, w0 = lane * per;
-  int c = 0;
-  for (int i = 0; i < per; ++i)
-    if (w0 + i < nw) c += __popcll(bm[w0 + i]);
-  int run = wave_incl_scan(c, lane) - c;
-  for (int i = 0; i < per; ++i)
-    if (w0 + i < nw) {
-      pfx[w0 + i] = run;
-      run += __popcll(bm[w0 + i]);
-    }
-}
-
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// One wave per row: exact top-k among the row's candidates (val / col [rows][cap], count cnt[row]).
-// Up to 64 PL candidates live in registers; larger counts (degenerate rows, e.g. all-equal scores)
-// take the same steps reading the buffer from memory.  Writes (idx, val) in column order, pads
-// slots [k, kmax) with (0, 0), re-zeroes cnt[row] for the next step.
-template <int PL>
-__global__ __launch_bounds__(256) void topk_cand_select_kernel(const float* __restrict__ cval, const int* __restrict__ ccol,
-                                                             int* __restrict__ ccnt, const int* __restrict__ kv,
-                                                             int* __restrict__ idx, float* __restrict__ val, long rows,
-                                                             int B, int n, int cap, int kmax, int relu) {
-  __shared__ uint64_t bm[4][2][CS_WORDS];
-  __shared__ int pfx[4][CS_WORDS];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long row = (long)blockIdx.x * 4 + w;
-  if (row >= rows) return;  // per-wave work only: no block barrier below
-  const int kk = kv[row / B];
-  const int count = min(ccnt[row], cap);
-  const int k = max(0, min(kk, count));
-  const int nw = n >> 6;
-  const float* CV = cval + row * (long)cap;
-  const int* CC = ccol + row * (long)cap;
-  int* I = idx + row * kmax;
-  float* V = val + row * kmax;
-  uint64_t* tie = bm[w][0];
-  uint64_t* pick = bm[w][1];
-  int* pf = pfx[w];
-  const bool inreg = count <= 64 * PL;
-  uint32_t key[PL];
-  int col[PL];
-  float vv[PL];
-  if (inreg) {
-#pragma unroll
-    for (int i = 0; i < PL; ++i) {
-      const int pidx = i * 64 + lane;
-      const bool ok = pidx < count;
-      vv[i] = ok ? CV[pidx] : 0.f;
-      col[i] = ok ? CC[pidx] : 0;
-      key[i] = ok ? order_key(vv[i]) : 0u;  // 0 sorts below every real key
-    }
-  }
-  // count of keys >= cand over the row's candidates (registers or memory)
-  auto count_ge = [&](uint32_t cand, bool strict) -> int {
-    int c = 0;
-    if (inreg) {
-#pragma unroll
-      for (int i = 0; i < PL; ++i) c += (strict ? key[i] > cand : key[i] >= cand) ? 1 : 0;
-    } else {
-      for (int pidx = lane; pidx < count; pidx += 64) {
-        const uint32_t kq = order_key(CV[pidx]);
-        c += (strict ? kq > cand : kq >= cand) ? 1 : 0;
-      }
-    }
-    return wave_total(c);
-  };
-  uint32_t t = 0;
-  int need = 0;
-  if (k > 0 && inreg) {
-    int gt;
-    t = wave_kth_key<PL>(key, k, lane, reinterpret_cast<uint32_t*>(pfx[w]), &gt);
-    need = k - gt;  // ties at t to take, lowest columns first
-  } else if (k > 0) {
-#pragma unroll 1
-    for (int b = 31; b >= 0; --b) {
-      const uint32_t cand = t | (1u << b);
-      if (count_ge(cand, false) >= k) t = cand;
-    }
-    need = k - count_ge(t, true);
-  }
-  for (int i = lane; i < nw; i += 64) tie[i] = pick[i] = 0ull;
-  wave_lds_sync();
-  // ties at the threshold -> bitmap, ranked in column order
-  auto for_each = [&](auto&& fn) {
-    if (inreg) {
-#pragma unroll
-      for (int i = 0; i < PL; ++i)
-        if (i * 64 + lane < count) fn(key[i], col[i], vv[i]);
-    } else {
-      for (int pidx = lane; pidx < count; pidx += 64) {
-        const float v = CV[pidx];
-        fn(order_key(v), CC[pidx], v);
-      }
-    }
-  };
-  if (k > 0) {
-    for_each([&](uint32_t kq, int c, float) {
-      if (kq == t) atomicOr(reinterpret_cast<unsigned long long*>(tie + (c >> 6)), 1ull << (c & 63));
-    });
-    wave_lds_sync();
-    bitmap_prefix(tie, pf, nw, lane);
-    wave_lds_sync();
-    for_each([&](uint32_t kq, int c, float) {
-      const uint64_t bit = 1ull << (c & 63);
-      const bool take = kq > t || (kq == t && pf[c >> 6] + __popcll(tie[c >> 6] & (bit - 1)) < need);
-      if (take) atomicOr(reinterpret_cast<unsigned long long*>(pick + (c >> 6)), bit);
-    });
-    wave_lds_sync();
-    bitmap_prefix(pick, pf, nw, lane);
-    wave_lds_sync();
-    for_each([&](uint32_t kq, int c, float v) {
-      const uint64_t bit = 1ull << (c & 63);
-      if (pick[c >> 6] & bit) {
-        const int rank = pf[c >> 6] + __popcll(pick[c >> 6] & (bit - 1));
-        I[rank] = c;
-        V[rank] = relu ? fmaxf(v, 0.f) : v;
-      }
-    });
-  }
-  for (int j = k + lane; j < kmax; j += 64) {
-    I[j] = 0;
-    V[j] = 0.f;
-  }
-  if (lane == 0) ccnt[row] = 0;
-}
-
 }  // namespace scamd
 
 using namespace scamd;
@@ -1268,28 +1026,6 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
   SC_T(4) SC_T(8) SC_T(16) SC_T(24) SC_T(32) SC_T(48) SC_T(64)
 #undef SC_T
   return 1;
-}
-
-int sc_topk_row_bound(const float* sub, const int* k, float* lo, int G, int B, int m, hipStream_t stream) {
-  if (m % 4 || m < 4) return 1;
-  const long rows = (long)G * B;
-  dim3 grid((unsigned)((rows + 3) / 4));
-#define SC_RB(P) \
-  if (m <= 64 * P) { hipLaunchKernelGGL((topk_row_bound_kernel<P>), grid, dim3(256), 0, stream, sub, k, lo, rows, B, m); \
-    return hipGetLastError() == hipSuccess ? 0 : 3; }
-  SC_RB(4) SC_RB(8) SC_RB(16) SC_RB(32)
-#undef SC_RB
-  return 1;
-}
-
-int sc_topk_cand_select(const float* cval, const int* ccol, int* ccnt, const int* k, int* idx, float* val, int G, int B,
-                        int n, int cap, int kmax, int relu, hipStream_t stream) {
-  if (n % 64 || n > 64 * CS_WORDS || cap < 1) return 1;
-  const long rows = (long)G * B;
-  // (32 candidates per lane in registers: a bound from every 8th feature leaves ~8 k per row)
-  hipLaunchKernelGGL((topk_cand_select_kernel<32>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream, cval, ccol,
-                     ccnt, k, idx, val, rows, B, n, cap, kmax, relu);
-  return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const void* D, const void* X, long sx,

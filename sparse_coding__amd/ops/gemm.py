@@ -38,8 +38,11 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 # 128x128 blocks with the BK32 x 3-stage ring (cfg 13: 48 KB of LDS instead of 64, so one more
 # workgroup co-resides per CU) -- 0.2932 / 0.2947 vs 0.3100 / 0.3088 ms per step with BK64 x 2
 # (isolated kernel timings showed only ~1 us: the gain is in-step co-residency)
-_CFG_DEFAULT = {EPI_ENC: 13, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 13,
-                EPI_DC_MASK: 13, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
+# Round 5 (profiles/r5/batch4/): the same BK32 x 3 ring with the software-pipelined K loop (cfg bit 4:
+# 13 | 16 = 29; the next K-tile's fragments are read while the current tile's MFMAs run, three waves
+# per SIMD kept) -- step median 0.2893 vs 0.2915 ms over 4 alternating runs each on one box.
+_CFG_DEFAULT = {EPI_ENC: 29, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 29,
+                EPI_DC_MASK: 29, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
 _CFG_OVERRIDE = None
 
 
@@ -58,7 +61,8 @@ _env_cfgs()
 SHAPES = {1: (128, 128), 2: (256, 128), 3: (256, 256)}
 # cfg bits 2-3 select the K pipeline: 0 BK64 x 2-stage LDS ring (default), 1 BK32 x 4,
 # 2 BK32 x 2 (smallest LDS footprint: most co-resident blocks), 3 BK32 x 3 (the
-# alternatives exist for the step's epilogues and the weight-gradient layout only).
+# alternatives exist for the step's epilogues and the weight-gradient layout only); bit 4: the
+# software-pipelined K loop on the 128x128 BK32 rings.
 PIPES = {0: (64, 2), 1: (32, 4), 2: (32, 2), 3: (32, 3)}
 
 
@@ -380,40 +384,6 @@ def matmul_nt(a, b, out, alpha=1.0):
     epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
     _need(tuple(out.shape) == (G, M, N) and out.is_contiguous(), "out shape")
     _launch(epi, 3, M, N, K, 0, G, [_op(a, K, sa)] * 2, [_op(b, K, N * K)] * 2, [out], [alpha], N, M * N)
-
-
-def matmul_nt_rows(a, b, out, row_stride: int, alpha=1.0):
-    """out[g] = alpha * a @ b[g, ::row_stride]^T without a copy: the GEMM reads every
-    ``row_stride``-th row of ``b`` [G, N, K] (leading dimension row_stride K); a: [M, K] or [G, M, K];
-    out fp32 / bf16 [G, M, N / row_stride]."""
-    G, N, K = b.shape
-    M = a.shape[-2]
-    _bf16(a, "a"); _bf16(b, "b")
-    _need(N % row_stride == 0, f"N={N} is not a multiple of the row stride {row_stride}")
-    Ns = N // row_stride
-    sa = 0 if a.dim() == 2 else M * K
-    epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
-    _need(tuple(out.shape) == (G, M, Ns) and out.is_contiguous(), "out shape")
-    _launch(epi, 3, M, Ns, K, 0, G, [_op(a, K, sa)] * 2, [_op(b, row_stride * K, N * K)] * 2, [out], [alpha], Ns, M * Ns)
-
-
-def topk_candidates(x, w, lo, cval, ccol, ccnt, cfg=0):
-    """Top-k candidate GEMM (EPI_TOPK): scores x w[g]^T are never stored; each score >= the row's lower
-    bound ``lo`` [G, B] is appended to the row's buffers ``cval`` / ``ccol`` [G, B, cap] (count
-    ``ccnt`` [G, B] int32, zero on entry).  x: [B, d] (shared) or [G, B, d] bf16, w: [G, n, d] bf16."""
-    G, n, d = w.shape
-    B = x.shape[-2]
-    _bf16(x, "x"); _bf16(w, "w")
-    sx = _x_stride(x, B, d, G)
-    cap = cval.shape[-1]
-    _need(lo.dtype == torch.float32 and tuple(lo.shape) == (G, B) and lo.is_contiguous(), "lo fp32 [G, B]")
-    _need(cval.dtype == torch.float32 and tuple(cval.shape) == (G, B, cap) and cval.is_contiguous(), "cval")
-    _need(ccol.dtype == torch.int32 and tuple(ccol.shape) == (G, B, cap) and ccol.is_contiguous(), "ccol")
-    _need(ccnt.dtype == torch.int32 and tuple(ccnt.shape) == (G, B) and ccnt.is_contiguous(), "ccnt")
-    _need(B % TILE_M == 0 and n % TILE_N == 0 and d % TILE_K == 0, f"B={B}, n={n}, d={d} must tile 128x128x64")
-    rc = _lib.lib().sc_gemm_topk(_lib.ptr(x), d, sx, _lib.ptr(w), d, n * d, _lib.ptr(lo), _lib.ptr(cval),
-                                 _lib.ptr(ccol), _lib.ptr(ccnt), cap, B, n, d, G, int(cfg), _lib.stream_handle())
-    _lib.check(rc, "sc_gemm_topk")
 
 
 def matmul_nn(a, b, out, alpha=1.0):

@@ -34,42 +34,6 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
     return idx, val
 
 
-def row_bound(sub: torch.Tensor, k: torch.Tensor, lo: torch.Tensor):
-    """lo [G, B] fp32 <- a lower bound of each row's k-th largest score: the k-th largest of the row's
-    sub-scores ``sub`` [G, B, m] (the scores of a subset of the dictionary), lowered by 4 ulps; -inf
-    where k > m (csrc/topk.hip ``topk_row_bound_kernel``)."""
-    G, B, m = sub.shape
-    if sub.dtype != torch.float32 or not sub.is_contiguous() or m % 4:
-        raise ValueError("sub must be contiguous fp32 [G, B, m], m % 4 == 0")
-    if k.dtype != torch.int32 or k.numel() != G:
-        raise ValueError("k must be int32[G]")
-    if lo.dtype != torch.float32 or tuple(lo.shape) != (G, B) or not lo.is_contiguous():
-        raise ValueError("lo must be contiguous fp32 [G, B]")
-    rc = _lib.lib().sc_topk_row_bound(_lib.ptr(sub), _lib.ptr(k), _lib.ptr(lo), G, B, m, _lib.stream_handle())
-    _lib.check(rc, "sc_topk_row_bound")
-
-
-def cand_select(cval, ccol, ccnt, k, kmax: int, out, relu: bool = True):
-    """Exact per-row top-k among the candidates an ``EPI_TOPK`` GEMM appended (``gemm.topk_candidates``):
-    ``cval`` fp32 / ``ccol`` int32 [G, B, cap], counts ``ccnt`` int32 [G, B] (re-zeroed here).  Writes
-    ``out`` = (idx int32, val fp32) [G, B, kmax] in column order, slots >= k[g] = (0, 0); ties at the
-    threshold go to the lowest columns (csrc/topk.hip ``topk_cand_select_kernel``)."""
-    G, B, cap = cval.shape
-    idx, val = out
-    n = int(ccol.shape[-1]) if ccol.dim() == 3 else cap
-    for t, dt in ((cval, torch.float32), (ccol, torch.int32)):
-        if t.dtype != dt or tuple(t.shape) != (G, B, cap) or not t.is_contiguous():
-            raise ValueError("candidate buffers must be contiguous [G, B, cap] (fp32 values, int32 columns)")
-    if ccnt.dtype != torch.int32 or tuple(ccnt.shape) != (G, B) or not ccnt.is_contiguous():
-        raise ValueError("ccnt must be contiguous int32 [G, B]")
-    if (tuple(idx.shape) != (G, B, kmax) or tuple(val.shape) != (G, B, kmax) or idx.dtype != torch.int32
-            or val.dtype != torch.float32 or not idx.is_contiguous() or not val.is_contiguous()):
-        raise ValueError("out must be contiguous (int32, fp32) [G, B, kmax]")
-    rc = _lib.lib().sc_topk_cand_select(_lib.ptr(cval), _lib.ptr(ccol), _lib.ptr(ccnt), _lib.ptr(k), _lib.ptr(idx),
-                                        _lib.ptr(val), G, B, n, cap, kmax, int(relu), _lib.stream_handle())
-    _lib.check(rc, "sc_topk_cand_select")
-
-
 def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dscv=None, prev_idx=None,
                 dense_from: int = 0):
     """Sparse decode + residual (bf16 r_out [G, B, d]) + per-row squared error; with the dense

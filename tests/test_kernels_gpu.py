@@ -1191,60 +1191,3 @@ def test_topk_sparse_wgrad_matches_dense(out_dtype):
         picked[g, idx[g, :, : int(k[g])].reshape(-1).long()] = True
     assert float(sparse[~picked].float().abs().max()) == 0.0
 
-
-@pytest.mark.parametrize("G,B,n,d,ks", [(4, 256, 6144, 768, (8, 33, 128, 200)), (3, 128, 2048, 256, (1, 64, 256))])
-def test_topk_candidate_pipeline_matches_torch_topk(G, B, n, d, ks):
-    """Candidate top-k: the sub-score bound + EPI_TOPK candidate GEMM + candidate select
-    pick exactly torch.topk of the fp32 scores the plain GEMM computes (same kernel family, so the same
-    fp32 values), values bit-equal, column order, ties to the lowest columns; a zero row (every score
-    tied: n candidates, the memory path) and a row of duplicated features; counts re-zeroed; the fp32
-    score matrix is never materialised by the pipeline."""
-    from sparse_coding__amd.ops import gemm
-    from sparse_coding__amd.ops import topk as T
-
-    torch.manual_seed(44)
-    gen = torch.Generator(device=DEV).manual_seed(44)
-    x = _bf(B, d, gen=gen)
-    x[3] = 0  # all scores 0
-    w = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV, generator=gen), dim=-1).to(torch.bfloat16)
-    w[:, 40:48] = w[:, 8:9]  # duplicated features: tied scores at arbitrary thresholds
-    k = torch.tensor(ks, device=DEV, dtype=torch.int32)
-    kmax = max(ks)
-    scores = torch.empty(G, B, n, device=DEV)
-    gemm.matmul_nt(x, w, scores)
-    s = 8
-    sub = torch.empty(G, B, n // s, device=DEV)
-    lo = torch.empty(G, B, device=DEV)
-    cval = torch.full((G, B, n), float("nan"), device=DEV)
-    ccol = torch.full((G, B, n), -1, device=DEV, dtype=torch.int32)
-    ccnt = torch.zeros(G, B, device=DEV, dtype=torch.int32)
-    idx = torch.full((G, B, kmax), -7, device=DEV, dtype=torch.int32)
-    val = torch.full((G, B, kmax), float("nan"), device=DEV)
-    gemm.matmul_nt_rows(x, w, sub, s)
-    torch.testing.assert_close(sub, scores[:, :, ::s], rtol=0, atol=0)
-    T.row_bound(sub, k, lo)
-    gemm.topk_candidates(x, w, lo, cval, ccol, ccnt)
-    torch.cuda.synchronize()
-    counts = ccnt.clone()
-    T.cand_select(cval, ccol, ccnt, k, kmax, out=(idx, val), relu=False)
-    torch.cuda.synchronize()
-    assert int(ccnt.abs().sum()) == 0
-    for g in range(G):
-        kg = min(int(k[g]), n // s)
-        # every candidate is a real score >= the bound, and at least k of them were found
-        assert int(counts[g].min()) >= kg, (g, int(counts[g].min()))
-        assert int(counts[g, 3]) == n  # the zero row: every score ties at the bound
-        ref_v, ref_i = torch.topk(scores[g], kg, dim=-1)
-        got_i = idx[g, :, :kg].long()
-        assert got_i.diff(dim=-1).gt(0).all()  # column order, no duplicates
-        torch.testing.assert_close(val[g, :, :kg], scores[g].gather(-1, got_i), rtol=0, atol=0)
-        torch.testing.assert_close(val[g, :, :kg].sort(-1).values, ref_v.sort(-1).values, rtol=0, atol=0)
-        # the k-th value's ties go to the lowest columns (zero row: columns 0 .. k-1)
-        assert torch.equal(got_i[3], torch.arange(kg, device=DEV))
-        assert (idx[g, :, kg:] == 0).all() and (val[g, :, kg:] == 0).all()
-    # deterministic despite the atomic append order
-    gemm.topk_candidates(x, w, lo, cval, ccol, ccnt)
-    idx2, val2 = torch.empty_like(idx), torch.empty_like(val)
-    T.cand_select(cval, ccol, ccnt, k, kmax, out=(idx2, val2), relu=False)
-    torch.cuda.synchronize()
-    assert torch.equal(idx2, idx) and torch.equal(val2, val)
