@@ -15,9 +15,6 @@ struct Shape {
 using S128 = Shape<2, 2, 4, 4>;
 using S256x128 = Shape<2, 2, 8, 4>;
 using S256 = Shape<2, 4, 8, 4>;
-// 128 rows x 256 columns, 8 waves of 64x64 (the 128x128 block's per-wave tile): half the operand
-// bytes per FLOP of 128x128 on the same registers; on the BK32 x 3 ring 72 KB of LDS, two blocks per CU
-using S128x256 = Shape<2, 4, 4, 4>;
 // Partial-sum buffers (scalar parts, column parts, row-dot parts, squared-norm
 // parts) are laid out on a 128x128 sub-tile grid whatever the block shape, so the
 // consumers (loss / bias / Adam kernels) do not depend on the GEMM configuration.

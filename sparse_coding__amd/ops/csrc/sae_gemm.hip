@@ -33,8 +33,7 @@ int sc_gemm_shape(int M, int N, int G, int nprob) {
 // layout: bit0 = A is K-major, bit1 = B is K-major.
 // cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256;
 // bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4 (128x128 blocks: BK64 x 3),
-// 2: BK32 x 2, 3: BK32 x 3); bit 4: 128x128 on the BK32 rings with the software-pipelined K loop;
-// bit 5: 128x256 blocks (8 waves of 64x64) on the BK32 x 3 ring.
+// 2: BK32 x 2, 3: BK32 x 3); bit 4: 128x128 on the BK32 rings with the software-pipelined K loop.
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             const ScOperand* a /* [nprob][2] */, const ScOperand* b /* [nprob][2] */,
             void* const* c /* [nprob] */, const float* alpha /* [nprob] */, long ldc, long sc,
@@ -77,11 +76,8 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   int shape = cfg & 3;
   const int pipe = (cfg >> 2) & 3;  // 0: BK64 x 2 stages, 1: BK32 x 4, 2: BK32 x 2, 3: BK32 x 3
   const bool p32 = (cfg >> 4) & 1;  // 128x128 BK32 rings: the software-pipelined K loop
-  if (cfg & 32) {  // 128x256 blocks (8 waves of 64x64) on the BK32 x 3 ring
-    if (!fits<S128x256>(M, N)) return 6;
-    if (pipe == 3) return launch<S128x256, 32, 3, false>(epi, ak, bk, p, nprob, stream);
-    return 8;
-  }
+  // (128x256 blocks of eight 64x64 waves on the BK32 x 3 ring measured slower for the K = 512
+  // step GEMMs -- 0.2914 vs 0.2886 ms/step, profiles/r5/batch5 -- and were removed)
   if (shape == 0) shape = sc_gemm_shape(M, N, G, nprob);
   switch (shape) {
     case 3:

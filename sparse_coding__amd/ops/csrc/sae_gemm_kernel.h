@@ -130,17 +130,14 @@ constexpr int epi_scratch_floats() { return 2 * S::WGM * S::BN + S::NW; }
 // 32 banks -- a group is 16 rows at one column, and the chunk XOR alone gives only 8 distinct
 // bank pairs (2-way, measured: 64 extra cycles per wave); the half swap makes them 16.
 // ds_read_b128 serves 16-lane groups on 64 banks: 2 rows x 8 chunks, distinct with the XOR.
-constexpr int STAGE_ROW = 128;
-// the staging area starts after the epilogue's reduction scratch (epi_scratch_floats), 4 KB aligned
-template <class S>
-constexpr int stage_off() { return ((epi_scratch_floats<S>() * 4 + 4095) / 4096) * 4096; }
+constexpr int STAGE_OFF = 4096, STAGE_ROW = 128;
 template <class S>
 constexpr int stage_wave() { return S::WI * 16 * STAGE_ROW; }  // a wave's (16 WI) x 64 bf16 sub-tile
 __device__ __forceinline__ int stage_at(int row, int byte) {  // 8-byte granule of (row, byte)
   return row * STAGE_ROW + ((((byte >> 4) ^ (row >> 1)) & 7) << 4) + ((((byte >> 3) ^ row) & 1) << 3);
 }
 template <class S>
-constexpr int stage_bytes() { return stage_off<S>() + S::NW * stage_wave<S>(); }
+constexpr int stage_bytes() { return STAGE_OFF + S::NW * stage_wave<S>(); }
 
 template <class S, int EPI, bool AUX_EARLY, bool STAGE = false, bool FSTAGE = false>
 __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)[S::WI][S::WJ],
@@ -157,8 +154,8 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   const bool p1 = pi != 0;
   const int rowb = m0 + wr * (WI * 16) + (lane & 15);
   const int colb = n0 + wc * (WJ * 16) + 4 * (lane >> 4);
-  static_assert(!STAGE || ((WI == 4 || WI == 8) && WJ == 4), "stage layout");
-  char* stage = reinterpret_cast<char*>(red) + stage_off<S>() + wid * stage_wave<S>();
+  static_assert(!STAGE || ((WI == 4 || WI == 8) && WJ == 4 && 2 * S::WGM * BN + NW <= STAGE_OFF / 4), "stage layout");
+  char* stage = reinterpret_cast<char*>(red) + STAGE_OFF + wid * stage_wave<S>();
   // one 4-wide bf16 output fragment (rows rowb + 16 i, columns colb + 16 j .. +3)
   auto put = [&](uint16_t* C, int i, int j, ushort4 h) {
     if constexpr (STAGE) {
@@ -613,11 +610,9 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   }
 }
 
-// (the software-pipelined BK32 x 3 loop: three waves per SIMD, so three blocks co-reside per CU;
-// 128x256 blocks on the BK32 rings: four waves per SIMD, two blocks of eight waves per CU)
+// (the software-pipelined BK32 x 3 loop: three waves per SIMD, so three blocks co-reside per CU)
 template <class S, bool AK, bool BKM, int EPI, int BKT, int NST, bool P32 = false>
-__global__ __launch_bounds__(S::NT, (S::NW == 8 && S::WI == 4 && BKT == 32) ? 4 : (P32 && NST == 3) ? 3 : 1)
-void sae_gemm_kernel(GemmParams p) {
+__global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : 1) void sae_gemm_kernel(GemmParams p) {
   constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
   constexpr int TA = BM * BKT * 2, TBB = BN * BKT * 2;  // bytes per operand tile
   constexpr int PPWA = TA / 1024 / NW, PPWB = TBB / 1024 / NW;  // LDS-DMA pieces per wave

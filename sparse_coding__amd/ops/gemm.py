@@ -87,7 +87,7 @@ class force_shape:
 
 
 def shape_fits(cfg: int, M: int, N: int) -> bool:
-    bm, bn = (128, 256) if int(cfg) & 32 else SHAPES.get(int(cfg) & 3, (128, 128))
+    bm, bn = SHAPES.get(int(cfg) & 3, (128, 128))
     return M % bm == 0 and N % bn == 0
 
 
@@ -114,8 +114,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
-    _need(((cfg & 3) == 0 and not cfg & 32) or shape_fits(cfg, M, N),
-          f"block shape of cfg {cfg} does not tile M={M}, N={N}")
+    _need((cfg & 3) == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg & 3)} does not tile M={M}, N={N}")
     nprob = len(outs)
     A = (_lib.ScOperand * (2 * nprob))(*a_ops)
     Bo = (_lib.ScOperand * (2 * nprob))(*b_ops)
