@@ -413,14 +413,23 @@ def timed(runner, groups, info, B):
     from sparse_coding__amd.parallel.dist import all_reduce_max, barrier
 
     steps = sum(groups)
+    # (diagnostic only: device events on the current stream around the same region -- what the GPU
+    # saw from the first timed launch to the last, without the host's first-launch latency)
+    cuda = torch.cuda.is_available()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)] if cuda else None
     barrier(info)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if ev:
+        ev[0].record()
     runner.run(groups)
     runner.finish()  # work the last timed step still has in flight (cross-step pipelining)
+    if ev:
+        ev[1].record()
     torch.cuda.synchronize()
     barrier(info)
     elapsed = all_reduce_max(time.perf_counter() - t0, info)
+    runner.gpu_event_ms = (all_reduce_max(ev[0].elapsed_time(ev[1]) / 1e3, info) * 1e3 / steps) if ev else None
     return 1e3 * elapsed / steps, B * info.world_size * steps / elapsed
 
 
@@ -736,6 +745,8 @@ def main(argv=None):
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
+            "gpu_event_ms_per_step": (round(runner.gpu_event_ms, 4)
+                                      if getattr(runner, "gpu_event_ms", None) is not None else None),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_ACT_PER_S, 2),

@@ -16,7 +16,9 @@ k differs, ``autoencoders/ensemble.py:100-116``; math of ``autoencoders/topk_enc
                                            dictionary row summing its picks; the others: ONE
                                            MFMA GEMM with two K segments over the scattered
                                            (dense bf16) code / dscore
-5. Adam with the row-norm Jacobian (D_hat = dict / |dict|) + bf16 shadow, step counter on device
+5. the step tail, ONE launch (csrc/adam.hip ``sc_topk_tail``): Adam with the row-norm Jacobian
+   (D_hat = dict / |dict|) + bf16 shadow, the per-model MSE from the decode's per-row squared errors,
+   the next step's batch gather (multi-step source graphs) and the device step counter
 
 ``enable_graph()`` captures the whole step as one HIP graph (two, alternating the pick buffers:
 step t clears step t-1's picks).
@@ -24,6 +26,7 @@ step t clears step t-1's picks).
 
 from __future__ import annotations
 
+import os
 from typing import Optional, Union
 
 import torch
@@ -104,23 +107,23 @@ class FusedTopKEnsemble:
         if grad_dtype not in ("fp32", "bf16"):
             raise ValueError(f"grad_dtype must be 'fp32' or 'bf16', got {grad_dtype!r}")
         self.g = torch.empty(G, n, d, device=dev, dtype=bf if grad_dtype == "bf16" else torch.float32)
-        self._se = torch.zeros(G, device=dev)
         self.mse = torch.zeros(G, device=dev)
+        # fused tail (SC_TOPK_TAIL=0: Adam + torch reductions + counter increment as separate launches)
+        self._tail = os.environ.get("SC_TOPK_TAIL", "1") not in ("", "0") and d <= 1024
+        self._ticket = torch.zeros(adam_ops.TICKET_INTS, device=dev, dtype=torch.int32)
         self.x_static = torch.zeros(B, d, device=dev, dtype=bf)
         self.use_graph = False
         self._graphs = None
         self._src_graphs = None
 
     # ------------------------------------------------------------------ the step
-    def _step_kernels(self, x, cur: int):
+    def _step_kernels(self, x, cur: int, gather=None):
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
         idx, prev = self.idx_buf[cur], self.idx_buf[1 - cur]
         gemm_ops.matmul_nt(x, self.shadow, self.scores)
         topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val))
         topk_ops.decode_grad(idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
                              self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from)
-        torch.sum(self.row_se, dim=1, out=self._se)
-        torch.mul(self._se, 1.0 / (B * d), out=self.mse)
         alpha = 2.0 / (B * d)
         gs = self.sparse_g
         if gs:
@@ -128,10 +131,18 @@ class FusedTopKEnsemble:
             topk_ops.sparse_wgrad(self.lists, self.val, self.dscv, self.r, x, self.g[:gs], alpha)
         if gs < G:
             gemm_ops.weight_grads([[(self.codebuf[gs:], self.r[gs:]), (self.dscbuf[gs:], x)]], [self.g[gs:]], alpha)
+        if self._tail:
+            adam_ops.topk_tail(self.params["dict"], self.g, self.m["dict"], self.v["dict"], self.shadow, self.norms,
+                               self.lr, *self.betas, self.eps, self.step_dev, self.row_se, self.mse, 1.0 / (B * d),
+                               self._ticket, gather=gather)
+            return
+        torch.mul(torch.sum(self.row_se, dim=1), 1.0 / (B * d), out=self.mse)
         adam_ops.adam_rows([dict(p=self.params["dict"], g=self.g, m=self.m["dict"], v=self.v["dict"],
                                  shadow=self.shadow, norms=self.norms, norm=True)],
                            self.lr, self.step_count + 1, *self.betas, self.eps, step_dev=self.step_dev)
         self.step_dev.add_(1)
+        if gather is not None:
+            raise RuntimeError("the next-batch gather needs the fused tail")
 
     def enable_graph(self, enabled: bool = True):
         """Replay the whole step from a HIP graph (one per pick-buffer parity); the batch goes
@@ -169,9 +180,13 @@ class FusedTopKEnsemble:
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            # each step's batch: the first step's own gather kernel; later steps' rows are fetched by the
+            # previous step's tail (one launch fewer per step) when the source allows it
+            nxt = source.tail_gather(self.x_static) if (self._tail and hasattr(source, "tail_gather")) else None
             for i in range(steps):
-                source.gather(self.x_static, self.step_dev)
-                self._step_kernels(self.x_static, cur0 ^ (i & 1))
+                if i == 0 or nxt is None:
+                    source.gather(self.x_static, self.step_dev)
+                self._step_kernels(self.x_static, cur0 ^ (i & 1), gather=nxt if i + 1 < steps else None)
         return g
 
     def run_source(self, source, steps: int):

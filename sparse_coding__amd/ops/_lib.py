@@ -97,6 +97,9 @@ def signatures():
                          c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
                          c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long,
                          c_int, c_long, c_void_p, c_int, c_long, c_void_p, c_void_p],
+        "sc_topk_tail": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                         c_void_p, c_float, c_float, c_float, c_void_p, c_int, c_void_p, c_int, c_float, c_void_p,
+                         c_void_p, c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long, c_void_p],
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
         "sc_basis_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int,
                            c_void_p],

@@ -170,6 +170,45 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
     _lib.check(rc, "sc_step_tail")
 
 
+def topk_tail(p, g, m, v, shadow, norms, lr, b1, b2, eps, step_dev, row_se, mse, se_scale, ticket, gather=None):
+    """The end of a top-k step as ONE launch (csrc/adam.hip ``sc_topk_tail``): row Adam with the norm
+    Jacobian on the dictionary stack ``p`` [G, n, d] (as ``adam_rows``, bf16 shadow + row norms),
+    ``mse[g] = se_scale * sum(row_se[g])`` (row_se [G, B] per-row squared errors), the NEXT step's batch
+    fetch with ``gather`` = (ring buffer [N, d], perm int64, ep0 int32 [1], out [rows, d]), and the
+    device step counter ``step_dev`` read by every block and advanced by the last one."""
+    G, n, d = p.shape
+    gbf16 = g.dtype == torch.bfloat16
+    for name, t, want in (("p", p, torch.float32), ("m", m, torch.float32), ("v", v, torch.float32),
+                          ("g", g, torch.bfloat16 if gbf16 else torch.float32)):
+        if t.dtype != want or tuple(t.shape) != (G, n, d) or not t.is_contiguous():
+            raise ValueError(f"topk_tail tensor {name} must be contiguous {want} {(G, n, d)}")
+    if d % 256 or d > 1024:
+        raise ValueError(f"topk_tail needs d in 256..1024, a multiple of 256 (got {d})")
+    if shadow.dtype != torch.bfloat16 or shadow.numel() != G * n * d or norms.numel() != G * n:
+        raise ValueError("shadow must be bf16 [G, n, d] and norms [G, n]")
+    if (row_se.dtype != torch.float32 or row_se.dim() != 2 or row_se.shape[0] != G or not row_se.is_contiguous()
+            or mse.dtype != torch.float32 or mse.numel() != G):
+        raise ValueError("row_se must be contiguous fp32 [G, rows] and mse fp32 [G]")
+    if ticket.dtype != torch.int32 or ticket.numel() < TICKET_INTS or step_dev is None:
+        raise ValueError("ticket must be int32 and step_dev a device counter")
+    gbuf = perm = ep0 = gout = None
+    grows = row_bytes = nbuf = nperm = 0
+    if gather is not None:
+        gbuf, perm, ep0, gout = gather
+        row_bytes = gbuf.shape[-1] * gbuf.element_size()
+        if (row_bytes % 16 or gout.dtype != gbuf.dtype or gout.shape[-1] != gbuf.shape[-1] or not gout.is_contiguous()
+                or perm.dtype != torch.int64 or ep0.dtype != torch.int32):
+            raise ValueError("gather: contiguous rows of 16-byte multiples, int64 perm, int32 ep0")
+        grows, nbuf, nperm = gout.shape[0], gbuf.shape[0], perm.numel()
+    rc = _lib.lib().sc_topk_tail(
+        _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), _lib.ptr(shadow), _lib.ptr(norms), G, n, d,
+        _lib.ptr(lr), b1, b2, eps, _lib.ptr(step_dev), int(gbf16), _lib.ptr(row_se), row_se.shape[1],
+        float(se_scale), _lib.ptr(mse), _lib.ptr(ticket), _lib.ptr(gbuf), nbuf, _lib.ptr(perm), nperm,
+        _lib.ptr(ep0), _lib.ptr(gout), grows, row_bytes, _lib.stream_handle(),
+    )
+    _lib.check(rc, "sc_topk_tail")
+
+
 def bias_sq_parts(bias, bsq, parity: int):
     """bsq[parity] = per-32-column sums of bias^2 (what the step tail reads as |b|^2)."""
     G, n = bias.shape

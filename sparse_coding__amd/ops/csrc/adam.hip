@@ -362,6 +362,9 @@ struct TailArgs {
   // masked ensembles: the row-Adam blocks cover only live rows (lcomp: live-row prefix lpre[g] over
   // the models, the same for every set; compact row rc of set s -> row g n + rc - lpre[g] of model g)
   int lcomp, lG, lpre[17];
+  // top-k step tail (sc_topk_tail): the loss blocks reduce per-row squared errors instead of the SAE
+  // epilogue partials -- mse[g] = se_scale * sum_r row_se[g][r]; no bias blocks
+  const float* row_se; int se_rows; float se_scale; float* mse;
 };
 
 __device__ __forceinline__ void tail_loss(const BiasArgs& a, const TailArgs& t, int g, int par) {
@@ -396,6 +399,16 @@ __device__ __forceinline__ void tail_loss(const BiasArgs& a, const TailArgs& t, 
     o[4] = l0 / a.B;
     o[5] = bnorm;
   }
+}
+
+__device__ __forceinline__ void tail_mse(const TailArgs& t, int g) {
+  __shared__ float red[8];
+  const float* rs = t.row_se + (long)g * t.se_rows;
+  float se = 0.f;
+#pragma unroll 4
+  for (int r = threadIdx.x; r < t.se_rows; r += 256) se += rs[r];
+  se = block_sum_256(se, red);
+  if (threadIdx.x == 0) t.mse[g] = se * t.se_scale;
 }
 
 __device__ __forceinline__ void tail_bias(const BiasArgs& a, const TailArgs& t, int bx, int g, int step, int par) {
@@ -451,7 +464,8 @@ __global__ __launch_bounds__(256) void step_tail_kernel(AdamArgs a, BiasArgs b, 
   const int step = *a.step;          // completed steps before this one (t); read by every block
   const int par = step & 1;
   if (bid < t.nloss) {
-    tail_loss(b, t, bid, par);
+    if (t.row_se) tail_mse(t, bid);
+    else tail_loss(b, t, bid, par);
   } else if (bid < t.nloss + t.nbias) {
     const int k = bid - t.nloss, nb = b.n / 32;
     tail_bias(b, t, k % nb, k / nb, step, par);
@@ -613,6 +627,7 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
   t.row_vec = (int)(row_bytes / 16);
   t.nloss = G; t.nbias = G * (n / 32); t.ngather = gbuf ? (int)((grows + 3) / 4) : 0;
   t.lcomp = 0; t.lG = G;
+  t.row_se = nullptr; t.se_rows = 0; t.se_scale = 0.f; t.mse = nullptr;
   long arows = total;
   // host copy of a masked ensemble's live sizes (full-stack sets only, G <= 16): launch live rows only
   if (live_h && live && row0 == 0 && G <= 16 && rows_per_model > 0 && rows[0] == (long)G * rows_per_model &&
@@ -627,6 +642,48 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
     }
   }
   const long blocks = t.nloss + t.nbias + t.ngather + (arows + 3) / 4;
+#define SC_TAIL(NVV)                                                                                   \
+  case NVV:                                                                                            \
+    if (gbf16) hipLaunchKernelGGL((step_tail_kernel<NVV, true>), dim3(blocks), dim3(256), 0, stream, a, ba, t); \
+    else hipLaunchKernelGGL((step_tail_kernel<NVV, false>), dim3(blocks), dim3(256), 0, stream, a, ba, t);      \
+    break;
+  switch (d / 256) {
+    SC_TAIL(1) SC_TAIL(2) SC_TAIL(3) SC_TAIL(4)
+    default: return 1;
+  }
+#undef SC_TAIL
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// Top-k step tail (engine/topk.py): row Adam with the norm Jacobian over the [G n, d] dictionary stack
+// + the per-model MSE from the decode's per-row squared errors (mse[g] = se_scale sum_r row_se[g][r])
+// + the next step's batch gather (gbuf != nullptr), and the device step counter advanced by the last
+// block: one launch instead of Adam + two torch reductions + the counter increment + a gather.
+int sc_topk_tail(float* p, const void* g, float* m, float* v, void* shadow, float* norms, int G, int n, int d,
+                 const float* lr, float b1, float b2, float eps, int* step, int gbf16, const float* row_se,
+                 int se_rows, float se_scale, float* mse, int* ticket, const void* gbuf, long nbuf,
+                 const long* perm, long nperm, const int* ep0, void* gout, long grows, long row_bytes,
+                 hipStream_t stream) {
+  if (d % 256 || d > 1024 || G < 1 || n < 1 || !step || !ticket || !row_se || !mse || se_rows < 1) return 1;
+  if (gbuf && (row_bytes % 16 || nbuf < 1)) return 1;
+  AdamArgs a;
+  a.set[0] = {p, g, m, v, reinterpret_cast<uint16_t*>(shadow), norms, G * n, 1};
+  a.set[1] = a.set[0];
+  a.set[1].rows = 0;
+  a.nset = 1; a.d = d; a.rows_per_model = n; a.lr = lr;
+  a.b1 = b1; a.b2 = b2; a.eps = eps; a.bc1 = 1.f; a.bc2 = 1.f; a.step = step;
+  a.nsplit = 1; a.gstride = 0; a.row0 = 0; a.live = nullptr;
+  BiasArgs ba = {};
+  ba.step = step; ba.nmodels = G; ba.n = n;
+  TailArgs t = {};
+  t.ticket = ticket;
+  t.gbuf = reinterpret_cast<const u32x4_t*>(gbuf); t.nbuf = nbuf; t.perm = perm; t.nperm = nperm; t.ep0 = ep0;
+  t.gout = reinterpret_cast<u32x4_t*>(gout); t.grows = gbuf ? grows : 0;
+  t.row_vec = (int)(row_bytes / 16);
+  t.nloss = G; t.nbias = 0; t.ngather = gbuf ? (int)((grows + 3) / 4) : 0;
+  t.lcomp = 0; t.lG = G;
+  t.row_se = row_se; t.se_rows = se_rows; t.se_scale = se_scale; t.mse = mse;
+  const long blocks = t.nloss + t.ngather + ((long)G * n + 3) / 4;
 #define SC_TAIL(NVV)                                                                                   \
   case NVV:                                                                                            \
     if (gbf16) hipLaunchKernelGGL((step_tail_kernel<NVV, true>), dim3(blocks), dim3(256), 0, stream, a, ba, t); \

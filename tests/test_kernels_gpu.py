@@ -412,6 +412,31 @@ def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype):
         torch.testing.assert_close(mse[g], loss.detach(), rtol=1e-2, atol=1e-5)
 
 
+def test_topk_tail_matches_separate_launches():
+    """The fused top-k tail (one launch: row Adam + per-model MSE + step counter) == the separate
+    Adam launch, torch reductions and counter increment: masters, moments, shadows bit-equal over
+    three steps, MSE to fp32 rounding, the device counter advanced once per step."""
+    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
+    from sparse_coding__amd.models.topk import TopKEncoder
+
+    torch.manual_seed(23)
+    d, n, B = 768, 1024, 256
+    models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
+    fused, split = (FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3) for _ in range(2))
+    assert fused._tail
+    split._tail = False
+    for t in range(3):
+        x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
+        mf, ms = fused.step_batch(x).clone(), split.step_batch(x).clone()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(mf, ms, rtol=1e-5, atol=0)
+        assert int(fused.step_dev.item()) == int(split.step_dev.item()) == t + 1
+    for a, b in ((fused.params["dict"], split.params["dict"]), (fused.m["dict"], split.m["dict"]),
+                 (fused.v["dict"], split.v["dict"]), (fused.shadow, split.shadow), (fused.norms, split.norms)):
+        assert torch.equal(a, b)
+    assert not fused._ticket.any()  # the completion counters reset themselves
+
+
 def test_fused_topk_graph_matches_eager():
     """The two captured step graphs (alternating pick buffers: step t clears step t-1's picks
     in the dense buffers) == eager steps, bitwise, over several steps."""
