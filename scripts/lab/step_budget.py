@@ -22,10 +22,21 @@ def kind(name):
             break
     short = n.split("::")[-1][:40]
     if "sae_gemm_kernel" in name:
-        # template args carry the epilogue id: sae_gemm_kernel<S, AK, BKM, EPI, BKT, NST>
-        inside = name[name.find("<") + 1:name.rfind(">")] if "<" in name else ""
-        parts = [p.strip() for p in inside.split(",")]
-        short = "gemm epi=" + (parts[3] if len(parts) > 3 else "?") + " " + (parts[0].split("::")[-1] if parts else "")
+        # template args carry the epilogue id: sae_gemm_kernel<S, AK, BKM, EPI, BKT, NST[, P32]> with S itself a
+        # template (scamd::Shape<WGM, WGN, WI, WJ>): split at top-level commas only
+        inside = n[n.find("<") + 1:n.rfind(">")] if "<" in n else ""
+        parts, depth, cur = [], 0, ""
+        for ch in inside:
+            depth += {"<": 1, ">": -1}.get(ch, 0)
+            if ch == "," and depth == 0:
+                parts.append(cur.strip())
+                cur = ""
+            else:
+                cur += ch
+        parts.append(cur.strip())
+        shape = parts[0].split("::")[-1].replace(" ", "") if parts else "?"
+        short = f"gemm epi={parts[3] if len(parts) > 3 else '?'} {shape} bk{parts[4] if len(parts) > 4 else '?'}" \
+                f"x{parts[5] if len(parts) > 5 else '?'}{' p32' if len(parts) > 6 and parts[6] == 'true' else ''}"
     return short
 
 

@@ -3,11 +3,15 @@
 Per step, for all models at once (reference runs a Python loop over models because
 k differs, ``autoencoders/ensemble.py:100-116``; math of ``autoencoders/topk_encoder.py:19-40``):
 
-1. scores = x D_hat^T                     grouped MFMA GEMM (fp32 out)
-2. (idx, val) = top-k(scores), ReLU       exact select, per-model k on device (a select fused
-                                           into the scores GEMM -- candidate append above a
-                                           sampled bound -- measured 1.51 vs 1.01 ms/step at
-                                           config 4, profiles/r5/topk_candidates/)
+1. scores = x D_hat^T                     grouped MFMA GEMM, bf16 epilogue (fp32 accumulation)
+2. (idx, val) = top-k(scores), ReLU       per-model k on device; the picks are the fp32 top-k:
+                                           bf16 rounding is monotone, so only keys equal to the
+                                           k-th largest bf16 key are ambiguous, and those are
+                                           ranked by exact fp32 recomputes <x, D_hat[j]>
+                                           (``scores_dtype='fp32'``: the fp32 score matrix and
+                                           its select; a select fused into the scores GEMM --
+                                           candidate append above a sampled bound -- measured
+                                           1.51 vs 1.01 ms/step, profiles/r5/topk_candidates/)
 3. x_hat = sum val D_hat[idx]; R = x_hat - x; code gradients <R, D_hat[idx]>
                                            one wave per row (sparse gather from L2); the
                                            previous step's dense-buffer picks are cleared here
@@ -51,7 +55,7 @@ def auto_sparse_k(B: int, n: int, d: int, margin: float = 1.3) -> int:
 
 class FusedTopKEnsemble:
     def __init__(self, models, sig=None, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999), eps=1e-8,
-                 grad_dtype: str = "bf16", sparse_k: Union[int, str] = "auto"):
+                 grad_dtype: str = "bf16", sparse_k: Union[int, str] = "auto", scores_dtype: Optional[str] = None):
         from ..models.topk import TopKEncoder
 
         self.sig = sig or TopKEncoder
@@ -79,7 +83,11 @@ class FusedTopKEnsemble:
         self.shadow = torch.empty(G, n, d, device=dev, dtype=bf)
         self.norms = torch.ones(G, n, device=dev)
         adam_ops.shadow_rows(self.params["dict"], self.shadow, self.norms, normalize=True)
-        self.scores = torch.empty(G, B, n, device=dev)
+        # score matrix: bf16 by default (half the HBM round trip of fp32; SC_TOPK_SCORES=fp32 to compare)
+        sdt = scores_dtype or os.environ.get("SC_TOPK_SCORES", "bf16")
+        if sdt not in ("fp32", "bf16"):
+            raise ValueError(f"scores_dtype must be 'fp32' or 'bf16', got {sdt!r}")
+        self.scores = torch.empty(G, B, n, device=dev, dtype=torch.bfloat16 if sdt == "bf16" else torch.float32)
         # pick buffers, alternating per step: the decode of step t zeroes step t-1's picks in the
         # dense code / dscore buffers (no separate clear launch)
         self.idx_buf = torch.zeros(2, G, B, kmax, device=dev, dtype=torch.int32)
@@ -121,7 +129,7 @@ class FusedTopKEnsemble:
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
         idx, prev = self.idx_buf[cur], self.idx_buf[1 - cur]
         gemm_ops.matmul_nt(x, self.shadow, self.scores)
-        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val))
+        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow)
         topk_ops.decode_grad(idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
                              self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from)
         alpha = 2.0 / (B * d)
@@ -217,6 +225,7 @@ class FusedTopKEnsemble:
     def encode(self, x):
         """Dense top-k codes [G, B, n] for ``x`` [B, d] with the current dictionaries."""
         xb = x.to(self.device, torch.bfloat16).contiguous()
+        # (inference: fp32 scores, so the codes carry the GEMM's fp32 values)
         scores = torch.empty(self.n_models, x.shape[0], self.n, device=self.device)
         gemm_ops.matmul_nt(xb, self.shadow, scores)
         idx, val = topk_ops.topk_select(scores, self.k, self.kmax)

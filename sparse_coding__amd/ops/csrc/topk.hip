@@ -607,6 +607,268 @@ __global__ __launch_bounds__(256) void topk_block_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// Select on bf16 scores (the scores GEMM's bf16 epilogue: half the bytes of the fp32 score matrix
+// written and read).  Keys are the 16-bit orderable bf16 patterns.  bf16 rounding is monotone, so the
+// row's k-th largest bf16 key t is the rounding of its k-th largest fp32 score: every key > t belongs
+// to the fp32 top-k and every fp32 top-k member has a key >= t -- only the keys EQUAL to t are
+// ambiguous.  When they outnumber the slots left (and there are at most TIE_CAP of them), wave 0
+// recomputes their exact fp32 scores <x_b, D_hat[g][j]> (the GEMM's bf16 operands, fp32 accumulation)
+// and keeps the largest, ties to the lower column.  Kept values are the bf16 scores (after ReLU): the
+// precision the codes are stored in downstream.  Same bracket as topk_block_kernel (16-bit bisections);
+// more than BR_CAP keys at the bracket (heavy ties, e.g. an all-zero row) fall back to a full
+// bisection with ties taken in column order.
+__device__ __forceinline__ uint32_t order16(uint32_t h) {
+  return (h & 0x8000u) ? (~h & 0xffffu) : (h | 0x8000u);  // larger bf16 -> larger key
+}
+constexpr int TIE_CAP = 64;
+
+template <int PL>
+__device__ __forceinline__ bool bracket_select16(const uint32_t (&key)[PL], int k, int tid, int lane, int w,
+                                                 const uint16_t* S, int* I, float* V, int relu, uint32_t* mx,
+                                                 uint32_t* ckey, int* ccol, int* wsum, uint32_t* sres, int* tcol,
+                                                 float* tsc, int* tkeep, const uint16_t* Xr, const uint16_t* Dg, int d) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < PL; ++i) m = max(m, key[i]);
+  mx[tid] = m;
+  __syncthreads();
+  if (w == 0) {
+    const uint32_t a0 = mx[lane], a1 = mx[lane + 64], a2 = mx[lane + 128], a3 = mx[lane + 192];
+    uint32_t t = 0;
+#pragma unroll 1
+    for (int b = 15; b >= 0; --b) {
+      const uint32_t cand = t | (1u << b);
+      const int cnt = __popcll(__ballot(a0 >= cand)) + __popcll(__ballot(a1 >= cand)) +
+                      __popcll(__ballot(a2 >= cand)) + __popcll(__ballot(a3 >= cand));
+      if (cnt >= k) t = cand;
+    }
+    if (lane == 0) sres[0] = t;
+  }
+  __syncthreads();
+  const uint32_t lo = sres[0];
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < PL; ++i) c += key[i] >= lo ? 1 : 0;
+  const int incl = wave_incl_scan(c, lane);
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int off = incl - c, total = 0;
+#pragma unroll
+  for (int ww = 0; ww < 4; ++ww) {
+    if (ww < w) off += wsum[ww];
+    total += wsum[ww];
+  }
+  if (total > BR_CAP) return false;
+#pragma unroll
+  for (int i = 0; i < PL / 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (key[8 * i + j] >= lo) {
+        ckey[off] = key[8 * i + j];
+        ccol[off] = (i * 256 + tid) * 8 + j;
+        ++off;
+      }
+  __syncthreads();
+  if (w == 0) {
+    const int nq = (total + 63) >> 6;
+    uint32_t ck[BR_CAP / 64];
+#pragma unroll
+    for (int q = 0; q < BR_CAP / 64; ++q) ck[q] = (q < nq && q * 64 + lane < total) ? ckey[q * 64 + lane] : 0u;
+    uint32_t t = 0;
+#pragma unroll 1
+    for (int b = 15; b >= 0; --b) {
+      const uint32_t cand = t | (1u << b);
+      int cnt = 0;
+#pragma unroll
+      for (int q = 0; q < BR_CAP / 64; ++q)
+        if (q < nq) cnt += __popcll(__ballot(ck[q] >= cand));
+      if (cnt >= k) t = cand;
+    }
+    int gt = 0, nt = 0;
+#pragma unroll
+    for (int q = 0; q < BR_CAP / 64; ++q)
+      if (q < nq) {
+        gt += __popcll(__ballot(ck[q] > t));
+        nt += __popcll(__ballot(ck[q] == t && q * 64 + lane < total));
+      }
+    const int need = k - gt;
+    // ambiguous ties: exact fp32 scores of the keys equal to t, the `need` largest kept
+    const bool exact = Xr && nt > need && nt <= TIE_CAP;
+    if (exact) {
+      int e0 = 0;
+#pragma unroll
+      for (int q = 0; q < BR_CAP / 64; ++q)
+        if (q < nq) {
+          const bool eq = ck[q] == t && q * 64 + lane < total;
+          const uint64_t me = __ballot(eq);
+          if (eq) tcol[e0 + lanes_below(me)] = ccol[q * 64 + lane];
+          e0 += __popcll(me);
+        }
+      for (int e = 0; e < nt; ++e) {
+        const uint16_t* Dr = Dg + (long)tcol[e] * d;
+        float dot = 0.f;
+        for (int x = lane * 4; x < d; x += 256) {
+          const ushort4 a = *reinterpret_cast<const ushort4*>(Xr + x);
+          const ushort4 r = *reinterpret_cast<const ushort4*>(Dr + x);
+          dot += bf2f(a.x) * bf2f(r.x) + bf2f(a.y) * bf2f(r.y) + bf2f(a.z) * bf2f(r.z) + bf2f(a.w) * bf2f(r.w);
+        }
+        dot = wave_sum(dot);
+        if (lane == 0) tsc[e] = dot;
+      }
+      if (lane < nt) {
+        const float sv = tsc[lane];
+        const int cv = tcol[lane];
+        int rank = 0;
+        for (int e = 0; e < nt; ++e) {
+          const float so = tsc[e];
+          rank += (so > sv || (so == sv && tcol[e] < cv)) ? 1 : 0;
+        }
+        tkeep[lane] = rank < need ? 1 : 0;
+      }
+    }
+    int base = 0, ties = 0;
+#pragma unroll
+    for (int q = 0; q < BR_CAP / 64; ++q) {
+      if (q < nq) {
+        const uint32_t kk = ck[q];
+        const bool eq = kk == t && q * 64 + lane < total;
+        const uint64_t me = __ballot(eq);
+        const int te = ties + lanes_below(me);
+        const bool take = kk > t || (eq && (exact ? tkeep[te] != 0 : te < need));
+        const uint64_t mt = __ballot(take);
+        if (take) {
+          const int pos = base + lanes_below(mt);
+          const int col = ccol[q * 64 + lane];
+          const float sv = bf2f(S[col]);
+          I[pos] = col;
+          V[pos] = relu ? fmaxf(sv, 0.f) : sv;
+        }
+        base += __popcll(mt);
+        ties += __popcll(me);
+      }
+    }
+  }
+  return true;
+}
+
+template <int PL>
+__global__ __launch_bounds__(256) void topk_bf16_kernel(const uint16_t* __restrict__ scores, const int* __restrict__ kv,
+                                                      int* __restrict__ idx, float* __restrict__ val, int B, int n,
+                                                      int kmax, int absolute, int relu, const uint16_t* __restrict__ X,
+                                                      long sx, const uint16_t* __restrict__ D, int d) {
+  static_assert(PL % 8 == 0, "8 keys per 16-byte load");
+  __shared__ int red[2][4];
+  __shared__ int wsum[2][4];
+  __shared__ uint32_t bmx[256];
+  __shared__ uint32_t bkey[BR_CAP];
+  __shared__ int bcol[BR_CAP];
+  __shared__ int bsum[4];
+  __shared__ uint32_t bres[1];
+  __shared__ int tcol[TIE_CAP], tkeep[TIE_CAP];
+  __shared__ float tsc[TIE_CAP];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long row = blockIdx.x;
+  const int g = (int)(row / B), b = (int)(row % B);
+  const int k = min(kv[g], n);
+  const uint16_t* S = scores + row * n;
+  int* I = idx + row * kmax;
+  float* V = val + row * kmax;
+  uint32_t key[PL];
+#pragma unroll
+  for (int i = 0; i < PL / 8; ++i) {
+    const int c = (i * 256 + tid) * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(S + (min(c, n - 8) & ~7));
+    const uint32_t live = 0u - (uint32_t)(c < n);
+    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t h = (wv[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+      key[8 * i + j] = order16(absolute ? (h & 0x7fffu) : h) & live;
+    }
+  }
+  const uint16_t* Xr = X ? X + (long)g * sx + (long)b * d : nullptr;
+  const uint16_t* Dg = D ? D + (long)g * n * d : nullptr;
+  bool done = false;
+  if (k > 0 && k <= 256)
+    done = bracket_select16<PL>(key, k, tid, lane, w, S, I, V, relu, bmx, bkey, bcol, bsum, bres, tcol, tsc, tkeep,
+                                absolute ? nullptr : Xr, Dg, d);
+  int par = 0;
+  auto block_total = [&](int c) {
+    c = wave_total(c);
+    if (lane == 0) red[par][w] = c;
+    __syncthreads();
+    const int tot = red[par][0] + red[par][1] + red[par][2] + red[par][3];
+    par ^= 1;
+    return tot;
+  };
+  if (k > 0 && !done) {  // full 16-bit bisection; ties at the threshold in column order
+    uint32_t t = 0;
+#pragma unroll 1
+    for (int bb = 15; bb >= 0; --bb) {
+      const uint32_t cand = t | (1u << bb);
+      int cnt = 0;
+#pragma unroll
+      for (int i = 0; i < PL; ++i) cnt += key[i] >= cand ? 1 : 0;
+      if (block_total(cnt) >= k) t = cand;
+    }
+    int c2 = 0;
+#pragma unroll
+    for (int i = 0; i < PL; ++i) c2 += key[i] > t ? 1 : 0;
+    const int need_ties = k - block_total(c2);
+    int base = 0, ties_seen = 0;
+#pragma unroll
+    for (int i = 0; i < PL / 8; ++i) {
+      int neq = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) neq += key[8 * i + j] == t ? 1 : 0;
+      const int ie = wave_incl_scan(neq, lane);
+      if (lane == 63) wsum[par][w] = ie;
+      __syncthreads();
+      int tie_rank = ties_seen + ie - neq, tie_tot = 0;
+      for (int ww = 0; ww < 4; ++ww) {
+        if (ww < w) tie_rank += wsum[par][ww];
+        tie_tot += wsum[par][ww];
+      }
+      par ^= 1;
+      bool take[8];
+      int ns = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t kk = key[8 * i + j];
+        take[j] = kk > t || (kk == t && tie_rank < need_ties);
+        tie_rank += kk == t ? 1 : 0;
+        ns += take[j] ? 1 : 0;
+      }
+      const int is = wave_incl_scan(ns, lane);
+      if (lane == 63) wsum[par][w] = is;
+      __syncthreads();
+      int pos = base + is - ns, tot = 0;
+      for (int ww = 0; ww < 4; ++ww) {
+        if (ww < w) pos += wsum[par][ww];
+        tot += wsum[par][ww];
+      }
+      par ^= 1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (take[j]) {
+          const int c = (i * 256 + tid) * 8 + j;
+          const float sv = bf2f(S[c]);
+          I[pos] = c;
+          V[pos] = relu ? fmaxf(sv, 0.f) : sv;
+          ++pos;
+        }
+      }
+      base += tot;
+      ties_seen += tie_tot;
+    }
+  }
+  for (int j = k + tid; j < kmax; j += 256) {
+    I[j] = 0;
+    V[j] = 0.f;
+  }
+}
+
 // One wave per (model, row).  D: [G][n][d] bf16 normalised dictionary (gathered rows).
 // Decode gathers the k dictionary rows four at a time (indices and values are
 // wave-uniform scalar loads issued ahead of the row loads).  The k code gradients
@@ -1025,6 +1287,25 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   SC_T(4) SC_T(8) SC_T(16) SC_T(24) SC_T(32) SC_T(48) SC_T(64)
 #undef SC_T
+  return 1;
+}
+
+// Per-row top-k of bf16 scores [G][B][n] (see topk_bf16_kernel).  X ([B][d], or [G][B][d] with sx = B d)
+// and D ([G][n][d]) are the scores GEMM's bf16 operands, read to resolve ambiguous ties exactly (null:
+// ties in column order); absolute = select by |score| (no exact tie resolution).
+int sc_topk_select_bf16(const void* scores, const int* k, int* idx, float* val, int G, int B, int n, int kmax,
+                        int absolute, int relu, const void* X, long sx, const void* D, int d, hipStream_t stream) {
+  if (n % 8 || n < 8 || kmax < 1 || (X && (!D || d % 4 || d < 4))) return 1;
+  dim3 grid((unsigned)G * B);
+  const uint16_t* S = reinterpret_cast<const uint16_t*>(scores);
+  const uint16_t* Xp = reinterpret_cast<const uint16_t*>(X);
+  const uint16_t* Dp = reinterpret_cast<const uint16_t*>(D);
+#define SC_B16(P) \
+  if (n <= 256 * P) { hipLaunchKernelGGL((topk_bf16_kernel<P>), grid, dim3(256), 0, stream, S, k, idx, val, B, n, kmax, \
+                                         absolute, relu, Xp, sx, Dp, d); \
+    return hipGetLastError() == hipSuccess ? 0 : 3; }
+  SC_B16(8) SC_B16(16) SC_B16(24) SC_B16(32) SC_B16(48) SC_B16(64)
+#undef SC_B16
   return 1;
 }
 

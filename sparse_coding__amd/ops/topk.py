@@ -8,16 +8,23 @@ from . import _lib
 
 
 def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool = False, relu: bool = True,
-                out=None):
-    """Per-row top-k of ``scores`` [G, B, n] fp32 with per-model ``k`` (int32 [G]).
+                out=None, x: torch.Tensor = None, D: torch.Tensor = None):
+    """Per-row top-k of ``scores`` [G, B, n] (fp32, or bf16) with per-model ``k`` (int32 [G]).
 
     Returns (idx int32 [G, B, kmax], val fp32 [G, B, kmax]); slots >= k[g] are (0, 0.0).
     ``absolute`` selects by |score| (PCA-style) and keeps the signed value; ``relu``
     clamps kept values at 0 (TopKEncoder semantics).  ``out``: optional (idx, val) to fill
-    (contiguous, e.g. a model slice of larger buffers)."""
+    (contiguous, e.g. a model slice of larger buffers).
+
+    bf16 scores (the scores GEMM's bf16 epilogue): the picks are the fp32 top-k of the scores the
+    GEMM accumulated -- bf16 rounding is monotone, so only keys equal to the k-th largest bf16 key
+    are ambiguous, and with ``x`` ([B, d] or [G, B, d] bf16) and ``D`` ([G, n, d] bf16, the GEMM's
+    operands) those are ranked by their exact fp32 scores (ties to the lower column; without them,
+    or beyond 64 such keys, by column).  Values are the bf16 scores."""
     G, B, n = scores.shape
-    if scores.dtype != torch.float32 or not scores.is_contiguous():
-        raise ValueError("scores must be contiguous fp32")
+    bf = scores.dtype == torch.bfloat16
+    if scores.dtype not in (torch.float32, torch.bfloat16) or not scores.is_contiguous():
+        raise ValueError("scores must be contiguous fp32 or bf16")
     if k.dtype != torch.int32 or k.numel() != G:
         raise ValueError("k must be int32[G]")
     if out is not None:
@@ -28,6 +35,21 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
     else:
         idx = torch.empty(G, B, kmax, device=scores.device, dtype=torch.int32)
         val = torch.empty(G, B, kmax, device=scores.device, dtype=torch.float32)
+    if bf:
+        sx = d = 0
+        if x is not None:
+            if D is None or D.dtype != torch.bfloat16 or tuple(D.shape[:2]) != (G, n) or not D.is_contiguous():
+                raise ValueError("D must be contiguous bf16 [G, n, d] with x")
+            d = D.shape[2]
+            if (x.dtype != torch.bfloat16 or not x.is_contiguous() or x.shape[-1] != d
+                    or tuple(x.shape[:-1]) not in ((B,), (G, B))):
+                raise ValueError("x must be contiguous bf16 [B, d] or [G, B, d]")
+            sx = B * d if x.dim() == 3 else 0
+        rc = _lib.lib().sc_topk_select_bf16(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n,
+                                            kmax, int(absolute), int(relu), _lib.ptr(x), sx,
+                                            _lib.ptr(D if x is not None else None), d, _lib.stream_handle())
+        _lib.check(rc, "sc_topk_select_bf16")
+        return idx, val
     rc = _lib.lib().sc_topk_select(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n, kmax,
                                    int(absolute), int(relu), _lib.stream_handle())
     _lib.check(rc, "sc_topk_select")

@@ -335,6 +335,59 @@ def test_topk_select_exact(n):
     torch.testing.assert_close(va[2].abs().sort(-1).values, ref)
 
 
+@pytest.mark.parametrize("n", [6144, 1024])
+def test_topk_select_bf16_picks_are_fp32_topk(n):
+    """Select on the scores GEMM's bf16 output: the picks are the top-k of the fp32 scores the GEMM
+    accumulated (bf16 ties at the threshold ranked by exact recomputes from x and D), the values
+    are the bf16 scores; clustered near-equal scores, duplicated atoms and an all-zero row (heavy
+    ties: full-bisection fallback, column order)."""
+    from sparse_coding__amd.ops import gemm as gemm_ops
+    from sparse_coding__amd.ops import topk as T
+
+    torch.manual_seed(9)
+    G, B, d = 3, 128, 768
+    D = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1)
+    # model 0: 40 atoms within bf16 resolution of atom 100 -> their scores cluster on rows aligned with it
+    D[0, 100:140] = D[0, 100] + 2e-3 * torch.randn(40, d, device=DEV)
+    D[1, 7] = D[1, 5]  # a duplicated atom: exactly equal scores, the lower column first
+    D = D.to(torch.bfloat16).contiguous()
+    x = torch.randn(B, d, device=DEV)
+    x[:32] += 10.0 * D[0, 100].float()
+    x[40] = 0.0  # every score zero
+    x = x.to(torch.bfloat16).contiguous()
+    sb = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
+    gemm_ops.matmul_nt(x, D, sb)
+    exact = torch.einsum("bd,gnd->gbn", x.double(), D.double())
+    k = torch.tensor([8, 64, 128], device=DEV, dtype=torch.int32)
+    idx, val = T.topk_select(sb, k, 128, x=x, D=D)
+    torch.cuda.synchronize()
+    tol = 1e-5 * exact.abs().amax().item()
+    nres = 0
+    for g in range(G):
+        kg = int(k[g])
+        pick = idx[g, :, :kg].long()
+        assert pick.sort(-1).values.diff(dim=-1).gt(0).all()  # no duplicates
+        assert (idx[g, :, kg:] == 0).all() and (val[g, :, kg:] == 0).all()
+        assert torch.equal(val[g, :, :kg], sb[g].gather(-1, pick).float().clamp(min=0))
+        e = exact[g]
+        kth = e.topk(kg, dim=-1).values[:, -1:]
+        got = e.gather(-1, pick)
+        mask = torch.ones_like(e, dtype=torch.bool).scatter_(-1, pick, False)
+        rows = torch.arange(B, device=DEV) != 40
+        assert (got[rows] >= kth[rows] - tol).all()  # every pick is in the fp32 top-k ...
+        assert (e[rows].masked_fill(~mask[rows], -1e30) <= kth[rows] + tol).all()  # ... and nothing above it left out
+        # rows whose bf16 threshold key has more ties than slots left: the exact path ranked them
+        sf = sb[g].float()
+        kb = sf.topk(kg, dim=-1).values[:, -1:]
+        nres += int(((sf == kb).sum(-1) > kg - (sf > kb).sum(-1))[rows].sum())
+    assert nres > 0  # the clustered rows exercise the exact tie resolution
+    assert set(idx[0, 40, :8].tolist()) == set(range(8))  # all-zero row: ties by column
+    has5, has7 = (idx[1, :, :64] == 5).any(-1), (idx[1, :, :64] == 7).any(-1)
+    assert not (has7 & ~has5).any()  # equal exact scores: the lower column first
+    idx2, val2 = T.topk_select(sb, k, 128, x=x, D=D)
+    assert torch.equal(idx2, idx) and torch.equal(val2, val)  # deterministic
+
+
 def test_topk_scatter_and_clear_roundtrip():
     from sparse_coding__amd.ops import topk as T
 
