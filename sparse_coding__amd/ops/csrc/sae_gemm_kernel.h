@@ -1036,7 +1036,9 @@ int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t strea
   }
   const dim3 grid((unsigned)((comp ? comp * nprob : n_blocks<S>(p.M, p.N, p.G, nprob)) * p.ksplit)), block(S::NT);
   if constexpr (!FULL) {
-    if (epi == EPI_BF16 || epi >= EPI_ENC_ACT || (epi == EPI_F32 && (ak || bk))) return 8;
+    // (the BK32 rings: the fused step epilogues, the fp32 weight-gradient layout and the bf16 plain
+    // epilogue in the top-k layouts -- scores x D^T, codes^T R)
+    if (epi >= EPI_ENC_ACT || (epi == EPI_F32 && (ak || bk)) || (epi == EPI_BF16 && ak != bk)) return 8;
   }
 #define SC_L(AKV, BKV, E) hipLaunchKernelGGL((sae_gemm_kernel<S, AKV, BKV, E, BKT, NST, P32>), grid, block, 0, stream, p)
   // Only the (layout, epilogue) pairs the engine uses are instantiated for the fused
@@ -1071,6 +1073,9 @@ int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t strea
         if (ak && bk) SC_L(true, true, EPI_BF16);
         else if (ak) SC_L(true, false, EPI_BF16);
         else if (bk) SC_L(false, true, EPI_BF16);
+        else SC_L(false, false, EPI_BF16);
+      } else {
+        if (ak) SC_L(true, true, EPI_BF16);
         else SC_L(false, false, EPI_BF16);
       }
       break;

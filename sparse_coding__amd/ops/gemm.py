@@ -44,17 +44,24 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 _CFG_DEFAULT = {EPI_ENC: 29, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 29,
                 EPI_DC_MASK: 29, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
 _CFG_OVERRIDE = None
+_CFG_LAYOUT = {}  # (epi, operand layout) -> cfg: overrides _CFG_DEFAULT for that layout only
 
 
 def _env_cfgs():
-    """``SC_GEMM_CFG="epi:cfg,..."`` (e.g. ``0:13,6:13,7:13``) overrides per-epilogue defaults -- for
-    same-box A/B runs of whole steps (scripts/gemm_lab.py times the kernels in isolation)."""
+    """``SC_GEMM_CFG="epi:cfg,..."`` (e.g. ``0:13,6:13,7:13``) overrides per-epilogue defaults, and
+    ``epi/layout:cfg`` (e.g. ``4/3:29``) one operand layout of an epilogue only (bit 0: A K-major,
+    bit 1: B K-major) -- for same-box A/B runs of whole steps (scripts/gemm_lab.py times the kernels
+    in isolation)."""
     import os
 
     spec = os.environ.get("SC_GEMM_CFG", "").strip()
     for item in filter(None, spec.split(",")):
-        epi, cfg = item.split(":")
-        _CFG_DEFAULT[int(epi)] = int(cfg)
+        key, cfg = item.split(":")
+        if "/" in key:
+            epi, layout = key.split("/")
+            _CFG_LAYOUT[(int(epi), int(layout))] = int(cfg)
+        else:
+            _CFG_DEFAULT[int(key)] = int(cfg)
 
 
 _env_cfgs()
@@ -113,7 +120,9 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
             nact_k=None, nact_host=None):
     _need(M % TILE_M == 0 and N % TILE_N == 0, f"M={M}, N={N} must be multiples of 128")
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
-    cfg = int(cfg if cfg is not None else (_CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_DEFAULT[epi]))
+    if cfg is None:
+        cfg = _CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_LAYOUT.get((epi, layout), _CFG_DEFAULT[epi])
+    cfg = int(cfg)
     _need((cfg & 3) == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg & 3)} does not tile M={M}, N={N}")
     nprob = len(outs)
     A = (_lib.ScOperand * (2 * nprob))(*a_ops)

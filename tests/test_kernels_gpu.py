@@ -153,6 +153,26 @@ def _sae_epilogues(G, B, d, n):
     _close(gt, gd + ge, rtol=1e-3, atol=1e-6)
 
 
+@pytest.mark.parametrize("cfg", [1 | 2 << 2, 1 | 3 << 2, 1 | 2 << 2 | 16, 1 | 3 << 2 | 16])
+def test_bf16_epilogue_on_bk32_rings(cfg):
+    """The plain bf16 epilogue on the 128x128 BK32 rings in the two top-k layouts: scores x D^T (both
+    operands K-major) and the two-segment weight gradient codes^T R + dscore^T x (both M/N-major)."""
+    from sparse_coding__amd.ops import gemm
+
+    torch.manual_seed(21)
+    G, B, n, d = 2, 256, 512, 768
+    x, D = _bf(B, d), _bf(G, n, d)
+    c, r, s = _bf(G, B, n), _bf(G, B, d), _bf(G, B, n)
+    out = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
+    g = torch.empty(G, n, d, device=DEV, dtype=torch.bfloat16)
+    with gemm.force_shape(cfg):
+        gemm.matmul_nt(x, D, out)
+        gemm.weight_grads([[(c, r), (s, x)]], [g], 0.5)
+    _close(out, x.float() @ D.float().transpose(1, 2), rtol=1e-2, atol=1e-2)
+    ref = 0.5 * (c.float().transpose(1, 2) @ r.float() + s.float().transpose(1, 2) @ x.float())
+    _close(g, ref, rtol=1e-2, atol=1e-2)
+
+
 def test_adam_rows_matches_autograd():
     from sparse_coding__amd.ops import adam as adam_ops
 
