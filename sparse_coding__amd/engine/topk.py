@@ -3,11 +3,8 @@
 Per step, for all models at once (reference runs a Python loop over models because
 k differs, ``autoencoders/ensemble.py:100-116``; math of ``autoencoders/topk_encoder.py:19-40``):
 
-1. scores = x D_hat^T                     grouped MFMA GEMM, bf16 epilogue (fp32 accumulation) that
-                                           also writes each row's maximum per 32-column group
-2. (idx, val) = top-k(scores), ReLU       per-model k on device; the k-th largest group maximum
-                                           bounds the k-th score, so only groups reaching it are
-                                           read (k = 8: ~1/20 of the row); the picks are the fp32 top-k:
+1. scores = x D_hat^T                     grouped MFMA GEMM, bf16 epilogue (fp32 accumulation)
+2. (idx, val) = top-k(scores), ReLU       per-model k on device; the picks are the fp32 top-k:
                                            bf16 rounding is monotone, so only keys equal to the
                                            k-th largest bf16 key are ambiguous, and those are
                                            ranked by exact fp32 recomputes <x, D_hat[j]>
@@ -91,11 +88,6 @@ class FusedTopKEnsemble:
         if sdt not in ("fp32", "bf16"):
             raise ValueError(f"scores_dtype must be 'fp32' or 'bf16', got {sdt!r}")
         self.scores = torch.empty(G, B, n, device=dev, dtype=torch.bfloat16 if sdt == "bf16" else torch.float32)
-        # the scores epilogue's per-32-column row maxima: the select reads only the groups that can hold a
-        # pick (SC_TOPK_GROUPMAX=0: it brackets every whole row itself)
-        self.gmax = (torch.empty(G, B, n // 32, device=dev, dtype=torch.bfloat16)
-                     if sdt == "bf16" and n % 32 == 0 and n <= 8192
-                     and os.environ.get("SC_TOPK_GROUPMAX", "1") not in ("", "0") else None)
         # pick buffers, alternating per step: the decode of step t zeroes step t-1's picks in the
         # dense code / dscore buffers (no separate clear launch)
         self.idx_buf = torch.zeros(2, G, B, kmax, device=dev, dtype=torch.int32)
@@ -136,9 +128,8 @@ class FusedTopKEnsemble:
     def _step_kernels(self, x, cur: int, gather=None):
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
         idx, prev = self.idx_buf[cur], self.idx_buf[1 - cur]
-        gemm_ops.matmul_nt(x, self.shadow, self.scores, group_max=self.gmax)
-        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow,
-                             group_max=self.gmax)
+        gemm_ops.matmul_nt(x, self.shadow, self.scores)
+        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow)
         topk_ops.decode_grad(idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
                              self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from)
         alpha = 2.0 / (B * d)

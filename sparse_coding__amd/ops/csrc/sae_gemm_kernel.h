@@ -273,33 +273,15 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   }
   if constexpr (EPI == EPI_BF16) {
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
-    // optional (p.part set: the top-k scores GEMM): per output row and 32-column group the largest
-    // bf16 output, [G][M][N/32] bf16 bits -- bf16 rounding is monotone, so it is the rounded maximum
-    // of the fp32 scores; the select reads these instead of bracketing the whole row itself
-    uint16_t* GM = p.part ? reinterpret_cast<uint16_t*>(p.part) + (long)g * p.M * (p.N / 32) : nullptr;
 #pragma unroll
-    for (int i = 0; i < WI; ++i) {
-      float gmx[WJ / 2];
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
       for (int j = 0; j < WJ; ++j) {
         ushort4 h;
         h.x = f2bf(alpha * acc[i][j][0]); h.y = f2bf(alpha * acc[i][j][1]);
         h.z = f2bf(alpha * acc[i][j][2]); h.w = f2bf(alpha * acc[i][j][3]);
         put(C, i, j, h);
-        const float m = fmaxf(fmaxf(bf2f(h.x), bf2f(h.y)), fmaxf(bf2f(h.z), bf2f(h.w)));
-        gmx[j / 2] = (j & 1) ? fmaxf(gmx[j / 2], m) : m;
       }
-      if (GM) {  // (block-uniform) the 4 lanes holding a row's 16-column fragment: lanes l ^ 16, l ^ 32
-#pragma unroll
-        for (int q = 0; q < WJ / 2; ++q) {
-          float m = gmx[q];
-          m = fmaxf(m, __shfl_xor(m, 16, 64));
-          m = fmaxf(m, __shfl_xor(m, 32, 64));
-          if ((lane >> 4) == 0)
-            GM[(long)(rowb + i * 16) * (p.N / 32) + (n0 + wc * (WJ * 16) + q * 32) / 32] = f2bf(m);
-        }
-      }
-    }
     flush(C);
     return;
   }

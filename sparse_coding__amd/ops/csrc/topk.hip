@@ -623,106 +623,6 @@ __device__ __forceinline__ uint32_t order16(uint32_t h) {
 }
 constexpr int TIE_CAP = 64;
 
-// Wave 0: the exact top-k among `total` candidate keys parked in LDS (ckey / ccol; every key > the
-// threshold and every key equal to it is among them): 16-bit bisection, exact fp32 ranking of
-// ambiguous threshold ties (see above), output in candidate order.
-__device__ __forceinline__ void finish16(int k, int lane, int total, const uint16_t* S, int* I, float* V, int relu,
-                                         const uint32_t* ckey, const int* ccol, int* tcol, float* tsc, int* tkeep,
-                                         const uint16_t* Xr, const uint16_t* Dg, int d) {
-  const int nq = (total + 63) >> 6;
-  uint32_t ck[BR_CAP / 64];
-#pragma unroll
-  for (int q = 0; q < BR_CAP / 64; ++q) ck[q] = (q < nq && q * 64 + lane < total) ? ckey[q * 64 + lane] : 0u;
-  uint32_t t = 0;
-#pragma unroll 1
-  for (int b = 15; b >= 0; --b) {
-    const uint32_t cand = t | (1u << b);
-    int cnt = 0;
-#pragma unroll
-    for (int q = 0; q < BR_CAP / 64; ++q)
-      if (q < nq) cnt += __popcll(__ballot(ck[q] >= cand));
-    if (cnt >= k) t = cand;
-  }
-  int gt = 0, nt = 0;
-#pragma unroll
-  for (int q = 0; q < BR_CAP / 64; ++q)
-    if (q < nq) {
-      gt += __popcll(__ballot(ck[q] > t));
-      nt += __popcll(__ballot(ck[q] == t && q * 64 + lane < total));
-    }
-  const int need = k - gt;
-  // ambiguous ties: exact fp32 scores of the keys equal to t, the `need` largest kept
-  const bool exact = Xr && nt > need && nt <= TIE_CAP;
-  if (exact) {
-    int e0 = 0;
-#pragma unroll
-    for (int q = 0; q < BR_CAP / 64; ++q)
-      if (q < nq) {
-        const bool eq = ck[q] == t && q * 64 + lane < total;
-        const uint64_t me = __ballot(eq);
-        if (eq) tcol[e0 + lanes_below(me)] = ccol[q * 64 + lane];
-        e0 += __popcll(me);
-      }
-    for (int e = 0; e < nt; ++e) {
-      const uint16_t* Dr = Dg + (long)tcol[e] * d;
-      float dot = 0.f;
-      for (int x = lane * 4; x < d; x += 256) {
-        const ushort4 a = *reinterpret_cast<const ushort4*>(Xr + x);
-        const ushort4 r = *reinterpret_cast<const ushort4*>(Dr + x);
-        dot += bf2f(a.x) * bf2f(r.x) + bf2f(a.y) * bf2f(r.y) + bf2f(a.z) * bf2f(r.z) + bf2f(a.w) * bf2f(r.w);
-      }
-      dot = wave_sum(dot);
-      if (lane == 0) tsc[e] = dot;
-    }
-    if (lane < nt) {
-      const float sv = tsc[lane];
-      const int cv = tcol[lane];
-      int rank = 0;
-      for (int e = 0; e < nt; ++e) {
-        const float so = tsc[e];
-        rank += (so > sv || (so == sv && tcol[e] < cv)) ? 1 : 0;
-      }
-      tkeep[lane] = rank < need ? 1 : 0;
-    }
-  }
-  int base = 0, ties = 0;
-#pragma unroll
-  for (int q = 0; q < BR_CAP / 64; ++q) {
-    if (q < nq) {
-      const uint32_t kk = ck[q];
-      const bool eq = kk == t && q * 64 + lane < total;
-      const uint64_t me = __ballot(eq);
-      const int te = ties + lanes_below(me);
-      const bool take = kk > t || (eq && (exact ? tkeep[te] != 0 : te < need));
-      const uint64_t mt = __ballot(take);
-      if (take) {
-        const int pos = base + lanes_below(mt);
-        const int col = ccol[q * 64 + lane];
-        const float sv = bf2f(S[col]);
-        I[pos] = col;
-        V[pos] = relu ? fmaxf(sv, 0.f) : sv;
-      }
-      base += __popcll(mt);
-      ties += __popcll(me);
-    }
-  }
-}
-
-// Wave 0: the k-th largest of the 256 keys in mx (a lower bound lo of the row's k-th largest key when
-// each is the maximum of a disjoint set of keys: at least k keys reach it).
-__device__ __forceinline__ uint32_t kth_of_256(const uint32_t* mx, int k, int lane) {
-  const uint32_t a0 = mx[lane], a1 = mx[lane + 64], a2 = mx[lane + 128], a3 = mx[lane + 192];
-  uint32_t t = 0;
-#pragma unroll 1
-  for (int b = 15; b >= 0; --b) {
-    const uint32_t cand = t | (1u << b);
-    const int cnt = __popcll(__ballot(a0 >= cand)) + __popcll(__ballot(a1 >= cand)) +
-                    __popcll(__ballot(a2 >= cand)) + __popcll(__ballot(a3 >= cand));
-    if (cnt >= k) t = cand;
-  }
-  return t;
-}
-
 template <int PL>
 __device__ __forceinline__ bool bracket_select16(const uint32_t (&key)[PL], int k, int tid, int lane, int w,
                                                  const uint16_t* S, int* I, float* V, int relu, uint32_t* mx,
@@ -734,7 +634,15 @@ __device__ __forceinline__ bool bracket_select16(const uint32_t (&key)[PL], int 
   mx[tid] = m;
   __syncthreads();
   if (w == 0) {
-    const uint32_t t = kth_of_256(mx, k, lane);
+    const uint32_t a0 = mx[lane], a1 = mx[lane + 64], a2 = mx[lane + 128], a3 = mx[lane + 192];
+    uint32_t t = 0;
+#pragma unroll 1
+    for (int b = 15; b >= 0; --b) {
+      const uint32_t cand = t | (1u << b);
+      const int cnt = __popcll(__ballot(a0 >= cand)) + __popcll(__ballot(a1 >= cand)) +
+                      __popcll(__ballot(a2 >= cand)) + __popcll(__ballot(a3 >= cand));
+      if (cnt >= k) t = cand;
+    }
     if (lane == 0) sres[0] = t;
   }
   __syncthreads();
@@ -762,82 +670,85 @@ __device__ __forceinline__ bool bracket_select16(const uint32_t (&key)[PL], int 
         ++off;
       }
   __syncthreads();
-  if (w == 0) finish16(k, lane, total, S, I, V, relu, ckey, ccol, tcol, tsc, tkeep, Xr, Dg, d);
-  return true;
-}
-
-// Candidates from the scores GEMM's row-group maxima (GM: the largest bf16 score of each 32-column
-// group, ng = n / 32 <= 256 groups): the k-th largest group maximum lo bounds the row's k-th largest
-// key from below, and only the groups whose maximum reaches lo can hold keys >= lo -- only those groups
-// are read (k = 8 reads ~1/20 of the row at n = 6144).  Returns false (block-uniform) when more than
-// BR_CAP keys reach lo.
-__device__ __forceinline__ bool group_select16(int k, int tid, int lane, int w, int ng, const uint16_t* S,
-                                               const uint16_t* GMr, int* I, float* V, int relu, uint32_t* mx,
-                                               uint32_t* ckey, int* ccol, int* wsum, uint32_t* sres, int* glist,
-                                               int* tcol, float* tsc, int* tkeep, const uint16_t* Xr,
-                                               const uint16_t* Dg, int d) {
-  const uint32_t gk = tid < ng ? order16(GMr[tid]) : 0u;
-  mx[tid] = gk;
-  __syncthreads();
   if (w == 0) {
-    const uint32_t t = kth_of_256(mx, k, lane);
-    if (lane == 0) sres[0] = t;
-  }
-  __syncthreads();
-  const uint32_t lo = sres[0];
-  // the groups reaching lo, in group order
-  const int sel = (tid < ng && gk >= lo) ? 1 : 0;
-  const int gi = wave_incl_scan(sel, lane);
-  if (lane == 63) wsum[w] = gi;
-  __syncthreads();
-  int goff = gi - sel, nsel = 0;
+    const int nq = (total + 63) >> 6;
+    uint32_t ck[BR_CAP / 64];
 #pragma unroll
-  for (int ww = 0; ww < 4; ++ww) {
-    if (ww < w) goff += wsum[ww];
-    nsel += wsum[ww];
-  }
-  if (sel) glist[goff] = tid;
-  __syncthreads();
-  // read the selected groups: 4 threads per group, 8 keys (16 bytes) each, up to 4 slots per thread --
-  // once to count the keys >= lo, once more (cache hits) to park them (no key array held across)
-  auto slot_keys = [&](int s, uint32_t (&kk)[8]) {
-    const int col0 = glist[s >> 2] * 32 + (s & 3) * 8;
-    const uint4 v = *reinterpret_cast<const uint4*>(S + col0);
-    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    for (int q = 0; q < BR_CAP / 64; ++q) ck[q] = (q < nq && q * 64 + lane < total) ? ckey[q * 64 + lane] : 0u;
+    uint32_t t = 0;
+#pragma unroll 1
+    for (int b = 15; b >= 0; --b) {
+      const uint32_t cand = t | (1u << b);
+      int cnt = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) kk[j] = order16((wv[j >> 1] >> (16 * (j & 1))) & 0xffffu);
-    return col0;
-  };
-  int c = 0;
-  for (int s = tid; s < nsel * 4; s += 256) {
-    uint32_t kk[8];
-    slot_keys(s, kk);
+      for (int q = 0; q < BR_CAP / 64; ++q)
+        if (q < nq) cnt += __popcll(__ballot(ck[q] >= cand));
+      if (cnt >= k) t = cand;
+    }
+    int gt = 0, nt = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) c += kk[j] >= lo ? 1 : 0;
-  }
-  const int incl = wave_incl_scan(c, lane);
-  if (lane == 63) wsum[w] = incl;
-  __syncthreads();
-  int off = incl - c, total = 0;
-#pragma unroll
-  for (int ww = 0; ww < 4; ++ww) {
-    if (ww < w) off += wsum[ww];
-    total += wsum[ww];
-  }
-  if (total > BR_CAP) return false;
-  for (int s = tid; s < nsel * 4; s += 256) {
-    uint32_t kk[8];
-    const int col0 = slot_keys(s, kk);
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (kk[j] >= lo) {
-        ckey[off] = kk[j];
-        ccol[off] = col0 + j;
-        ++off;
+    for (int q = 0; q < BR_CAP / 64; ++q)
+      if (q < nq) {
+        gt += __popcll(__ballot(ck[q] > t));
+        nt += __popcll(__ballot(ck[q] == t && q * 64 + lane < total));
       }
+    const int need = k - gt;
+    // ambiguous ties: exact fp32 scores of the keys equal to t, the `need` largest kept
+    const bool exact = Xr && nt > need && nt <= TIE_CAP;
+    if (exact) {
+      int e0 = 0;
+#pragma unroll
+      for (int q = 0; q < BR_CAP / 64; ++q)
+        if (q < nq) {
+          const bool eq = ck[q] == t && q * 64 + lane < total;
+          const uint64_t me = __ballot(eq);
+          if (eq) tcol[e0 + lanes_below(me)] = ccol[q * 64 + lane];
+          e0 += __popcll(me);
+        }
+      for (int e = 0; e < nt; ++e) {
+        const uint16_t* Dr = Dg + (long)tcol[e] * d;
+        float dot = 0.f;
+        for (int x = lane * 4; x < d; x += 256) {
+          const ushort4 a = *reinterpret_cast<const ushort4*>(Xr + x);
+          const ushort4 r = *reinterpret_cast<const ushort4*>(Dr + x);
+          dot += bf2f(a.x) * bf2f(r.x) + bf2f(a.y) * bf2f(r.y) + bf2f(a.z) * bf2f(r.z) + bf2f(a.w) * bf2f(r.w);
+        }
+        dot = wave_sum(dot);
+        if (lane == 0) tsc[e] = dot;
+      }
+      if (lane < nt) {
+        const float sv = tsc[lane];
+        const int cv = tcol[lane];
+        int rank = 0;
+        for (int e = 0; e < nt; ++e) {
+          const float so = tsc[e];
+          rank += (so > sv || (so == sv && tcol[e] < cv)) ? 1 : 0;
+        }
+        tkeep[lane] = rank < need ? 1 : 0;
+      }
+    }
+    int base = 0, ties = 0;
+#pragma unroll
+    for (int q = 0; q < BR_CAP / 64; ++q) {
+      if (q < nq) {
+        const uint32_t kk = ck[q];
+        const bool eq = kk == t && q * 64 + lane < total;
+        const uint64_t me = __ballot(eq);
+        const int te = ties + lanes_below(me);
+        const bool take = kk > t || (eq && (exact ? tkeep[te] != 0 : te < need));
+        const uint64_t mt = __ballot(take);
+        if (take) {
+          const int pos = base + lanes_below(mt);
+          const int col = ccol[q * 64 + lane];
+          const float sv = bf2f(S[col]);
+          I[pos] = col;
+          V[pos] = relu ? fmaxf(sv, 0.f) : sv;
+        }
+        base += __popcll(mt);
+        ties += __popcll(me);
+      }
+    }
   }
-  __syncthreads();
-  if (w == 0) finish16(k, lane, total, S, I, V, relu, ckey, ccol, tcol, tsc, tkeep, Xr, Dg, d);
   return true;
 }
 
@@ -845,8 +756,7 @@ template <int PL>
 __global__ __launch_bounds__(256) void topk_bf16_kernel(const uint16_t* __restrict__ scores, const int* __restrict__ kv,
                                                       int* __restrict__ idx, float* __restrict__ val, int B, int n,
                                                       int kmax, int absolute, int relu, const uint16_t* __restrict__ X,
-                                                      long sx, const uint16_t* __restrict__ D, int d,
-                                                      const uint16_t* __restrict__ GM) {
+                                                      long sx, const uint16_t* __restrict__ D, int d) {
   static_assert(PL % 8 == 0, "8 keys per 16-byte load");
   __shared__ int red[2][4];
   __shared__ int wsum[2][4];
@@ -857,7 +767,6 @@ __global__ __launch_bounds__(256) void topk_bf16_kernel(const uint16_t* __restri
   __shared__ uint32_t bres[1];
   __shared__ int tcol[TIE_CAP], tkeep[TIE_CAP];
   __shared__ float tsc[TIE_CAP];
-  __shared__ int glist[256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const long row = blockIdx.x;
   const int g = (int)(row / B), b = (int)(row % B);
@@ -865,20 +774,6 @@ __global__ __launch_bounds__(256) void topk_bf16_kernel(const uint16_t* __restri
   const uint16_t* S = scores + row * n;
   int* I = idx + row * kmax;
   float* V = val + row * kmax;
-  const uint16_t* Xr = X ? X + (long)g * sx + (long)b * d : nullptr;
-  const uint16_t* Dg = D ? D + (long)g * n * d : nullptr;
-  bool done = false;
-  // the GEMM's row-group maxima (signed scores only): read just the groups that can hold candidates
-  if (GM && !absolute && k > 0 && k <= 256)
-    done = group_select16(k, tid, lane, w, n / 32, S, GM + row * (n / 32), I, V, relu, bmx, bkey, bcol, bsum, bres,
-                          glist, tcol, tsc, tkeep, Xr, Dg, d);
-  if (done) {
-    for (int j = k + tid; j < kmax; j += 256) {
-      I[j] = 0;
-      V[j] = 0.f;
-    }
-    return;
-  }
   uint32_t key[PL];
 #pragma unroll
   for (int i = 0; i < PL / 8; ++i) {
@@ -892,6 +787,9 @@ __global__ __launch_bounds__(256) void topk_bf16_kernel(const uint16_t* __restri
       key[8 * i + j] = order16(absolute ? (h & 0x7fffu) : h) & live;
     }
   }
+  const uint16_t* Xr = X ? X + (long)g * sx + (long)b * d : nullptr;
+  const uint16_t* Dg = D ? D + (long)g * n * d : nullptr;
+  bool done = false;
   if (k > 0 && k <= 256)
     done = bracket_select16<PL>(key, k, tid, lane, w, S, I, V, relu, bmx, bkey, bcol, bsum, bres, tcol, tsc, tkeep,
                                 absolute ? nullptr : Xr, Dg, d);
@@ -1392,23 +1290,19 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
   return 1;
 }
 
-// Per-row top-k of bf16 scores [G][B][n] (see topk_bf16_kernel / group_select16).  X ([B][d], or [G][B][d] with sx = B d)
+// Per-row top-k of bf16 scores [G][B][n] (see topk_bf16_kernel).  X ([B][d], or [G][B][d] with sx = B d)
 // and D ([G][n][d]) are the scores GEMM's bf16 operands, read to resolve ambiguous ties exactly (null:
 // ties in column order); absolute = select by |score| (no exact tie resolution).
-// GM (optional): the scores GEMM's row-group maxima [G][B][n/32] bf16 (n % 32 == 0, n <= 8192).
 int sc_topk_select_bf16(const void* scores, const int* k, int* idx, float* val, int G, int B, int n, int kmax,
-                        int absolute, int relu, const void* X, long sx, const void* D, int d, const void* GM,
-                        hipStream_t stream) {
+                        int absolute, int relu, const void* X, long sx, const void* D, int d, hipStream_t stream) {
   if (n % 8 || n < 8 || kmax < 1 || (X && (!D || d % 4 || d < 4))) return 1;
-  if (GM && (n % 32 || n > 256 * 32)) return 1;
-  const uint16_t* GMp = reinterpret_cast<const uint16_t*>(GM);
   dim3 grid((unsigned)G * B);
   const uint16_t* S = reinterpret_cast<const uint16_t*>(scores);
   const uint16_t* Xp = reinterpret_cast<const uint16_t*>(X);
   const uint16_t* Dp = reinterpret_cast<const uint16_t*>(D);
 #define SC_B16(P) \
   if (n <= 256 * P) { hipLaunchKernelGGL((topk_bf16_kernel<P>), grid, dim3(256), 0, stream, S, k, idx, val, B, n, kmax, \
-                                         absolute, relu, Xp, sx, Dp, d, GMp); \
+                                         absolute, relu, Xp, sx, Dp, d); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   SC_B16(8) SC_B16(16) SC_B16(24) SC_B16(32) SC_B16(48) SC_B16(64)
 #undef SC_B16

@@ -384,21 +384,15 @@ def rowmax_nt(a, b, alpha=1.0, cfg=None):
     return out[0] if squeeze else out
 
 
-def matmul_nt(a, b, out, alpha=1.0, group_max=None):
-    """out[g] = alpha * a[g] @ b[g]^T; a: [M, K] or [G, M, K]; b: [G, N, K]; out bf16/fp32 [G, M, N].
-    ``group_max`` (bf16 ``out`` only): [G, M, N/32] bf16, each row's largest output per 32-column group
-    (the top-k select's candidate bound, written by the same epilogue)."""
+def matmul_nt(a, b, out, alpha=1.0):
+    """out[g] = alpha * a[g] @ b[g]^T; a: [M, K] or [G, M, K]; b: [G, N, K]; out bf16/fp32 [G, M, N]."""
     G, N, K = b.shape
     M = a.shape[-2]
     _bf16(a, "a"); _bf16(b, "b")
     sa = 0 if a.dim() == 2 else M * K
     epi = EPI_F32 if out.dtype == torch.float32 else EPI_BF16
     _need(tuple(out.shape) == (G, M, N) and out.is_contiguous(), "out shape")
-    if group_max is not None:
-        _need(epi == EPI_BF16 and N % 32 == 0 and group_max.dtype == torch.bfloat16 and group_max.is_contiguous()
-              and tuple(group_max.shape) == (G, M, N // 32), "group_max must be contiguous bf16 [G, M, N/32]")
-    _launch(epi, 3, M, N, K, 0, G, [_op(a, K, sa)] * 2, [_op(b, K, N * K)] * 2, [out], [alpha], N, M * N,
-            part=group_max)
+    _launch(epi, 3, M, N, K, 0, G, [_op(a, K, sa)] * 2, [_op(b, K, N * K)] * 2, [out], [alpha], N, M * N)
 
 
 def matmul_nn(a, b, out, alpha=1.0):

@@ -355,14 +355,12 @@ def test_topk_select_exact(n):
     torch.testing.assert_close(va[2].abs().sort(-1).values, ref)
 
 
-@pytest.mark.parametrize("gm", [False, True])
 @pytest.mark.parametrize("n", [6144, 1024])
-def test_topk_select_bf16_picks_are_fp32_topk(n, gm):
+def test_topk_select_bf16_picks_are_fp32_topk(n):
     """Select on the scores GEMM's bf16 output: the picks are the top-k of the fp32 scores the GEMM
     accumulated (bf16 ties at the threshold ranked by exact recomputes from x and D), the values
     are the bf16 scores; clustered near-equal scores, duplicated atoms and an all-zero row (heavy
-    ties: full-bisection fallback, column order).  ``gm``: with the epilogue's per-32-column row
-    maxima (checked against the output), the select reads only the groups that can hold a pick."""
+    ties: full-bisection fallback, column order)."""
     from sparse_coding__amd.ops import gemm as gemm_ops
     from sparse_coding__amd.ops import topk as T
 
@@ -378,13 +376,10 @@ def test_topk_select_bf16_picks_are_fp32_topk(n, gm):
     x[40] = 0.0  # every score zero
     x = x.to(torch.bfloat16).contiguous()
     sb = torch.empty(G, B, n, device=DEV, dtype=torch.bfloat16)
-    gmax = torch.empty(G, B, n // 32, device=DEV, dtype=torch.bfloat16) if gm else None
-    gemm_ops.matmul_nt(x, D, sb, group_max=gmax)
-    if gm:
-        assert torch.equal(gmax, sb.view(G, B, n // 32, 32).amax(-1))
+    gemm_ops.matmul_nt(x, D, sb)
     exact = torch.einsum("bd,gnd->gbn", x.double(), D.double())
     k = torch.tensor([8, 64, 128], device=DEV, dtype=torch.int32)
-    idx, val = T.topk_select(sb, k, 128, x=x, D=D, group_max=gmax)
+    idx, val = T.topk_select(sb, k, 128, x=x, D=D)
     torch.cuda.synchronize()
     tol = 1e-5 * exact.abs().amax().item()
     nres = 0
@@ -409,11 +404,8 @@ def test_topk_select_bf16_picks_are_fp32_topk(n, gm):
     assert set(idx[0, 40, :8].tolist()) == set(range(8))  # all-zero row: ties by column
     has5, has7 = (idx[1, :, :64] == 5).any(-1), (idx[1, :, :64] == 7).any(-1)
     assert not (has7 & ~has5).any()  # equal exact scores: the lower column first
-    idx2, val2 = T.topk_select(sb, k, 128, x=x, D=D, group_max=gmax)
+    idx2, val2 = T.topk_select(sb, k, 128, x=x, D=D)
     assert torch.equal(idx2, idx) and torch.equal(val2, val)  # deterministic
-    if gm:  # the same picks as the whole-row bracket (output order may differ)
-        idx3, _ = T.topk_select(sb, k, 128, x=x, D=D)
-        assert torch.equal(idx3.sort(-1).values, idx.sort(-1).values)
 
 
 def test_topk_scatter_and_clear_roundtrip():
