@@ -97,6 +97,8 @@ def parse(argv=None):
                     help="create the process group even at N=1 and run the N>1 code path (rehearses the "
                          "sharded step with real RCCL collectives on a one-GPU box)")
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--no-comm-calibration", action="store_true",
+                    help="N > 1: skip timing the node's collectives before choosing the mode (link model only)")
     ap.add_argument("--wgrad-dtype", choices=["fp32", "bf16"], default="fp32",
                     help="single GPU: storage of the weight gradients between the wgrad GEMM and Adam (the "
                          "moments, masters and the update stay fp32)")
@@ -671,6 +673,11 @@ def main(argv=None):
 
     shape = comm_model.StepShape(models=args.models, n=n, d=args.d, batch=B, t1_ms=T1_MS,
                                  untied=args.kind == "untied", es_ms=dict(ES_MS))
+    # N > 1: this node's own collective rates at the step's payloads replace the link model's constants
+    # (reported as "comm_calibration")
+    calib = None
+    if info.world_size > 1 and not args.no_comm_calibration:
+        calib = comm_model.calibrate(info, shape)
     par = args.parallelism
     if par == "auto":
         # N > 1: the mode the per-N comm/compute model predicts fastest (ensemble-axis sharding at
@@ -771,6 +778,7 @@ def main(argv=None):
             "predicted_ms_per_step": {m: comm_model.predict(m, info.world_size, shape, args.dp_chunks)["ms_per_step"]
                                       for m in ("dp", "zero1", "es")} if distributed else None,
             "comm_bytes_other_modes": {m: comm_bytes(m, args, max(info.world_size, 8)) for m in ("dp", "zero1", "es")},
+            "comm_calibration": calib,
             "model_activations_per_s": round(value * args.models, 1),
             "baseline_note": "vs_baseline divides by BASELINE.md row 12 (reference math, same shapes, "
                              "1.86k act/s, 8-vCPU sandbox); no published GPU throughput exists.  "

@@ -16,8 +16,10 @@ Link model.  The 8 MI355X of a node are fully connected by xGMI: every pair has 
 GB/s is the bidirectional raw rate).  A ring collective over N GPUs built from RCCL's channels can
 drive at most N-1 links per GPU at once; ``LINK_EFF`` discounts protocol and scheduling overheads
 (RCCL bus bandwidth on xGMI meshes sits well under the raw link sum).  Every number here is an
-input of the model, not a measurement of this node -- the bench prints the prediction next to the
-measured step so the two can be compared on the driver's 8-GPU runs.
+input of the model, not a measurement of this node -- unless ``calibrate()`` measured the node's own
+collectives first (the bench does at N > 1 and reports them): its bus rates then replace the link
+model per mode.  The bench prints the prediction next to the measured step so the two can be compared
+on the driver's 8-GPU runs.
 
 Overlap model.  ``dp`` with K model chunks overlaps chunk k's all-reduce with chunk k+1's compute
 (and, cross-step, the last chunk's with the next step's first chunk): up to (K-1)/K of the step's
@@ -28,6 +30,7 @@ the gather outlasts the group).
 
 from __future__ import annotations
 
+import time
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
@@ -55,6 +58,7 @@ class StepShape:
     untied: bool = True
     adam_ms: float = 0.08          # Adam share of t1 (HBM-bound; divides by N under zero1 / es)
     es_ms: Dict[int, float] = field(default_factory=dict)  # measured per-rank ES steps, if any
+    bus: Dict[str, float] = field(default_factory=dict)    # measured bus GB/s per mode (calibrate())
 
     @property
     def params(self) -> int:
@@ -84,7 +88,8 @@ def predict(mode: str, world: int, shape: StepShape, dp_chunks: int = 2,
     if grad_bytes_per_elem is None:
         grad_bytes_per_elem = 2 if mode == "zero1" else 4  # zero1: bf16 transport by default
     nbytes = bytes_per_gpu(mode, world, shape, grad_bytes_per_elem)
-    comm_ms = nbytes / (bus_gbps(world) * 1e9) * 1e3 if world > 1 else 0.0
+    bw = shape.bus.get(mode) or bus_gbps(world)
+    comm_ms = nbytes / (bw * 1e9) * 1e3 if world > 1 else 0.0
     if mode == "es":
         compute = shape.es_ms.get(world, shape.t1_ms - shape.adam_ms * (1 - 1 / world))
         hide = compute  # the next group's gather runs under this group's replay
@@ -97,7 +102,59 @@ def predict(mode: str, world: int, shape: StepShape, dp_chunks: int = 2,
     exposed = max(0.0, comm_ms - hide)
     return {"ms_per_step": round(compute + exposed, 4), "compute_ms": round(compute, 4),
             "comm_ms": round(comm_ms, 4), "exposed_comm_ms": round(exposed, 4),
-            "bytes_per_gpu": nbytes, "bus_GBps": round(bus_gbps(world), 1) if world > 1 else None}
+            "bytes_per_gpu": nbytes, "bus_GBps": round(bw, 1) if world > 1 else None,
+            "bus_source": ("measured" if shape.bus.get(mode) else "link model") if world > 1 else None}
+
+
+def calibrate(info, shape: StepShape, reps: int = 5) -> Optional[Dict[str, Dict[str, float]]]:
+    """Time this node's own collectives at the step's payloads (collective: every rank calls it; N > 1).
+
+    * ``all_gather`` of each rank's B x d bf16 batch (the ``es`` payload);
+    * ``all_reduce`` of the fp32 weight + bias gradients (the ``dp`` payload; ``zero1`` moves the same
+      ring volume as reduce-scatter + all-gather, so it takes this rate).
+    Median of ``reps`` timed runs after two warmups, barrier + device synchronize around each.  Bus
+    bandwidth as RCCL reports it: all-reduce 2 (N-1)/N x bytes / t, all-gather (N-1)/N x N x bytes / t.
+    Fills ``shape.bus`` (GB/s per mode) and returns the measurements (None on one rank)."""
+    import torch
+    import torch.distributed as dist
+
+    if not getattr(info, "enabled", False) or info.world_size <= 1:
+        return None
+    world = info.world_size
+    dev = info.device if info.backend == "nccl" else torch.device("cpu")
+    cuda = dev.type == "cuda"
+
+    def timed(fn):
+        for _ in range(2):
+            fn()
+        ts = []
+        for _ in range(reps):
+            dist.barrier()
+            if cuda:
+                torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            fn()
+            if cuda:
+                torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t)
+        ts.sort()
+        return ts[len(ts) // 2]
+
+    f = (world - 1) / world
+    out = {"backend": info.backend}
+    x = torch.ones(shape.batch, shape.d, dtype=torch.bfloat16, device=dev)
+    parts = [torch.empty_like(x) for _ in range(world)]
+    t = timed(lambda: dist.all_gather(parts, x))
+    nb = x.numel() * x.element_size()
+    out["all_gather"] = {"bytes_per_rank": nb, "ms": round(t * 1e3, 4), "bus_GBps": round(f * world * nb / t / 1e9, 2)}
+    g = torch.ones(shape.params, dtype=torch.float32, device=dev)
+    t = timed(lambda: dist.all_reduce(g))
+    nb = g.numel() * 4
+    out["all_reduce"] = {"bytes": nb, "ms": round(t * 1e3, 4), "bus_GBps": round(2 * f * nb / t / 1e9, 2)}
+    del x, parts, g
+    shape.bus.update({"es": out["all_gather"]["bus_GBps"], "dp": out["all_reduce"]["bus_GBps"],
+                      "zero1": out["all_reduce"]["bus_GBps"]})
+    return out
 
 
 def best_mode(world: int, shape: StepShape, dp_chunks: int = 2, allow_es: bool = True) -> str:

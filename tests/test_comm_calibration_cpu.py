@@ -1,0 +1,67 @@
+"""``comm_model.calibrate`` (what bench.py runs at N > 1 before choosing the mode): 2 gloo ranks time
+their own all-gather / all-reduce at the step's payloads; the measured bus rates replace the link
+model in ``predict`` and ``best_mode``."""
+
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from sparse_coding__amd.parallel import comm_model
+    from sparse_coding__amd.parallel.dist import DistInfo
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    info = DistInfo(rank, world, rank, torch.device("cpu"), "gloo")
+    shape = comm_model.StepShape(models=2, n=256, d=128, batch=256, t1_ms=0.3)
+    calib = comm_model.calibrate(info, shape, reps=3)
+    pred = {m: comm_model.predict(m, world, shape) for m in ("dp", "zero1", "es")}
+    q.put((rank, calib, dict(shape.bus), pred, comm_model.best_mode(world, shape)))
+    dist.destroy_process_group()
+
+
+def test_calibrate_two_gloo_ranks():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (c, b, pr, bm)) for r, c, b, pr, bm in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        calib, bus, pred, best = res[r]
+        assert calib["backend"] == "gloo"
+        assert calib["all_gather"]["bytes_per_rank"] == 256 * 128 * 2
+        assert calib["all_reduce"]["bytes"] == 2 * (2 * 256 * 128 + 256) * 4
+        assert calib["all_gather"]["ms"] > 0 and calib["all_reduce"]["bus_GBps"] > 0
+        assert bus == {"es": calib["all_gather"]["bus_GBps"], "dp": calib["all_reduce"]["bus_GBps"],
+                       "zero1": calib["all_reduce"]["bus_GBps"]}
+        for m in ("dp", "zero1", "es"):
+            assert pred[m]["bus_source"] == "measured" and pred[m]["bus_GBps"] == round(bus[m], 1)
+        assert best in ("dp", "zero1", "es")
+
+
+def test_calibrate_is_a_no_op_on_one_rank():
+    from sparse_coding__amd.parallel import comm_model
+    from sparse_coding__amd.parallel.dist import DistInfo
+
+    shape = comm_model.StepShape(models=8, n=2048, d=512, batch=2048, t1_ms=0.3)
+    assert comm_model.calibrate(DistInfo(), shape) is None and shape.bus == {}
+    assert comm_model.predict("dp", 8, shape)["bus_source"] == "link model"
