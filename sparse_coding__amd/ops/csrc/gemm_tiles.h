@@ -83,10 +83,6 @@ struct GemmParams {
   // (the consumer -- the Adam kernel for weight gradients -- sums the slabs).
   int ksplit;
   long split_stride;
-  // K rotation (cfg bit 6): each output tile walks its K-tiles starting at (tm + tn) mod nk, so the
-  // blocks that share an operand panel and start together request different K-slices of it instead of
-  // the same L2 lines in lockstep (unsplit launches; the fp32 sums change order, deterministically)
-  int krot;
   // masked ensembles: per-group live extent of the n dimension when it is M / K (may be null)
   const int* nact_m;
   const int* nact_k;

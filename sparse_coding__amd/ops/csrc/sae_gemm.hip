@@ -33,8 +33,7 @@ int sc_gemm_shape(int M, int N, int G, int nprob) {
 // layout: bit0 = A is K-major, bit1 = B is K-major.
 // cfg bits 0-1: 0 = automatic shape, 1 = 128x128, 2 = 256x128, 3 = 256x256;
 // bits 2-3: K pipeline (0: BK64 x 2-stage LDS ring, 1: BK32 x 4 (128x128 blocks: BK64 x 3),
-// 2: BK32 x 2, 3: BK32 x 3); bit 4: 128x128 on the BK32 rings with the software-pipelined K loop;
-// bit 6: K rotation (GemmParams::krot).
+// 2: BK32 x 2, 3: BK32 x 3); bit 4: 128x128 on the BK32 rings with the software-pipelined K loop.
 int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
             const ScOperand* a /* [nprob][2] */, const ScOperand* b /* [nprob][2] */,
             void* const* c /* [nprob] */, const float* alpha /* [nprob] */, long ldc, long sc,
@@ -66,7 +65,6 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   p.dotpart = dotpart; p.dc_tied = dc_tied;
   p.cmask = reinterpret_cast<uint64_t*>(cmask);
   p.ksplit = ksplit; p.split_stride = split_stride;
-  p.krot = (cfg >> 6) & 1;
   p.act = act; p.ascale = ascale;
   p.cmask2 = reinterpret_cast<uint64_t*>(cmask2); p.rcol = rcol;
   p.nact_m = nact_m; p.nact_k = nact_k;

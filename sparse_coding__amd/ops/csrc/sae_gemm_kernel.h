@@ -713,19 +713,15 @@ __global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : 1) void sae_gemm_ker
   const uint32_t sa0 = AK ? BKT * 2 : (uint32_t)(BKT * oa0.ld * 2), sa1 = AK ? BKT * 2 : (uint32_t)(BKT * oa1.ld * 2);
   const uint32_t sb0 = BKM ? BKT * 2 : (uint32_t)(BKT * ob0.ld * 2), sb1 = BKM ? BKT * 2 : (uint32_t)(BKT * ob1.ld * 2);
 
-  // K rotation: logical K-tile t (ring slot t % NST) fetches physical K-tile t + krot, wrapped
-  const int krot = (p.krot && p.ksplit == 1 && nk > kbeg) ? (int)((uint32_t)(tm + tn) % (uint32_t)(nk - kbeg)) : 0;
 #define SC_ISSUE(t)                                                              \
   do {                                                                           \
     char* dst_ = smem + ((t) % NST) * STG;                                       \
-    int tt_ = (t) + krot;                                                        \
-    if (tt_ >= nk) tt_ -= nk - kbeg;                                             \
-    if (!SEG2 || tt_ < nk1) {                                                    \
-      issue_pieces<PPWA>(ra0, va0, (uint32_t)tt_ * sa0, dst_, wid);              \
-      issue_pieces<PPWB>(rb0, vb0, (uint32_t)tt_ * sb0, dst_ + TA, wid);         \
+    if (!SEG2 || (t) < nk1) {                                                    \
+      issue_pieces<PPWA>(ra0, va0, (uint32_t)(t) * sa0, dst_, wid);              \
+      issue_pieces<PPWB>(rb0, vb0, (uint32_t)(t) * sb0, dst_ + TA, wid);         \
     } else if constexpr (SEG2) {                                                 \
-      issue_pieces<PPWA>(ra1, va1, (uint32_t)(tt_ - nk1) * sa1, dst_, wid);      \
-      issue_pieces<PPWB>(rb1, vb1, (uint32_t)(tt_ - nk1) * sb1, dst_ + TA, wid); \
+      issue_pieces<PPWA>(ra1, va1, (uint32_t)((t) - nk1) * sa1, dst_, wid);      \
+      issue_pieces<PPWB>(rb1, vb1, (uint32_t)((t) - nk1) * sb1, dst_ + TA, wid); \
     }                                                                            \
   } while (0)
 

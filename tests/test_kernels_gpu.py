@@ -86,8 +86,7 @@ def test_identity_asymmetric():
 
 
 PIPE_CFGS = [1 | 1 << 2, 1 | 2 << 2, 1 | 3 << 2, 3 | 1 << 2, 3 | 2 << 2, 3 | 3 << 2,  # deeper K pipelines
-             1 | 2 << 2 | 16, 1 | 3 << 2 | 16,  # 128x128 BK32 rings, software-pipelined K loop
-             1 | 64, 3 | 64, 1 | 3 << 2 | 16 | 64]  # K rotation
+             1 | 2 << 2 | 16, 1 | 3 << 2 | 16]  # 128x128 BK32 rings, software-pipelined K loop
 
 
 @pytest.mark.parametrize("cfg", SHAPE_CFGS + PIPE_CFGS)
@@ -252,7 +251,7 @@ def test_weight_grads_bf16_out_matches_fp32():
         assert torch.equal(o16, o32.to(torch.bfloat16)), cfg
 
 
-@pytest.mark.parametrize("cfg", SHAPE_CFGS + [1 | 3 << 2 | 16, 1 | 64, 3 | 64])
+@pytest.mark.parametrize("cfg", SHAPE_CFGS + [1 | 3 << 2 | 16])
 @pytest.mark.parametrize("kind", ["untied", "tied"])
 def test_fused_step_matches_functional_ensemble(kind, cfg):
     from sparse_coding__amd.ops import gemm

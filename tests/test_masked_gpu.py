@@ -18,7 +18,7 @@ def _lib():
     yield
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 1 | 64])  # (1 | 64: K rotation, same in both launches)
+@pytest.mark.parametrize("cfg", [1, 3])
 def test_compacted_masked_launches_match_full(cfg):
     from sparse_coding__amd.ops import gemm
 
