@@ -278,7 +278,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
                                                         float* __restrict__ Aout, int B, int T,
                                                         uint16_t* __restrict__ Ysave, uint16_t* __restrict__ Asave,
                                                         float* __restrict__ Vsum, uint16_t* __restrict__ Qslab,
-                                                        float* __restrict__ epart, int krot) {
+                                                        float* __restrict__ epart) {
   constexpr int n = NW * 128;  // 8 waves x NW 16-column tiles
   constexpr int nrb = n * 2;
   constexpr int R = FR * RT;   // rows per workgroup
@@ -290,10 +290,6 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int g = bid / rb, r0 = (bid % rb) * R;
   const uint16_t* Gg = Gm + (long)g * n * n;
-  // k rotation (krot): the workgroups of one model stream the same Gm; each starts its k walk at its
-  // own offset so they do not request the same L2 lines in lockstep (the k sum changes order)
-  const int rot = krot ? (int)(((long)(bid % rb) * 32 * PF) % n) : 0;
-  auto kphys = [&](int k) { const int kp = k + rot; return kp >= n ? kp - n : kp; };
   const float eta = eta_[g], thr = MODE == 2 ? 0.f : eta_[g] * lam_[g];
   const int row = lane & 15, q = lane >> 4;
   const int nbase = w * NW * 16;
@@ -332,7 +328,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
 #pragma unroll
   for (int s = 0; s < PF; ++s)
 #pragma unroll
-    for (int t = 0; t < NH; ++t) gq[s][t] = gfrag(0, t, kphys(s * 32));
+    for (int t = 0; t < NH; ++t) gq[s][t] = gfrag(0, t, s * 32);
   for (int it = 0; it < T; ++it) {
     const char* Ycur = Ybuf + (it & 1) * (R * nrb);
     char* Ynxt = Ybuf + ((it + 1) & 1) * (R * nrb);
@@ -377,7 +373,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
           const int kk = k0 + s * 32;
           bf16x8_t fy[RT];
 #pragma unroll
-          for (int u = 0; u < RT; ++u) fy[u] = lds_frag(Ycur, u * FR + row, kphys(kk) + 8 * q, nrb);
+          for (int u = 0; u < RT; ++u) fy[u] = lds_frag(Ycur, u * FR + row, kk + 8 * q, nrb);
 #pragma unroll
           for (int t = 0; t < NH; ++t)
 #pragma unroll
@@ -386,7 +382,7 @@ __global__ __launch_bounds__(FNT, 1) void fista_gram_kernel(const float* __restr
           const int kn = kk + PF * 32;
           const bool wrap = kn >= n;
 #pragma unroll
-          for (int t = 0; t < NH; ++t) gq[s][t] = wrap ? gfrag(hn, t, kphys(kn - n)) : gfrag(h, t, kphys(kn));
+          for (int t = 0; t < NH; ++t) gq[s][t] = wrap ? gfrag(hn, t, kn - n) : gfrag(h, t, kn);
         }
       }
       // FISTA update of this half: Y += eta (C - Z); A = relu(Y - eta lambda); Y = A + mom (A - A_prev)
@@ -552,8 +548,6 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
   const uint16_t* gm = reinterpret_cast<const uint16_t*>(Gm);
   uint16_t* ys = reinterpret_cast<uint16_t*>(Ysave);
   uint16_t* as = reinterpret_cast<uint16_t*>(Asave);
-  // SC_FISTA_KROT=1: per-workgroup k rotation of the Gm stream (see fista_gram_kernel)
-  static const int krot = getenv("SC_FISTA_KROT") ? atoi(getenv("SC_FISTA_KROT")) : 0;
   // 32-row workgroups when they still give >= 2 per CU (256 CUs); else 16 rows (rows = 16 forces it)
   const bool two = (B % (2 * FR) == 0) && (long)G * (B / (2 * FR)) >= 512 && rows != 16;
   const dim3 g2(G * (B / (2 * FR))), g1(G * (B / FR));
@@ -562,9 +556,9 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
 #define SC_GM(NWV, H2, PF2, H1, PF1, MV)                                                                   \
   {                                                                                                        \
     if (two) hipLaunchKernelGGL((fista_gram_kernel<NWV, 2, H2, PF2, MV>), g2, dim3(FNT), 0, stream, C, gm, A0, eta, lam, \
-                                mom, A, B, T, ys, as, Vsum, qs, epart, krot);                                               \
+                                mom, A, B, T, ys, as, Vsum, qs, epart);                                               \
     else hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1, MV>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, \
-                            mom, A, B, T, ys, as, Vsum, qs, epart, krot);                                                   \
+                            mom, A, B, T, ys, as, Vsum, qs, epart);                                                   \
     return hipGetLastError() == hipSuccess ? 0 : 3;                                                        \
   }
   // (NW, halves, ring depth) of the 32-row and 16-row solve, then of the slab-saving solve and
@@ -579,7 +573,7 @@ int sc_fista_gram(const float* C, const void* Gm, const float* A0, const float* 
   }
 #define SC_G1(NWV, H1, PF1, MV)                                                                            \
   hipLaunchKernelGGL((fista_gram_kernel<NWV, 1, H1, PF1, MV>), g1, dim3(FNT), 0, stream, C, gm, A0, eta, lam, mom, A, B, \
-                     T, ys, as, Vsum, qs, epart, krot);                                                                     \
+                     T, ys, as, Vsum, qs, epart);                                                                     \
   return hipGetLastError() == hipSuccess ? 0 : 3;
   SC_G(2, 1, 4, 1, 4, SC_GM(2, 1, 4, 1, 4, 1), SC_GM(2, 1, 4, 1, 4, 2))
   SC_G(4, 1, 4, 1, 8, SC_GM(4, 1, 4, 1, 4, 1), SC_GM(4, 4, 1, 1, 2, 2))
