@@ -1,6 +1,6 @@
 """Runs each kernel of the fused SAE step (config 2 shapes, as the engine launches them: the
 code gradient from the encoder's activity mask, the fused step tail) a few times, plus the top-k
-select of config 4 and a config-5 FISTA solve (d = n = 1024, 8 models, 20 iterations), for
+scores GEMM (bf16 out) and select of config 4 and a config-5 FISTA solve (d = n = 1024, 8 models, 20 iterations), for
 rocprofv3 counter collection (scripts/gpu.sh pmc)."""
 import os
 import sys
@@ -27,14 +27,16 @@ for _ in range(5):
     gemm.decode_residual(e.c, e.dec_shadow, x, e.r, e.dec_part)
     gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart, mask=e.cmask)
     gemm.weight_grads([[(e.c, e.r)], [(e.dpre, x)]], [e.g_dec, e.g_enc], 1e-6)
-    gemm.code_grad_wgrad(e.r, e.dec_shadow, x, e.cmask, e.l1, e.g_enc, e.colpart, 1e-6)  # fused dc + enc wgrad
     e._apply_update_kernels()  # the fused step tail (row Adam + losses + bias Adam)
 torch.cuda.synchronize()
-# config 4 top-k select: 8 models, B=2048, n=6144
-scores = torch.randn(8, 2048, 6144, device=dev)
+# config 4 top-k: bf16 scores GEMM + select (8 models, B=2048, d=768, n=6144)
+xt = (torch.randn(2048, 768, device=dev) * 0.3).to(torch.bfloat16)
+Dt = torch.nn.functional.normalize(torch.randn(8, 6144, 768, device=dev), dim=-1).to(torch.bfloat16)
+scores = torch.empty(8, 2048, 6144, device=dev, dtype=torch.bfloat16)
 k = torch.tensor([8, 16, 24, 32, 48, 64, 96, 128], dtype=torch.int32, device=dev)
 for _ in range(3):
-    topk_ops.topk_select(scores, k, 128)
+    gemm.matmul_nt(xt, Dt, scores)
+    topk_ops.topk_select(scores, k, 128, x=xt, D=Dt)
 torch.cuda.synchronize()
 # config 5 FISTA: Gram-form persistent solve, 8 models, d = n = 1024, B = 2048
 from sparse_coding__amd.ops import fista as F  # noqa: E402
