@@ -42,6 +42,9 @@ def test_bench_two_ranks_shared_gpu_gloo():
     assert alt["parallelism"] == "dp2" and "error" not in alt, alt
     assert alt["value"] > 0 and "gloo" in alt["collective_path"]
     assert alt["consistency"]["max_abs_delta"] == 0.0
+    cal = rec["comm_calibration"]  # the node's own collective rates, timed before the mode was chosen
+    assert cal["backend"] == "gloo" and cal["all_gather"]["bytes_per_rank"] == 2048 * 512 * 2
+    assert cal["all_reduce"]["bus_GBps"] > 0
 
 
 def test_bench_more_gpus_than_present_fails_fast():
