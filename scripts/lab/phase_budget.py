@@ -1,5 +1,6 @@
 """Per-phase budget of a GEMM launch from gemm_phases' per-workgroup stamps (one CSV per kernel:
-start / fill / kloop / epi in us, hw_id, xcc_id).  Reports the medians of each phase, the kernel span,
+raw s_memtime ticks at start / first K-tile landed / K loop done / epilogue done, s_memrealtime at
+start and end, hw_id, xcc_id).  Reports the medians of each phase, the kernel span,
 how full the co-resident slots were (sum of workgroup lifetimes / (span x slots)) and the tail: the
 time from the first CU going idle for good to the last workgroup's end.
 
@@ -17,19 +18,22 @@ for f in sorted(glob.glob(os.path.join(d, "*.csv"))):
     if not rows:
         continue
     t = [[int(r[k]) for k in ("t0", "t1", "t2", "t3")] for r in rows]
-    # shader clock from s_memtime vs s_memrealtime (100 MHz) over the launch; 2.0 GHz if unusable
-    r0, r1 = min(int(r["rt0"]) for r in rows), max(int(r["rt3"]) for r in rows)
-    m0, m1 = min(x[0] for x in t), max(x[3] for x in t)
-    ghz = (m1 - m0) / ((r1 - r0) * 10.0) if r1 > r0 else 0.0
-    if not 0.5 < ghz < 3.5:
-        print(f"  (clock from stamps {ghz:.3g} GHz unusable; assuming 2.0)")
-        ghz = 2.0
+    rt = [(int(r["rt0"]), int(r["rt3"])) for r in rows]
+    # s_memtime is a per-XCD shader-clock counter (the XCDs' counters are not synchronised: never
+    # compare them across XCDs); s_memrealtime is the chip-wide 100 MHz clock.  Each block's shader
+    # clock is its own memtime span over its realtime span; start / end on the realtime axis.
+    ghz_b = [(x[3] - x[0]) / ((b - a) * 10.0) if b > a else 0.0 for x, (a, b) in zip(t, rt)]
+    good = [g for g in ghz_b if 0.5 < g < 3.5]
+    ghz = st.median(good) if good else 2.0
+    if not good:
+        print("  (no usable block clock; assuming 2.0 GHz)")
     us = lambda ticks: ticks / ghz / 1e3  # noqa: E731
-    start = [us(x[0] - m0) for x in t]
+    r_min = min(a for a, _ in rt)
+    start = [(a - r_min) / 100.0 for a, _ in rt]
     fill = [us(x[1] - x[0]) for x in t]
     kl = [us(x[2] - x[1]) for x in t]
     ep = [us(x[3] - x[2]) for x in t]
-    end = [s + a + b + c for s, a, b, c in zip(start, fill, kl, ep)]
+    end = [(b - r_min) / 100.0 for _, b in rt]
     life = [e - s for s, e in zip(start, end)]
     span = max(end) - min(start)
     # CU identity: HW_ID (SE, SH, CU fields) + XCC
@@ -45,6 +49,6 @@ for f in sorted(glob.glob(os.path.join(d, "*.csv"))):
     slots = int(sys.argv[2]) if len(sys.argv) > 2 else max(1, round(sum(life) / span / ncu + 0.5))
     eff = sum(life) / (span * ncu * slots)
     name = os.path.basename(f)[:-4]
-    print(f"{name:18s} blocks {len(rows):5d} on {ncu:3d} CUs (per CU {min(per_cu)}-{max(per_cu)}), span {span:6.1f} us; "
+    print(f"{name:18s} clock {ghz:4.2f} GHz; blocks {len(rows):5d} on {ncu:3d} CUs (per CU {min(per_cu)}-{max(per_cu)}), span {span:6.1f} us; "
           f"median fill {st.median(fill):5.2f} kloop {st.median(kl):6.2f} epi {st.median(ep):5.2f} life {st.median(life):6.2f} us; "
           f"slot fill {100 * eff:5.1f} % at {slots}/CU; tail after first idle CU {span - (first_idle - min(start)):5.1f} us")
