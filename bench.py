@@ -103,7 +103,7 @@ def parse(argv=None):
                     help="single GPU: storage of the weight gradients between the wgrad GEMM and Adam (the "
                          "moments, masters and the update stay fp32)")
     ap.add_argument("--graph-group", type=int, default=None,
-                    help="steps per graph replay (default: engine/graph_plan.tile's choice, <= 8)")
+                    help="steps per graph replay (default: engine/graph_plan.tile's choice, <= 10)")
     ap.add_argument("--settle-mode", choices=["gemm", "step"], default="step",
                     help="settle load: 'gemm' = the grouped GEMM on scratch operands; 'step' = the same fused "
                          "step on a scratch ensemble of the benchmark's shapes (discarded, shares no state)")
@@ -146,7 +146,7 @@ def fvu_l0(dicts, x):
 # single-GPU fused step: at most this many optimizer steps per HIP graph replay (each replay
 # boundary costs an ~9 us idle gap on MI355X); engine/graph_plan.py picks the group size so that
 # the warmup replays every graph the timed region replays
-GRAPH_STEPS = 8
+GRAPH_STEPS = 10
 
 
 class Runner:

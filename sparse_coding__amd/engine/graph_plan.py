@@ -1,14 +1,18 @@
 """How a run of optimizer steps is cut into multi-step HIP graph replays.
 
-Every graph-replay boundary costs an idle gap on MI355X (~9 us), so steps are replayed in
-groups of up to ``max_group`` steps per graph.  A freshly captured graph is also slow on its first
-launches (upload, cold instruction caches), so a timed region should only replay graphs that
-were already replayed before it.  ``tile(steps, warmup)`` picks one group size S (and at most one
-remainder graph) for the ``steps`` timed steps such that the ``warmup`` steps can replay every
-graph the timed region uses, ending with an S-group right before the timed region.
+Every graph-replay boundary costs an idle gap on MI355X (~9 us and more), so steps are replayed in
+groups of up to ``max_group`` steps per graph and ``tile(steps, warmup)`` picks the group size S (and
+at most one remainder graph) that needs the FEWEST replays for the ``steps`` timed steps; among equal
+counts it prefers a tiling whose every graph the ``warmup`` steps can replay first (ending with an
+S-group right before the timed region), then the larger group.  Round 4 preferred coverage first (a
+freshly captured graph ran slow on its first launches); since every graph is uploaded right after
+capture (``hipGraphUpload``), the driver's 20 / 5 command measured faster with two 10-step replays
+(the timed graph not replayed in warmup) than with four covered 5-step replays: 0.3008 vs 0.3059
+ms/step median of six interleaved runs, 0.2935 vs 0.2969 of three on another box
+(profiles/r5/batch20/, batch6/).
 
-Example: 20 timed / 5 warmup steps -> S = 5: warmup [5], timed [5, 5, 5, 5] (one graph, four
-replays); 200 / 20 -> S = 8: warmup [4, 8, 8], timed [8] * 25.
+Example: 20 timed / 5 warmup steps -> S = 10: warmup [5] (its own graph), timed [10, 10];
+200 / 20 -> S = 10: warmup [10, 10], timed [10] * 20.
 """
 
 from __future__ import annotations
@@ -29,7 +33,7 @@ class Tiling:
         return sorted(set(self.timed) | set(self.warm))
 
 
-def tile(steps: int, warmup: int, max_group: int = 8, exact: bool = False) -> Tiling:
+def tile(steps: int, warmup: int, max_group: int = 10, exact: bool = False) -> Tiling:
     """``exact``: use group size ``max_group`` (capped at ``steps``) whatever the warmup covers."""
     steps, warmup = int(steps), int(warmup)
     if steps < 1 or warmup < 0:
@@ -41,7 +45,7 @@ def tile(steps: int, warmup: int, max_group: int = 8, exact: bool = False) -> Ti
         need = s + r  # one replay of each timed graph; the S-group last
         replays = steps // s + (1 if r else 0)
         ok = warmup >= need
-        key = (not ok, replays, -s)  # covered first, then fewest replays, then the larger group
+        key = (replays, not ok, -s)  # fewest replays, then covered, then the larger group
         if best is None or key < best[0]:
             best = (key, s, r, ok)
     _, s, r, ok = best

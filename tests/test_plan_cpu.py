@@ -11,7 +11,7 @@ from sparse_coding__amd.parallel import comm_model
 def test_tile_covers_and_counts(steps, warmup):
     t = tile(steps, warmup)
     assert sum(t.timed) == steps and sum(t.warm) == warmup
-    assert max(t.timed) <= 8 and len(set(t.timed)) <= 2  # one group size + at most one remainder
+    assert max(t.timed) <= 10 and len(set(t.timed)) <= 2  # one group size + at most one remainder
     if t.covered:  # every timed graph replayed in the warmup, a timed-size group last
         assert set(t.timed) <= set(t.warm) and t.warm[-1] == t.group
     else:
@@ -19,8 +19,9 @@ def test_tile_covers_and_counts(steps, warmup):
 
 
 def test_tile_driver_command_and_long_run():
-    assert tile(20, 5).timed == (5, 5, 5, 5) and tile(20, 5).warm == (5,)
-    assert tile(200, 20).timed == (8,) * 25 and tile(200, 20).warm == (4, 8, 8)
+    assert tile(20, 5).timed == (10, 10) and tile(20, 5).warm == (5,) and not tile(20, 5).covered
+    assert tile(200, 20).timed == (10,) * 20 and tile(200, 20).warm == (10, 10) and tile(200, 20).covered
+    assert tile(192, 32).timed == (10,) * 19 + (2,) and tile(192, 32).covered
     assert tile(20, 5, 8, exact=True).timed == (8, 8, 4)
     assert chunks(19, 8) == [8, 8, 3] and count_pattern(5) == (True, False, False, False, False)
     assert count_pattern(17, 8) == tuple(i in (0, 8, 16) for i in range(17))
