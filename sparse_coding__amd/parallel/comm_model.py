@@ -118,6 +118,8 @@ def calibrate(info, shape: StepShape, reps: int = 5) -> Optional[Dict[str, Dict[
     import torch
     import torch.distributed as dist
 
+    from .dist import barrier
+
     if not getattr(info, "enabled", False) or info.world_size <= 1:
         return None
     world = info.world_size
@@ -129,7 +131,7 @@ def calibrate(info, shape: StepShape, reps: int = 5) -> Optional[Dict[str, Dict[
             fn()
         ts = []
         for _ in range(reps):
-            dist.barrier()
+            barrier(info)
             if cuda:
                 torch.cuda.synchronize(dev)
             t = time.perf_counter()
