@@ -88,8 +88,6 @@ class FusedTopKEnsemble:
         if sdt not in ("fp32", "bf16"):
             raise ValueError(f"scores_dtype must be 'fp32' or 'bf16', got {sdt!r}")
         self.scores = torch.empty(G, B, n, device=dev, dtype=torch.bfloat16 if sdt == "bf16" else torch.float32)
-        # bf16 select: a wave per row by default (SC_TOPK_SELECT=block: a block per row)
-        self._select_kernel = "block" if os.environ.get("SC_TOPK_SELECT") == "block" else "wave"
         # pick buffers, alternating per step: the decode of step t zeroes step t-1's picks in the
         # dense code / dscore buffers (no separate clear launch)
         self.idx_buf = torch.zeros(2, G, B, kmax, device=dev, dtype=torch.int32)
@@ -131,8 +129,7 @@ class FusedTopKEnsemble:
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
         idx, prev = self.idx_buf[cur], self.idx_buf[1 - cur]
         gemm_ops.matmul_nt(x, self.shadow, self.scores)
-        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow,
-                             kernel=self._select_kernel)
+        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow)
         topk_ops.decode_grad(idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
                              self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from)
         alpha = 2.0 / (B * d)

@@ -623,92 +623,6 @@ __device__ __forceinline__ uint32_t order16(uint32_t h) {
 }
 constexpr int TIE_CAP = 64;
 
-// One wave: the exact top-k among `total` (<= CAP) candidate keys parked in LDS (ckey / ccol; every key
-// above the threshold and every key equal to it is among them): 16-bit bisection, exact fp32 ranking of
-// ambiguous threshold ties (see above), output in candidate order.
-template <int CAP>
-__device__ __forceinline__ void finish16(int k, int lane, int total, const uint16_t* S, int* I, float* V, int relu,
-                                         const uint32_t* ckey, const int* ccol, int* tcol, float* tsc, int* tkeep,
-                                         const uint16_t* Xr, const uint16_t* Dg, int d) {
-  const int nq = (total + 63) >> 6;
-  uint32_t ck[CAP / 64];
-#pragma unroll
-  for (int q = 0; q < CAP / 64; ++q) ck[q] = (q < nq && q * 64 + lane < total) ? ckey[q * 64 + lane] : 0u;
-  uint32_t t = 0;
-#pragma unroll 1
-  for (int b = 15; b >= 0; --b) {
-    const uint32_t cand = t | (1u << b);
-    int cnt = 0;
-#pragma unroll
-    for (int q = 0; q < CAP / 64; ++q)
-      if (q < nq) cnt += __popcll(__ballot(ck[q] >= cand));
-    if (cnt >= k) t = cand;
-  }
-  int gt = 0, nt = 0;
-#pragma unroll
-  for (int q = 0; q < CAP / 64; ++q)
-    if (q < nq) {
-      gt += __popcll(__ballot(ck[q] > t));
-      nt += __popcll(__ballot(ck[q] == t && q * 64 + lane < total));
-    }
-  const int need = k - gt;
-  // ambiguous ties: exact fp32 scores of the keys equal to t, the `need` largest kept
-  const bool exact = Xr && nt > need && nt <= TIE_CAP;
-  if (exact) {
-    int e0 = 0;
-#pragma unroll
-    for (int q = 0; q < CAP / 64; ++q)
-      if (q < nq) {
-        const bool eq = ck[q] == t && q * 64 + lane < total;
-        const uint64_t me = __ballot(eq);
-        if (eq) tcol[e0 + lanes_below(me)] = ccol[q * 64 + lane];
-        e0 += __popcll(me);
-      }
-    for (int e = 0; e < nt; ++e) {
-      const uint16_t* Dr = Dg + (long)tcol[e] * d;
-      float dot = 0.f;
-      for (int x = lane * 4; x < d; x += 256) {
-        const ushort4 a = *reinterpret_cast<const ushort4*>(Xr + x);
-        const ushort4 r = *reinterpret_cast<const ushort4*>(Dr + x);
-        dot += bf2f(a.x) * bf2f(r.x) + bf2f(a.y) * bf2f(r.y) + bf2f(a.z) * bf2f(r.z) + bf2f(a.w) * bf2f(r.w);
-      }
-      dot = wave_sum(dot);
-      if (lane == 0) tsc[e] = dot;
-    }
-    if (lane < nt) {
-      const float sv = tsc[lane];
-      const int cv = tcol[lane];
-      int rank = 0;
-      for (int e = 0; e < nt; ++e) {
-        const float so = tsc[e];
-        rank += (so > sv || (so == sv && tcol[e] < cv)) ? 1 : 0;
-      }
-      tkeep[lane] = rank < need ? 1 : 0;
-    }
-  }
-  int base = 0, ties = 0;
-#pragma unroll
-  for (int q = 0; q < CAP / 64; ++q) {
-    if (q < nq) {
-      const uint32_t kk = ck[q];
-      const bool eq = kk == t && q * 64 + lane < total;
-      const uint64_t me = __ballot(eq);
-      const int te = ties + lanes_below(me);
-      const bool take = kk > t || (eq && (exact ? tkeep[te] != 0 : te < need));
-      const uint64_t mt = __ballot(take);
-      if (take) {
-        const int pos = base + lanes_below(mt);
-        const int col = ccol[q * 64 + lane];
-        const float sv = bf2f(S[col]);
-        I[pos] = col;
-        V[pos] = relu ? fmaxf(sv, 0.f) : sv;
-      }
-      base += __popcll(mt);
-      ties += __popcll(me);
-    }
-  }
-}
-
 template <int PL>
 __device__ __forceinline__ bool bracket_select16(const uint32_t (&key)[PL], int k, int tid, int lane, int w,
                                                  const uint16_t* S, int* I, float* V, int relu, uint32_t* mx,
@@ -756,7 +670,85 @@ __device__ __forceinline__ bool bracket_select16(const uint32_t (&key)[PL], int 
         ++off;
       }
   __syncthreads();
-  if (w == 0) finish16<BR_CAP>(k, lane, total, S, I, V, relu, ckey, ccol, tcol, tsc, tkeep, Xr, Dg, d);
+  if (w == 0) {
+    const int nq = (total + 63) >> 6;
+    uint32_t ck[BR_CAP / 64];
+#pragma unroll
+    for (int q = 0; q < BR_CAP / 64; ++q) ck[q] = (q < nq && q * 64 + lane < total) ? ckey[q * 64 + lane] : 0u;
+    uint32_t t = 0;
+#pragma unroll 1
+    for (int b = 15; b >= 0; --b) {
+      const uint32_t cand = t | (1u << b);
+      int cnt = 0;
+#pragma unroll
+      for (int q = 0; q < BR_CAP / 64; ++q)
+        if (q < nq) cnt += __popcll(__ballot(ck[q] >= cand));
+      if (cnt >= k) t = cand;
+    }
+    int gt = 0, nt = 0;
+#pragma unroll
+    for (int q = 0; q < BR_CAP / 64; ++q)
+      if (q < nq) {
+        gt += __popcll(__ballot(ck[q] > t));
+        nt += __popcll(__ballot(ck[q] == t && q * 64 + lane < total));
+      }
+    const int need = k - gt;
+    // ambiguous ties: exact fp32 scores of the keys equal to t, the `need` largest kept
+    const bool exact = Xr && nt > need && nt <= TIE_CAP;
+    if (exact) {
+      int e0 = 0;
+#pragma unroll
+      for (int q = 0; q < BR_CAP / 64; ++q)
+        if (q < nq) {
+          const bool eq = ck[q] == t && q * 64 + lane < total;
+          const uint64_t me = __ballot(eq);
+          if (eq) tcol[e0 + lanes_below(me)] = ccol[q * 64 + lane];
+          e0 += __popcll(me);
+        }
+      for (int e = 0; e < nt; ++e) {
+        const uint16_t* Dr = Dg + (long)tcol[e] * d;
+        float dot = 0.f;
+        for (int x = lane * 4; x < d; x += 256) {
+          const ushort4 a = *reinterpret_cast<const ushort4*>(Xr + x);
+          const ushort4 r = *reinterpret_cast<const ushort4*>(Dr + x);
+          dot += bf2f(a.x) * bf2f(r.x) + bf2f(a.y) * bf2f(r.y) + bf2f(a.z) * bf2f(r.z) + bf2f(a.w) * bf2f(r.w);
+        }
+        dot = wave_sum(dot);
+        if (lane == 0) tsc[e] = dot;
+      }
+      if (lane < nt) {
+        const float sv = tsc[lane];
+        const int cv = tcol[lane];
+        int rank = 0;
+        for (int e = 0; e < nt; ++e) {
+          const float so = tsc[e];
+          rank += (so > sv || (so == sv && tcol[e] < cv)) ? 1 : 0;
+        }
+        tkeep[lane] = rank < need ? 1 : 0;
+      }
+    }
+    int base = 0, ties = 0;
+#pragma unroll
+    for (int q = 0; q < BR_CAP / 64; ++q) {
+      if (q < nq) {
+        const uint32_t kk = ck[q];
+        const bool eq = kk == t && q * 64 + lane < total;
+        const uint64_t me = __ballot(eq);
+        const int te = ties + lanes_below(me);
+        const bool take = kk > t || (eq && (exact ? tkeep[te] != 0 : te < need));
+        const uint64_t mt = __ballot(take);
+        if (take) {
+          const int pos = base + lanes_below(mt);
+          const int col = ccol[q * 64 + lane];
+          const float sv = bf2f(S[col]);
+          I[pos] = col;
+          V[pos] = relu ? fmaxf(sv, 0.f) : sv;
+        }
+        base += __popcll(mt);
+        ties += __popcll(me);
+      }
+    }
+  }
   return true;
 }
 
@@ -1259,149 +1251,6 @@ __global__ __launch_bounds__(256) void topk_scatter_kernel(const int* __restrict
 }
 
 
-// Wave-per-row bf16 select (n <= 64 * PW): the row's keys live in one wave's VGPRs, two 16-bit keys
-// per register (lane L holds columns (i 64 + L) 8 + j), so there are no block barriers and no idle
-// waves while wave 0 of a block bisects: every wave brackets its own row.  The bracket: the k-th
-// largest of 256 group maxima (each lane's keys split into 4 disjoint groups) bounds the k-th key
-// from below; the keys reaching it are compacted into the wave's own LDS slice and finish16 picks the
-// exact top-k (fp32 recomputes of ambiguous threshold ties, as topk_bf16_kernel).  Over WCAP
-// candidates (heavy ties): full 16-bit bisection in registers, ties in column order.
-template <int PW>
-__global__ __launch_bounds__(256) void topk_bf16_wave_kernel(const uint16_t* __restrict__ scores,
-                                                           const int* __restrict__ kv, int* __restrict__ idx,
-                                                           float* __restrict__ val, long rows, int B, int n, int kmax,
-                                                           int absolute, int relu, const uint16_t* __restrict__ X,
-                                                           long sx, const uint16_t* __restrict__ D, int d) {
-  static_assert(PW % 8 == 0, "8 keys per 16-byte load");
-  constexpr int WCAP = 512, NP = PW / 2;  // candidates per wave; packed key pairs per lane
-  __shared__ uint32_t ckey_s[4][WCAP];
-  __shared__ int ccol_s[4][WCAP];
-  __shared__ int tcol_s[4][TIE_CAP], tkeep_s[4][TIE_CAP];
-  __shared__ float tsc_s[4][TIE_CAP];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long row = (long)blockIdx.x * 4 + w;
-  if (row >= rows) return;  // (the whole wave)
-  const int g = (int)(row / B), b = (int)(row % B);
-  const int k = min(kv[g], n);
-  const uint16_t* S = scores + row * n;
-  int* I = idx + row * kmax;
-  float* V = val + row * kmax;
-  // kp[4 i + q]: columns (i 64 + lane) 8 + 2 q (low half) and + 2 q + 1 (high half)
-  uint32_t kp[NP];
-#pragma unroll
-  for (int i = 0; i < PW / 8; ++i) {
-    const int c = (i * 64 + lane) * 8;
-    const uint4 v = *reinterpret_cast<const uint4*>(S + (min(c, n - 8) & ~7));
-    const uint32_t live = 0u - (uint32_t)(c < n);
-    const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t lo = wv[q] & 0xffffu, hi = wv[q] >> 16;
-      const uint32_t klo = order16(absolute ? (lo & 0x7fffu) : lo), khi = order16(absolute ? (hi & 0x7fffu) : hi);
-      kp[4 * i + q] = (klo | (khi << 16)) & live;
-    }
-  }
-  auto key_lo = [](uint32_t x) { return x & 0xffffu; };
-  auto key_hi = [](uint32_t x) { return x >> 16; };
-  // (an empty asm "redefines" the packed pairs before each pass, so the compiler re-extracts the halves
-  // there instead of keeping both unpacked halves of every pair live across passes: 2x the registers)
-  auto repack = [&]() {
-#pragma unroll
-    for (int p = 0; p < NP; ++p) asm volatile("" : "+v"(kp[p]));
-  };
-  bool done = false;
-  if (k > 0 && k <= 256) {
-    uint32_t m[4] = {0u, 0u, 0u, 0u};
-    repack();
-#pragma unroll
-    for (int p = 0; p < NP; ++p) m[p & 3] = max(m[p & 3], max(key_lo(kp[p]), key_hi(kp[p])));
-    uint32_t lo = 0;
-#pragma unroll 1
-    for (int bb = 15; bb >= 0; --bb) {
-      const uint32_t cand = lo | (1u << bb);
-      const int cnt = __popcll(__ballot(m[0] >= cand)) + __popcll(__ballot(m[1] >= cand)) +
-                      __popcll(__ballot(m[2] >= cand)) + __popcll(__ballot(m[3] >= cand));
-      if (cnt >= k) lo = cand;
-    }
-    int c = 0;
-    repack();
-#pragma unroll
-    for (int p = 0; p < NP; ++p) c += (key_lo(kp[p]) >= lo ? 1 : 0) + (key_hi(kp[p]) >= lo ? 1 : 0);
-    const int incl = wave_incl_scan(c, lane);
-    const int total = __builtin_amdgcn_readlane(incl, 63);
-    if (total <= WCAP) {
-      int off = incl - c;
-      repack();
-#pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        const int col = ((p >> 2) * 64 + lane) * 8 + 2 * (p & 3);
-        if (key_lo(kp[p]) >= lo) { ckey_s[w][off] = key_lo(kp[p]); ccol_s[w][off] = col; ++off; }
-        if (key_hi(kp[p]) >= lo) { ckey_s[w][off] = key_hi(kp[p]); ccol_s[w][off] = col + 1; ++off; }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const uint16_t* Xr = (X && !absolute) ? X + (long)g * sx + (long)b * d : nullptr;
-      const uint16_t* Dg = D ? D + (long)g * n * d : nullptr;
-      finish16<WCAP>(k, lane, total, S, I, V, relu, ckey_s[w], ccol_s[w], tcol_s[w], tsc_s[w], tkeep_s[w], Xr, Dg, d);
-      done = true;
-    }
-  }
-  if (k > 0 && !done) {  // full 16-bit bisection in registers; ties at the threshold in column order
-    uint32_t t = 0;
-#pragma unroll 1
-    for (int bb = 15; bb >= 0; --bb) {
-      const uint32_t cand = t | (1u << bb);
-      int cnt = 0;
-      repack();
-#pragma unroll
-      for (int p = 0; p < NP; ++p) cnt += (key_lo(kp[p]) >= cand ? 1 : 0) + (key_hi(kp[p]) >= cand ? 1 : 0);
-      if (wave_total(cnt) >= k) t = cand;
-    }
-    int c2 = 0;
-    repack();
-#pragma unroll
-    for (int p = 0; p < NP; ++p) c2 += (key_lo(kp[p]) > t ? 1 : 0) + (key_hi(kp[p]) > t ? 1 : 0);
-    const int need_ties = k - wave_total(c2);
-    int base = 0, ties_seen = 0;
-#pragma unroll
-    for (int i = 0; i < PW / 8; ++i) {  // chunk i: columns [512 i, 512 i + 512), lane-major = column order
-      int neq = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) neq += (key_lo(kp[4 * i + q]) == t ? 1 : 0) + (key_hi(kp[4 * i + q]) == t ? 1 : 0);
-      const int ie = wave_incl_scan(neq, lane);
-      int tie_rank = ties_seen + ie - neq;
-      bool take[8];
-      int ns = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t kk = (j & 1) ? key_hi(kp[4 * i + j / 2]) : key_lo(kp[4 * i + j / 2]);
-        take[j] = kk > t || (kk == t && tie_rank < need_ties);
-        tie_rank += kk == t ? 1 : 0;
-        ns += take[j] ? 1 : 0;
-      }
-      const int is = wave_incl_scan(ns, lane);
-      int pos = base + is - ns;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (take[j]) {
-          const int col = (i * 64 + lane) * 8 + j;
-          const float sv = bf2f(S[col]);
-          I[pos] = col;
-          V[pos] = relu ? fmaxf(sv, 0.f) : sv;
-          ++pos;
-        }
-      }
-      base += __builtin_amdgcn_readlane(is, 63);
-      ties_seen += __builtin_amdgcn_readlane(ie, 63);
-    }
-  }
-  for (int j = k + lane; j < kmax; j += 64) {
-    I[j] = 0;
-    V[j] = 0.f;
-  }
-}
-
 }  // namespace scamd
 
 using namespace scamd;
@@ -1441,29 +1290,16 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
   return 1;
 }
 
-// Per-row top-k of bf16 scores [G][B][n] (topk_bf16_wave_kernel; block = 1 or past 8192 columns:
-// topk_bf16_kernel).  X ([B][d], or [G][B][d] with sx = B d)
+// Per-row top-k of bf16 scores [G][B][n] (see topk_bf16_kernel).  X ([B][d], or [G][B][d] with sx = B d)
 // and D ([G][n][d]) are the scores GEMM's bf16 operands, read to resolve ambiguous ties exactly (null:
 // ties in column order); absolute = select by |score| (no exact tie resolution).
 int sc_topk_select_bf16(const void* scores, const int* k, int* idx, float* val, int G, int B, int n, int kmax,
-                        int absolute, int relu, const void* X, long sx, const void* D, int d, int block,
-                        hipStream_t stream) {
+                        int absolute, int relu, const void* X, long sx, const void* D, int d, hipStream_t stream) {
   if (n % 8 || n < 8 || kmax < 1 || (X && (!D || d % 4 || d < 4))) return 1;
   dim3 grid((unsigned)G * B);
   const uint16_t* S = reinterpret_cast<const uint16_t*>(scores);
   const uint16_t* Xp = reinterpret_cast<const uint16_t*>(X);
   const uint16_t* Dp = reinterpret_cast<const uint16_t*>(D);
-  // wave per row (no block barriers) up to 128 keys per lane; block = 1: the block-per-row kernel
-  if (!block && n <= 64 * 128) {
-    const long rows = (long)G * B;
-    dim3 wgrid((unsigned)((rows + 3) / 4));
-#define SC_W16(P) \
-    if (n <= 64 * P) { hipLaunchKernelGGL((topk_bf16_wave_kernel<P>), wgrid, dim3(256), 0, stream, S, k, idx, val, rows, B, \
-                                          n, kmax, absolute, relu, Xp, sx, Dp, d); \
-      return hipGetLastError() == hipSuccess ? 0 : 3; }
-    SC_W16(16) SC_W16(32) SC_W16(64) SC_W16(96) SC_W16(128)
-#undef SC_W16
-  }
 #define SC_B16(P) \
   if (n <= 256 * P) { hipLaunchKernelGGL((topk_bf16_kernel<P>), grid, dim3(256), 0, stream, S, k, idx, val, B, n, kmax, \
                                          absolute, relu, Xp, sx, Dp, d); \

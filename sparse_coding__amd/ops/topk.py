@@ -8,7 +8,7 @@ from . import _lib
 
 
 def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool = False, relu: bool = True,
-                out=None, x: torch.Tensor = None, D: torch.Tensor = None, kernel: str = "wave"):
+                out=None, x: torch.Tensor = None, D: torch.Tensor = None):
     """Per-row top-k of ``scores`` [G, B, n] (fp32, or bf16) with per-model ``k`` (int32 [G]).
 
     Returns (idx int32 [G, B, kmax], val fp32 [G, B, kmax]); slots >= k[g] are (0, 0.0).
@@ -20,8 +20,7 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
     GEMM accumulated -- bf16 rounding is monotone, so only keys equal to the k-th largest bf16 key
     are ambiguous, and with ``x`` ([B, d] or [G, B, d] bf16) and ``D`` ([G, n, d] bf16, the GEMM's
     operands) those are ranked by their exact fp32 scores (ties to the lower column; without them,
-    or beyond 64 such keys, by column).  Values are the bf16 scores.  ``kernel``: "wave" (a wave per row,
-    n <= 8192) or "block" (a block per row) for bf16 scores."""
+    or beyond 64 such keys, by column).  Values are the bf16 scores."""
     G, B, n = scores.shape
     bf = scores.dtype == torch.bfloat16
     if scores.dtype not in (torch.float32, torch.bfloat16) or not scores.is_contiguous():
@@ -48,8 +47,7 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
             sx = B * d if x.dim() == 3 else 0
         rc = _lib.lib().sc_topk_select_bf16(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n,
                                             kmax, int(absolute), int(relu), _lib.ptr(x), sx,
-                                            _lib.ptr(D if x is not None else None), d, int(kernel == "block"),
-                                            _lib.stream_handle())
+                                            _lib.ptr(D if x is not None else None), d, _lib.stream_handle())
         _lib.check(rc, "sc_topk_select_bf16")
         return idx, val
     rc = _lib.lib().sc_topk_select(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n, kmax,

@@ -355,9 +355,8 @@ def test_topk_select_exact(n):
     torch.testing.assert_close(va[2].abs().sort(-1).values, ref)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "block"])
 @pytest.mark.parametrize("n", [6144, 1024])
-def test_topk_select_bf16_picks_are_fp32_topk(n, kernel):
+def test_topk_select_bf16_picks_are_fp32_topk(n):
     """Select on the scores GEMM's bf16 output: the picks are the top-k of the fp32 scores the GEMM
     accumulated (bf16 ties at the threshold ranked by exact recomputes from x and D), the values
     are the bf16 scores; clustered near-equal scores, duplicated atoms and an all-zero row (heavy
@@ -380,7 +379,7 @@ def test_topk_select_bf16_picks_are_fp32_topk(n, kernel):
     gemm_ops.matmul_nt(x, D, sb)
     exact = torch.einsum("bd,gnd->gbn", x.double(), D.double())
     k = torch.tensor([8, 64, 128], device=DEV, dtype=torch.int32)
-    idx, val = T.topk_select(sb, k, 128, x=x, D=D, kernel=kernel)
+    idx, val = T.topk_select(sb, k, 128, x=x, D=D)
     torch.cuda.synchronize()
     tol = 1e-5 * exact.abs().amax().item()
     nres = 0
@@ -405,10 +404,8 @@ def test_topk_select_bf16_picks_are_fp32_topk(n, kernel):
     assert set(idx[0, 40, :8].tolist()) == set(range(8))  # all-zero row: ties by column
     has5, has7 = (idx[1, :, :64] == 5).any(-1), (idx[1, :, :64] == 7).any(-1)
     assert not (has7 & ~has5).any()  # equal exact scores: the lower column first
-    idx2, val2 = T.topk_select(sb, k, 128, x=x, D=D, kernel=kernel)
+    idx2, val2 = T.topk_select(sb, k, 128, x=x, D=D)
     assert torch.equal(idx2, idx) and torch.equal(val2, val)  # deterministic
-    other, _ = T.topk_select(sb, k, 128, x=x, D=D, kernel="block" if kernel == "wave" else "wave")
-    assert torch.equal(other.sort(-1).values, idx.sort(-1).values)  # both kernels pick the same set
 
 
 def test_topk_scatter_and_clear_roundtrip():
