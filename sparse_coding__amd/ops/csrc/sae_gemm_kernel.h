@@ -610,16 +610,15 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   }
 }
 
-// (the software-pipelined BK32 x 3 loop: three waves per SIMD, so three blocks co-reside per CU)
+// One output tile (logical block `bid`) of a grouped GEMM launch, with its LDS ring at `smem`.
 template <class S, bool AK, bool BKM, int EPI, int BKT, int NST, bool P32 = false>
-__global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : 1) void sae_gemm_kernel(GemmParams p) {
+__device__ __forceinline__ void gemm_block(const GemmParams& p, const int bid, char* smem) {
   constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
   constexpr int TA = BM * BKT * 2, TBB = BN * BKT * 2;  // bytes per operand tile
   constexpr int PPWA = TA / 1024 / NW, PPWB = TBB / 1024 / NW;  // LDS-DMA pieces per wave
   constexpr int LPT = PPWA + PPWB;                       // DMA instructions per wave per K-tile
   constexpr int STG = TA + TBB;
   static_assert(PPWA * NW * 1024 == TA && PPWB * NW * 1024 == TBB, "tile must split into whole pieces");
-  __shared__ __attribute__((aligned(16))) char smem[NST * STG];
   SC_STAMP(0);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -629,7 +628,6 @@ __global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : 1) void sae_gemm_ker
   const int ptm = p.M / PT, ptn = p.N / PT;  // partial-buffer grid (128 x 128 sub-tiles)
   const int per_split = p.ncomp ? p.ctotal : tiles_m * tiles_n * p.G;
   const int per_prob = per_split * p.ksplit;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int pi = (int)fdiv(bid, p.f_prob);
   int rem = bid - pi * per_prob;
   const int ksi = (int)fdiv(rem, p.f_split);
@@ -973,6 +971,13 @@ __global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : 1) void sae_gemm_ker
   sae_epilogue<S, EPI, AUX_EARLY, STAGE, FSTAGE>(p, acc, auxv, biasv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn,
                                                  tiles_n, cptr, alpha, dead);
   SC_STAMP(3);
+}
+
+// (the software-pipelined BK32 x 3 loop: three waves per SIMD, so three blocks co-reside per CU)
+template <class S, bool AK, bool BKM, int EPI, int BKT, int NST, bool P32 = false>
+__global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : 1) void sae_gemm_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[NST * (S::BM + S::BN) * BKT * 2];
+  gemm_block<S, AK, BKM, EPI, BKT, NST, P32>(p, xcd_remap(blockIdx.x, gridDim.x), smem);
 }
 
 
