@@ -144,6 +144,30 @@ int main(int argc, char** argv) {
     run("dec_128", n_blocks<S128>(B, d, G, 1), [&] { launch<S128, 64, 2>(EPI_DEC, true, false, p, 1, 0); });
 #endif
   }
+#ifdef LAB_MASKED
+  {  // masked decoder (the masked-ensemble config: live sizes 512 * linspace(1, 5, 8) of a 2560 stack,
+     // K range cut per model on the device): which blocks share a CU, and how long each CU is busy
+    const int ns = 2560;
+    uint16_t *cm, *wm;
+    int* nact;
+    const int live[8] = {512, 804, 1097, 1389, 1682, 1974, 2267, 2560};
+    (void)hipMalloc(&cm, (long)G * B * ns * 2);
+    (void)hipMalloc(&wm, (long)G * ns * d * 2);
+    (void)hipMalloc(&nact, 8 * 4);
+    (void)hipMemcpy(nact, live, sizeof live, hipMemcpyHostToDevice);
+    fill_bf16(cm, (long)G * B * ns, 1.0f, 6);
+    fill_bf16(wm, (long)G * ns * d, 0.1f, 7);
+    GemmParams p{};
+    p.prob[0].a[0] = p.prob[0].a[1] = {cm, ns, (long)B * ns};
+    p.prob[0].b[0] = p.prob[0].b[1] = {wm, d, (long)ns * d};
+    p.prob[0].c = r; p.prob[0].alpha = 1.f; p.nprob = 1;
+    p.M = B; p.N = d; p.K1 = ns; p.K2 = 0; p.G = G; p.ldc = d; p.sc = (long)B * d;
+    p.aux = x; p.ldaux = d; p.saux = 0; p.part = part; p.ksplit = 1; p.nact_k = nact;
+    run("dec_masked", n_blocks<S128>(B, d, G, 1), [&] { launch<S128, 64, 2>(EPI_DEC, true, false, p, 1, 0); });
+    p.nact_k = nullptr;
+    run("dec_unmasked2560", n_blocks<S128>(B, d, G, 1), [&] { launch<S128, 64, 2>(EPI_DEC, true, false, p, 1, 0); });
+  }
+#endif
   {  // code gradient: dpre = 1[c > 0] (R Wd^T + l d / 2), activity from the bitmask, 128x128 BK32x3
     GemmParams p{};
     float* l1;

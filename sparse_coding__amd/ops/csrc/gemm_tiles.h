@@ -86,6 +86,9 @@ struct GemmParams {
   // masked ensembles: per-group live extent of the n dimension when it is M / K (may be null)
   const int* nact_m;
   const int* nact_k;
+  // masked decoder (nact_k only): block pairing so the two tiles that share a CU carry models g and
+  // G-1-g (set by the launcher, see sae_gemm_kernel.h pair_order)
+  int pair_k;
   // host-precomputed divisors of the block -> tile decomposition (set by the launcher)
   FDiv f_prob, f_split, f_plane, f_tn, f_ksplit;
   // --- EPI_ENC_ACT / EPI_DC_ACT: activation mode and the threshold SAE's per-feature s^2

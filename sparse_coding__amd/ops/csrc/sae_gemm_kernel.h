@@ -49,6 +49,7 @@
 #include "gemm_tiles.h"
 
 #include <algorithm>
+#include <stdlib.h>
 
 namespace scamd {
 
@@ -654,6 +655,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& p, const int bid, c
     // with model-major order the XCD-aware remap hands each XCD one model's tiles and the XCD
     // holding the largest model bounds the launch (measured 0.83x of unmasked at 60% live)
     g = rem % p.G;
+    if (p.pair_k && ((rem >> 5) & 1)) g = p.G - 1 - g;  // (bijective: a tile row's G entries flip together)
     const int t = rem / p.G;
     tm = (int)fdiv(t, p.f_tn);
     tn = t - tm * tiles_n;
@@ -1031,6 +1033,23 @@ long compact_tiles(int epi, GemmParams& p) {
   return total;
 }
 
+// Host: the masked decoder's block pairing.  Its per-model K range (live size) sets each tile's cost,
+// and a CU's two co-resident tiles share its operand feed, so a CU is busy for about the SUM of its
+// tiles' K ranges.  The hardware places blocks j and j + 32 of one XCD's dispatch sequence (j = blockIdx
+// / 8) on the same CU (per-block HW_ID stamps, profiles/r5/batch28/); with the model index varying
+// fastest both carried the same model, so the CUs holding the largest model paired two full-K tiles and
+// set the launch.  Flipping the model index of every second run of 32 logical tiles (g -> G-1-g) pairs
+// g with G-1-g instead: every CU then carries about the mean K range.  Needs the XCD runs of xcd_remap
+// to start on multiples of 32 and G | 32; otherwise the order is unchanged.
+inline int pair_order(const GemmParams& p, long comp, long nwg, int nprob) {
+  static const int enabled = [] {
+    const char* e = getenv("SC_PAIR_K");
+    return e ? atoi(e) : 1;
+  }();
+  return enabled && !comp && p.nact_k && !p.nactive && !p.nact_m && p.ksplit == 1 && nprob == 1 && p.G >= 2 &&
+         32 % p.G == 0 && nwg % 256 == 0;
+}
+
 template <class S, int BKT, int NST, bool FULL = true, bool P32 = false>
 int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t stream) {
   set_divisors<S>(p);
@@ -1040,6 +1059,7 @@ int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t strea
     p.f_prob = make_fdiv((uint32_t)(comp * p.ksplit));
   }
   const dim3 grid((unsigned)((comp ? comp * nprob : n_blocks<S>(p.M, p.N, p.G, nprob)) * p.ksplit)), block(S::NT);
+  p.pair_k = pair_order(p, comp, grid.x, nprob);
   if constexpr (!FULL) {
     // (the BK32 rings: the fused step epilogues, the fp32 weight-gradient layout and the bf16 plain
     // epilogue in the top-k layouts -- scores x D^T, codes^T R)
