@@ -55,7 +55,8 @@ def auto_sparse_k(B: int, n: int, d: int, margin: float = 1.3) -> int:
 
 class FusedTopKEnsemble:
     def __init__(self, models, sig=None, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999), eps=1e-8,
-                 grad_dtype: str = "bf16", sparse_k: Union[int, str] = "auto", scores_dtype: Optional[str] = None):
+                 grad_dtype: str = "bf16", sparse_k: Union[int, str] = "auto", scores_dtype: Optional[str] = None,
+                 gemm_k: Optional[int] = None):
         from ..models.topk import TopKEncoder
 
         self.sig = sig or TopKEncoder
@@ -108,6 +109,19 @@ class FusedTopKEnsemble:
         # the decode scatters codes / code gradients only for the dense-wgrad models (config 4:
         # 1.054 vs 1.059 ms/step scattering for all, profiles/r4/topk_scatter/)
         self._dense_from = gs
+        # decode + code gradients: the trailing models with k >= gemm_k run them as two dense MFMA GEMMs
+        # over the scattered codes (EPI_DEC: R = codes D_hat - x with per-tile R^2 partials; EPI_DC:
+        # dscore = 1[code > 0] (R D_hat^T)) instead of the per-row gather, whose cost grows with k
+        # (0 or unset: every model gathers; SC_TOPK_GEMM_K)
+        gk = int(os.environ.get("SC_TOPK_GEMM_K", "0") if gemm_k is None else gemm_k)
+        gg = G
+        while gk > 0 and gg > gs and ks[gg - 1] >= gk:
+            gg -= 1
+        self.gemm_g0 = gg
+        if gg < G:
+            self._gm_part = torch.zeros(G - gg, (B // 128) * (d // 128), device=dev)
+            self._gm_colpart = torch.empty(G - gg, B // 128, n, device=dev)
+            self._gm_l1 = torch.zeros(G - gg, device=dev)
         self.lists = topk_ops.SlotLists(gs, B, n, ks, kmax, dev) if gs else None
         self.dscv = torch.zeros(G, B, kmax, device=dev) if gs else None
         # bf16 dictionary gradient by default: the dense GEMM's bf16 epilogue + Adam's bf16 loads
@@ -130,8 +144,13 @@ class FusedTopKEnsemble:
         idx, prev = self.idx_buf[cur], self.idx_buf[1 - cur]
         gemm_ops.matmul_nt(x, self.shadow, self.scores)
         topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow)
+        gg = self.gemm_g0
         topk_ops.decode_grad(idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
-                             self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from)
+                             self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from, gemm_from=gg)
+        if gg < G:
+            gemm_ops.decode_residual(self.codebuf[gg:], self.shadow[gg:], x, self.r[gg:], self._gm_part)
+            gemm_ops.code_grad(self.r[gg:], self.shadow[gg:], self.codebuf[gg:], self._gm_l1, self.dscbuf[gg:],
+                               self._gm_colpart)
         alpha = 2.0 / (B * d)
         gs = self.sparse_g
         if gs:
@@ -142,9 +161,11 @@ class FusedTopKEnsemble:
         if self._tail:
             adam_ops.topk_tail(self.params["dict"], self.g, self.m["dict"], self.v["dict"], self.shadow, self.norms,
                                self.lr, *self.betas, self.eps, self.step_dev, self.row_se, self.mse, 1.0 / (B * d),
-                               self._ticket, gather=gather)
+                               self._ticket, gather=gather, se_part=self._gm_part if gg < G else None, se_g0=gg)
             return
         torch.mul(torch.sum(self.row_se, dim=1), 1.0 / (B * d), out=self.mse)
+        if gg < G:
+            torch.mul(torch.sum(self._gm_part, dim=1), 1.0 / (B * d), out=self.mse[gg:])
         adam_ops.adam_rows([dict(p=self.params["dict"], g=self.g, m=self.m["dict"], v=self.v["dict"],
                                  shadow=self.shadow, norms=self.norms, norm=True)],
                            self.lr, self.step_count + 1, *self.betas, self.eps, step_dev=self.step_dev)

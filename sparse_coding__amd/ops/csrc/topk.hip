@@ -885,7 +885,7 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
     const int* __restrict__ idx, const float* __restrict__ val, const int* __restrict__ kv,
     const uint16_t* __restrict__ D, const uint16_t* __restrict__ X, long sx, uint16_t* __restrict__ R,
     float* __restrict__ row_se, uint16_t* __restrict__ codebuf, uint16_t* __restrict__ dscbuf, int G, int B,
-    int n, int d, int kmax, float* __restrict__ dscv, const int* __restrict__ prev_idx, int g_dense0) {
+    int n, int d, int kmax, float* __restrict__ dscv, const int* __restrict__ prev_idx, int g_dense0, int g_gemm0) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)G * B) return;
@@ -893,6 +893,22 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
   const int k = min(kv[g], kmax);
   const int* I = idx + row * kmax;
   const float* V = val + row * kmax;
+  if (g >= g_gemm0) {
+    // models from g_gemm0 decode and take their code gradients as dense MFMA GEMMs over the code
+    // buffer (engine/topk.py): only the scatter of the codes here (previous picks cleared first)
+    if (!codebuf) return;
+    uint16_t* Cb = codebuf + row * (long)n;
+    if (prev_idx) {
+      const int* P = prev_idx + row * kmax;
+      for (int j = lane; j < kmax; j += 64) Cb[P[j]] = 0;
+      __builtin_amdgcn_s_waitcnt(0);
+    }
+    for (int j = lane; j < k; j += 64) {
+      const float w = V[j];
+      if (w > 0.f) Cb[I[j]] = f2bf(w);
+    }
+    return;
+  }
   const uint16_t* Dg = D + (long)g * n * d;
   float acc[NV * 4];
 #pragma unroll
@@ -1311,7 +1327,7 @@ int sc_topk_select_bf16(const void* scores, const int* k, int* idx, float* val, 
 
 int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const void* D, const void* X, long sx,
                         void* R, float* row_se, void* codebuf, void* dscbuf, int G, int B, int n, int d, int kmax,
-                        hipStream_t stream, float* dscv, const int* prev_idx, int g_dense0) {
+                        hipStream_t stream, float* dscv, const int* prev_idx, int g_dense0, int g_gemm0) {
   if (d % 4) return 1;
   const int nv = (d + 255) / 256;
   dim3 grid(((long)G * B + 3) / 4);
@@ -1319,7 +1335,7 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
   if (nv <= V) { hipLaunchKernelGGL((topk_decode_grad_kernel<V>), grid, dim3(256), 0, stream, idx, val, k, \
       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx, reinterpret_cast<uint16_t*>(R), \
       row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx, \
-      g_dense0); \
+      g_dense0, g_gemm0); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   SC_D(1) SC_D(2) SC_D(3) SC_D(4) SC_D(8) SC_D(16)
 #undef SC_D

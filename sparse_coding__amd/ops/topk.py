@@ -2,6 +2,8 @@
 
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 
 from . import _lib
@@ -57,14 +59,16 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
 
 
 def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dscv=None, prev_idx=None,
-                dense_from: int = 0):
+                dense_from: int = 0, gemm_from: Optional[int] = None):
     """Sparse decode + residual (bf16 r_out [G, B, d]) + per-row squared error; with the dense
     buffers, also scatter codes and code gradients <R, D[idx]> (units of R) for the wgrad GEMM;
     with ``dscv`` ([G, B, kmax] fp32) also the per-slot code gradients for ``sparse_wgrad``.
     ``prev_idx``: the previous step's picks ([G, B, kmax]), zeroed in the dense buffers first
     (instead of a ``clear`` after the previous weight gradient).  ``dense_from``: models below it
     (slot-list weight gradient) get their per-slot ``dscv`` only -- nothing is scattered into (or
-    cleared from) their dense buffers, which stay zero."""
+    cleared from) their dense buffers, which stay zero.  ``gemm_from``: models from it only get their
+    codes scattered into ``codebuf`` (previous picks cleared) -- their decode and code gradients run as
+    dense GEMMs over that buffer (engine/topk.py); nothing else of theirs is written here."""
     if prev_idx is not None and (prev_idx.shape != idx.shape or prev_idx.dtype != torch.int32
                                  or not prev_idx.is_contiguous()):
         raise ValueError("prev_idx must be contiguous int32 of idx's shape")
@@ -74,7 +78,7 @@ def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dsc
     rc = _lib.lib().sc_topk_decode_grad(_lib.ptr(idx), _lib.ptr(val), _lib.ptr(k), _lib.ptr(D), _lib.ptr(x), sx,
                                         _lib.ptr(r_out), _lib.ptr(row_se), _lib.ptr(codebuf), _lib.ptr(dscbuf),
                                         G, B, n, d, kmax, _lib.stream_handle(), _lib.ptr(dscv), _lib.ptr(prev_idx),
-                                        int(dense_from))
+                                        int(dense_from), int(G if gemm_from is None else gemm_from))
     _lib.check(rc, "sc_topk_decode_grad")
 
 

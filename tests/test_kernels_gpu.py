@@ -425,15 +425,18 @@ def test_topk_scatter_and_clear_roundtrip():
     assert int(code.ne(0).sum()) == 0
 
 
-@pytest.mark.parametrize("sparse_k,grad_dtype", [(0, "fp32"), (0, "bf16"), (1000, "fp32"), ("auto", "bf16")])
-def test_fused_topk_matches_autograd(sparse_k, grad_dtype):
+@pytest.mark.parametrize("sparse_k,grad_dtype,gemm_k", [(0, "fp32", 0), (0, "bf16", 0), (1000, "fp32", 0),
+                                                        ("auto", "bf16", 0), (0, "fp32", 16), (8, "bf16", 64)])
+def test_fused_topk_matches_autograd(sparse_k, grad_dtype, gemm_k):
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
     from sparse_coding__amd.models.topk import TopKEncoder
 
     torch.manual_seed(7)
     d, n, B = 256, 1024, 256
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
-    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, sparse_k=sparse_k, grad_dtype=grad_dtype)
+    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, sparse_k=sparse_k, grad_dtype=grad_dtype,
+                            gemm_k=gemm_k)
+    assert eng.gemm_g0 == {0: 3, 16: 1, 64: 2}[gemm_k]
     assert eng.g.dtype == (torch.bfloat16 if grad_dtype == "bf16" else torch.float32)
     assert eng.sparse_g == {0: 0, 1000: 3}.get(sparse_k, eng.sparse_g)
     x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
@@ -451,12 +454,13 @@ def test_fused_topk_matches_autograd(sparse_k, grad_dtype):
         assert agree.float().mean() > 0.97, agree.float().mean()
 
 
-@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
-def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype):
+@pytest.mark.parametrize("grad_dtype,gemm_k", [("fp32", 0), ("bf16", 0), ("bf16", 48)])
+def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype, gemm_k):
     """Config 4 shape (GPT-2-small residual d = 768, n = 6144, B = 2048, k = 8 .. 128): the
     dictionary gradient of EVERY model -- slot-list path for the small k, dense GEMM for the
-    rest -- against fp32 autograd of the top-k loss at the engine's own picks and the bf16
-    operands it multiplies; relative Frobenius error <= 1e-2."""
+    rest; with ``gemm_k`` the large-k models' decode and code gradients as dense GEMMs too --
+    against fp32 autograd of the top-k loss at the engine's own picks and the bf16 operands it
+    multiplies; relative Frobenius error <= 1e-2."""
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
     from sparse_coding__amd.models.topk import TopKEncoder
 
@@ -464,8 +468,9 @@ def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype):
     d, n, B = 768, 6144, 2048
     ks = [8, 16, 24, 32, 48, 64, 96, 128]
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in ks]
-    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, grad_dtype=grad_dtype)
+    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, grad_dtype=grad_dtype, gemm_k=gemm_k)
     assert 0 < eng.sparse_g < len(ks)  # both wgrad paths are exercised
+    assert eng.gemm_g0 == (4 if gemm_k else len(ks))
     D0 = eng.shadow.float().clone()
     feats = torch.nn.functional.normalize(torch.randn(4096, d, device=DEV), dim=-1)
     x = ((torch.relu(torch.randn(B, 4096, device=DEV) - 1.5) * 3.0) @ feats).to(torch.bfloat16)
@@ -485,17 +490,19 @@ def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype):
         torch.testing.assert_close(mse[g], loss.detach(), rtol=1e-2, atol=1e-5)
 
 
-def test_topk_tail_matches_separate_launches():
+@pytest.mark.parametrize("gemm_k", [0, 16])
+def test_topk_tail_matches_separate_launches(gemm_k):
     """The fused top-k tail (one launch: row Adam + per-model MSE + step counter) == the separate
     Adam launch, torch reductions and counter increment: masters, moments, shadows bit-equal over
-    three steps, MSE to fp32 rounding, the device counter advanced once per step."""
+    three steps, MSE to fp32 rounding, the device counter advanced once per step (``gemm_k``: the
+    GEMM-decoded models' MSE from the decoder's tile partials)."""
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
     from sparse_coding__amd.models.topk import TopKEncoder
 
     torch.manual_seed(23)
     d, n, B = 768, 1024, 256
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
-    fused, split = (FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3) for _ in range(2))
+    fused, split = (FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, gemm_k=gemm_k) for _ in range(2))
     assert fused._tail
     split._tail = False
     for t in range(3):
@@ -510,7 +517,8 @@ def test_topk_tail_matches_separate_launches():
     assert not fused._ticket.any()  # the completion counters reset themselves
 
 
-def test_fused_topk_graph_matches_eager():
+@pytest.mark.parametrize("gemm_k", [0, 16])
+def test_fused_topk_graph_matches_eager(gemm_k):
     """The two captured step graphs (alternating pick buffers: step t clears step t-1's picks
     in the dense buffers) == eager steps, bitwise, over several steps."""
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
@@ -519,7 +527,7 @@ def test_fused_topk_graph_matches_eager():
     torch.manual_seed(13)
     d, n, B = 256, 1024, 256
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
-    engs = [FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, sparse_k=8) for _ in range(2)]
+    engs = [FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, sparse_k=8, gemm_k=gemm_k) for _ in range(2)]
     engs[1].enable_graph()
     assert engs[0].sparse_g == 1
     for s in range(5):
