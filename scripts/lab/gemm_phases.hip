@@ -126,13 +126,18 @@ int main(int argc, char** argv) {
     p.prob[0].c = c; p.prob[0].alpha = 1.f; p.nprob = 1;
     p.M = B; p.N = n; p.K1 = d; p.K2 = 0; p.G = G; p.ldc = n; p.sc = (long)B * n;
     p.bias = bias; p.sbias = n; p.part = part; p.cmask = cmask; p.ksplit = 1;
-#ifndef LAB_BIG
+#if defined(LAB_256x128)
+    run("enc_256x128", n_blocks<S256x128>(B, n, G, 1), [&] { launch<S256x128, 64, 2>(EPI_ENC, true, true, p, 1, 0); });
+    run("nt_bf16_256x128", n_blocks<S256x128>(B, n, G, 1), [&] { launch<S256x128, 64, 2>(EPI_BF16, true, true, p, 1, 0); });
+    run("enc_128_bk32x3", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 32, 3, false, true>(EPI_ENC, true, true, p, 1, 0); });
+#elif !defined(LAB_BIG)
     run("enc_128_bk32x3", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 32, 3, false>(EPI_ENC, true, true, p, 1, 0); });
     run("enc_128", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 64, 2>(EPI_ENC, true, true, p, 1, 0); });
 #else
     run("enc_256", n_blocks<S256>(B, n, G, 1), [&] { launch<S256, 64, 2>(EPI_ENC, true, true, p, 1, 0); });
 #endif
   }
+#ifndef LAB_256x128
   {  // decoder: R = c Wd - x, 128x128
     GemmParams p{};
     p.prob[0].a[0] = p.prob[0].a[1] = {c, n, (long)B * n};
@@ -200,6 +205,7 @@ int main(int argc, char** argv) {
     run("wgrad_128", n_blocks<S128>(n, d, G, 2), [&] { launch<S128, 64, 2>(EPI_F32, false, false, p, 2, 0); });
 #endif
   }
+#endif
   printf("{\"status\": \"%s\"}\n", hipGetErrorString(hipGetLastError()));
   return 0;
 }

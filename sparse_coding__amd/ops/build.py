@@ -98,7 +98,8 @@ def _stale(target: Path, deps, key: str = None) -> bool:
 # Per-source extra flags.  sae_gemm.hip (128x128 blocks, software-pipelined K loop with two
 # MFMA groups per iteration) uses the VGPR form of the MFMA: with AGPR accumulators the
 # register allocator rotated them through v_accvgpr copies every iteration.
-EXTRA_FLAGS = {"sae_gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+EXTRA_FLAGS = {"sae_gemm.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
+               "sae_gemm_256x128.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def _compile_one(src: Path, force: bool) -> Path:

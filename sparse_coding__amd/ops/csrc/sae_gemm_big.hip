@@ -1,5 +1,5 @@
-// 256x128 and 256x256 block instantiations of the grouped SAE GEMM (see
-// sae_gemm_kernel.h).  Built WITHOUT -amdgpu-mfma-vgpr-form: these shapes keep 128
+// 256x256 block instantiations of the grouped SAE GEMM (see sae_gemm_kernel.h; 256x128 blocks:
+// sae_gemm_256x128.hip).  Built WITHOUT -amdgpu-mfma-vgpr-form: these shapes keep 128
 // accumulator registers per wave in AGPRs.
 #include "sae_gemm_kernel.h"
 
@@ -12,10 +12,7 @@ int launch_big(int shape, int pipe, int epi, bool ak, bool bk, const GemmParams&
     if (pipe == 2) return launch<S256, 32, 2, false>(epi, ak, bk, p, nprob, stream);
     return launch<S256, 64, 2>(epi, ak, bk, p, nprob, stream);
   }
-  // (256x128 on the BK32 rings, two blocks per CU, measured slower in the step: 0.302-0.307 vs
-  // 0.296-0.297 ms, profiles/r5/batch3/cfg14.jsonl)
-  if (pipe) return 8;
-  return launch<S256x128, 64, 2>(epi, ak, bk, p, nprob, stream);
+  return launch_256x128(pipe, epi, ak, bk, p, nprob, stream);
 }
 
 }  // namespace scamd

@@ -783,7 +783,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& p, const int bid, c
     for (int i = 0; i < WI; ++i) fa[i] = load_frag<AK, BKT>(la, wr * (WI * 16) + i * 16, ks, lane);
   };
 
-  if constexpr (BKT == 64 && S::BM == 128 && S::BN == 128) {
+  if constexpr (BKT == 64 && S::BN == 128 && (S::BM == 128 || S::BM == 256)) {
     // Software-pipelined K loop.  The fragments of K-step s+1 are read from LDS into the
     // second register set while the MFMAs of step s run, one LDS read slotted between
     // every few MFMAs (sched_group_barrier), so no MFMA waits on an LDS round trip.  The
@@ -1113,5 +1113,6 @@ int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t strea
 
 // 256x128 / 256x256 launches (sae_gemm_big.hip)
 int launch_big(int shape, int pipe, int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream);
+int launch_256x128(int pipe, int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream);
 
 }  // namespace scamd
