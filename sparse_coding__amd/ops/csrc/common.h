@@ -106,6 +106,28 @@ __device__ __forceinline__ float block_sum_lds(float v, float* red) {
   return r;
 }
 
+// Two block-wide sums behind ONE LDS-only barrier, for a block's last reduction: `red` (>= 2 NW
+// floats) is not reused afterwards, so the barrier that protects a reused scratch is not needed.
+// Every thread gets both totals (same summation order as block_sum_lds: bit-identical).
+template <int NW>
+__device__ __forceinline__ float2 block_sum2_final(float a, float b, float* red) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[2 * w] = a;
+    red[2 * w + 1] = b;
+  }
+  lds_barrier();
+  float2 r = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    r.x += red[2 * i];
+    r.y += red[2 * i + 1];
+  }
+  return r;
+}
+
 // Bijective XCD-aware block remap (MI355X has 8 XCDs, each with its own L2).
 // Hardware hands consecutive block ids to different XCDs round-robin; this
 // gives each XCD a contiguous run of logical tiles so neighbouring tiles that

@@ -119,7 +119,7 @@ __device__ __forceinline__ long long sc_memrealtime() {
 // barrier in here is LDS-only (lgkmcnt(0) + s_barrier), so in-flight global stores and
 // LDS-DMA prefetches of a persistent block are not drained.
 template <class S>
-constexpr int epi_scratch_floats() { return 2 * S::WGM * S::BN + S::NW; }
+constexpr int epi_scratch_floats() { return 2 * S::WGM * S::BN + 2 * S::NW; }
 
 // LDS-staged bf16 output stores (STAGE, 128x128 tile kernel: the ring is free after the K
 // loop): each wave parks its 64x64 bf16 sub-tile in LDS in the MFMA layout, then streams it
@@ -143,6 +143,7 @@ constexpr int stage_bytes() { return STAGE_OFF + S::NW * stage_wave<S>(); }
 template <class S, int EPI, bool AUX_EARLY, bool STAGE = false, bool FSTAGE = false>
 __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)[S::WI][S::WJ],
                                              const uint2 (&auxv)[S::WI][S::WJ], const f32x4_t (&biasv)[S::WJ],
+                                             const uint64_t (&mkv)[S::WI / 4],
                                              float* red, int pi, int g, int m0, int n0, int tn, int tiles_n,
                                              void* cptr, float alpha, bool dead = false) {
   constexpr int BM = S::BM, BN = S::BN, NT = S::NT, NW = S::NW, WI = S::WI, WJ = S::WJ, WGN = S::WGN;
@@ -155,7 +156,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   const bool p1 = pi != 0;
   const int rowb = m0 + wr * (WI * 16) + (lane & 15);
   const int colb = n0 + wc * (WJ * 16) + 4 * (lane >> 4);
-  static_assert(!STAGE || ((WI == 4 || WI == 8) && WJ == 4 && 2 * S::WGM * BN + NW <= STAGE_OFF / 4), "stage layout");
+  static_assert(!STAGE || ((WI == 4 || WI == 8) && WJ == 4 && 2 * S::WGM * BN + 2 * NW <= STAGE_OFF / 4), "stage layout");
   char* stage = reinterpret_cast<char*>(red) + STAGE_OFF + wid * stage_wave<S>();
   // one 4-wide bf16 output fragment (rows rowb + 16 i, columns colb + 16 j .. +3)
   auto put = [&](uint16_t* C, int i, int j, ushort4 h) {
@@ -422,8 +423,10 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
         if (l0_from_mask) l0 += (float)(__popc(mw[k][0]) + __popc(mw[k][1]));
       }
     }
-    l1 = block_sum_lds<NW>(l1, red + RED_SUM);  // its barriers also publish the colred_lane writes
-    l0 = block_sum_lds<NW>(l0, red + RED_SUM);
+    // one barrier: publishes the colred_lane writes too; `red` is not written after it
+    const float2 sums = block_sum2_final<NW>(l1, l0, red + RED_SUM);
+    l1 = sums.x;
+    l0 = sums.y;
     if (counting) colred_store(p.colpart, 0);
     scalar_partial(p.part, 2, 0, l1);
     scalar_partial(p.part, 2, 1, l0);
@@ -451,7 +454,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
       if (rcol) colred_lane(cs, j, 0);
     }
     flush(C);
-    se = block_sum_lds<NW>(se, red + RED_SUM);  // its barriers also publish the colred_lane writes
+    se = block_sum2_final<NW>(se, 0.f, red + RED_SUM).x;  // its barrier also publishes colred_lane's writes
     if (rcol) colred_store(p.rcol, 0);
     scalar_partial(p.part, 1, 0, se);
     return;
@@ -500,9 +503,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
     // EPI_DC with the code activity read from the encoder's bitmask (no norm-Jacobian dots)
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     const float add = p.l1[g] * p.l1_add_scale;
-    uint64_t mk[WI / 4];  // this lane's activity words (one 8-byte load per 64x64 block)
-#pragma unroll
-    for (int k = 0; k < WI / 4; ++k) mk[k] = p.cmask[mask_word(p, g, rowb - (lane & 15) + 64 * k, colb - 4 * (lane >> 4), lane)];
+    const uint64_t (&mk)[WI / 4] = mkv;  // this lane's activity words, fetched before the K loop
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
       f32x4_t cs = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -749,6 +750,15 @@ __device__ __forceinline__ void gemm_block(const GemmParams& p, const int bid, c
         auxv[i][j] = *reinterpret_cast<const uint2*>(X + (long)(rowb + i * 16) * p.ldaux + colb + j * 16);
   }
 
+  // The masked code gradient's activity words (one 8-byte load per 64x64 block; 2 registers even
+  // on the pipelined ring), fetched before the K loop like AUX_EARLY so their latency hides.
+  uint64_t mkv[WI / 4];
+  if constexpr (EPI == EPI_DC_MASK) {
+#pragma unroll
+    for (int k = 0; k < WI / 4; ++k)
+      mkv[k] = p.cmask[mask_word(p, g, rowb - (lane & 15) + 64 * k, colb - 4 * (lane >> 4), lane)];
+  }
+
   // The ReLU encoder epilogue's bias: loaded here, before the K-loop prologue issues its DMAs (so
   // the counted vmcnt waits below still see only tile DMAs as younger), its latency hidden.
   f32x4_t biasv[WJ];
@@ -970,7 +980,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& p, const int bid, c
   lds_barrier();  // all reads of the ring done before smem is reused below
   constexpr bool STAGE = (S::WI == 4 || S::WI == 8) && S::WJ == 4 && NST * STG >= stage_bytes<S>();
   constexpr bool FSTAGE = EPI == EPI_F32 && S::WJ == 4 && NST * STG >= S::NW * S::WI * 16 * STAGE_ROW;
-  sae_epilogue<S, EPI, AUX_EARLY, STAGE, FSTAGE>(p, acc, auxv, biasv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn,
+  sae_epilogue<S, EPI, AUX_EARLY, STAGE, FSTAGE>(p, acc, auxv, biasv, mkv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn,
                                                  tiles_n, cptr, alpha, dead);
   SC_STAMP(3);
 }
