@@ -88,7 +88,14 @@ class FusedTopKEnsemble:
         sdt = scores_dtype or os.environ.get("SC_TOPK_SCORES", "bf16")
         if sdt not in ("fp32", "bf16"):
             raise ValueError(f"scores_dtype must be 'fp32' or 'bf16', got {sdt!r}")
-        self.scores = torch.empty(G, B, n, device=dev, dtype=torch.bfloat16 if sdt == "bf16" else torch.float32)
+        # bf16 scores from the library GEMM (SC_TOPK_SCORES_GEMM=blas): x D_all^T over the stacked
+        # dictionaries as ONE plain hipBLASLt GEMM (the scores need no fused epilogue), written
+        # [B, G, n]; the select reads that layout directly
+        self._scores_blas = sdt == "bf16" and os.environ.get("SC_TOPK_SCORES_GEMM", "sc") == "blas"
+        if self._scores_blas:
+            self.scores = torch.empty(B, G, n, device=dev, dtype=torch.bfloat16)
+        else:
+            self.scores = torch.empty(G, B, n, device=dev, dtype=torch.bfloat16 if sdt == "bf16" else torch.float32)
         # pick buffers, alternating per step: the decode of step t zeroes step t-1's picks in the
         # dense code / dscore buffers (no separate clear launch)
         self.idx_buf = torch.zeros(2, G, B, kmax, device=dev, dtype=torch.int32)
@@ -142,8 +149,12 @@ class FusedTopKEnsemble:
     def _step_kernels(self, x, cur: int, gather=None):
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
         idx, prev = self.idx_buf[cur], self.idx_buf[1 - cur]
-        gemm_ops.matmul_nt(x, self.shadow, self.scores)
-        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow)
+        if self._scores_blas:
+            torch.matmul(x, self.shadow.view(G * n, d).t(), out=self.scores.view(B, G * n))
+            topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow, layout="bgn")
+        else:
+            gemm_ops.matmul_nt(x, self.shadow, self.scores)
+            topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow)
         gg = self.gemm_g0
         topk_ops.decode_grad(idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
                              self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from, gemm_from=gg)

@@ -98,7 +98,7 @@ def signatures():
                          c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long,
                          c_int, c_long, c_void_p, c_int, c_long, c_void_p, c_void_p],
         "sc_topk_select_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-                                c_void_p, c_long, c_void_p, c_int, c_void_p],
+                                c_void_p, c_long, c_void_p, c_int, c_void_p, c_int],
         "sc_topk_tail": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_void_p, c_float, c_float, c_float, c_void_p, c_int, c_void_p, c_int, c_float, c_void_p,
                          c_void_p, c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long, c_void_p,

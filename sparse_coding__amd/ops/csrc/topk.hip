@@ -756,7 +756,7 @@ template <int PL>
 __global__ __launch_bounds__(256) void topk_bf16_kernel(const uint16_t* __restrict__ scores, const int* __restrict__ kv,
                                                       int* __restrict__ idx, float* __restrict__ val, int B, int n,
                                                       int kmax, int absolute, int relu, const uint16_t* __restrict__ X,
-                                                      long sx, const uint16_t* __restrict__ D, int d) {
+                                                      long sx, const uint16_t* __restrict__ D, int d, int bgn) {
   static_assert(PL % 8 == 0, "8 keys per 16-byte load");
   __shared__ int red[2][4];
   __shared__ int wsum[2][4];
@@ -768,10 +768,15 @@ __global__ __launch_bounds__(256) void topk_bf16_kernel(const uint16_t* __restri
   __shared__ int tcol[TIE_CAP], tkeep[TIE_CAP];
   __shared__ float tsc[TIE_CAP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const long row = blockIdx.x;
-  const int g = (int)(row / B), b = (int)(row % B);
+  // bgn: scores laid out [B][G][n] (one library GEMM x D_all^T over the stacked dictionaries); the
+  // blocks then walk that layout in memory order; bgn == 2: the model index rotated by the batch row so
+  // an XCD (block % 8) does not get one model's rows -- k, and the select's cost, differ per model
+  const int G = (int)(gridDim.x / B);
+  const int b = bgn ? (int)(blockIdx.x / G) : (int)(blockIdx.x % B);
+  const int g = bgn ? (int)((blockIdx.x % G + (bgn == 2 ? b : 0)) % G) : (int)(blockIdx.x / B);
+  const long row = (long)g * B + b;  // output row (idx / val are [G][B][kmax])
   const int k = min(kv[g], n);
-  const uint16_t* S = scores + row * n;
+  const uint16_t* S = scores + (bgn ? (long)b * G + g : row) * n;
   int* I = idx + row * kmax;
   float* V = val + row * kmax;
   uint32_t key[PL];
@@ -1306,11 +1311,12 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
   return 1;
 }
 
-// Per-row top-k of bf16 scores [G][B][n] (see topk_bf16_kernel).  X ([B][d], or [G][B][d] with sx = B d)
+// Per-row top-k of bf16 scores [G][B][n], or [B][G][n] with bgn (see topk_bf16_kernel).  X ([B][d], or [G][B][d] with sx = B d)
 // and D ([G][n][d]) are the scores GEMM's bf16 operands, read to resolve ambiguous ties exactly (null:
 // ties in column order); absolute = select by |score| (no exact tie resolution).
 int sc_topk_select_bf16(const void* scores, const int* k, int* idx, float* val, int G, int B, int n, int kmax,
-                        int absolute, int relu, const void* X, long sx, const void* D, int d, hipStream_t stream) {
+                        int absolute, int relu, const void* X, long sx, const void* D, int d, hipStream_t stream,
+                        int bgn) {
   if (n % 8 || n < 8 || kmax < 1 || (X && (!D || d % 4 || d < 4))) return 1;
   dim3 grid((unsigned)G * B);
   const uint16_t* S = reinterpret_cast<const uint16_t*>(scores);
@@ -1318,7 +1324,7 @@ int sc_topk_select_bf16(const void* scores, const int* k, int* idx, float* val, 
   const uint16_t* Dp = reinterpret_cast<const uint16_t*>(D);
 #define SC_B16(P) \
   if (n <= 256 * P) { hipLaunchKernelGGL((topk_bf16_kernel<P>), grid, dim3(256), 0, stream, S, k, idx, val, B, n, kmax, \
-                                         absolute, relu, Xp, sx, Dp, d); \
+                                         absolute, relu, Xp, sx, Dp, d, bgn); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   SC_B16(8) SC_B16(16) SC_B16(24) SC_B16(32) SC_B16(48) SC_B16(64)
 #undef SC_B16

@@ -2,6 +2,7 @@
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -9,9 +10,15 @@ import torch
 from . import _lib
 
 
+# [B, G, n] select order: 1 = memory order (model fastest), 2 = model rotated by the batch row
+_BGN_ORDER = int(os.environ.get("SC_TOPK_BGN_ORDER", "2"))
+
+
 def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool = False, relu: bool = True,
-                out=None, x: torch.Tensor = None, D: torch.Tensor = None):
+                out=None, x: torch.Tensor = None, D: torch.Tensor = None, layout: str = "gbn"):
     """Per-row top-k of ``scores`` [G, B, n] (fp32, or bf16) with per-model ``k`` (int32 [G]).
+    ``layout="bgn"`` (bf16 only): ``scores`` is [B, G, n] -- one library GEMM of the batch against the
+    stacked dictionaries writes that layout.
 
     Returns (idx int32 [G, B, kmax], val fp32 [G, B, kmax]); slots >= k[g] are (0, 0.0).
     ``absolute`` selects by |score| (PCA-style) and keeps the signed value; ``relu``
@@ -23,8 +30,15 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
     are ambiguous, and with ``x`` ([B, d] or [G, B, d] bf16) and ``D`` ([G, n, d] bf16, the GEMM's
     operands) those are ranked by their exact fp32 scores (ties to the lower column; without them,
     or beyond 64 such keys, by column).  Values are the bf16 scores."""
-    G, B, n = scores.shape
+    if layout not in ("gbn", "bgn"):
+        raise ValueError(f"layout must be 'gbn' or 'bgn', got {layout!r}")
+    if layout == "bgn":
+        B, G, n = scores.shape
+    else:
+        G, B, n = scores.shape
     bf = scores.dtype == torch.bfloat16
+    if layout == "bgn" and not bf:
+        raise ValueError("the [B, G, n] layout is for bf16 scores")
     if scores.dtype not in (torch.float32, torch.bfloat16) or not scores.is_contiguous():
         raise ValueError("scores must be contiguous fp32 or bf16")
     if k.dtype != torch.int32 or k.numel() != G:
@@ -49,7 +63,8 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
             sx = B * d if x.dim() == 3 else 0
         rc = _lib.lib().sc_topk_select_bf16(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n,
                                             kmax, int(absolute), int(relu), _lib.ptr(x), sx,
-                                            _lib.ptr(D if x is not None else None), d, _lib.stream_handle())
+                                            _lib.ptr(D if x is not None else None), d, _lib.stream_handle(),
+                                            (_BGN_ORDER if layout == "bgn" else 0))
         _lib.check(rc, "sc_topk_select_bf16")
         return idx, val
     rc = _lib.lib().sc_topk_select(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n, kmax,

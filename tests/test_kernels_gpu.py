@@ -406,6 +406,17 @@ def test_topk_select_bf16_picks_are_fp32_topk(n):
     assert not (has7 & ~has5).any()  # equal exact scores: the lower column first
     idx2, val2 = T.topk_select(sb, k, 128, x=x, D=D)
     assert torch.equal(idx2, idx) and torch.equal(val2, val)  # deterministic
+    # the [B, G, n] layout (one library GEMM over the stacked dictionaries) selects identically
+    idx3, val3 = T.topk_select(sb.transpose(0, 1).contiguous(), k, 128, x=x, D=D, layout="bgn")
+    assert torch.equal(idx3, idx) and torch.equal(val3, val)
+    sl = torch.matmul(x, D.view(G * n, d).t()).view(B, G, n)  # hipBLASLt's bf16 scores
+    idx4, _ = T.topk_select(sl, k, 128, x=x, D=D, layout="bgn")
+    for g in range(G):
+        kg = int(k[g])
+        e, pick = exact[g], idx4[g, :, :kg].long()
+        kth = e.topk(kg, dim=-1).values[:, -1:]
+        rows = torch.arange(B, device=DEV) != 40
+        assert (e.gather(-1, pick)[rows] >= kth[rows] - 2 * tol).all()  # fp32 top-k up to accumulation order
 
 
 def test_topk_scatter_and_clear_roundtrip():
@@ -488,6 +499,30 @@ def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype, gemm_k):
         rel = ((eng.g[g].float() - ref).norm() / ref.norm()).item()
         assert rel < 1e-2, (g, k, g < eng.sparse_g, rel)
         torch.testing.assert_close(mse[g], loss.detach(), rtol=1e-2, atol=1e-5)
+
+
+def test_topk_library_scores_gemm_matches(monkeypatch):
+    """SC_TOPK_SCORES_GEMM=blas: the scores as one hipBLASLt GEMM over the stacked dictionaries
+    ([B, G, n]) -- the same picks up to fp32 accumulation-order near-ties, the same training."""
+    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
+    from sparse_coding__amd.models.topk import TopKEncoder
+
+    torch.manual_seed(29)
+    d, n, B = 768, 2048, 512
+    models = [TopKEncoder.init(d, n, k, device=DEV) for k in (8, 32, 96)]
+    ref = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3)
+    monkeypatch.setenv("SC_TOPK_SCORES_GEMM", "blas")
+    lib = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3)
+    assert lib._scores_blas and tuple(lib.scores.shape) == (B, 3, n)
+    for _ in range(3):
+        x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
+        m0, m1 = ref.step_batch(x).clone(), lib.step_batch(x).clone()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(m1, m0, rtol=2e-3, atol=1e-6)
+        same = (ref.idx.sort(-1).values == lib.idx.sort(-1).values).float().mean().item()
+        assert same > 0.99, same
+    diff = (lib.params["dict"] - ref.params["dict"]).abs()
+    assert diff.max().item() <= 3.5e-3 and diff.gt(1e-5).float().mean().item() < 0.02  # near-tie picks only
 
 
 @pytest.mark.parametrize("gemm_k", [0, 16])
