@@ -739,7 +739,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& p, const int bid, c
   // The DEC / DC epilogues read a bf16 tile of x / c at the output positions:
   // fetch it before the K loop so its HBM latency hides under the MFMAs (small
   // per-wave tiles only; at 128x64 per wave the registers are needed by the loop).
-  constexpr bool AUX_EARLY = (EPI == EPI_DEC || EPI == EPI_DC || EPI == EPI_DC_ACT) && WI * WJ <= 16;
+  constexpr bool AUX_EARLY = (EPI == EPI_DEC || EPI == EPI_DC || EPI == EPI_DC_ACT) && WI * WJ <= 16 && !P32;
   uint2 auxv[WI][WJ];
   if constexpr (AUX_EARLY) {
     const uint16_t* X = p.aux + (long)g * p.saux;
