@@ -53,6 +53,15 @@ def auto_sparse_k(B: int, n: int, d: int, margin: float = 1.3) -> int:
     return int(dense / (per_k * margin))
 
 
+def gemm_decode_start(ks, sparse_g: int, gemm_k: int) -> int:
+    """First model of the trailing run with k >= gemm_k that decodes through the dense GEMMs (models
+    below ``sparse_g`` take the slot-list weight gradient and always gather); len(ks) when none."""
+    gg = len(ks)
+    while gemm_k > 0 and gg > sparse_g and ks[gg - 1] >= gemm_k:
+        gg -= 1
+    return gg
+
+
 class FusedTopKEnsemble:
     def __init__(self, models, sig=None, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999), eps=1e-8,
                  grad_dtype: str = "bf16", sparse_k: Union[int, str] = "auto", scores_dtype: Optional[str] = None,
@@ -121,10 +130,7 @@ class FusedTopKEnsemble:
         # dscore = 1[code > 0] (R D_hat^T)) instead of the per-row gather, whose cost grows with k
         # (0 or unset: every model gathers; SC_TOPK_GEMM_K)
         gk = int(os.environ.get("SC_TOPK_GEMM_K", "0") if gemm_k is None else gemm_k)
-        gg = G
-        while gk > 0 and gg > gs and ks[gg - 1] >= gk:
-            gg -= 1
-        self.gemm_g0 = gg
+        self.gemm_g0 = gg = gemm_decode_start(ks, gs, gk)
         if gg < G:
             self._gm_part = torch.zeros(G - gg, (B // 128) * (d // 128), device=dev)
             self._gm_colpart = torch.empty(G - gg, B // 128, n, device=dev)
