@@ -89,6 +89,8 @@ def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dsc
         raise ValueError("prev_idx must be contiguous int32 of idx's shape")
     G, B, kmax = idx.shape
     n, d = D.shape[1], D.shape[2]
+    if gemm_from is not None and gemm_from < G and codebuf is None:
+        raise ValueError("gemm_from needs codebuf: those models' codes are only scattered there")
     sx = 0 if x.dim() == 2 else B * d
     rc = _lib.lib().sc_topk_decode_grad(_lib.ptr(idx), _lib.ptr(val), _lib.ptr(k), _lib.ptr(D), _lib.ptr(x), sx,
                                         _lib.ptr(r_out), _lib.ptr(row_se), _lib.ptr(codebuf), _lib.ptr(dscbuf),

@@ -28,3 +28,14 @@ def test_gemm_decode_start(ks, sparse_g, gemm_k, want):
     from sparse_coding__amd.engine.topk import gemm_decode_start
 
     assert gemm_decode_start(ks, sparse_g, gemm_k) == want
+
+
+def test_decode_grad_gemm_models_need_the_code_buffer():
+    from sparse_coding__amd.ops import topk as T
+
+    G, B, kmax, n, d = 2, 4, 8, 64, 256
+    idx = torch.zeros(G, B, kmax, dtype=torch.int32)
+    with pytest.raises(ValueError, match="codebuf"):
+        T.decode_grad(idx, torch.zeros(G, B, kmax), torch.tensor([4, 8], dtype=torch.int32),
+                      torch.zeros(G, n, d, dtype=torch.bfloat16), torch.zeros(B, d, dtype=torch.bfloat16),
+                      torch.zeros(G, B, d, dtype=torch.bfloat16), torch.zeros(G, B), gemm_from=1)
