@@ -119,6 +119,11 @@ def parse(argv=None):
                          "them (parallel/graphed.py, native communicator on its own stream: es all-gathers, dp "
                          "all-reduce, zero1 reduce-scatter / all-gather); 0 = host-issued collectives through "
                          "ProcessGroupNCCL between graph replays (parallel/ensemble_shard.py, data_parallel.py, zero.py)")
+    ap.add_argument("--fallback-reason", default=None,
+                    help="(set by launch_ranks when it relaunches after a watchdog exit) why this run uses "
+                         "host-issued collectives; reported as collectives.fallback")
+    ap.add_argument("--watchdog-scale", type=float, default=1.0,
+                    help="N > 1: multiplies every per-phase watchdog limit (WATCHDOG_S); 0 = no watchdog")
     return ap.parse_args(argv)
 
 
@@ -144,8 +149,9 @@ def fvu_l0(dicts, x):
 
 
 # single-GPU fused step: at most this many optimizer steps per HIP graph replay (each replay
-# boundary costs an ~9 us idle gap on MI355X); engine/graph_plan.py picks the group size so that
-# the warmup replays every graph the timed region replays
+# boundary costs an ~9 us idle gap on MI355X); engine/graph_plan.py picks the tiling with the fewest
+# timed replays -- the warmup replays the timed graphs first only when it is long enough
+# ("graph_replays.warm_covered" in the JSON; every graph is captured and uploaded before the warmup)
 GRAPH_STEPS = 10
 
 
@@ -467,6 +473,49 @@ def settle_step(device, ms: float, args):
     return out
 
 
+def time_layout(device, sig, args, models: int, rows: int, steps: int = 12, warm: int = 4) -> float:
+    """ms per fused training step of ``models`` SAEs of the benchmark's shape on ``rows`` rows (a
+    scratch ensemble, single-step graphs on a fixed random batch; nothing of the measured models)."""
+    from sparse_coding__amd.engine.fused import FusedSAEEnsemble
+
+    n = args.d * args.ratio
+    gen = torch.Generator(device=device).manual_seed(13)
+    scratch = [sig.init(args.d, n, 1e-3, device=device) for _ in range(models)]
+    eng = FusedSAEEnsemble(scratch, sig, lr=1e-3, batch_size=rows, device=device).enable_graph()
+    eng.x_static.copy_(torch.randn(rows, args.d, device=device, generator=gen).to(torch.bfloat16))
+    for _ in range(warm):
+        eng.step_batch(eng.x_static)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.step_batch(eng.x_static)
+    torch.cuda.synchronize()
+    ms = 1e3 * (time.perf_counter() - t0) / steps
+    del eng, scratch
+    return ms
+
+
+def calibrate_compute(info, args, sig, shape):
+    """N > 1 (collective): time the per-rank compute layout of each candidate mode ON THIS NODE -- all G
+    models on B rows (dp / zero1) and G/N models on N B rows (es) -- max over ranks, and feed them to
+    the comm model (``StepShape.use_measured_compute``) before ``best_mode``.  Untimed for the headline;
+    reported as ``compute_calibration`` next to ``predicted_ms_per_step``."""
+    from sparse_coding__amd.parallel.dist import all_reduce_max
+
+    world = info.world_size
+    if world <= 1 or args.engine != "fused" or info.device.type != "cuda":
+        return None
+    t1 = all_reduce_max(time_layout(info.device, sig, args, args.models, args.batch), info)
+    es = None
+    if args.models % world == 0:
+        es = all_reduce_max(time_layout(info.device, sig, args, args.models // world, args.batch * world), info)
+    shape.use_measured_compute(world, t1, es)
+    return {"what": "fused step of each mode's per-rank layout timed on this node (scratch ensembles, "
+                    "single-step graphs, max over ranks) -- the comm model's compute inputs",
+            "t1_ms": round(t1, 4), "es_ms": round(es, 4) if es else None,
+            "constants_replaced": {"t1_ms": T1_MS, "es_ms": ES_MS.get(world)}}
+
+
 def settle_clocks(device, ms: float):
     """Untimed, NON-training GPU load before the warmup: the grouped bf16 MFMA GEMM (the step's own
     kernel, plain epilogue) on scratch random operands for ``ms`` milliseconds.  MI355X raises its
@@ -494,6 +543,98 @@ def settle_clocks(device, ms: float):
             "ms": round(1e3 * (time.perf_counter() - t0), 1), "launches": launches}
 
 
+HANG_RC = 5  # a rank's exit code when the watchdog ended a hung phase (launch_ranks relaunches on it)
+HANG_DIR_ENV = "SC_BENCH_HANG_DIR"  # where a firing watchdog leaves its marker for launch_ranks
+
+
+class Watchdog:
+    """Bounds every multi-rank phase of the run so the first real N > 1 run cannot end without a
+    JSON line (a hang inside a captured RCCL collective blocks ``torch.cuda.synchronize()`` until the
+    process-group timeout, and no exception ever reaches ``ready_runner``'s fallback).
+
+    ``arm(phase, seconds)`` starts the clock for a phase, ``disarm()`` stops it.  When a phase
+    overruns, the watchdog thread prints the phase and rank, writes a marker ``rank<r>.json`` under
+    ``$SC_BENCH_HANG_DIR`` (set by ``launch_ranks``), emits ``pending`` -- a finished result record,
+    when the hang happens after the headline was measured (the alt-parallelism run, shutdown) -- and
+    ends the process with ``os._exit(HANG_RC)``.  No exec, no retry in this process: a device fault
+    or a hung collective leaves the process's HIP state unusable, so ``launch_ranks`` starts FRESH
+    ranks with ``--dist-graph 0``.  Reference: ``experiments/huge_batch_size.py:337-363`` (mp.spawn of
+    the DDP ranks; no hang handling there)."""
+
+    def __init__(self, info, enabled: bool, scale: float = 1.0):
+        import threading
+
+        self.info, self.enabled, self.scale = info, enabled, scale
+        self.pending = None  # a finished record rank 0 emits if a later phase hangs
+        self._lock = threading.Lock()
+        self._phase, self._deadline, self._gen = None, None, 0
+        self._wake = threading.Event()
+        self.fired = None
+        if enabled:
+            threading.Thread(target=self._watch, name="bench-watchdog", daemon=True).start()
+
+    def arm(self, phase: str, seconds: float):
+        with self._lock:
+            self._phase, self._deadline = phase, time.monotonic() + seconds * self.scale
+            self._gen += 1
+        self._wake.set()
+
+    def disarm(self):
+        with self._lock:
+            self._phase, self._deadline = None, None
+            self._gen += 1
+        self._wake.set()
+
+    def _watch(self):
+        while True:
+            with self._lock:
+                phase, deadline, gen = self._phase, self._deadline, self._gen
+            self._wake.clear()
+            if deadline is None:
+                self._wake.wait()
+                continue
+            left = deadline - time.monotonic()
+            if left > 0:
+                self._wake.wait(left)
+                continue
+            with self._lock:
+                if gen != self._gen:  # re-armed or disarmed meanwhile
+                    continue
+            self._fire(phase)
+            return
+
+    def fire_now(self, phase: str):
+        """End the process now as if ``phase`` had hung (a failure this process cannot recover from)."""
+        self._fire(phase)
+
+    def _fire(self, phase: str):
+        rank = getattr(self.info, "rank", 0)
+        self.fired = phase
+        print(f"[bench] watchdog: rank {rank} hung in phase '{phase}'; exiting {HANG_RC}", file=sys.stderr, flush=True)
+        where = os.environ.get(HANG_DIR_ENV)
+        if where:
+            try:
+                with open(os.path.join(where, f"rank{rank}.json"), "w") as f:
+                    json.dump({"rank": rank, "phase": phase, "emitted": self.pending is not None}, f)
+            except OSError:
+                pass
+        if self.pending is not None and getattr(self.info, "is_main", True):
+            rec = dict(self.pending)
+            rec.setdefault("watchdog", {"phase": phase, "note": "this phase hung after the headline was "
+                                                                 "measured; the record is complete up to it"})
+            try:
+                _emit(json.dumps(rec))
+            except Exception:
+                pass
+        sys.stderr.flush()
+        os._exit(HANG_RC)
+
+
+# per-phase limits (seconds) of the N > 1 watchdog; every one is far above a healthy run's time
+WATCHDOG_S = {"setup": 240.0, "first-replay": 120.0, "timed": 240.0, "eval": 300.0, "checks": 120.0,
+              "alt": 400.0, "shutdown": 60.0}
+
+
 def _agree(err, info):
     """Every rank's error (or None) -> the first one any rank reported (collective; the ranks must
     all take the same path afterwards or the next collective deadlocks)."""
@@ -506,19 +647,23 @@ def _agree(err, info):
     return next((f"rank {r}: {e}" for r, e in enumerate(everyone) if e is not None), None)
 
 
-def ready_runner(par, args, info, sig, models, ring, device, grad_dtype):
+def ready_runner(par, args, info, sig, models, ring, device, grad_dtype, wd=None, tag=""):
     """``make_runner`` + capture of every graph (+ the first warmup group for the in-graph RCCL path).
-    If capturing or first replaying the in-graph collectives fails on ANY rank, every rank drops that
+    If capturing or first replaying the in-graph collectives RAISES on any rank, every rank drops that
     runner and rebuilds the same configuration (fresh from ``models``) on host-issued collectives
-    (``--dist-graph 0``) in this process; the JSON reports it (``collectives.fallback``).
-    Returns (runner, tiling, warmup groups still to run)."""
+    (``--dist-graph 0``) in this process; the JSON reports it (``collectives.fallback``).  A HANG in
+    either phase is the watchdog's (``wd``): the rank exits ``HANG_RC`` and ``launch_ranks`` relaunches
+    fresh ranks on host-issued collectives.  Returns (runner, tiling, warmup groups still to run)."""
     from sparse_coding__amd.engine.graph_plan import tile
 
+    wd = wd or Watchdog(info, False)
     tiling = tile(args.steps, args.warmup, args.graph_group or GRAPH_STEPS, exact=bool(args.graph_group))
     warm = list(tiling.warm)
+    wd.arm(f"{tag}setup", WATCHDOG_S["setup"])
     runner = make_runner(par, args, info, sig, models, ring, device, grad_dtype)
     if runner.path != "rccl":
         runner.setup(tiling)
+        wd.disarm()
         return runner, tiling, warm
     err = None
     try:
@@ -527,17 +672,25 @@ def ready_runner(par, args, info, sig, models, ring, device, grad_dtype):
         err = f"capture of the in-graph collectives failed: {exc!r}"
     err = _agree(err, info)
     if err is None and warm:
+        wd.arm(f"{tag}first-replay", WATCHDOG_S["first-replay"])
+        replay_err = None
         try:
             runner.run(warm[:1])
             runner.finish()
             torch.cuda.synchronize()
         except Exception as exc:
-            err = f"first replay of the in-graph collectives failed: {exc!r}"
-        err = _agree(err, info)
+            replay_err = f"first replay of the in-graph collectives failed: {exc!r}"
+        if replay_err is not None and wd.enabled:
+            # a replay error may be a device fault, which is sticky: this process cannot rebuild on
+            # host collectives, fresh ranks can (launch_ranks relaunches on the watchdog's exit code)
+            wd.fire_now(f"{tag}first-replay raised: {replay_err}")
+        err = _agree(replay_err, info)
         if err is None:
             warm = warm[1:]
+    wd.disarm()
     if err is None:
         return runner, tiling, warm
+    wd.arm(f"{tag}fallback-setup", WATCHDOG_S["setup"])
     print(f"[bench] {err}; falling back to host-issued collectives (--dist-graph 0)", file=sys.stderr)
     try:
         runner.close()
@@ -546,12 +699,13 @@ def ready_runner(par, args, info, sig, models, ring, device, grad_dtype):
     runner = make_runner(par, args, info, sig, models, ring, device, grad_dtype, dist_graph=0)
     runner.fallback = err
     runner.setup(tiling)
+    wd.disarm()
     return runner, tiling, list(tiling.warm)
 
 
 def warm_and_time(runner, tiling, warm, args, info, B):
     """Graphs are captured (``ready_runner``); settle the clocks (untimed, non-training, reported), run
-    the warmup through the timed region's own graphs (the last warmup replay is a timed-size group),
+    the warmup (through the timed region's own graphs when it is long enough: ``tiling.covered``),
     then time exactly ``args.steps`` steps (engine/graph_plan.py)."""
     runner.settle = (settle_step(info.device, args.settle_ms, args) if args.settle_mode == "step"
                      else settle_clocks(info.device, args.settle_ms))
@@ -583,25 +737,64 @@ def launch_ranks(gpus: int, argv, script: str | None = None) -> int:
     (``mp.spawn(..., nprocs=torch.cuda.device_count())``)."""
     import subprocess
 
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           script or os.path.abspath(__file__)] + list(argv)
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    print(f"[bench] launching {gpus} ranks: {' '.join(cmd)}", file=sys.stderr)
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
-    emitted = 0
-    for line in proc.stdout:
-        if line.startswith("{") and '"metric"' in line:
-            _emit(line.strip())
-            emitted += 1
-        else:
-            sys.stderr.write(line)
-    rc = proc.wait()
+    import shutil
+    import tempfile
+
+    def once(args_):
+        hang_dir = tempfile.mkdtemp(prefix="sc_bench_hang_")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               script or os.path.abspath(__file__)] + list(args_)
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        env[HANG_DIR_ENV] = hang_dir
+        print(f"[bench] launching {gpus} ranks: {' '.join(cmd)}", file=sys.stderr)
+        proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+        emitted = 0
+        for line in proc.stdout:
+            if line.startswith("{") and '"metric"' in line and emitted == 0:
+                _emit(line.strip())
+                emitted += 1
+            else:
+                sys.stderr.write(line)
+        rc = proc.wait()
+        hangs = []
+        for name in sorted(os.listdir(hang_dir)):
+            try:
+                with open(os.path.join(hang_dir, name)) as f:
+                    hangs.append(json.load(f))
+            except (OSError, ValueError):
+                pass
+        shutil.rmtree(hang_dir, ignore_errors=True)
+        return rc, emitted, hangs
+
+    rc, emitted, hangs = once(argv)
+    if hangs and emitted == 0 and not _dist_graph_off(argv):
+        # a rank's watchdog ended a hung phase before any result: fresh ranks (the hung processes' HIP
+        # state is not reusable) on host-issued collectives, with the reason on record
+        phase = hangs[0]["phase"]
+        reason = f"in-graph hang: {phase} (rank {hangs[0]['rank']}); relaunched with --dist-graph 0"
+        print(f"[bench] {reason}", file=sys.stderr)
+        rc, emitted, hangs = once(list(argv) + ["--dist-graph", "0", "--fallback-reason", reason])
+    if emitted == 1 and rc != 0 and hangs:
+        # the result line is out and a watchdog ended a later phase (shutdown, the alt-parallelism run)
+        print(f"[bench] ranks exited {rc} after the result line (watchdog: {hangs})", file=sys.stderr)
+        return 0
     if rc == 0 and emitted != 1:
         print(f"[bench] the ranks exited 0 but printed {emitted} result lines", file=sys.stderr)
         return 4
     return rc
+
+
+def _dist_graph_off(argv) -> bool:
+    """True when ``argv`` already asks for host-issued collectives (``--dist-graph 0``)."""
+    argv = list(argv)
+    for i, a in enumerate(argv):
+        if a in ("--dist-graph", "--dp-graph") and i + 1 < len(argv):
+            return argv[i + 1] == "0"
+        if a.startswith(("--dist-graph=", "--dp-graph=")):
+            return a.split("=", 1)[1] == "0"
+    return False
 
 
 def check_world(args) -> str | None:
@@ -675,9 +868,13 @@ def main(argv=None):
                                  untied=args.kind == "untied", es_ms=dict(ES_MS))
     # N > 1: this node's own collective rates at the step's payloads replace the link model's constants
     # (reported as "comm_calibration")
-    calib = None
+    calib = compute_calib = None
     if info.world_size > 1 and not args.no_comm_calibration:
         calib = comm_model.calibrate(info, shape)
+        try:
+            compute_calib = calibrate_compute(info, args, sig, shape)
+        except Exception as exc:  # the constants stay; the failure is on record
+            compute_calib = {"error": repr(exc)}
     par = args.parallelism
     if par == "auto":
         # N > 1: the mode the per-N comm/compute model predicts fastest (ensemble-axis sharding at
@@ -693,11 +890,17 @@ def main(argv=None):
               file=sys.stderr)
         return 3
 
-    runner, tiling, warm = ready_runner(par, args, info, sig, models, ring, device, grad_dtype)
+    # N > 1: every multi-rank phase runs under the watchdog (a hang exits HANG_RC; launch_ranks relaunches)
+    wd = Watchdog(info, distributed and args.watchdog_scale > 0, args.watchdog_scale or 1.0)
+    runner, tiling, warm = ready_runner(par, args, info, sig, models, ring, device, grad_dtype, wd=wd)
+    if runner.fallback is None and args.fallback_reason:
+        runner.fallback = args.fallback_reason
+    wd.arm("timed", WATCHDOG_S["timed"])
     ms, value = warm_and_time(runner, tiling, warm, args, info, B)
 
     quality = None
     trained = args.warmup + args.steps
+    wd.arm("eval", WATCHDOG_S["eval"])
     if not args.no_eval:
         if trained < args.quality_steps:  # untimed: train on toward convergence before evaluating
             from sparse_coding__amd.engine.graph_plan import chunks
@@ -713,36 +916,13 @@ def main(argv=None):
     torch.cuda.synchronize()
     # cross-rank check of the run just timed (collective): replicas identical (dp / zero1) or the same
     # global batches on every rank (es)
+    wd.arm("checks", WATCHDOG_S["checks"])
     consistency = runner.consistency() if distributed and runner.consistency is not None else None
     devices = rank_devices(info, runner.comm)
     rccl_ranks = runner.comm.count() if runner.comm is not None and hasattr(runner.comm, "count") else None
     runner.close()
 
-    # N > 1: also time the other multi-GPU strategy on the same models (untimed for the
-    # headline; reported under "alt_parallelism" so both the gradient all-reduce path --
-    # BASELINE config 3's mechanism -- and the ensemble-sharded path are on record)
-    alt = None
-    if distributed and args.compare_parallelism and args.models % info.world_size == 0:
-        other = "dp" if par in ("es", "zero1") else "es"
-        alt_models = [sig.init(args.d, n, float(l1), device=device) for l1 in l1s]
-        alt = {"parallelism": f"{other}{info.world_size}",
-               "predicted_ms_per_step": comm_model.predict(other, info.world_size, shape, args.dp_chunks),
-               "dp_chunks": args.dp_chunks if other == "dp" else None,
-               "comm_bytes_per_gpu_per_step": comm_bytes(other, args, info.world_size)}
-        try:
-            alt_runner, a_tiling, a_warm = ready_runner(other, args, info, sig, alt_models, ring, device, grad_dtype)
-            a_ms, a_value = warm_and_time(alt_runner, a_tiling, a_warm, args, info, B)
-            alt_runner.finish()
-            torch.cuda.synchronize()
-            alt.update(value=round(a_value, 1), ms_per_step=round(a_ms, 4),
-                       collective_path=PATH_NAMES.get(alt_runner.path, alt_runner.path),
-                       fallback=alt_runner.fallback,
-                       consistency=alt_runner.consistency() if alt_runner.consistency is not None else None)
-            alt_runner.close()
-        except Exception as exc:  # the headline run above stands on its own; the failure is on record
-            print(f"[bench] alt parallelism {other} failed: {exc!r}", file=sys.stderr)
-            alt.update(value=None, ms_per_step=None, error=repr(exc))
-
+    rec = None
     if info.is_main:
         rec = {
             "metric": METRIC,
@@ -779,13 +959,14 @@ def main(argv=None):
                                       for m in ("dp", "zero1", "es")} if distributed else None,
             "comm_bytes_other_modes": {m: comm_bytes(m, args, max(info.world_size, 8)) for m in ("dp", "zero1", "es")},
             "comm_calibration": calib,
+            "compute_calibration": compute_calib,
             "model_activations_per_s": round(value * args.models, 1),
             "baseline_note": "vs_baseline divides by BASELINE.md row 12 (reference math, same shapes, "
                              "1.86k act/s, 8-vCPU sandbox); no published GPU throughput exists.  "
                              "vs_eager_same_box divides by this repo's PyTorch-eager vmap(grad)+Adam "
                              "engine on the same MI355X (profiles/bench_eager_r2.json)",
             # how the steps were cut into HIP graph replays: all graphs captured + uploaded before
-            # warmup; the warmup replays every graph the timed region replays (engine/graph_plan.py)
+            # warmup; warm_covered = the warmup replayed every timed graph first (engine/graph_plan.py)
             "settle": getattr(runner, "settle", None),
             "graph_replays": {"timed": list(tiling.timed), "warmup": list(tiling.warm),
                               "warm_covered": tiling.covered} if par == "dp" and not distributed
@@ -803,15 +984,49 @@ def main(argv=None):
             "rank_devices": devices,
             "consistency": consistency,
         }
-        if alt is not None:
-            rec["alt_parallelism"] = alt
         if quality is not None:
             rec["fvu_at_l0"] = [{"l1": float(l), "l0": round(a, 2), "fvu": round(b, 4)}
                                 for l, (a, b) in zip(l1s, quality)]
             rec["fvu_eval"] = {"train_steps": trained, "held_out_rows": int(held_out.shape[0]),
                                "act_norm": args.act_norm}
+        wd.pending = rec  # the headline is measured: a hang from here on still emits it
+
+    # N > 1: also time the other multi-GPU strategy on the same models (untimed for the
+    # headline; reported under "alt_parallelism" so both the gradient all-reduce path --
+    # BASELINE config 3's mechanism -- and the ensemble-sharded path are on record)
+    if distributed and args.compare_parallelism and args.models % info.world_size == 0:
+        other = "dp" if par in ("es", "zero1") else "es"
+        alt_models = [sig.init(args.d, n, float(l1), device=device) for l1 in l1s]
+        alt = {"parallelism": f"{other}{info.world_size}",
+               "predicted_ms_per_step": comm_model.predict(other, info.world_size, shape, args.dp_chunks),
+               "dp_chunks": args.dp_chunks if other == "dp" else None,
+               "comm_bytes_per_gpu_per_step": comm_bytes(other, args, info.world_size)}
+        if rec is not None:
+            rec["alt_parallelism"] = dict(alt, value=None, ms_per_step=None, error="did not finish (watchdog)")
+        try:
+            alt_runner, a_tiling, a_warm = ready_runner(other, args, info, sig, alt_models, ring, device, grad_dtype,
+                                                        wd=wd, tag="alt-")
+            wd.arm("alt-timed", WATCHDOG_S["alt"])
+            a_ms, a_value = warm_and_time(alt_runner, a_tiling, a_warm, args, info, B)
+            alt_runner.finish()
+            torch.cuda.synchronize()
+            alt.update(value=round(a_value, 1), ms_per_step=round(a_ms, 4),
+                       collective_path=PATH_NAMES.get(alt_runner.path, alt_runner.path),
+                       fallback=alt_runner.fallback,
+                       consistency=alt_runner.consistency() if alt_runner.consistency is not None else None)
+            alt_runner.close()
+        except Exception as exc:  # the headline run above stands on its own; the failure is on record
+            print(f"[bench] alt parallelism {other} failed: {exc!r}", file=sys.stderr)
+            alt.update(value=None, ms_per_step=None, error=repr(exc))
+        if rec is not None:
+            rec["alt_parallelism"] = alt
+
+    if rec is not None:
+        wd.pending = None
         _emit(json.dumps(rec))
+    wd.arm("shutdown", WATCHDOG_S["shutdown"])
     shutdown(info)
+    wd.disarm()
     return 0
 
 

@@ -53,19 +53,9 @@ def auto_sparse_k(B: int, n: int, d: int, margin: float = 1.3) -> int:
     return int(dense / (per_k * margin))
 
 
-def gemm_decode_start(ks, sparse_g: int, gemm_k: int) -> int:
-    """First model of the trailing run with k >= gemm_k that decodes through the dense GEMMs (models
-    below ``sparse_g`` take the slot-list weight gradient and always gather); len(ks) when none."""
-    gg = len(ks)
-    while gemm_k > 0 and gg > sparse_g and ks[gg - 1] >= gemm_k:
-        gg -= 1
-    return gg
-
-
 class FusedTopKEnsemble:
     def __init__(self, models, sig=None, lr=1e-3, batch_size=256, device="cuda", betas=(0.9, 0.999), eps=1e-8,
-                 grad_dtype: str = "bf16", sparse_k: Union[int, str] = "auto", scores_dtype: Optional[str] = None,
-                 gemm_k: Optional[int] = None):
+                 grad_dtype: str = "bf16", sparse_k: Union[int, str] = "auto", scores_dtype: Optional[str] = None):
         from ..models.topk import TopKEncoder
 
         self.sig = sig or TopKEncoder
@@ -97,14 +87,9 @@ class FusedTopKEnsemble:
         sdt = scores_dtype or os.environ.get("SC_TOPK_SCORES", "bf16")
         if sdt not in ("fp32", "bf16"):
             raise ValueError(f"scores_dtype must be 'fp32' or 'bf16', got {sdt!r}")
-        # bf16 scores from the library GEMM (SC_TOPK_SCORES_GEMM=blas): x D_all^T over the stacked
-        # dictionaries as ONE plain hipBLASLt GEMM (the scores need no fused epilogue), written
-        # [B, G, n]; the select reads that layout directly
-        self._scores_blas = sdt == "bf16" and os.environ.get("SC_TOPK_SCORES_GEMM", "sc") == "blas"
-        if self._scores_blas:
-            self.scores = torch.empty(B, G, n, device=dev, dtype=torch.bfloat16)
-        else:
-            self.scores = torch.empty(G, B, n, device=dev, dtype=torch.bfloat16 if sdt == "bf16" else torch.float32)
+        # (a hipBLASLt scores GEMM over the stacked dictionaries with a [B, G, n] select measured no
+        # consistent gain over four boxes: scripts/lab/topk_blas_gemmk_r5.patch)
+        self.scores = torch.empty(G, B, n, device=dev, dtype=torch.bfloat16 if sdt == "bf16" else torch.float32)
         # pick buffers, alternating per step: the decode of step t zeroes step t-1's picks in the
         # dense code / dscore buffers (no separate clear launch)
         self.idx_buf = torch.zeros(2, G, B, kmax, device=dev, dtype=torch.int32)
@@ -125,16 +110,8 @@ class FusedTopKEnsemble:
         # the decode scatters codes / code gradients only for the dense-wgrad models (config 4:
         # 1.054 vs 1.059 ms/step scattering for all, profiles/r4/topk_scatter/)
         self._dense_from = gs
-        # decode + code gradients: the trailing models with k >= gemm_k run them as two dense MFMA GEMMs
-        # over the scattered codes (EPI_DEC: R = codes D_hat - x with per-tile R^2 partials; EPI_DC:
-        # dscore = 1[code > 0] (R D_hat^T)) instead of the per-row gather, whose cost grows with k
-        # (0 or unset: every model gathers; SC_TOPK_GEMM_K)
-        gk = int(os.environ.get("SC_TOPK_GEMM_K", "0") if gemm_k is None else gemm_k)
-        self.gemm_g0 = gg = gemm_decode_start(ks, gs, gk)
-        if gg < G:
-            self._gm_part = torch.zeros(G - gg, (B // 128) * (d // 128), device=dev)
-            self._gm_colpart = torch.empty(G - gg, B // 128, n, device=dev)
-            self._gm_l1 = torch.zeros(G - gg, device=dev)
+        # (decoding the large-k models as dense MFMA GEMMs over the scattered codes measured +3-5 %:
+        # scripts/lab/topk_blas_gemmk_r5.patch; every model decodes by the per-row gather)
         self.lists = topk_ops.SlotLists(gs, B, n, ks, kmax, dev) if gs else None
         self.dscv = torch.zeros(G, B, kmax, device=dev) if gs else None
         # bf16 dictionary gradient by default: the dense GEMM's bf16 epilogue + Adam's bf16 loads
@@ -155,19 +132,10 @@ class FusedTopKEnsemble:
     def _step_kernels(self, x, cur: int, gather=None):
         G, B, n, d = self.n_models, self.batch_size, self.n, self.d
         idx, prev = self.idx_buf[cur], self.idx_buf[1 - cur]
-        if self._scores_blas:
-            torch.matmul(x, self.shadow.view(G * n, d).t(), out=self.scores.view(B, G * n))
-            topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow, layout="bgn")
-        else:
-            gemm_ops.matmul_nt(x, self.shadow, self.scores)
-            topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow)
-        gg = self.gemm_g0
+        gemm_ops.matmul_nt(x, self.shadow, self.scores)
+        topk_ops.topk_select(self.scores, self.k, self.kmax, out=(idx, self.val), x=x, D=self.shadow)
         topk_ops.decode_grad(idx, self.val, self.k, self.shadow, x, self.r, self.row_se, self.codebuf,
-                             self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from, gemm_from=gg)
-        if gg < G:
-            gemm_ops.decode_residual(self.codebuf[gg:], self.shadow[gg:], x, self.r[gg:], self._gm_part)
-            gemm_ops.code_grad(self.r[gg:], self.shadow[gg:], self.codebuf[gg:], self._gm_l1, self.dscbuf[gg:],
-                               self._gm_colpart)
+                             self.dscbuf, dscv=self.dscv, prev_idx=prev, dense_from=self._dense_from)
         alpha = 2.0 / (B * d)
         gs = self.sparse_g
         if gs:
@@ -178,11 +146,9 @@ class FusedTopKEnsemble:
         if self._tail:
             adam_ops.topk_tail(self.params["dict"], self.g, self.m["dict"], self.v["dict"], self.shadow, self.norms,
                                self.lr, *self.betas, self.eps, self.step_dev, self.row_se, self.mse, 1.0 / (B * d),
-                               self._ticket, gather=gather, se_part=self._gm_part if gg < G else None, se_g0=gg)
+                               self._ticket, gather=gather)
             return
         torch.mul(torch.sum(self.row_se, dim=1), 1.0 / (B * d), out=self.mse)
-        if gg < G:
-            torch.mul(torch.sum(self._gm_part, dim=1), 1.0 / (B * d), out=self.mse[gg:])
         adam_ops.adam_rows([dict(p=self.params["dict"], g=self.g, m=self.m["dict"], v=self.v["dict"],
                                  shadow=self.shadow, norms=self.norms, norm=True)],
                            self.lr, self.step_count + 1, *self.betas, self.eps, step_dev=self.step_dev)

@@ -58,7 +58,7 @@ def signatures():
                            c_void_p],
         "sc_topk_decode_grad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
                                 c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                                c_int, c_int],
+                                c_int],
         "sc_topk_sparse_wgrad": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
                                  c_int, c_int, c_int, c_int, c_int, c_float, c_int, c_void_p],
         "sc_topk_slot_lists": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
@@ -98,11 +98,10 @@ def signatures():
                          c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long,
                          c_int, c_long, c_void_p, c_int, c_long, c_void_p, c_void_p],
         "sc_topk_select_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
-                                c_void_p, c_long, c_void_p, c_int, c_void_p, c_int],
+                                c_void_p, c_long, c_void_p, c_int, c_void_p],
         "sc_topk_tail": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                          c_void_p, c_float, c_float, c_float, c_void_p, c_int, c_void_p, c_int, c_float, c_void_p,
-                         c_void_p, c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long, c_void_p,
-                         c_void_p, c_int, c_int],
+                         c_void_p, c_void_p, c_long, c_void_p, c_long, c_void_p, c_void_p, c_long, c_long, c_void_p],
         "sc_hessian_ema": [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p],
         "sc_basis_apply": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int,
                            c_void_p],

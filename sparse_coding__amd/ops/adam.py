@@ -170,15 +170,12 @@ def step_tail(sets, lr, b1, b2, eps, step_dev, bias, bias_m, bias_v, colpart, en
     _lib.check(rc, "sc_step_tail")
 
 
-def topk_tail(p, g, m, v, shadow, norms, lr, b1, b2, eps, step_dev, row_se, mse, se_scale, ticket, gather=None,
-              se_part=None, se_g0=None):
+def topk_tail(p, g, m, v, shadow, norms, lr, b1, b2, eps, step_dev, row_se, mse, se_scale, ticket, gather=None):
     """The end of a top-k step as ONE launch (csrc/adam.hip ``sc_topk_tail``): row Adam with the norm
     Jacobian on the dictionary stack ``p`` [G, n, d] (as ``adam_rows``, bf16 shadow + row norms),
     ``mse[g] = se_scale * sum(row_se[g])`` (row_se [G, B] per-row squared errors), the NEXT step's batch
     fetch with ``gather`` = (ring buffer [N, d], perm int64, ep0 int32 [1], out [rows, d]), and the
-    device step counter ``step_dev`` read by every block and advanced by the last one.
-    ``se_part`` [G - se_g0, tiles] fp32: models from ``se_g0`` sum these squared-error partials (the
-    decoder GEMM's per-tile epilogue partials) instead of ``row_se``."""
+    device step counter ``step_dev`` read by every block and advanced by the last one."""
     G, n, d = p.shape
     gbf16 = g.dtype == torch.bfloat16
     for name, t, want in (("p", p, torch.float32), ("m", m, torch.float32), ("v", v, torch.float32),
@@ -203,18 +200,11 @@ def topk_tail(p, g, m, v, shadow, norms, lr, b1, b2, eps, step_dev, row_se, mse,
                 or perm.dtype != torch.int64 or ep0.dtype != torch.int32):
             raise ValueError("gather: contiguous rows of 16-byte multiples, int64 perm, int32 ep0")
         grows, nbuf, nperm = gout.shape[0], gbuf.shape[0], perm.numel()
-    se_n = 0
-    if se_part is not None:
-        if (se_g0 is None or not 0 <= se_g0 < G or se_part.dtype != torch.float32 or not se_part.is_contiguous()
-                or se_part.dim() != 2 or se_part.shape[0] != G - se_g0):
-            raise ValueError("se_part must be contiguous fp32 [G - se_g0, tiles]")
-        se_n = se_part.shape[1]
     rc = _lib.lib().sc_topk_tail(
         _lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), _lib.ptr(shadow), _lib.ptr(norms), G, n, d,
         _lib.ptr(lr), b1, b2, eps, _lib.ptr(step_dev), int(gbf16), _lib.ptr(row_se), row_se.shape[1],
         float(se_scale), _lib.ptr(mse), _lib.ptr(ticket), _lib.ptr(gbuf), nbuf, _lib.ptr(perm), nperm,
         _lib.ptr(ep0), _lib.ptr(gout), grows, row_bytes, _lib.stream_handle(),
-        _lib.ptr(se_part), se_n, int(se_g0 or 0),
     )
     _lib.check(rc, "sc_topk_tail")
 

@@ -365,7 +365,6 @@ struct TailArgs {
   // top-k step tail (sc_topk_tail): the loss blocks reduce per-row squared errors instead of the SAE
   // epilogue partials -- mse[g] = se_scale * sum_r row_se[g][r]; no bias blocks
   const float* row_se; int se_rows; float se_scale; float* mse;
-  const float* se_part; int se_part_n; int se_g0;  // models >= se_g0: sum se_part rows instead
 };
 
 __device__ __forceinline__ void tail_loss(const BiasArgs& a, const TailArgs& t, int g, int par) {
@@ -405,14 +404,9 @@ __device__ __forceinline__ void tail_loss(const BiasArgs& a, const TailArgs& t, 
 __device__ __forceinline__ void tail_mse(const TailArgs& t, int g) {
   __shared__ float red[8];
   float se = 0.f;
-  if (g >= t.se_g0) {  // models whose decode ran as a GEMM: its per-tile partials
-    const float* sp = t.se_part + (long)(g - t.se_g0) * t.se_part_n;
-    for (int r = threadIdx.x; r < t.se_part_n; r += 256) se += sp[r];
-  } else {
-    const float* rs = t.row_se + (long)g * t.se_rows;
+  const float* rs = t.row_se + (long)g * t.se_rows;
 #pragma unroll 4
-    for (int r = threadIdx.x; r < t.se_rows; r += 256) se += rs[r];
-  }
+  for (int r = threadIdx.x; r < t.se_rows; r += 256) se += rs[r];
   se = block_sum_256(se, red);
   if (threadIdx.x == 0) t.mse[g] = se * t.se_scale;
 }
@@ -634,7 +628,6 @@ int sc_step_tail(int nset, float* const* p, const void* const* g, float* const* 
   t.nloss = G; t.nbias = G * (n / 32); t.ngather = gbuf ? (int)((grows + 3) / 4) : 0;
   t.lcomp = 0; t.lG = G;
   t.row_se = nullptr; t.se_rows = 0; t.se_scale = 0.f; t.mse = nullptr;
-  t.se_part = nullptr; t.se_part_n = 0; t.se_g0 = 0;
   long arows = total;
   // host copy of a masked ensemble's live sizes (full-stack sets only, G <= 16): launch live rows only
   if (live_h && live && row0 == 0 && G <= 16 && rows_per_model > 0 && rows[0] == (long)G * rows_per_model &&
@@ -670,9 +663,8 @@ int sc_topk_tail(float* p, const void* g, float* m, float* v, void* shadow, floa
                  const float* lr, float b1, float b2, float eps, int* step, int gbf16, const float* row_se,
                  int se_rows, float se_scale, float* mse, int* ticket, const void* gbuf, long nbuf,
                  const long* perm, long nperm, const int* ep0, void* gout, long grows, long row_bytes,
-                 hipStream_t stream, const float* se_part, int se_part_n, int se_g0) {
+                 hipStream_t stream) {
   if (d % 256 || d > 1024 || G < 1 || n < 1 || !step || !ticket || !row_se || !mse || se_rows < 1) return 1;
-  if (se_part && (se_part_n < 1 || se_g0 < 0 || se_g0 > G)) return 1;
   if (gbuf && (row_bytes % 16 || nbuf < 1)) return 1;
   AdamArgs a;
   a.set[0] = {p, g, m, v, reinterpret_cast<uint16_t*>(shadow), norms, G * n, 1};
@@ -691,7 +683,6 @@ int sc_topk_tail(float* p, const void* g, float* m, float* v, void* shadow, floa
   t.nloss = G; t.nbias = 0; t.ngather = gbuf ? (int)((grows + 3) / 4) : 0;
   t.lcomp = 0; t.lG = G;
   t.row_se = row_se; t.se_rows = se_rows; t.se_scale = se_scale; t.mse = mse;
-  t.se_part = se_part; t.se_part_n = se_part_n; t.se_g0 = se_part ? se_g0 : G;
   const long blocks = t.nloss + t.ngather + ((long)G * n + 3) / 4;
 #define SC_TAIL(NVV)                                                                                   \
   case NVV:                                                                                            \

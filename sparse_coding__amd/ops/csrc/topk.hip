@@ -756,7 +756,7 @@ template <int PL>
 __global__ __launch_bounds__(256) void topk_bf16_kernel(const uint16_t* __restrict__ scores, const int* __restrict__ kv,
                                                       int* __restrict__ idx, float* __restrict__ val, int B, int n,
                                                       int kmax, int absolute, int relu, const uint16_t* __restrict__ X,
-                                                      long sx, const uint16_t* __restrict__ D, int d, int bgn) {
+                                                      long sx, const uint16_t* __restrict__ D, int d) {
   static_assert(PL % 8 == 0, "8 keys per 16-byte load");
   __shared__ int red[2][4];
   __shared__ int wsum[2][4];
@@ -768,15 +768,10 @@ __global__ __launch_bounds__(256) void topk_bf16_kernel(const uint16_t* __restri
   __shared__ int tcol[TIE_CAP], tkeep[TIE_CAP];
   __shared__ float tsc[TIE_CAP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // bgn: scores laid out [B][G][n] (one library GEMM x D_all^T over the stacked dictionaries); the
-  // blocks then walk that layout in memory order; bgn == 2: the model index rotated by the batch row so
-  // an XCD (block % 8) does not get one model's rows -- k, and the select's cost, differ per model
-  const int G = (int)(gridDim.x / B);
-  const int b = bgn ? (int)(blockIdx.x / G) : (int)(blockIdx.x % B);
-  const int g = bgn ? (int)((blockIdx.x % G + (bgn == 2 ? b : 0)) % G) : (int)(blockIdx.x / B);
-  const long row = (long)g * B + b;  // output row (idx / val are [G][B][kmax])
+  const int b = (int)(blockIdx.x % B), g = (int)(blockIdx.x / B);
+  const long row = (long)g * B + b;  // scores row [G][B][n]; idx / val are [G][B][kmax]
   const int k = min(kv[g], n);
-  const uint16_t* S = scores + (bgn ? (long)b * G + g : row) * n;
+  const uint16_t* S = scores + row * n;
   int* I = idx + row * kmax;
   float* V = val + row * kmax;
   uint32_t key[PL];
@@ -890,7 +885,7 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
     const int* __restrict__ idx, const float* __restrict__ val, const int* __restrict__ kv,
     const uint16_t* __restrict__ D, const uint16_t* __restrict__ X, long sx, uint16_t* __restrict__ R,
     float* __restrict__ row_se, uint16_t* __restrict__ codebuf, uint16_t* __restrict__ dscbuf, int G, int B,
-    int n, int d, int kmax, float* __restrict__ dscv, const int* __restrict__ prev_idx, int g_dense0, int g_gemm0) {
+    int n, int d, int kmax, float* __restrict__ dscv, const int* __restrict__ prev_idx, int g_dense0) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)G * B) return;
@@ -898,22 +893,6 @@ __global__ __launch_bounds__(256, OCC) void topk_decode_grad_kernel(
   const int k = min(kv[g], kmax);
   const int* I = idx + row * kmax;
   const float* V = val + row * kmax;
-  if (g >= g_gemm0) {
-    // models from g_gemm0 decode and take their code gradients as dense MFMA GEMMs over the code
-    // buffer (engine/topk.py): only the scatter of the codes here (previous picks cleared first)
-    if (!codebuf) return;
-    uint16_t* Cb = codebuf + row * (long)n;
-    if (prev_idx) {
-      const int* P = prev_idx + row * kmax;
-      for (int j = lane; j < kmax; j += 64) Cb[P[j]] = 0;
-      __builtin_amdgcn_s_waitcnt(0);
-    }
-    for (int j = lane; j < k; j += 64) {
-      const float w = V[j];
-      if (w > 0.f) Cb[I[j]] = f2bf(w);
-    }
-    return;
-  }
   const uint16_t* Dg = D + (long)g * n * d;
   float acc[NV * 4];
 #pragma unroll
@@ -1311,12 +1290,11 @@ int sc_topk_select(const float* scores, const int* k, int* idx, float* val, int 
   return 1;
 }
 
-// Per-row top-k of bf16 scores [G][B][n], or [B][G][n] with bgn (see topk_bf16_kernel).  X ([B][d], or [G][B][d] with sx = B d)
+// Per-row top-k of bf16 scores [G][B][n] (see topk_bf16_kernel).  X ([B][d], or [G][B][d] with sx = B d)
 // and D ([G][n][d]) are the scores GEMM's bf16 operands, read to resolve ambiguous ties exactly (null:
 // ties in column order); absolute = select by |score| (no exact tie resolution).
 int sc_topk_select_bf16(const void* scores, const int* k, int* idx, float* val, int G, int B, int n, int kmax,
-                        int absolute, int relu, const void* X, long sx, const void* D, int d, hipStream_t stream,
-                        int bgn) {
+                        int absolute, int relu, const void* X, long sx, const void* D, int d, hipStream_t stream) {
   if (n % 8 || n < 8 || kmax < 1 || (X && (!D || d % 4 || d < 4))) return 1;
   dim3 grid((unsigned)G * B);
   const uint16_t* S = reinterpret_cast<const uint16_t*>(scores);
@@ -1324,7 +1302,7 @@ int sc_topk_select_bf16(const void* scores, const int* k, int* idx, float* val, 
   const uint16_t* Dp = reinterpret_cast<const uint16_t*>(D);
 #define SC_B16(P) \
   if (n <= 256 * P) { hipLaunchKernelGGL((topk_bf16_kernel<P>), grid, dim3(256), 0, stream, S, k, idx, val, B, n, kmax, \
-                                         absolute, relu, Xp, sx, Dp, d, bgn); \
+                                         absolute, relu, Xp, sx, Dp, d); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   SC_B16(8) SC_B16(16) SC_B16(24) SC_B16(32) SC_B16(48) SC_B16(64)
 #undef SC_B16
@@ -1333,7 +1311,7 @@ int sc_topk_select_bf16(const void* scores, const int* k, int* idx, float* val, 
 
 int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const void* D, const void* X, long sx,
                         void* R, float* row_se, void* codebuf, void* dscbuf, int G, int B, int n, int d, int kmax,
-                        hipStream_t stream, float* dscv, const int* prev_idx, int g_dense0, int g_gemm0) {
+                        hipStream_t stream, float* dscv, const int* prev_idx, int g_dense0) {
   if (d % 4) return 1;
   const int nv = (d + 255) / 256;
   dim3 grid(((long)G * B + 3) / 4);
@@ -1341,7 +1319,7 @@ int sc_topk_decode_grad(const int* idx, const float* val, const int* k, const vo
   if (nv <= V) { hipLaunchKernelGGL((topk_decode_grad_kernel<V>), grid, dim3(256), 0, stream, idx, val, k, \
       reinterpret_cast<const uint16_t*>(D), reinterpret_cast<const uint16_t*>(X), sx, reinterpret_cast<uint16_t*>(R), \
       row_se, reinterpret_cast<uint16_t*>(codebuf), reinterpret_cast<uint16_t*>(dscbuf), G, B, n, d, kmax, dscv, prev_idx, \
-      g_dense0, g_gemm0); \
+      g_dense0); \
     return hipGetLastError() == hipSuccess ? 0 : 3; }
   SC_D(1) SC_D(2) SC_D(3) SC_D(4) SC_D(8) SC_D(16)
 #undef SC_D

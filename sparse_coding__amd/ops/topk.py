@@ -10,15 +10,9 @@ import torch
 from . import _lib
 
 
-# [B, G, n] select order: 1 = memory order (model fastest), 2 = model rotated by the batch row
-_BGN_ORDER = int(os.environ.get("SC_TOPK_BGN_ORDER", "2"))
-
-
 def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool = False, relu: bool = True,
-                out=None, x: torch.Tensor = None, D: torch.Tensor = None, layout: str = "gbn"):
+                out=None, x: torch.Tensor = None, D: torch.Tensor = None):
     """Per-row top-k of ``scores`` [G, B, n] (fp32, or bf16) with per-model ``k`` (int32 [G]).
-    ``layout="bgn"`` (bf16 only): ``scores`` is [B, G, n] -- one library GEMM of the batch against the
-    stacked dictionaries writes that layout.
 
     Returns (idx int32 [G, B, kmax], val fp32 [G, B, kmax]); slots >= k[g] are (0, 0.0).
     ``absolute`` selects by |score| (PCA-style) and keeps the signed value; ``relu``
@@ -29,16 +23,17 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
     GEMM accumulated -- bf16 rounding is monotone, so only keys equal to the k-th largest bf16 key
     are ambiguous, and with ``x`` ([B, d] or [G, B, d] bf16) and ``D`` ([G, n, d] bf16, the GEMM's
     operands) those are ranked by their exact fp32 scores (ties to the lower column; without them,
-    or beyond 64 such keys, by column).  Values are the bf16 scores."""
-    if layout not in ("gbn", "bgn"):
-        raise ValueError(f"layout must be 'gbn' or 'bgn', got {layout!r}")
-    if layout == "bgn":
-        B, G, n = scores.shape
-    else:
-        G, B, n = scores.shape
+    or beyond 64 such keys, by column).  Values are the bf16 scores.
+
+    Limits of the exact-fp32 guarantee (bf16 scores): the bracket path resolves the ambiguous keys for
+    k <= 256 with at most BR_CAP bracket candidates and TIE_CAP = 64 keys tied at the k-th bf16 key
+    (csrc/topk.hip); past those limits the select falls back to bisection / radix on the bf16 keys and
+    ties at the threshold are taken in column order -- a pick may then differ from the fp32 top-k at
+    a near-tie (as it may between training, bf16 scores, and ``encode()``, fp32 scores)."""
+    if scores.dim() != 3:
+        raise ValueError("scores must be [G, B, n]")
+    G, B, n = scores.shape
     bf = scores.dtype == torch.bfloat16
-    if layout == "bgn" and not bf:
-        raise ValueError("the [B, G, n] layout is for bf16 scores")
     if scores.dtype not in (torch.float32, torch.bfloat16) or not scores.is_contiguous():
         raise ValueError("scores must be contiguous fp32 or bf16")
     if k.dtype != torch.int32 or k.numel() != G:
@@ -63,8 +58,7 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
             sx = B * d if x.dim() == 3 else 0
         rc = _lib.lib().sc_topk_select_bf16(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n,
                                             kmax, int(absolute), int(relu), _lib.ptr(x), sx,
-                                            _lib.ptr(D if x is not None else None), d, _lib.stream_handle(),
-                                            (_BGN_ORDER if layout == "bgn" else 0))
+                                            _lib.ptr(D if x is not None else None), d, _lib.stream_handle())
         _lib.check(rc, "sc_topk_select_bf16")
         return idx, val
     rc = _lib.lib().sc_topk_select(_lib.ptr(scores), _lib.ptr(k), _lib.ptr(idx), _lib.ptr(val), G, B, n, kmax,
@@ -74,28 +68,24 @@ def topk_select(scores: torch.Tensor, k: torch.Tensor, kmax: int, absolute: bool
 
 
 def decode_grad(idx, val, k, D, x, r_out, row_se, codebuf=None, dscbuf=None, dscv=None, prev_idx=None,
-                dense_from: int = 0, gemm_from: Optional[int] = None):
+                dense_from: int = 0):
     """Sparse decode + residual (bf16 r_out [G, B, d]) + per-row squared error; with the dense
     buffers, also scatter codes and code gradients <R, D[idx]> (units of R) for the wgrad GEMM;
     with ``dscv`` ([G, B, kmax] fp32) also the per-slot code gradients for ``sparse_wgrad``.
     ``prev_idx``: the previous step's picks ([G, B, kmax]), zeroed in the dense buffers first
     (instead of a ``clear`` after the previous weight gradient).  ``dense_from``: models below it
     (slot-list weight gradient) get their per-slot ``dscv`` only -- nothing is scattered into (or
-    cleared from) their dense buffers, which stay zero.  ``gemm_from``: models from it only get their
-    codes scattered into ``codebuf`` (previous picks cleared) -- their decode and code gradients run as
-    dense GEMMs over that buffer (engine/topk.py); nothing else of theirs is written here."""
+    cleared from) their dense buffers, which stay zero."""
     if prev_idx is not None and (prev_idx.shape != idx.shape or prev_idx.dtype != torch.int32
                                  or not prev_idx.is_contiguous()):
         raise ValueError("prev_idx must be contiguous int32 of idx's shape")
     G, B, kmax = idx.shape
     n, d = D.shape[1], D.shape[2]
-    if gemm_from is not None and gemm_from < G and codebuf is None:
-        raise ValueError("gemm_from needs codebuf: those models' codes are only scattered there")
     sx = 0 if x.dim() == 2 else B * d
     rc = _lib.lib().sc_topk_decode_grad(_lib.ptr(idx), _lib.ptr(val), _lib.ptr(k), _lib.ptr(D), _lib.ptr(x), sx,
                                         _lib.ptr(r_out), _lib.ptr(row_se), _lib.ptr(codebuf), _lib.ptr(dscbuf),
                                         G, B, n, d, kmax, _lib.stream_handle(), _lib.ptr(dscv), _lib.ptr(prev_idx),
-                                        int(dense_from), int(G if gemm_from is None else gemm_from))
+                                        int(dense_from))
     _lib.check(rc, "sc_topk_decode_grad")
 
 

@@ -59,6 +59,20 @@ class StepShape:
     adam_ms: float = 0.08          # Adam share of t1 (HBM-bound; divides by N under zero1 / es)
     es_ms: Dict[int, float] = field(default_factory=dict)  # measured per-rank ES steps, if any
     bus: Dict[str, float] = field(default_factory=dict)    # measured bus GB/s per mode (calibrate())
+    compute_source: str = "constants"  # "measured on this node" once use_measured_compute() ran
+
+    def use_measured_compute(self, world: int, t1_ms: Optional[float], es_ms: Optional[float]):
+        """Replace the compute inputs with steps timed on this node (bench.py ``calibrate_compute``):
+        ``t1_ms`` = one GPU's step of all G models on B rows (dp / zero1 per-rank layout), ``es_ms`` =
+        the ensemble-sharded per-rank layout (G/N models on N B rows).  ``best_mode`` then ranks the
+        modes on these numbers instead of the builder box's constants."""
+        if t1_ms:
+            self.t1_ms = float(t1_ms)
+        if es_ms:
+            self.es_ms = dict(self.es_ms)
+            self.es_ms[world] = float(es_ms)
+        if t1_ms or es_ms:
+            self.compute_source = "measured on this node"
 
     @property
     def params(self) -> int:
@@ -103,7 +117,8 @@ def predict(mode: str, world: int, shape: StepShape, dp_chunks: int = 2,
     return {"ms_per_step": round(compute + exposed, 4), "compute_ms": round(compute, 4),
             "comm_ms": round(comm_ms, 4), "exposed_comm_ms": round(exposed, 4),
             "bytes_per_gpu": nbytes, "bus_GBps": round(bw, 1) if world > 1 else None,
-            "bus_source": ("measured" if shape.bus.get(mode) else "link model") if world > 1 else None}
+            "bus_source": ("measured" if shape.bus.get(mode) else "link model") if world > 1 else None,
+            "compute_source": shape.compute_source}
 
 
 def calibrate(info, shape: StepShape, reps: int = 5) -> Optional[Dict[str, Dict[str, float]]]:

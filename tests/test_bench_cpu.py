@@ -116,3 +116,69 @@ def test_cross_rank_consistency_checks_gloo():
     for r in range(2):
         assert res[r]["same"] == 0.0 and res[r]["diff"] == 0.5
         assert res[r]["bsame"] == 0.0 and res[r]["bdiff"] > 0
+
+
+HANG_PROBE = r'''
+import json, os, sys
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+if "--dist-graph" not in sys.argv:
+    # the in-graph run: rank 1's watchdog fires in the timed region (marker + exit 5, no JSON)
+    if rank == 1:
+        with open(os.path.join(os.environ["SC_BENCH_HANG_DIR"], "rank1.json"), "w") as f:
+            json.dump({"rank": 1, "phase": "timed", "emitted": False}, f)
+        sys.exit(5)
+    sys.exit(0)
+if rank == 0:
+    print(json.dumps({"metric": "probe", "argv": sys.argv[1:]}), flush=True)
+'''
+
+
+def test_launch_ranks_relaunches_on_host_collectives_after_a_watchdog_hang(tmp_path, capfd):
+    """A rank whose watchdog ended a hung in-graph phase (marker + HANG_RC, no result line) makes the
+    launcher start FRESH ranks with --dist-graph 0 and the reason on record; their line is forwarded."""
+    script = tmp_path / "hang.py"
+    script.write_text(HANG_PROBE)
+    got = bench.launch_ranks(2, ["--gpus", "2", "--steps", "2"], script=str(script))
+    out, err = capfd.readouterr()
+    assert got == 0, err
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1, out
+    argv = json.loads(lines[0])["argv"]
+    assert argv[:4] == ["--gpus", "2", "--steps", "2"]
+    assert argv[argv.index("--dist-graph") + 1] == "0"
+    assert "in-graph hang: timed (rank 1)" in argv[argv.index("--fallback-reason") + 1]
+    # already on host collectives: a second hang is not retried
+    assert bench._dist_graph_off(["--dist-graph", "0"]) and bench._dist_graph_off(["--dp-graph=0"])
+    assert not bench._dist_graph_off(["--dist-graph", "1"]) and not bench._dist_graph_off([])
+
+
+WD_PROBE = r'''
+import json, os, sys, time
+sys.path.insert(0, sys.argv[1])
+import bench
+class Info: rank, is_main = 0, True
+wd = bench.Watchdog(Info(), True)
+wd.arm("capture", 30.0)
+wd.arm("first-replay", 0.2)    # re-armed: the capture limit no longer applies
+wd.disarm()
+time.sleep(0.5)                 # disarmed: nothing fires
+wd.pending = {"metric": "probe", "value": 1.0}
+wd.arm("alt-timed", 0.2)
+time.sleep(30)
+print("not reached")
+'''
+
+
+def test_watchdog_exits_with_marker_and_pending_record(tmp_path):
+    """The watchdog ends a process whose armed phase overruns: exit HANG_RC, a marker naming the phase,
+    and the pending (already measured) record on stdout; a disarmed or re-armed phase never fires."""
+    script = tmp_path / "wd.py"
+    script.write_text(WD_PROBE)
+    env = dict(os.environ, SC_BENCH_HANG_DIR=str(tmp_path))
+    p = subprocess.run([sys.executable, str(script), ROOT], capture_output=True, text=True, env=env, timeout=60)
+    assert p.returncode == bench.HANG_RC, p.stderr
+    assert "hung in phase 'alt-timed'" in p.stderr and "not reached" not in p.stdout
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rec["metric"] == "probe" and rec["watchdog"]["phase"] == "alt-timed"
+    marker = json.loads((tmp_path / "rank0.json").read_text())
+    assert marker == {"rank": 0, "phase": "alt-timed", "emitted": True}

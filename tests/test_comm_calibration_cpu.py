@@ -65,3 +65,29 @@ def test_calibrate_is_a_no_op_on_one_rank():
     shape = comm_model.StepShape(models=8, n=2048, d=512, batch=2048, t1_ms=0.3)
     assert comm_model.calibrate(DistInfo(), shape) is None and shape.bus == {}
     assert comm_model.predict("dp", 8, shape)["bus_source"] == "link model"
+
+
+def test_best_mode_uses_measured_compute_when_given():
+    """bench.py's ``calibrate_compute`` feeds the per-rank steps timed on the node into the model:
+    ``best_mode`` must rank the modes on them, not on the builder box's constants."""
+    from sparse_coding__amd.parallel import comm_model
+
+    def shape():
+        s = comm_model.StepShape(models=8, n=2048, d=512, batch=2048, t1_ms=0.30, es_ms={8: 0.24})
+        s.bus.update({"es": 200.0, "dp": 200.0, "zero1": 200.0})
+        return s
+
+    base = shape()
+    assert comm_model.best_mode(8, base) == "es"
+    assert comm_model.predict("es", 8, base)["compute_source"] == "constants"
+    # on this node the sharded layout turned out slow: the measured numbers flip the choice
+    slow_es = shape()
+    slow_es.use_measured_compute(8, t1_ms=0.30, es_ms=0.90)
+    p = comm_model.predict("es", 8, slow_es)
+    assert p["compute_ms"] == 0.90 and p["compute_source"] == "measured on this node"
+    assert comm_model.best_mode(8, slow_es) != "es"
+    # and a measured t1 moves the dp / zero1 predictions
+    fast = shape()
+    fast.use_measured_compute(8, t1_ms=0.10, es_ms=None)
+    assert comm_model.predict("dp", 8, fast)["compute_ms"] == 0.10
+    assert fast.es_ms == {8: 0.24}

@@ -406,17 +406,6 @@ def test_topk_select_bf16_picks_are_fp32_topk(n):
     assert not (has7 & ~has5).any()  # equal exact scores: the lower column first
     idx2, val2 = T.topk_select(sb, k, 128, x=x, D=D)
     assert torch.equal(idx2, idx) and torch.equal(val2, val)  # deterministic
-    # the [B, G, n] layout (one library GEMM over the stacked dictionaries) selects identically
-    idx3, val3 = T.topk_select(sb.transpose(0, 1).contiguous(), k, 128, x=x, D=D, layout="bgn")
-    assert torch.equal(idx3, idx) and torch.equal(val3, val)
-    sl = torch.matmul(x, D.view(G * n, d).t()).view(B, G, n)  # hipBLASLt's bf16 scores
-    idx4, _ = T.topk_select(sl, k, 128, x=x, D=D, layout="bgn")
-    for g in range(G):
-        kg = int(k[g])
-        e, pick = exact[g], idx4[g, :, :kg].long()
-        kth = e.topk(kg, dim=-1).values[:, -1:]
-        rows = torch.arange(B, device=DEV) != 40
-        assert (e.gather(-1, pick)[rows] >= kth[rows] - 2 * tol).all()  # fp32 top-k up to accumulation order
 
 
 def test_topk_scatter_and_clear_roundtrip():
@@ -436,18 +425,16 @@ def test_topk_scatter_and_clear_roundtrip():
     assert int(code.ne(0).sum()) == 0
 
 
-@pytest.mark.parametrize("sparse_k,grad_dtype,gemm_k", [(0, "fp32", 0), (0, "bf16", 0), (1000, "fp32", 0),
-                                                        ("auto", "bf16", 0), (0, "fp32", 16), (8, "bf16", 64)])
-def test_fused_topk_matches_autograd(sparse_k, grad_dtype, gemm_k):
+@pytest.mark.parametrize("sparse_k,grad_dtype", [(0, "fp32"), (0, "bf16"), (1000, "fp32"), ("auto", "bf16"),
+                                                (8, "bf16")])
+def test_fused_topk_matches_autograd(sparse_k, grad_dtype):
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
     from sparse_coding__amd.models.topk import TopKEncoder
 
     torch.manual_seed(7)
     d, n, B = 256, 1024, 256
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
-    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, sparse_k=sparse_k, grad_dtype=grad_dtype,
-                            gemm_k=gemm_k)
-    assert eng.gemm_g0 == {0: 3, 16: 1, 64: 2}[gemm_k]
+    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, sparse_k=sparse_k, grad_dtype=grad_dtype)
     assert eng.g.dtype == (torch.bfloat16 if grad_dtype == "bf16" else torch.float32)
     assert eng.sparse_g == {0: 0, 1000: 3}.get(sparse_k, eng.sparse_g)
     x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
@@ -465,12 +452,11 @@ def test_fused_topk_matches_autograd(sparse_k, grad_dtype, gemm_k):
         assert agree.float().mean() > 0.97, agree.float().mean()
 
 
-@pytest.mark.parametrize("grad_dtype,gemm_k", [("fp32", 0), ("bf16", 0), ("bf16", 48)])
-def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype, gemm_k):
+@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
+def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype):
     """Config 4 shape (GPT-2-small residual d = 768, n = 6144, B = 2048, k = 8 .. 128): the
     dictionary gradient of EVERY model -- slot-list path for the small k, dense GEMM for the
-    rest; with ``gemm_k`` the large-k models' decode and code gradients as dense GEMMs too --
-    against fp32 autograd of the top-k loss at the engine's own picks and the bf16 operands it
+    rest -- against fp32 autograd of the top-k loss at the engine's own picks and the bf16 operands it
     multiplies; relative Frobenius error <= 1e-2."""
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
     from sparse_coding__amd.models.topk import TopKEncoder
@@ -479,9 +465,8 @@ def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype, gemm_k):
     d, n, B = 768, 6144, 2048
     ks = [8, 16, 24, 32, 48, 64, 96, 128]
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in ks]
-    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, grad_dtype=grad_dtype, gemm_k=gemm_k)
+    eng = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, grad_dtype=grad_dtype)
     assert 0 < eng.sparse_g < len(ks)  # both wgrad paths are exercised
-    assert eng.gemm_g0 == (4 if gemm_k else len(ks))
     D0 = eng.shadow.float().clone()
     feats = torch.nn.functional.normalize(torch.randn(4096, d, device=DEV), dim=-1)
     x = ((torch.relu(torch.randn(B, 4096, device=DEV) - 1.5) * 3.0) @ feats).to(torch.bfloat16)
@@ -501,43 +486,17 @@ def test_fused_topk_gradient_config4_matches_fp32_autograd(grad_dtype, gemm_k):
         torch.testing.assert_close(mse[g], loss.detach(), rtol=1e-2, atol=1e-5)
 
 
-def test_topk_library_scores_gemm_matches(monkeypatch):
-    """SC_TOPK_SCORES_GEMM=blas: the scores as one hipBLASLt GEMM over the stacked dictionaries
-    ([B, G, n]) -- the same picks up to fp32 accumulation-order near-ties, the same training."""
-    from sparse_coding__amd.engine.topk import FusedTopKEnsemble
-    from sparse_coding__amd.models.topk import TopKEncoder
-
-    torch.manual_seed(29)
-    d, n, B = 768, 2048, 512
-    models = [TopKEncoder.init(d, n, k, device=DEV) for k in (8, 32, 96)]
-    ref = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3)
-    monkeypatch.setenv("SC_TOPK_SCORES_GEMM", "blas")
-    lib = FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3)
-    assert lib._scores_blas and tuple(lib.scores.shape) == (B, 3, n)
-    for _ in range(3):
-        x = torch.randn(B, d, device=DEV).to(torch.bfloat16)
-        m0, m1 = ref.step_batch(x).clone(), lib.step_batch(x).clone()
-        torch.cuda.synchronize()
-        torch.testing.assert_close(m1, m0, rtol=2e-3, atol=1e-6)
-        same = (ref.idx.sort(-1).values == lib.idx.sort(-1).values).float().mean().item()
-        assert same > 0.99, same
-    diff = (lib.params["dict"] - ref.params["dict"]).abs()
-    assert diff.max().item() <= 3.5e-3 and diff.gt(1e-5).float().mean().item() < 0.02  # near-tie picks only
-
-
-@pytest.mark.parametrize("gemm_k", [0, 16])
-def test_topk_tail_matches_separate_launches(gemm_k):
+def test_topk_tail_matches_separate_launches():
     """The fused top-k tail (one launch: row Adam + per-model MSE + step counter) == the separate
     Adam launch, torch reductions and counter increment: masters, moments, shadows bit-equal over
-    three steps, MSE to fp32 rounding, the device counter advanced once per step (``gemm_k``: the
-    GEMM-decoded models' MSE from the decoder's tile partials)."""
+    three steps, MSE to fp32 rounding, the device counter advanced once per step."""
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
     from sparse_coding__amd.models.topk import TopKEncoder
 
     torch.manual_seed(23)
     d, n, B = 768, 1024, 256
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
-    fused, split = (FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, gemm_k=gemm_k) for _ in range(2))
+    fused, split = (FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3) for _ in range(2))
     assert fused._tail
     split._tail = False
     for t in range(3):
@@ -552,8 +511,7 @@ def test_topk_tail_matches_separate_launches(gemm_k):
     assert not fused._ticket.any()  # the completion counters reset themselves
 
 
-@pytest.mark.parametrize("gemm_k", [0, 16])
-def test_fused_topk_graph_matches_eager(gemm_k):
+def test_fused_topk_graph_matches_eager():
     """The two captured step graphs (alternating pick buffers: step t clears step t-1's picks
     in the dense buffers) == eager steps, bitwise, over several steps."""
     from sparse_coding__amd.engine.topk import FusedTopKEnsemble
@@ -562,7 +520,7 @@ def test_fused_topk_graph_matches_eager(gemm_k):
     torch.manual_seed(13)
     d, n, B = 256, 1024, 256
     models = [TopKEncoder.init(d, n, k, device=DEV) for k in (4, 16, 64)]
-    engs = [FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, sparse_k=8, gemm_k=gemm_k) for _ in range(2)]
+    engs = [FusedTopKEnsemble(models, batch_size=B, device=DEV, lr=1e-3, sparse_k=8) for _ in range(2)]
     engs[1].enable_graph()
     assert engs[0].sparse_g == 1
     for s in range(5):
