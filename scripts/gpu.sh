@@ -19,6 +19,7 @@
 #              (default 2); run i of variant v appends to gpurun_out/ab/v<v>.jsonl, then a summary.
 #              e.g. AB_CMD="scripts/bench_configs.py topk --steps 40" AB_VALUES="--sparse-k 0|--sparse-k auto"
 #   ktest:K    pytest tests/test_kernels_gpu.py tests/test_train_gpu.py -k K
+#   pytest:FILE[::K]  one GPU test file (optionally -k K)
 #   profile:CMD  rocprofv3 --kernel-trace --stats of "python3 CMD" (top-20 summary)
 # Extra bench flags: BENCH_ARGS env.
 set -o pipefail
@@ -76,6 +77,12 @@ PY
         done
       done
       grep -o '"ms_per_step": [0-9.]*\|"solve_ms_all_models": [0-9.]*' "$O"/ab/*.jsonl ;;
+    pytest:*)
+      # pytest:FILE[::K] -- one GPU test file (optionally -k K), one process
+      local spec="${s#pytest:}" f k=""
+      f="${spec%%::*}"; [[ "$spec" == *::* ]] && k="${spec#*::}"
+      timeout -k 10 900 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread ${k:+-k "$k"} > "$O/pytest_$(basename "$f" .py).log" 2>&1
+      local rc=$?; tail -15 "$O/pytest_$(basename "$f" .py).log"; return $rc ;;
     ktest:*)
       timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_train_gpu.py -x -q --timeout 300 --timeout-method thread -k "${s#ktest:}" > "$O/ktest.log" 2>&1
       local rc=$?; tail -15 "$O/ktest.log"; return $rc ;;

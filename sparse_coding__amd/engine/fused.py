@@ -280,6 +280,14 @@ class FusedSAEEnsemble:
         else:
             adam_ops.shadow_rows(self.params["encoder"], self.enc_shadow, self.norms, normalize=True)
 
+    def refresh_decoder_shadow(self):
+        """Rebuild only the decoder's bf16 shadow and row norms (untied SAEs; after an out-of-band edit
+        of the decoder alone, e.g. the FISTA basis update) -- the encoder shadow is left as it is."""
+        if self.kind != "untied":
+            self.refresh_shadows()
+            return
+        adam_ops.shadow_rows(self.params["decoder"], self.dec_shadow, self.norms, normalize=True)
+
     def prepare(self, x):
         """The kernels' input: ``x`` itself, or its per-model centred copy for tied SAEs
         with non-identity centering (threshold SAEs: x - centering, learned)."""

@@ -262,17 +262,19 @@ class EnsembleTrainer:
         return self.last_loss
 
     def _fista_update(self, batch, codes):
-        x = batch.to(self.device, torch.float32)
         if self.kind == "fused-sae":
             eng = self.impl
-            new, _, _ = self.fista(eng.params["decoder"], x, eng.c.float(), eng.l1)
+            # the bf16 batch as it is (the GPU FISTA path multiplies bf16 operands; no fp32 copy)
+            x = batch.to(self.device) if batch.dtype == torch.bfloat16 else batch.to(self.device, torch.float32)
+            new, _, _ = self.fista(eng.params["decoder"], x, eng.c, eng.l1)
             eng.params["decoder"].copy_(new)
-            eng.refresh_shadows()
-        else:
-            ens = self.impl
-            l1 = ens.buffers["l1_alpha"]
-            new, _, _ = self.fista(ens.params["decoder"], x, codes.float(), l1)
-            ens.params["decoder"].data.copy_(new)
+            eng.refresh_decoder_shadow()
+            return
+        x = batch.to(self.device, torch.float32)
+        ens = self.impl
+        l1 = ens.buffers["l1_alpha"]
+        new, _, _ = self.fista(ens.params["decoder"], x, codes.float(), l1)
+        ens.params["decoder"].data.copy_(new)
 
     # ------------------------------------------------------------------ export / state
     def hyperparams(self, ensemble_hyperparams: Sequence[str] = (), buffer_hyperparams: Sequence[str] = ("l1_alpha",),
@@ -327,8 +329,12 @@ class EnsembleTrainer:
     def state_dict(self) -> Dict[str, Any]:
         st = {"kind": self.kind, "steps": self.steps, "name": self.name, "args": self.args}
         if self.kind == "zero1-eager":
-            raise NotImplementedError("checkpoint of the eager ZeRO-1 trainer (its moments are sharded)")
-        if self.kind.endswith("-graphed"):
+            # the sharded moments gathered whole (collective: every rank calls state_dict)
+            from torch.utils import _pytree as pytree
+
+            st["impl"] = {"params": pytree.tree_map(lambda t: t.detach().clone(), self.impl.params),
+                          "zero": [c.state_dict() for c in self.dp.chunks]}
+        elif self.kind.endswith("-graphed"):
             self.dp.gather_masters()  # ZeRO-1: every rank's masters / moments complete
             st["impl"] = self.impl.state_dict()
         elif self.kind == "fused-sae":
@@ -352,6 +358,13 @@ class EnsembleTrainer:
         if self.kind in ("fused-sae", "analytic", "fista-loss", "fista-loss-fused", "unrolled", "dp-graphed",
                          "zero1-graphed"):
             self.impl.load_state_dict(imp)
+        elif self.kind == "zero1-eager":
+            from torch.utils import _pytree as pytree
+
+            for a, b in zip(pytree.tree_leaves(self.impl.params), pytree.tree_leaves(imp["params"])):
+                a.data.copy_(b)
+            for c, zst in zip(self.dp.chunks, imp["zero"]):
+                c.load_state_dict(zst)
         elif self.kind == "fused-topk":
             for d_ in ("params", "m", "v"):
                 for k, t in imp[d_].items():

@@ -149,8 +149,30 @@ class FistaDictUpdater:
     _eta: Optional[object] = None  # EtaTracker state when eta_method == "tracked"
 
     def __call__(self, decoder: torch.Tensor, batch: torch.Tensor, codes: torch.Tensor, l1: torch.Tensor):
-        """decoder [G, n, d] raw; batch [B, d]; codes [G, B, n]; returns (new decoder, residual, A)."""
+        """decoder [G, n, d] raw; batch [B, d]; codes [G, B, n]; returns (new decoder, residual, A).
+
+        On the GPU with the Gram-form shapes (``fista_ops.gram_solve_ok``) the step runs the hot path:
+        X D^T and D D^T on the MFMA GEMM, eta from the solver's own Gram (``EtaTracker.from_gram``),
+        the persistent solve, the residual by the decoder GEMM's epilogue (bf16, negated) and the basis
+        update on those bf16 operands -- no fp32 GEMM, no operand copies; the returned residual is then
+        the bf16 one (fp32 view)."""
         D = unit_rows(decoder.float())
+        if self.backend != "torch" and fista_ops.gram_solve_ok(batch, D):
+            tracker = None
+            if self.eta_method == "tracked":
+                if self._eta is None:
+                    self._eta = fista_ops.EtaTracker()
+                tracker = self._eta
+            eta = None if tracker is not None else fista_ops.step_size(D, self.eta_method)
+            A, Ab, Rn, _, _ = fista_ops.gram_solve(batch, D, l1, codes, self.num_iter, eta=eta, tracker=tracker)
+            G, n = D.shape[0], D.shape[1]
+            H0 = self.hessian if (self.persist_hessian and self.hessian is not None) else torch.zeros(G, n, device=D.device)
+            H = fista_ops.hessian_ema(H0, A, ACT_HISTORY_LEN)
+            if self.persist_hessian:
+                self.hessian = H
+            new = fista_ops.quadratic_basis_update(D, None, A, H, self.lowest_activation, self.step,
+                                                   normalize=self.normalize, A_bf16=Ab, res_neg_bf16=Rn)
+            return new, Rn.float().neg_(), A
         if self.eta_method == "tracked":
             if self._eta is None:
                 self._eta = fista_ops.EtaTracker()

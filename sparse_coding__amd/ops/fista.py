@@ -66,10 +66,21 @@ class EtaTracker:
         self.margin = margin
         self.v = None
         self.calls = 0
+        self.space = "dtd"  # which Gram the eigenvector lives in: D^T D [d, d] or D D^T [n, n]
 
     def __call__(self, D: torch.Tensor) -> torch.Tensor:
         D = D.float()
-        gram = D.transpose(-1, -2) @ D  # [G, d, d], same nonzero spectrum as D D^T
+        return self._track(D.transpose(-1, -2) @ D, "dtd")  # [G, d, d], same nonzero spectrum as D D^T
+
+    def from_gram(self, gram: torch.Tensor) -> torch.Tensor:
+        """The same estimate from a Gram matrix D D^T [G, n, n] fp32 the caller already has -- the
+        solver's own (``gram_solve``: bf16 D, fp32 accumulation), so eta bounds the operator the
+        iterations actually apply and no separate fp32 D^T D product is needed."""
+        return self._track(gram, "ddt")
+
+    def _track(self, gram: torch.Tensor, space: str) -> torch.Tensor:
+        if space != self.space:  # the warm eigenvector belongs to the other Gram: refresh exactly
+            self.space, self.v = space, None
         if self.v is None or self.v.shape[:2] != gram.shape[:2] or self.calls % self.refresh_every == 0:
             vals, vecs = torch.linalg.eigh(gram)
             self.v = vecs[..., -1:].contiguous()
@@ -85,11 +96,12 @@ class EtaTracker:
         return 1.0 / ((1.0 + self.margin) * lam)
 
     def state_dict(self):
-        return {"v": None if self.v is None else self.v.detach().clone(), "calls": self.calls}
+        return {"v": None if self.v is None else self.v.detach().clone(), "calls": self.calls, "space": self.space}
 
     def load_state_dict(self, st):
         self.v = None if st.get("v") is None else st["v"].clone()
         self.calls = int(st.get("calls", 0))
+        self.space = st.get("space", "dtd")
 
 
 def fista_torch(X, D, lam, A0=None, iters=500, eta=None) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -146,13 +158,10 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
         eta = step_size(D)
     eta = eta.to(dev).float().contiguous()
     lam = torch.as_tensor(lam, device=dev, dtype=torch.float32).reshape(G).contiguous()
-    Xb = X.to(torch.bfloat16)
-    if Xb.dim() == 2:
-        Xb = Xb.expand(G, *Xb.shape)
-    Xb = Xb.contiguous()
+    Xb = X.to(torch.bfloat16).contiguous()  # [B, d] stays shared: the grouped GEMMs take a stride-0 operand
     Db = D.to(torch.bfloat16).contiguous()
     A = torch.empty(G, B, n, device=dev)
-    a0 = A0.float().contiguous() if A0 is not None else None
+    a0 = _f32(A0) if A0 is not None else None
     mom = momentum_schedule(max(iters, 1)).to(dev)
     if form == "auto":
         form = "gram" if (n <= d and n in GRAM_N) else "direct"
@@ -163,7 +172,7 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
         if B % 128 == 0:
             gemm.matmul_nt(Xb, Db, C)                   # C = X D^T (MFMA, fp32 out)
         else:
-            torch.bmm(Xb.float(), Db.float().transpose(1, 2), out=C)
+            torch.matmul(Xb.float(), Db.float().transpose(1, 2), out=C)
         Gm = torch.empty(G, n, n, device=dev, dtype=torch.bfloat16)
         gemm.matmul_nt(Db, Db, Gm)                      # Gm = D D^T (bf16 out)
         # MFMA-fragment order (constant over the solve): [G][n/16 col tiles][n/32 k-steps][q][row][8]
@@ -173,6 +182,8 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
                                       _lib.ptr(mom), _lib.ptr(A), G, B, n, iters, _lib.stream_handle(), rows, 0,
                                       None, None, None, None, None)
     else:
+        if Xb.dim() == 2:  # (the direct-form solver reads a per-model X)
+            Xb = Xb.expand(G, *Xb.shape).contiguous()
         # both operands in MFMA-fragment order (see the Gram form): D [G][n/16][d/32][64][8] for the
         # (Res D^T) product, D^T [G][d/16][n/32][64][8] for the (Y D) product
         Dtb = Db.transpose(1, 2).reshape(G, d // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
@@ -188,6 +199,71 @@ def fista(X, D, lam, A0=None, iters=500, eta=None, backend: str = "auto", with_r
     # final residual in fp32 against the exact dictionary (one plain GEMM per model)
     Xf = X.float() if X.dim() == 3 else X.float().expand(G, *X.shape)
     return A, Xf - torch.bmm(A, D.float())
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    """``t`` as contiguous fp32 without a copy when it already is."""
+    return t if (t.dtype == torch.float32 and t.is_contiguous()) else t.float().contiguous()
+
+
+def gram_fragments(gm32: torch.Tensor) -> torch.Tensor:
+    """fp32 Gram [G, n, n] -> the Gram solver's bf16 MFMA-fragment order
+    [G][n/16 col tiles][n/32 k-steps][q][row][8] in one cast + permute pass."""
+    G, n, _ = gm32.shape
+    out = torch.empty(G, n // 16, n // 32, 4, 16, 8, device=gm32.device, dtype=torch.bfloat16)
+    out.copy_(gm32.view(G, n // 16, 16, n // 32, 4, 8).permute(0, 1, 3, 4, 2, 5))
+    return out
+
+
+def gram_solve_ok(X, D) -> bool:
+    """Shapes the dictionary-update hot path (``gram_solve``) takes: the Gram-form solver and the
+    step GEMMs (B, d multiples of 128, n one of GRAM_N and n <= d)."""
+    G, n, d = D.shape
+    return (D.is_cuda and _lib.available() and X.shape[-2] % 128 == 0 and d % 128 == 0 and n in GRAM_N
+            and n <= d and X.dim() == 2)
+
+
+def gram_solve(X, D, lam, A0, iters, eta=None, tracker: Optional[EtaTracker] = None, rows: int = 0):
+    """The GPU hot path of one FISTA dictionary step (``models.fista.FistaDictUpdater``): everything the
+    basis update needs, with no fp32 GEMM and no operand copies.
+
+    * C = X D^T and Gm = D D^T on the MFMA GEMM (bf16 operands, fp32 out; X [B, d] shared by the models);
+    * eta from ``tracker.from_gram(Gm)`` (the Gram the iterations apply) unless given;
+    * the persistent Gram-form solve (A fp32);
+    * Ab = bf16(A) once, and the NEGATED residual Rn = A D - X (bf16) by the decoder GEMM's EPI_DEC
+      epilogue, with per-tile sum(R^2) partials -- replacing the fp32 ``torch.bmm`` residual of
+      ``fista()`` (the basis update rounds A and the residual to bf16 for its own GEMM anyway).
+
+    Returns (A fp32 [G, B, n], Ab bf16, Rn bf16 [G, B, d], eta [G], se [G] = |X - A D|^2 per model).
+    Reference: ``autoencoders/fista.py:99-128`` (solve) and ``:131-138`` (the residual it hands on)."""
+    from . import gemm
+
+    G, n, d = D.shape
+    B = X.shape[-2]
+    dev = D.device
+    Xb = X.to(torch.bfloat16).contiguous()
+    Db = D.to(torch.bfloat16).contiguous()
+    C = torch.empty(G, B, n, device=dev)
+    gemm.matmul_nt(Xb, Db, C)
+    gm32 = torch.empty(G, n, n, device=dev)
+    gemm.matmul_nt(Db, Db, gm32)
+    if eta is None:
+        eta = tracker.from_gram(gm32) if tracker is not None else 1.0 / torch.linalg.eigvalsh(gm32).amax(dim=-1)
+    eta = eta.to(dev).float().contiguous()
+    Gm = gram_fragments(gm32)
+    del gm32
+    lam = torch.as_tensor(lam, device=dev, dtype=torch.float32).reshape(G).contiguous()
+    A = torch.empty(G, B, n, device=dev)
+    mom = momentum_schedule(max(iters, 1)).to(dev)
+    rc = _lib.lib().sc_fista_gram(_lib.ptr(C), _lib.ptr(Gm), _lib.ptr(_f32(A0) if A0 is not None else None),
+                                  _lib.ptr(eta), _lib.ptr(lam), _lib.ptr(mom), _lib.ptr(A), G, B, n, iters,
+                                  _lib.stream_handle(), rows, 0, None, None, None, None, None)
+    _lib.check(rc, "sc_fista_gram")
+    Ab = A.to(torch.bfloat16)
+    Rn = torch.empty(G, B, d, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(G, (B // 128) * (d // 128), device=dev)
+    gemm.decode_residual(Ab, Db, Xb, Rn, part)
+    return A, Ab, Rn, eta, part.sum(dim=1)
 
 
 def _hip_ok(*ts) -> bool:
@@ -210,7 +286,8 @@ def hessian_ema(H, A, history: int = 300, backend: str = "auto"):
 
 
 def quadratic_basis_update(D, Res, A, H, lowest_activation=0.001, step=0.001, nonneg=False,
-                           normalize: str = "column", backend: str = "auto", shadow_out=None):
+                           normalize: str = "column", backend: str = "auto", shadow_out=None,
+                           A_bf16=None, res_neg_bf16=None):
     """D' = D + (step Res^T A / B / (H + lowest))^T, then renormalise (reference :131-138).
 
     normalize="column" reproduces the reference (``D.norm(2, 0)``: per activation
@@ -220,11 +297,18 @@ def quadratic_basis_update(D, Res, A, H, lowest_activation=0.001, step=0.001, no
     HIP path: A^T Res by the grouped MFMA GEMM (bf16 operands, fp32 accumulation, the
     step/B scale in its epilogue), then one kernel adds the H-scaled update, clamps and
     renormalises (csrc/fista_update.hip); ``shadow_out`` (bf16 [G, n, d]) optionally receives
-    the bf16 copy the next solve multiplies by.
+    the bf16 copy the next solve multiplies by.  ``A_bf16`` / ``res_neg_bf16`` (HIP path, from
+    ``gram_solve``): the GEMM operands already in bf16, the residual NEGATED (A D - X); ``Res`` may
+    then be None.
     """
     G, B, n = A.shape
     d = D.shape[-1]
-    hip = backend != "torch" and _hip_ok(D, Res, A, H) and n % 128 == 0 and d % 128 == 0 and B % 64 == 0
+    if Res is None and res_neg_bf16 is None:
+        raise ValueError("quadratic_basis_update needs Res or res_neg_bf16")
+    hip = (backend != "torch" and _hip_ok(D, A, H) and (Res is None or Res.is_cuda) and n % 128 == 0
+           and d % 128 == 0 and B % 64 == 0)
+    if not hip and Res is None:
+        Res = -res_neg_bf16.float()
     if not hip:
         dB = step * torch.bmm(Res.transpose(1, 2).float(), A.float()) / B  # [G, d, n]
         dB = dB / (H.unsqueeze(1) + lowest_activation)
@@ -238,9 +322,13 @@ def quadratic_basis_update(D, Res, A, H, lowest_activation=0.001, step=0.001, no
     from . import gemm
 
     dBt = torch.empty(G, n, d, device=D.device)
-    gemm.weight_grads([[(A.to(torch.bfloat16).contiguous(), Res.to(torch.bfloat16).contiguous())]], [dBt], step / B)
+    if res_neg_bf16 is not None:  # A^T (A D - X) = -A^T Res
+        Ab = A_bf16 if A_bf16 is not None else A.to(torch.bfloat16)
+        gemm.weight_grads([[(Ab.contiguous(), res_neg_bf16.contiguous())]], [dBt], -step / B)
+    else:
+        gemm.weight_grads([[(A.to(torch.bfloat16).contiguous(), Res.to(torch.bfloat16).contiguous())]], [dBt], step / B)
     out = D.float().contiguous().clone()
-    rc = _lib.lib().sc_basis_apply(_lib.ptr(out), _lib.ptr(dBt), _lib.ptr(H.float().contiguous()),
+    rc = _lib.lib().sc_basis_apply(_lib.ptr(out), _lib.ptr(dBt), _lib.ptr(_f32(H)),
                                    _lib.ptr(shadow_out), G, n, d, float(lowest_activation), int(bool(nonneg)),
                                    1 if normalize == "row" else 0, _lib.stream_handle())
     _lib.check(rc, "sc_basis_apply")

@@ -40,8 +40,11 @@ class _Chunk:
     def __init__(self, engine, mode: str, info: DistInfo, grad_dtype):
         e = self.engine = engine
         kind = getattr(e, "kind", None)
-        if kind not in ("untied", "tied") or e.learned_center or e.nactive is not None:
-            raise NotImplementedError(f"graphed data parallel of engine kind {kind} (masked / learned centre)")
+        if kind not in ("untied", "tied") or e.learned_center:
+            raise NotImplementedError(f"graphed data parallel of engine kind {kind} (learned centre)")
+        # Masked ensembles (per-model live sizes, reference sae_ensemble.py:306-442): the compacted
+        # launches never write a dead row of the flat gradient (the engine zero-initialises it), so the
+        # reductions carry zeros there on every rank, and every update skips dead rows (``live``).
         # the reductions read the flat fp32 gradient buffer: drop any split-K slabs / bf16 copy the
         # engine picked for its own shape (FusedSAEEnsemble(wgrad_split='auto'))
         e.use_flat_grads()
@@ -171,10 +174,11 @@ class GraphedDataParallel:
             adam_ops.step_tail(sets, e.lr, *e.betas, e.eps, e.step_dev, e.params[e._bkey], e.m[e._bkey],
                                e.v[e._bkey], e.g_bias, e.enc_part, e.dec_part, e.l1, e.bias_decay, e.out,
                                e.batch_size, 1.0, e._bsq, e._ticket, cnt_part=e.cnt_part if e._counted else None,
-                               feat_count=e.feature_counts if e._counted else None, row0=lo, gather=gather)
+                               feat_count=e.feature_counts if e._counted else None, row0=lo, gather=gather,
+                               live=e.nactive)
         else:
             adam_ops.adam_rows(sets, e.lr, e.step_count + 1, *e.betas, e.eps, rows_per_model=n,
-                               step_dev=e.step_dev, row0=lo)
+                               step_dev=e.step_dev, row0=lo, live=e.nactive)
             e._bias_loss(update=True, reduced=True)
         if c.world > 1:  # every rank's updated shadows (and norms) for the chunk's next compute
             evs = []

@@ -342,6 +342,29 @@ class ZeroEagerChunk:
     def set_grad_scale(self, s: float):
         self.scale = s
 
+    def state_dict(self):
+        """The full (unsharded) Adam state: every rank's moment slices all-gathered into padded
+        flat vectors (collective: every rank calls it), so a checkpoint restores at any world size."""
+        full = {}
+        for k, t in (("m", self.m), ("v", self.v)):
+            flat = torch.zeros(self._padded, device=t.device)
+            flat[self.lo:self.hi] = t
+            if dist.is_initialized() and self.info.world_size > 1:
+                w = all_gather_async(flat, self.lo, self.hi)
+                if w is not None:
+                    w.wait()
+            full[k] = flat[: self._numel].clone()
+        full["count"] = self.count
+        return full
+
+    def load_state_dict(self, st):
+        """Restore this rank's slices from a ``state_dict()`` (written at any world size)."""
+        for k, t in (("m", self.m), ("v", self.v)):
+            flat = torch.zeros(self._padded, device=t.device)
+            flat[: self._numel] = st[k].to(t.device)
+            t.copy_(flat[self.lo:self.hi])
+        self.count = int(st["count"])
+
     def params(self):
         return [t.data for t in pytree.tree_leaves(self.ens.params)]
 

@@ -35,19 +35,20 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, mode, grad_dtype, chunks, rows, init, q):
+def _worker(rank, world, port, mode, grad_dtype, chunks, rows, init, q, sig_name="FunctionalSAE"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
     from sparse_coding__amd.data.ring import DeviceRing
     from sparse_coding__amd.engine.fused import FusedSAEEnsemble
     from sparse_coding__amd.engine.graph_plan import count_pattern
-    from sparse_coding__amd.models.signatures import FunctionalSAE
+    from sparse_coding__amd.models import signatures
     from sparse_coding__amd.parallel import graphed
     from sparse_coding__amd.parallel.data_parallel import split_models
     from sparse_coding__amd.parallel.dist import DistInfo
     from sparse_coding__amd.parallel.host_comm import HostComm
 
+    FunctionalSAE = getattr(signatures, sig_name)
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda:0")
@@ -110,27 +111,37 @@ def _worker(rank, world, port, mode, grad_dtype, chunks, rows, init, q):
         raise
 
 
-def _setup():
-    from sparse_coding__amd.models.signatures import FunctionalSAE
+MASKED_SIZES = (128, 256, 384, 512)  # live sizes of the masked ensemble (stacked to N_DICT)
+
+
+def _setup(sig_name="FunctionalSAE"):
+    from sparse_coding__amd.models import signatures
 
     torch.manual_seed(41)
-    init = [FunctionalSAE.init(D, N_DICT, l1) for l1 in L1S]
+    sig = getattr(signatures, sig_name)
+    if "Masked" in sig_name:
+        init = [sig.init(D, sz, N_DICT, l1) for sz, l1 in zip(MASKED_SIZES, L1S)]
+    else:
+        init = [sig.init(D, N_DICT, l1) for l1 in L1S]
     feats = torch.nn.functional.normalize(torch.randn(2048, D), dim=-1)
     rows = ((torch.relu(torch.randn(B * 64, 2048) - 2.0) @ feats) * 1.5).to(torch.bfloat16)
     return init, rows
 
 
-def _single(init, rows, world):
+def _single(init, rows, world, sig_name="FunctionalSAE"):
     """Single-process training of all models on the global batches (N B rows per step)."""
     from sparse_coding__amd.data.ring import DeviceRing
     from sparse_coding__amd.engine.fused import FusedSAEEnsemble
     from sparse_coding__amd.engine.graph_plan import count_pattern
-    from sparse_coding__amd.models.signatures import FunctionalSAE
+    from sparse_coding__amd.models import signatures
+
+    FunctionalSAE = getattr(signatures, sig_name)
 
     dev = torch.device("cuda:0")
     ring = DeviceRing(rows.shape[0], D, device=dev, seed=7)
     ring.push(rows.to(dev))
-    models = [({k: v.to(dev) for k, v in p.items()}, b) for p, b in init]
+    models = [({k: v.to(dev) for k, v in p.items()}, {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in b.items()})
+              for p, b in init]
     e = FusedSAEEnsemble(models, FunctionalSAE, lr=1e-3, batch_size=world * B, device=dev, wgrad_split=1)
     e.enable_graph().attach_source(ring.graph_source(world * B))
     for s in GROUPS:
@@ -139,14 +150,14 @@ def _single(init, rows, world):
     return e
 
 
-def _launch(world, mode, grad_dtype=torch.float32, chunks=1):
+def _launch(world, mode, grad_dtype=torch.float32, chunks=1, sig_name="FunctionalSAE"):
     import torch.multiprocessing as mp
 
-    init, rows = _setup()
+    init, rows = _setup(sig_name)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, grad_dtype, chunks, rows, init, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, grad_dtype, chunks, rows, init, q, sig_name))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -215,6 +226,25 @@ def test_graphed_ensemble_sharded_multirank(world):
         assert dc.max() <= 2 and (dc > 0).mean() < 0.01
         assert ex["step"] == sum(GROUPS)
     _HITS[(world, "es")] = set(res[0][2])
+
+
+@pytest.mark.parametrize("mode,chunks", [("dp", 2), ("zero1", 1)])
+def test_graphed_data_parallel_masked_multirank(mode, chunks):
+    """A masked ensemble (live sizes 128..512 stacked to 512) data-parallel over 2 gloo ranks: replicas
+    identical, equal to single-process global-batch training of the masked models, dead rows unmoved."""
+    world = 2
+    init, rows, res = _launch(world, mode, torch.float32, chunks, sig_name="FunctionalMaskedSAE")
+    ref = _single(init, rows, world, sig_name="FunctionalMaskedSAE")
+    assert ref.nactive is not None
+    p0s = {k: np.stack([p[k].numpy() for p, _ in init]) for k in res[0][0]}
+    for k in res[0][0]:
+        np.testing.assert_array_equal(res[0][0][k], res[1][0][k], err_msg=k)
+    for k, got in res[0][0].items():
+        rel = _rel_change(got, ref.params[k].cpu().numpy(), p0s[k])
+        assert rel < 2e-2, (k, rel)
+        for g, sz in enumerate(MASKED_SIZES):
+            np.testing.assert_array_equal(got[g, sz:], p0s[k][g, sz:], err_msg=f"{k} model {g} dead rows")
+    assert res[0][1]["step"] == sum(GROUPS)
 
 
 def _multirank_lines():

@@ -281,6 +281,44 @@ def test_trainer_graphed_data_parallel_one_rank(mode):
     assert st["kind"] == f"{mode}-graphed" and st["impl"]["step"] == 6
 
 
+@pytest.mark.parametrize("sig_name,mode", [("FunctionalMaskedTiedSAE", "dp"), ("FunctionalMaskedSAE", "dp"),
+                                           ("FunctionalMaskedSAE", "zero1")])
+def test_trainer_graphed_data_parallel_masked_one_rank(sig_name, mode):
+    """Masked ensembles (models of different live sizes stacked to one width, the reference's
+    dict_ratio experiment, big_sweep_experiments.py:546-580) train data-parallel on the graphed path:
+    EnsembleTrainer(parallel='dp' / 'zero1') at one RCCL rank == the plain fused masked trainer, and
+    the dead rows / columns stay exactly as initialised."""
+    from sparse_coding__amd.engine.trainer import EnsembleTrainer
+    from sparse_coding__amd.models import signatures as S
+    from sparse_coding__amd.parallel.dist import DistInfo
+
+    sig = getattr(S, sig_name)
+    torch.manual_seed(43)
+    d, n, B = 512, 1024, 256
+    sizes = (256, 512, 768, 1024)
+    models = [sig.init(d, sz, n, l1, device=DEV) for sz, l1 in zip(sizes, (1e-4, 1e-3, 3e-3, 1e-2))]
+    tr = EnsembleTrainer(models, sig, lr=1e-3, batch_size=B, device=DEV, parallel=mode,
+                         dist=DistInfo(device=torch.device(DEV)), args={"dict_size": n})
+    ref = EnsembleTrainer(models, sig, lr=1e-3, batch_size=B, device=DEV, args={"dict_size": n})
+    assert tr.kind == f"{mode}-graphed" and ref.kind == "fused-sae" and tr.impl.nactive is not None
+    feats = torch.nn.functional.normalize(torch.randn(2048, d, device=DEV), dim=-1)
+    for _ in range(6):
+        x = (torch.relu(torch.randn(B, 2048, device=DEV) - 2.0) @ feats).to(torch.bfloat16)
+        a = tr.step(x).clone()
+        b = ref.step(x).clone()
+    torch.cuda.synchronize()
+    tr.close()
+    torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-6)
+    for k in ref.impl.params:
+        p0 = torch.stack([m[0][k] for m in models])
+        rel = float((tr.impl.params[k] - ref.impl.params[k]).norm() / (ref.impl.params[k] - p0).norm())
+        assert rel < 1e-2, (k, rel)
+        for g, sz in enumerate(sizes):  # dead rows never move
+            assert torch.equal(tr.impl.params[k][g, sz:], p0[g, sz:]), (k, g)
+    lds = tr.to_learned_dicts(["dict_size"], ["l1_alpha"])
+    assert [ld.n_feats for ld, _ in lds] == list(sizes)
+
+
 def test_ring_gather_into_global_matches_indexing():
     """One launch fills rank r's slots of s consecutive global batches from the ring permutation
     (the in-place all-gather layout of graphed ensemble sharding); other ranks' slots untouched."""

@@ -896,6 +896,47 @@ def test_fista_dictionary_update_on_device(normalize, nonneg):
     torch.testing.assert_close(shadow.float(), got, rtol=1e-2, atol=1e-2)
 
 
+def test_fista_gram_hot_path_matches_fp32_dictionary_step():
+    """The GPU dictionary step's hot path (``ops.fista.gram_solve``: X D^T / D D^T on the MFMA GEMM, eta
+    from the solver's own Gram, the residual from the decoder GEMM's EPI_DEC epilogue in bf16, negated)
+    feeding ``quadratic_basis_update(A_bf16=, res_neg_bf16=)`` == the fp32 path (``fista()`` with its
+    fp32 residual, fp32 eigenvalue step size, fp32 basis update), to bf16 accuracy; the tracker's eta
+    from the Gram bounds the same spectrum as the exact eigh of D D^T."""
+    from sparse_coding__amd.models.fista import FistaDictUpdater
+    from sparse_coding__amd.ops import fista as F
+
+    torch.manual_seed(21)
+    G, B, n, d = 3, 256, 256, 384
+    D = torch.nn.functional.normalize(torch.randn(G, n, d, device=DEV), dim=-1)
+    X = (torch.randn(B, d, device=DEV) * 0.5).to(torch.bfloat16)
+    lam = torch.tensor([1e-3, 1e-2, 5e-2], device=DEV)
+    A0 = torch.relu(torch.randn(G, B, n, device=DEV) * 0.1).to(torch.bfloat16)
+    assert F.gram_solve_ok(X, D)
+    tracker = F.EtaTracker()
+    A, Ab, Rn, eta, se = F.gram_solve(X, D, lam, A0, 60, tracker=tracker)
+    eta_ref = F.step_size(D, "eigh")
+    torch.testing.assert_close(eta, eta_ref, rtol=5e-3, atol=0)  # bf16 Gram vs fp32 spectrum
+    assert tracker.space == "ddt" and tracker.v.shape == (G, n, 1)
+    A_ref, R_ref = F.fista(X, D, lam, A0, 60, eta, backend="hip", form="gram")
+    torch.testing.assert_close(A, A_ref, rtol=0, atol=0)  # the same solver on the same operands
+    assert torch.equal(Ab, A.to(torch.bfloat16))
+    rel = float((-Rn.float() - R_ref).norm() / R_ref.norm())
+    assert rel < 1e-2, rel
+    torch.testing.assert_close(se, R_ref.pow(2).sum(dim=(1, 2)), rtol=2e-2, atol=0)
+    H = torch.rand(G, n, device=DEV) * 0.1
+    ref = F.quadratic_basis_update(D, R_ref, A_ref, H, 0.001, 0.05, backend="torch")
+    got = F.quadratic_basis_update(D, None, A, H, 0.001, 0.05, A_bf16=Ab, res_neg_bf16=Rn)
+    rel = float(((got - D) - (ref - D)).norm() / (ref - D).norm())
+    assert rel < 2e-2, rel
+    # the updater takes the hot path on these shapes and matches its fp32 torch form
+    hot, ref_u = FistaDictUpdater(num_iter=40), FistaDictUpdater(num_iter=40, backend="torch", eta_method="eigh")
+    Dn, res, An = hot(D.clone(), X, A0, lam)
+    Dr, res_r, Ar = ref_u(D.clone(), X.float(), A0.float(), lam)
+    rel = float(((Dn - D) - (Dr - D)).norm() / (Dr - D).norm())
+    assert rel < 5e-2, rel
+    assert res.dtype == torch.float32 and res.shape == (G, B, d)
+
+
 def test_unrolled_fista_hip_adjoint_matches_fp32():
     """FISTA in the loss on the kernels.  Forward: the HIP solver's residual against the fp32
     loop.  Backward: the HIP adjoint sweep (grouped GEMMs + elementwise kernel + the K = T B

@@ -139,3 +139,56 @@ def test_zero1_bf16_transport_drift_gloo():
         assert rel <= 1e-3, (k, rel)
         for r in range(1, world):
             assert np.array_equal(res[r][k][1], res[0][k][1])  # bf16 replicas identical
+
+
+def _ckpt_worker(rank, world, port, init, out_q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from sparse_coding__amd.engine.trainer import EnsembleTrainer
+    from sparse_coding__amd.parallel.dist import init_distributed, shutdown
+
+    info = init_distributed("gloo")
+    gen = torch.Generator().manual_seed(3)
+    feats = torch.nn.functional.normalize(torch.randn(64, 16, generator=gen), dim=-1)
+    xs = [(torch.relu(torch.randn(64, 64, generator=gen) - 1.0) @ feats).chunk(world)[rank] for _ in range(5)]
+
+    def make():
+        return EnsembleTrainer([(dict(p), dict(b)) for p, b in init], FunctionalSAE, lr=1e-3, batch_size=32,
+                               device="cpu", dist=info, parallel="zero1")
+
+    a = make()
+    assert a.kind == "zero1-eager"
+    for x in xs[:3]:
+        a.step(x)
+    st = a.state_dict()  # collective: the moments of every rank's shard, gathered
+    for x in xs[3:]:
+        a.step(x)
+    b = make()
+    b.load_state_dict(st)
+    for x in xs[3:]:
+        b.step(x)
+    same = all(torch.equal(a.impl.params[k], b.impl.params[k]) for k in a.impl.params)
+    out_q.put((rank, same, int(st["impl"]["zero"][0]["count"]), int(st["impl"]["zero"][0]["m"].numel())))
+    shutdown(info)
+
+
+def test_zero1_eager_trainer_checkpoint_resumes_exactly_gloo():
+    """EnsembleTrainer(parallel='zero1') on CPU / gloo (the eager ZeRO-1 chunk, moments sharded over the
+    ranks): ``state_dict`` gathers the shards, and a fresh trainer loaded from it continues bit-identically."""
+    torch.manual_seed(6)
+    init = [FunctionalSAE.init(16, 32, l1) for l1 in (1e-4, 1e-2, 3e-3)]
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ckpt_worker, args=(r, world, port, init, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, rest) for r, *rest in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n_params = sum(t.numel() for p, _ in init for t in p.values())
+    for r in range(world):
+        same, count, numel = res[r]
+        assert same and count == 3 and numel == n_params
