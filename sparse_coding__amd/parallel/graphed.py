@@ -112,13 +112,17 @@ class GraphedDataParallel:
             c.red_ev = self.comm.all_reduce(e.grad_all, overlap=True)
             return
         evs = []
-        for i, (src, dst) in enumerate(zip(c.srcs, c.shards)):
-            if c.lowp:  # bf16 transport, fp32 accumulation on the row owner
+        if c.lowp:  # bf16 transport, fp32 accumulation on the row owner: every send buffer first, ...
+            for i, src in enumerate(c.srcs):
                 c.send[i].copy_(src.view(-1))
-                evs.append(self.comm.all_to_all(c.recv[i], c.send[i], overlap=True))
+        # ... then the chunk's collectives back to back on ONE fork of the comm stream (RcclComm._run:
+        # consecutive forks lose the next node's dependency under HIP graph capture)
+        for i, (src, dst) in enumerate(zip(c.srcs, c.shards)):
+            if c.lowp:
+                evs.append(self.comm.all_to_all(c.recv[i], c.send[i], overlap=True, fork=not evs))
             elif c.world > 1:
-                evs.append(self.comm.reduce_scatter(dst.view(-1), src.view(-1), overlap=True))
-        evs.append(self.comm.all_reduce(c.tail, overlap=True))
+                evs.append(self.comm.reduce_scatter(dst.view(-1), src.view(-1), overlap=True, fork=not evs))
+        evs.append(self.comm.all_reduce(c.tail, overlap=True, fork=not evs))
         c.red_ev = evs
 
     def _wait(self, evs):
@@ -184,8 +188,8 @@ class GraphedDataParallel:
             evs = []
             for sh in ([e.dec_shadow] if e.kind == "untied" else []) + [e.enc_shadow]:
                 flat = sh.view(-1)
-                evs.append(self.comm.all_gather(flat, flat[lo * d:hi * d], overlap=True))
-            evs.append(self.comm.all_gather(e.norms.view(-1), e.norms.view(-1)[lo:hi], overlap=True))
+                evs.append(self.comm.all_gather(flat, flat[lo * d:hi * d], overlap=True, fork=not evs))
+            evs.append(self.comm.all_gather(e.norms.view(-1), e.norms.view(-1)[lo:hi], overlap=True, fork=False))
             c.gath_ev = evs
 
     def _steps(self, pattern: Sequence[bool]):
@@ -369,12 +373,15 @@ class GraphedEnsembleSharded:
         glob = self._buffers(s)[:s]
         self.source.gather_into_global(glob, e.step_dev)
         B, r = self.B, self.es.info.rank
-        evs = [self.comm.all_gather(glob[k], glob[k][r * B:(r + 1) * B], overlap=True) for k in range(s)]
         cur = torch.cuda.current_stream(self.device)
         tail = bool(e._tail_ok)
         if tail:
             self._ep0.copy_(e.step_dev)  # the group's first step: the tail's index base
             flat = self._glob.view(-1, self.es.d)
+        # the s all-gathers on ONE fork of the comm stream (RcclComm._run: with one fork per collective,
+        # HIP graph capture dropped the dependency of the next node -- this ep0 copy, read by every
+        # tail -- on the gather above, and group replays raced; profiles/r6/graph_capture/)
+        evs = [self.comm.all_gather(glob[k], glob[k][r * B:(r + 1) * B], overlap=True, fork=k == 0) for k in range(s)]
         for k, count in enumerate(pattern):
             if k == 0 or not tail:
                 if evs[k] is not None:

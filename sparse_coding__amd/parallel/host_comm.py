@@ -53,7 +53,7 @@ class HostComm:
         return t.contiguous().reshape(-1).view(torch.uint8)
 
     # ------------------------------------------------------------------ collectives (RcclComm API)
-    def all_reduce(self, t: torch.Tensor, overlap: bool = False):
+    def all_reduce(self, t: torch.Tensor, overlap: bool = False, fork: bool = True):
         """In-place SUM over ranks."""
         self._note("all_reduce")
         if self.world == 1:
@@ -63,7 +63,7 @@ class HostComm:
         t.copy_(h.to(t.dtype))
         return None
 
-    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False):
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False, fork: bool = True):
         """out = this rank's 1/N block of the SUM of ``inp`` over ranks."""
         if inp.numel() != self.world * out.numel() or inp.dtype != out.dtype:
             raise ValueError("reduce_scatter: inp must hold world x out elements of the same dtype")
@@ -75,7 +75,7 @@ class HostComm:
         out.view(-1).copy_(h[self.rank * k:(self.rank + 1) * k].to(out.dtype))
         return None
 
-    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False):
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False, fork: bool = True):
         """out = concat over ranks of ``inp`` (rank-major); ``inp`` may be out's own block (in place)."""
         if out.numel() != self.world * inp.numel() or inp.dtype != out.dtype:
             raise ValueError("all_gather: out must hold world x inp elements of the same dtype")
@@ -89,7 +89,7 @@ class HostComm:
         out.view(-1).view(torch.uint8).copy_(torch.cat(parts))
         return None
 
-    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False):
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False, fork: bool = True):
         """out[j] = rank j's inp block for this rank (N equal blocks)."""
         if out.numel() != inp.numel() or inp.numel() % self.world or inp.dtype != out.dtype:
             raise ValueError("all_to_all: equal-size buffers of N blocks")
@@ -103,7 +103,7 @@ class HostComm:
         out.view(-1).view(torch.uint8).copy_(r)
         return None
 
-    def broadcast(self, t: torch.Tensor, root: int = 0, overlap: bool = False):
+    def broadcast(self, t: torch.Tensor, root: int = 0, overlap: bool = False, fork: bool = True):
         self._note("broadcast")
         if self.world == 1:
             return None

@@ -138,11 +138,19 @@ class RcclComm:
         """Make ``stream`` (default: the current stream) wait for every collective enqueued so far."""
         (stream or torch.cuda.current_stream(self.device)).wait_stream(self.stream)
 
-    def _run(self, fn, overlap: bool):
+    def _run(self, fn, overlap: bool, fork: bool = True):
         """Enqueue ``fn(stream)`` after the current stream's work.  ``overlap``: return an event
         recorded right after it on the comm stream (the consumer waits on exactly that op with
-        ``torch.cuda.current_stream().wait_event(ev)``); otherwise the current stream waits now."""
-        cur = self._enter()
+        ``torch.cuda.current_stream().wait_event(ev)``); otherwise the current stream waits now.
+        ``fork=False``: do not make the comm stream wait for the current stream again -- for the 2nd..
+        collectives of a batch issued back to back with no work on the current stream in between (the
+        first call's fork already orders them).  Under HIP graph capture on ROCm 7 (MI355X) the first
+        current-stream node after MORE than two consecutive forks lost its dependency on the nodes
+        before them and ran unordered across graph replays (profiles/r6/graph_capture/README.md), so
+        batches fork once."""
+        cur = torch.cuda.current_stream(self.device)
+        if fork:
+            self.stream.wait_stream(cur)
         fn(self.stream.cuda_stream)
         if not overlap:
             cur.wait_stream(self.stream)
@@ -160,41 +168,41 @@ class RcclComm:
         return _NCCL_DTYPES[t.dtype]
 
     # ------------------------------------------------------------------ collectives
-    def all_reduce(self, t: torch.Tensor, overlap: bool = False):
+    def all_reduce(self, t: torch.Tensor, overlap: bool = False, fork: bool = True):
         """In-place SUM over ranks."""
         dt = self._dt(t)
         return self._run(lambda s: _check(library().ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), dt, NCCL_SUM,
-                                                           self._comm, s), "ncclAllReduce"), overlap)
+                                                           self._comm, s), "ncclAllReduce"), overlap, fork)
 
-    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False):
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False, fork: bool = True):
         """out = this rank's 1/N block of the SUM of ``inp`` over ranks (inp.numel() == N out.numel())."""
         if inp.numel() != self.world * out.numel() or inp.dtype != out.dtype:
             raise ValueError("reduce_scatter: inp must hold world x out elements of the same dtype")
         dt = self._dt(out)
         self._dt(inp)
         return self._run(lambda s: _check(library().ncclReduceScatter(inp.data_ptr(), out.data_ptr(), out.numel(), dt,
-                                                               NCCL_SUM, self._comm, s), "ncclReduceScatter"), overlap)
+                                                               NCCL_SUM, self._comm, s), "ncclReduceScatter"), overlap, fork)
 
-    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False):
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False, fork: bool = True):
         """out = concat over ranks of ``inp`` (rank-major); ``inp`` may be out's own block (in place)."""
         if out.numel() != self.world * inp.numel() or inp.dtype != out.dtype:
             raise ValueError("all_gather: out must hold world x inp elements of the same dtype")
         dt = self._dt(out)
         return self._run(lambda s: _check(library().ncclAllGather(inp.data_ptr(), out.data_ptr(), inp.numel(), dt,
-                                                           self._comm, s), "ncclAllGather"), overlap)
+                                                           self._comm, s), "ncclAllGather"), overlap, fork)
 
-    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False):
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False, fork: bool = True):
         """out[j] = rank j's inp block for this rank (N equal blocks)."""
         if out.numel() != inp.numel() or inp.numel() % self.world or inp.dtype != out.dtype:
             raise ValueError("all_to_all: equal-size buffers of N blocks")
         dt = self._dt(out)
         return self._run(lambda s: _check(library().ncclAllToAll(inp.data_ptr(), out.data_ptr(), inp.numel() // self.world,
-                                                          dt, self._comm, s), "ncclAllToAll"), overlap)
+                                                          dt, self._comm, s), "ncclAllToAll"), overlap, fork)
 
-    def broadcast(self, t: torch.Tensor, root: int = 0, overlap: bool = False):
+    def broadcast(self, t: torch.Tensor, root: int = 0, overlap: bool = False, fork: bool = True):
         dt = self._dt(t)
         return self._run(lambda s: _check(library().ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), dt, int(root),
-                                                           self._comm, s), "ncclBroadcast"), overlap)
+                                                           self._comm, s), "ncclBroadcast"), overlap, fork)
 
     # ------------------------------------------------------------------ introspection
     def _query(self, fn: str) -> int:

@@ -52,13 +52,14 @@ class DelayedSimComm:
         if not self.sync:
             (stream or torch.cuda.current_stream(self.device)).wait_stream(self.stream)
 
-    def _run(self, name: str, fn, overlap: bool):
+    def _run(self, name: str, fn, overlap: bool, fork: bool = True):
         self.calls[name] = self.calls.get(name, 0) + 1
         if self.sync:  # the reference ordering: on the producer's stream, nothing in flight
             fn()
             return None
         cur = torch.cuda.current_stream(self.device)
-        self.stream.wait_stream(cur)
+        if fork:  # (RcclComm._run: the 2nd.. collectives of a back-to-back batch do not fork again)
+            self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             if self.cycles:
                 torch.cuda._sleep(self.cycles)
@@ -71,10 +72,10 @@ class DelayedSimComm:
         return ev
 
     # ------------------------------------------------------------------ collectives (N identical replicas)
-    def all_reduce(self, t: torch.Tensor, overlap: bool = False):
-        return self._run("all_reduce", lambda: t.mul_(self.world) if self.world > 1 else None, overlap)
+    def all_reduce(self, t: torch.Tensor, overlap: bool = False, fork: bool = True):
+        return self._run("all_reduce", lambda: t.mul_(self.world) if self.world > 1 else None, overlap, fork)
 
-    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False):
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False, fork: bool = True):
         if inp.numel() != self.world * out.numel() or inp.dtype != out.dtype:
             raise ValueError("reduce_scatter: inp must hold world x out elements of the same dtype")
         k = out.numel()
@@ -82,9 +83,9 @@ class DelayedSimComm:
         def fn():
             torch.mul(inp.reshape(-1)[self.rank * k:(self.rank + 1) * k], self.world, out=out.view(-1))
 
-        return self._run("reduce_scatter", fn, overlap)
+        return self._run("reduce_scatter", fn, overlap, fork)
 
-    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False):
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False, fork: bool = True):
         if out.numel() != self.world * inp.numel() or inp.dtype != out.dtype:
             raise ValueError("all_gather: out must hold world x inp elements of the same dtype")
         k = inp.numel()
@@ -97,9 +98,9 @@ class DelayedSimComm:
                 if dst.data_ptr() != src.data_ptr():  # (in place: this rank's block is already there)
                     dst.copy_(src)
 
-        return self._run("all_gather", fn, overlap)
+        return self._run("all_gather", fn, overlap, fork)
 
-    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False):
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False, fork: bool = True):
         if out.numel() != inp.numel() or inp.numel() % self.world or inp.dtype != out.dtype:
             raise ValueError("all_to_all: equal-size buffers of N blocks")
         k = inp.numel() // self.world
@@ -108,10 +109,10 @@ class DelayedSimComm:
             blk = inp.reshape(-1)[self.rank * k:(self.rank + 1) * k]
             out.view(self.world, k).copy_(blk.unsqueeze(0).expand(self.world, k))
 
-        return self._run("all_to_all", fn, overlap)
+        return self._run("all_to_all", fn, overlap, fork)
 
-    def broadcast(self, t: torch.Tensor, root: int = 0, overlap: bool = False):
-        return self._run("broadcast", lambda: None, overlap)
+    def broadcast(self, t: torch.Tensor, root: int = 0, overlap: bool = False, fork: bool = True):
+        return self._run("broadcast", lambda: None, overlap, fork)
 
     def count(self) -> int:
         return self.world

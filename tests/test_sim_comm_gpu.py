@@ -14,6 +14,10 @@ batch before the gather filled it) -- must NOT match.  Deleting the ``_wait(c.re
 ``GraphedDataParallel._update`` or either ``cur.wait_event`` of ``GraphedEnsembleSharded._steps``
 (parallel/graphed.py) is therefore caught.  ZeRO-1's shard gathers are not simulated faithfully
 (other ranks own other rows) and stay with the multi-rank gloo tests.
+
+These tests found a HIP graph-capture bug: with one comm-stream fork per collective, the first
+capturing-stream node after five or more consecutive forks lost its dependency and ran unordered across
+replays; the graphed classes now fork once per batch of collectives (profiles/r6/graph_capture/).
 """
 
 import pytest
@@ -133,8 +137,8 @@ class _NoEventGather:
     def __getattr__(self, k):
         return getattr(self._c, k)
 
-    def all_gather(self, out, inp, overlap=False):
-        self._c.all_gather(out, inp, overlap=overlap)
+    def all_gather(self, out, inp, overlap=False, fork=True):
+        self._c.all_gather(out, inp, overlap=overlap, fork=fork)
         return None
 
 
@@ -151,7 +155,7 @@ def _es(models, comm, ring, B, d, capture, world=2):
     return GraphedEnsembleSharded(es, comm, ring.graph_source(B, 0, world), capture=capture), es
 
 
-def _run_es(ges, groups=(3, 5, 3)):
+def _run_es(ges, groups=(3, 10, 5)):  # (10: the bench's group size -- 10 collectives per group graph)
     from sparse_coding__amd.engine.graph_plan import count_pattern
 
     ges.prime([count_pattern(s) for s in sorted(set(groups))])
@@ -175,7 +179,7 @@ def test_graphed_es_on_delayed_comm_matches_ordered_run():
     comm = DelayedSimComm(DEV, world=2, delay_us=50)
     got, got_es = _es(models, comm, rings[1], B, d, capture=True)
     _run_es(got)
-    assert comm.calls.get("all_gather", 0) >= 5
+    assert comm.calls.get("all_gather", 0) >= 10
     assert got_es.engine.n_models == 2
     assert _same([got_es.engine], [ref_es.engine])
     torch.testing.assert_close(got._glob, ref._glob, rtol=0, atol=0)
