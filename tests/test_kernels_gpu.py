@@ -408,6 +408,42 @@ def test_topk_select_bf16_picks_are_fp32_topk(n):
     assert torch.equal(idx2, idx) and torch.equal(val2, val)  # deterministic
 
 
+def test_topk_select_bf16_fallback_paths_are_a_bf16_topk():
+    """The bf16 select past its exact-tie limits (ops/topk.py docstring): k > 256 (no bracket path) and
+    more than TIE_CAP = 64 keys tied at the k-th bf16 key.  There the picks are still a top-k of the
+    bf16 keys -- every pick >= the k-th largest bf16 score, nothing above it left out, no duplicates --
+    with ties at the threshold taken in column order (the lowest tied columns)."""
+    from sparse_coding__amd.ops import topk as T
+
+    torch.manual_seed(17)
+    G, B, n = 2, 64, 2048
+    scores = torch.randn(G, B, n, device=DEV)
+    # model 1: 200 columns share one value just below the top 100 -> > 64 ties at the threshold
+    scores[1, :, 500:700] = -5.0
+    scores[1, :, 1000:1100] = 10.0 + torch.rand(B, 100, device=DEV)
+    scores[1, :, :500] = -9.0
+    scores[1, :, 700:1000] = -9.0
+    scores[1, :, 1100:] = -9.0
+    sb = scores.to(torch.bfloat16)
+    k = torch.tensor([300, 150], device=DEV, dtype=torch.int32)  # k > 256; 100 + 50 of 200 tied
+    idx, val = T.topk_select(sb, k, 300)
+    torch.cuda.synchronize()
+    sf = sb.float()
+    for g in range(G):
+        kg = int(k[g])
+        pick = idx[g, :, :kg].long()
+        assert pick.sort(-1).values.diff(dim=-1).gt(0).all()  # no duplicates
+        kth = sf[g].topk(kg, dim=-1).values[:, -1:]
+        assert (sf[g].gather(-1, pick) >= kth).all()
+        rest = sf[g].scatter(-1, pick, float("-inf"))
+        assert (rest <= kth).all()
+        assert torch.equal(val[g, :, :kg], sf[g].gather(-1, pick).clamp(min=0))
+    tied = idx[1, :, :150].long()
+    chosen = tied[(tied >= 500) & (tied < 700)].view(B, -1)  # the 50 tied columns taken per row
+    assert chosen.shape[1] == 50 and torch.equal(chosen.sort(-1).values,
+                                                 torch.arange(500, 550, device=DEV).expand(B, 50))
+
+
 def test_topk_scatter_and_clear_roundtrip():
     from sparse_coding__amd.ops import topk as T
 
