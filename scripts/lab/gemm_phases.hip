@@ -39,7 +39,11 @@ template <class F>
 static void run(const char* name, long nblocks, F launch) {
   long long* st;
   (void)hipMalloc(&st, nblocks * 8 * sizeof(long long));
+  long long* sub;
+  (void)hipMalloc(&sub, nblocks * 8 * sizeof(long long));
+  (void)hipMemset(sub, 0, nblocks * 8 * sizeof(long long));
   long long* null_ptr = nullptr;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(sc_sub_buf), &null_ptr, sizeof(void*));
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -52,10 +56,13 @@ static void run(const char* name, long nblocks, F launch) {
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, e0, e1);
   (void)hipMemcpyToSymbol(HIP_SYMBOL(sc_stamp_buf), &st, sizeof(void*));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(sc_sub_buf), &sub, sizeof(void*));
   launch();
   (void)hipDeviceSynchronize();
-  std::vector<long long> h(nblocks * 8);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(sc_sub_buf), &null_ptr, sizeof(void*));
+  std::vector<long long> h(nblocks * 8), hs(nblocks * 8);
   (void)hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(hs.data(), sub, hs.size() * 8, hipMemcpyDeviceToHost);
   // memtime ticks per ns from the whole launch's realtime (100 MHz) span
   long long t0 = h[0], tmax = 0, r0 = h[4], rmax = 0;
   for (long b = 0; b < nblocks; ++b) {
@@ -79,10 +86,12 @@ static void run(const char* name, long nblocks, F launch) {
     snprintf(path, sizeof path, "%s/%s.csv", g_raw_dir, name);
     FILE* fo = fopen(path, "w");
     if (fo) {
-      fprintf(fo, "block,t0,t1,t2,t3,rt0,rt3,hw_id,xcc_id\n");
+      fprintf(fo, "block,t0,t1,t2,t3,rt0,rt3,hw_id,xcc_id,e0,e1,e2,e3,e4,e5,e6\n");
       for (long b = 0; b < nblocks; ++b) {
         const long long* s = &h[b * 8];
-        fprintf(fo, "%ld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld\n", b, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]);
+        const long long* e = &hs[b * 8];
+        fprintf(fo, "%ld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld,%lld\n", b, s[0], s[1], s[2],
+                s[3], s[4], s[5], s[6], s[7], e[0], e[1], e[2], e[3], e[4], e[5], e[6]);
       }
       fclose(fo);
     }
@@ -95,6 +104,7 @@ static void run(const char* name, long nblocks, F launch) {
          k.p10, k.med, k.p90, e.p10, e.med, e.p90, l.p10, l.med, l.p90);
   fflush(stdout);
   (void)hipFree(st);
+  (void)hipFree(sub);
 }
 
 int main(int argc, char** argv) {
@@ -131,6 +141,8 @@ int main(int argc, char** argv) {
     run("nt_bf16_256x128", n_blocks<S256x128>(B, n, G, 1), [&] { launch<S256x128, 64, 2>(EPI_BF16, true, true, p, 1, 0); });
     run("enc_128_bk32x3", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 32, 3, false, true>(EPI_ENC, true, true, p, 1, 0); });
 #elif !defined(LAB_BIG)
+    // the product's encoder configuration (cfg 29: 128x128, BK32 x 3 ring, software-pipelined loop)
+    run("enc_128_p32", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 32, 3, false, true>(EPI_ENC, true, true, p, 1, 0); });
     run("enc_128_bk32x3", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 32, 3, false>(EPI_ENC, true, true, p, 1, 0); });
     run("enc_128", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 64, 2>(EPI_ENC, true, true, p, 1, 0); });
 #else
@@ -186,6 +198,7 @@ int main(int argc, char** argv) {
     p.M = B; p.N = n; p.K1 = d; p.K2 = 0; p.G = G; p.ldc = n; p.sc = (long)B * n;
     p.colpart = colpart; p.l1 = l1; p.l1_add_scale = d / 2.0f; p.cmask = cmask; p.ksplit = 1;
 #ifndef LAB_BIG
+    run("dc_128_p32", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 32, 3, false, true>(EPI_DC_MASK, true, true, p, 1, 0); });
     run("dc_128_bk32x3", n_blocks<S128>(B, n, G, 1), [&] { launch<S128, 32, 3, false>(EPI_DC_MASK, true, true, p, 1, 0); });
 #endif
   }

@@ -52,3 +52,12 @@ for f in sorted(glob.glob(os.path.join(d, "*.csv"))):
     print(f"{name:18s} clock {ghz:4.2f} GHz; blocks {len(rows):5d} on {ncu:3d} CUs (per CU {min(per_cu)}-{max(per_cu)}), span {span:6.1f} us; "
           f"median fill {st.median(fill):5.2f} kloop {st.median(kl):6.2f} epi {st.median(ep):5.2f} life {st.median(life):6.2f} us; "
           f"slot fill {100 * eff:5.1f} % at {slots}/CU; tail after first idle CU {span - (first_idle - min(start)):5.1f} us")
+    # epilogue sub-phases (wave 0), when the build stamped them (sae_gemm_kernel.h SC_SUB)
+    if rows and "e0" in rows[0] and any(int(r["e0"]) for r in rows):
+        def med(a, b):
+            v = [us(int(r[b]) - int(r[a])) for r in rows if int(r[a]) and int(r[b])]
+            return st.median(v) if v else float("nan")
+        parts = [("bias+ring barrier", "t2", "e6"), ("relu/put", "e0", "e1"), ("flush stores", "e1", "e2"),
+                 ("cmask stores", "e2", "e3"), ("block sum", "e3", "e4"), ("partials", "e4", "e5"),
+                 ("to end", "e5", "t3")]
+        print("    epilogue sub-phases (median us): " + ", ".join(f"{n} {med(a, b):.2f}" for n, a, b in parts))

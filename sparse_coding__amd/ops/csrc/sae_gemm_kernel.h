@@ -109,8 +109,15 @@ __device__ __forceinline__ long long sc_memrealtime() {
       if ((k) == 3) st_[5] = sc_memrealtime();                                           \
     }                                                                                    \
   } while (0)
+// sub-phases of the epilogue (wave 0's view), same lab builds: slots [block][8] of sc_sub_buf
+__device__ long long* sc_sub_buf;
+#define SC_SUB(k)                                                                          \
+  do {                                                                                     \
+    if (threadIdx.x == 0 && sc_sub_buf) sc_sub_buf[(long)blockIdx.x * 8 + (k)] = sc_memtime(); \
+  } while (0)
 #else
 #define SC_STAMP(k) do {} while (0)
+#define SC_SUB(k) do {} while (0)
 #endif
 
 // ------------------------------------------------------------------ epilogues
@@ -323,6 +330,7 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   };
 
   if constexpr (ENC) {
+    SC_SUB(0);
     uint16_t* C = reinterpret_cast<uint16_t*>(cptr) + (long)g * p.sc;
     const float* bias = p.bias + (long)g * p.sbias;
     const int nact = p.nactive ? p.nactive[g] : p.N;  // masked SAEs: live columns [0, nact)
@@ -413,7 +421,9 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
       }
       if (counting) colred_lane(cnt, j, 0);
     }
+    SC_SUB(1);
     flush(C);
+    SC_SUB(2);
     if (p.cmask) {
 #pragma unroll
       for (int k = 0; k < WI / 4; ++k) {
@@ -423,13 +433,16 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
         if (l0_from_mask) l0 += (float)(__popc(mw[k][0]) + __popc(mw[k][1]));
       }
     }
+    SC_SUB(3);
     // one barrier: publishes the colred_lane writes too; `red` is not written after it
     const float2 sums = block_sum2_final<NW>(l1, l0, red + RED_SUM);
     l1 = sums.x;
     l0 = sums.y;
+    SC_SUB(4);
     if (counting) colred_store(p.colpart, 0);
     scalar_partial(p.part, 2, 0, l1);
     scalar_partial(p.part, 2, 1, l0);
+    SC_SUB(5);
     return;
   }
   if constexpr (EPI == EPI_DEC) {
@@ -978,6 +991,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& p, const int bid, c
     for (int j = 0; j < WJ; ++j) biasv[j] = *reinterpret_cast<const f32x4_t*>(bias + colb + j * 16);
   }
   lds_barrier();  // all reads of the ring done before smem is reused below
+  SC_SUB(6);
   constexpr bool STAGE = (S::WI == 4 || S::WI == 8) && S::WJ == 4 && NST * STG >= stage_bytes<S>();
   constexpr bool FSTAGE = EPI == EPI_F32 && S::WJ == 4 && NST * STG >= S::NW * S::WI * 16 * STAGE_ROW;
   sae_epilogue<S, EPI, AUX_EARLY, STAGE, FSTAGE>(p, acc, auxv, biasv, mkv, reinterpret_cast<float*>(smem), pi, g, m0, n0, tn,
