@@ -1,6 +1,7 @@
 """Step-GEMM timings for every (block shape, K pipeline) configuration (config 2 shapes).
 
   python scripts/pipe_bench.py       -> one JSON line per (kernel, cfg)
+  PB_CFGS=1,5 PB_KERNELS=dec python scripts/pipe_bench.py   -> a subset
 cfg = shape | pipe << 2 (ops/gemm.py SHAPES / PIPES).
 """
 import json
@@ -33,8 +34,12 @@ def main():
         "dc": (lambda: gemm.code_grad(e.r, e.dec_shadow, e.c, e.l1, e.dpre, e.colpart), fl),
         "wgrad2": (lambda: gemm.weight_grads([[(e.c, e.r)], [(e.dpre, x)]], [e.g_dec, e.g_enc], 1e-6), 2 * fl),
     }
-    for cfg in (1, 5, 9, 13, 2, 3, 7, 11, 15):
+    cfgs = [int(c) for c in (os.environ.get("PB_CFGS") or "1,5,9,13,2,3,7,11,15").split(",")]
+    only = set(filter(None, (os.environ.get("PB_KERNELS") or "").split(",")))
+    for cfg in cfgs:
         for name, (fn, f) in kernels.items():
+            if only and name not in only:
+                continue
             if not gemm.shape_fits(cfg, B if name != "wgrad2" else n, n if name in ("enc", "enc_cnt", "dc") else d):
                 continue
             with gemm.force_shape(cfg):
@@ -44,7 +49,7 @@ def main():
                     print(json.dumps({"kernel": name, "cfg": cfg, "error": str(ex)[:80]}))
                     continue
             print(json.dumps({"kernel": name, "cfg": cfg, "shape": gemm.SHAPES[cfg & 3],
-                              "pipe": gemm.PIPES[cfg >> 2], "us": round(t, 2), "tflops": round(f / t / 1e6, 1)}),
+                              "pipe": gemm.PIPES[(cfg >> 2) & 3], "p32": bool(cfg & 16), "us": round(t, 2), "tflops": round(f / t / 1e6, 1)}),
                   flush=True)
 
 
