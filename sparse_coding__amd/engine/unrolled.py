@@ -5,6 +5,15 @@ Reference: ``autoencoders/residual_denoising_autoencoder.py:9-122`` (LISTA layer
 shrinkage and momentum, https://arxiv.org/pdf/2008.02683.pdf) and ``:125-201`` (residual
 denoising layers), trained by ``FunctionalEnsemble`` = ``vmap(grad(loss))`` per model.
 
+LISTA on the GPU trains through ``UnrolledEnsemble._lista_fused_step``: the forward and a hand-derived
+backward with no autograd, every product a grouped MFMA GEMM whose epilogue writes the operand the
+next product reads (bf16 residuals, bf16 code gradients, alpha-scaled signs folded in), the
+shrinkage/momentum of each layer one HIP pass each way (``sc_lista_fwd2`` / ``sc_lista_bwd2``: r, the
+bf16 copy of y', the L1 sums, the summed incoming gradients, the first layer's y0 = xs0 gradient), and
+the matrices' Adam the row kernel that also rewrites their bf16 shadows (the decoder's normalised:
+the unit-row Jacobian is applied there).  The autograd path (``grads``) stays for the residual
+family, the CPU and the tests.
+
 Here every model's parameters are stacked on a leading model axis and the loss of all models
 is written once in batched form.  Each layer's matrix products are grouped GEMMs over the
 model axis (``grouped_mm``: one ``csrc/sae_gemm`` launch per product -- bf16 MFMA operands,
@@ -198,6 +207,10 @@ class UnrolledEnsemble:
         self.m = {k: torch.zeros_like(v) for k, v in self.params.items()}
         self.v = {k: torch.zeros_like(v) for k, v in self.params.items()}
         self.step_count = 0
+        # bf16 shadows of the matrices for the explicit LISTA step (built on first use, rewritten by
+        # its Adam; dropped whenever the parameters change another way)
+        self._mats = ["decoder"] + [f"layer{i}.W" for i in range(self.n_layers)] if self.kind == "lista" else []
+        self._sh = None
 
     # ------------------------------------------------------------------ model
     def _layer(self, i, k):
@@ -245,6 +258,7 @@ class UnrolledEnsemble:
     @torch.no_grad()
     def apply_grads(self, grads):
         """torchopt Adam (eps_root = 0) with a per-model learning rate."""
+        self._sh = None
         self.step_count += 1
         b1, b2 = self.betas
         bc1 = 1.0 - b1 ** self.step_count
@@ -265,9 +279,159 @@ class UnrolledEnsemble:
             p.sub_(lr * (m / bc1) / ((v / bc2).sqrt() + self.eps))
 
     def step_batch(self, batch: torch.Tensor, expand_dims: bool = True):
-        grads, (total, l_rec, l_l1, c) = self.grads(batch)
-        self.apply_grads(grads)
+        if self._fused_ok(batch.shape[0]):
+            total, l_rec, l_l1, c = self._lista_fused_step(batch)
+        else:
+            grads, (total, l_rec, l_l1, c) = self.grads(batch)
+            self.apply_grads(grads)
         return {"loss": total, "l_reconstruction": l_rec, "l_l1": l_l1}, {"c": c}
+
+    # ------------------------------------------------------------------ explicit LISTA step (GPU)
+    def _fused_ok(self, B: int) -> bool:
+        G, n, d = self.params["decoder"].shape
+        return (self.kind == "lista" and self.device.type == "cuda" and B % 128 == 0 and n % 256 == 0
+                and d % 256 == 0 and d <= 4096 and (B * n) % 1024 == 0)
+
+    def _shadows(self):
+        from ..ops import adam as adam_ops
+
+        if self._sh is None:
+            self._sh = {}
+            for k in self._mats:
+                p = self.params[k].detach()
+                self._sh[k] = torch.empty(p.shape, device=self.device, dtype=torch.bfloat16)
+                adam_ops.shadow_rows(p, self._sh[k], normalize=(k == "decoder"))
+        return self._sh
+
+    @torch.no_grad()
+    def _lista_fused_grads(self, x: torch.Tensor):
+        """One LISTA training step of every model without autograd (see the module docstring).
+
+        Forward, layer i (E = x - y D, y_0 = xs_0 = x D^T):  a = E W^T,  r = y + a,
+        x_ = shrink(r, theta),  y' = x_ + m (x_ - xs);  c = y_L,  L = |c D - x|^2 / (B d) + l1 |c|_1 / B.
+        Backward, layer i (incoming dy', dxs'):  dr = shrink'(r) ((1 + m) dy' + dxs'),
+        dxs = -m dy',  dW = dr^T E,  dE = dr W,  dy = dr - dE D^T (+ dxs for i = 0),
+        dD_hat += -y^T dE (+ dy_0^T x, + c^T dL/dx_hat);  theta / m from block partials.
+        Reference: autoencoders/residual_denoising_autoencoder.py:26-36, :66-83."""
+        from ..ops import _lib
+        from ..ops import gemm as gemm_ops
+
+        G, n, d = self.params["decoder"].shape
+        B, L, dev = int(x.shape[0]), self.n_layers, self.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        sh = self._shadows()
+        Db = sh["decoder"]
+        xb = x.to(dev, torch.bfloat16).contiguous()
+        p = _lib.ptr
+        st = _lib.stream_handle()
+        rho = [self.params[f"layer{i}.rho"].detach() for i in range(L)]
+        ms = [r.clamp(0.0, 1.0).contiguous() for r in rho]
+        ths = [self.params[f"layer{i}.theta"].detach().contiguous() for i in range(L)]
+        part = torch.empty(G, (B // 128) * (d // 128), **f32)
+        absp = torch.empty(G * B * n // 1024, **f32)
+
+        # ---- forward
+        y = torch.empty(G, B, n, **f32)
+        gemm_ops.matmul_nt(xb, Db, y)  # y_0 = x D^T
+        yb, xs = y.to(torch.bfloat16), y
+        saved = []
+        for i in range(L):
+            rneg = torch.empty(G, B, d, **bf)
+            gemm_ops.decode_residual(yb, Db, xb, rneg, part)  # y D - x = -E
+            a = torch.empty(G, B, n, **f32)
+            gemm_ops.matmul_nt(rneg, sh[f"layer{i}.W"], a, alpha=-1.0)  # a = E W^T
+            xo, yo, yob = torch.empty(G, B, n, **f32), torch.empty(G, B, n, **f32), torch.empty(G, B, n, **bf)
+            _lib.check(_lib.lib().sc_lista_fwd2(p(y), p(a), p(xs), p(ths[i]), p(ms[i]), p(xo), p(yo), p(a), p(yob),
+                                                p(absp) if i == L - 1 else None, G, B, n, st), "sc_lista_fwd2")
+            saved.append((yb, a, xs, rneg))  # (a now holds r = y + a)
+            y, yb, xs = yo, yob, xo
+        c, cb = y, yb
+        rf = torch.empty(G, B, d, **bf)
+        gemm_ops.decode_residual(cb, Db, xb, rf, part)  # c D - x, with sum(r^2) partials
+        l_rec = part.sum(1) / (B * d)
+        l_l1 = self.l1 * absp.view(G, -1).sum(1) / B
+
+        # ---- backward
+        alpha = 2.0 / (B * d)
+        gc = torch.empty(G, B, n, **f32)
+        gemm_ops.matmul_nt(rf, Db, gc, alpha=alpha)  # d l_rec / dc
+        nterm = L + 2  # decoder terms of unit weight: one per layer, and dy_0^T x as two bf16 pieces
+        nslab = 1 + (nterm + 1) // 2
+        slabs = torch.empty(nslab, G, n, d, **f32)
+        gemm_ops.weight_grads([[(cb, rf)]], [slabs[0]], alpha)  # c^T dL/dx_hat
+        rb = 64
+        gth_part = torch.empty(G, B // rb, n, **f32)
+        gm_part = torch.empty(G, B // rb, n // 256, **f32)
+        gW, gth, grho, terms = {}, {}, {}, []
+        gy, gy2, gx, l1c = gc, None, None, (self.l1 / B).float().contiguous()
+        for i in reversed(range(L)):
+            yb_i, r_i, xs_i, rneg_i = saved[i]
+            first = i == 0
+            grb = torch.empty(G, B, n, **bf)
+            gr = None if first else torch.empty(G, B, n, **f32)
+            gxs = None if first else torch.empty(G, B, n, **f32)
+            ub = torch.empty(G, B, n, **bf) if first else None
+            _lib.check(_lib.lib().sc_lista_bwd2(p(gy), p(gy2), p(gx), p(r_i), None, p(xs_i), p(ths[i]), p(ms[i]),
+                                                p(l1c), p(gr), p(grb), p(gxs), p(ub), p(gth_part), p(gm_part),
+                                                G, B, n, rb, st), "sc_lista_bwd2")
+            gth[i] = gth_part.sum(1)
+            grho[i] = gm_part.sum((1, 2)) * ((rho[i] >= 0.0) & (rho[i] <= 1.0)).float()
+            gW[i] = torch.empty(G, n, d, **f32)
+            gemm_ops.weight_grads([[(grb, rneg_i)]], [gW[i]], -1.0)  # dW = dr^T E
+            ngE = torch.empty(G, B, d, **bf)
+            gemm_ops.matmul_nn(grb, sh[f"layer{i}.W"], ngE, alpha=-1.0)  # -dE = -dr W
+            t = torch.empty(G, B, n, **(bf if first else f32))
+            gemm_ops.matmul_nt(ngE, Db, t)  # dy through P = y D
+            terms.append((yb_i, ngE))
+            if first:
+                terms += [(ub, xb), (t, xb)]  # dy_0 = dr_0 + dxs_0 + t_0 (xs_0 is y_0)
+            gy, gy2, gx, l1c = gr, t, gxs, None
+        for s in range(nslab - 1):  # (an odd term count leaves the last slab one segment)
+            gemm_ops.weight_grads([terms[2 * s:2 * s + 2]], [slabs[1 + s]], 1.0)
+        return slabs, gW, gth, grho, (l_rec + l_l1, l_rec, l_l1, c)
+
+    def fused_grads(self, x: torch.Tensor):
+        """The explicit step's gradients in the autograd path's form (tests): the decoder's through
+        the unit-row Jacobian, the split slabs summed."""
+        slabs, gW, gth, grho, losses = self._lista_fused_grads(x)
+        dec = self.params["decoder"].detach()
+        nrm = torch.linalg.vector_norm(dec, dim=-1, keepdim=True).clamp_min(1e-8)
+        gh = slabs.sum(0)
+        out = {"decoder": gh / nrm - dec * (dec * gh).sum(-1, keepdim=True) / nrm ** 3}
+        for i in range(self.n_layers):
+            out[f"layer{i}.W"], out[f"layer{i}.theta"], out[f"layer{i}.rho"] = gW[i], gth[i], grho[i]
+        return out, losses
+
+    @torch.no_grad()
+    def _lista_fused_step(self, x: torch.Tensor):
+        from ..ops import adam as adam_ops
+
+        slabs, gW, gth, grho, losses = self._lista_fused_grads(x)
+        G, n, d = self.params["decoder"].shape
+        sh = self._sh
+        # ---- update: the row-Adam kernel (and the shadows) for the matrices, torch for the vectors
+        L = self.n_layers
+        self.step_count += 1
+        b1, b2 = self.betas
+        dec = self.params["decoder"]
+        adam_ops.adam_rows([dict(p=dec.data, g=slabs[0], m=self.m["decoder"], v=self.v["decoder"],
+                                 shadow=sh["decoder"], norms=None, norm=True)], self.lr, self.step_count, b1, b2,
+                           self.eps, nsplit=slabs.shape[0], gstride=G * n * d)
+        for i in range(L):
+            k = f"layer{i}.W"
+            adam_ops.adam_rows([dict(p=self.params[k].data, g=gW[i], m=self.m[k], v=self.v[k], shadow=sh[k],
+                                     norms=None, norm=False)], self.lr, self.step_count, b1, b2, self.eps)
+        bc1 = 1.0 - b1 ** self.step_count
+        bc2 = 1.0 - b2 ** self.step_count
+        for i in range(L):
+            for k, g in ((f"layer{i}.theta", gth[i]), (f"layer{i}.rho", grho[i])):
+                pk, m, v = self.params[k], self.m[k], self.v[k]
+                m.mul_(b1).add_(g, alpha=1.0 - b1)
+                v.mul_(b2).addcmul_(g, g, value=1.0 - b2)
+                lr = self.lr.view(-1, *([1] * (pk.dim() - 1)))
+                pk.sub_(lr * (m / bc1) / ((v / bc2).sqrt() + self.eps))
+        return losses
 
     # ------------------------------------------------------------------ export / state
     def unstack(self, device="cpu") -> List[tuple]:
@@ -296,3 +460,4 @@ class UnrolledEnsemble:
                 for k, t in sd[name].items():
                     getattr(self, name)[k].copy_(t)
         self.step_count = int(sd["step"])
+        self._sh = None

@@ -15,39 +15,59 @@
 
 namespace scamd {
 
-__global__ __launch_bounds__(256) void lista_fwd_kernel(const float4* __restrict__ y, const float4* __restrict__ a,
+// Optional outputs of the explicit (autograd-free) LISTA step, engine/unrolled.py: r = y + a (may
+// alias a: each thread reads its a before writing its r), a bf16 copy of y' (the next GEMM's
+// operand), and per-block sums of |y'| (the last layer's L1 term; a block's 1024 elements lie in
+// one model because B n % 1024 == 0).
+__global__ __launch_bounds__(256) void lista_fwd_kernel(const float4* __restrict__ y, const float4* a,
                                                         const float4* __restrict__ xs, const float* __restrict__ theta,
                                                         const float* __restrict__ m, float4* __restrict__ xo,
-                                                        float4* __restrict__ yo, int B, int n, long total4) {
+                                                        float4* __restrict__ yo, float4* r_out, ushort4* __restrict__ yob,
+                                                        float* __restrict__ absp, int B, int n, long total4) {
   const long t = (long)blockIdx.x * 256 + threadIdx.x;
-  if (t >= total4) return;
-  const long e = t * 4;
-  const int g = (int)(e / ((long)B * n));
-  const int j = (int)(e % n);
-  const float4 yv = y[t], av = a[t], xv = xs[t];
-  const float4 th = *reinterpret_cast<const float4*>(theta + (long)g * n + j);
-  const float mm = m[g];
-  float4 xn, yn;
-  auto one = [&](float yy, float aa, float x0, float tt, float& xo_, float& yo_) {
-    const float r = yy + aa;
-    const float mag = fmaxf(fabsf(r) - tt, 0.f);
-    xo_ = r > 0.f ? mag : (r < 0.f ? -mag : 0.f);
-    yo_ = xo_ + mm * (xo_ - x0);
-  };
-  one(yv.x, av.x, xv.x, th.x, xn.x, yn.x);
-  one(yv.y, av.y, xv.y, th.y, xn.y, yn.y);
-  one(yv.z, av.z, xv.z, th.z, xn.z, yn.z);
-  one(yv.w, av.w, xv.w, th.w, xn.w, yn.w);
-  xo[t] = xn;
-  yo[t] = yn;
+  float ab = 0.f;
+  if (t < total4) {
+    const long e = t * 4;
+    const int g = (int)(e / ((long)B * n));
+    const int j = (int)(e % n);
+    const float4 yv = y[t], av = a[t], xv = xs[t];
+    const float4 th = *reinterpret_cast<const float4*>(theta + (long)g * n + j);
+    const float mm = m[g];
+    float4 xn, yn, rv;
+    auto one = [&](float yy, float aa, float x0, float tt, float& xo_, float& yo_, float& r_) {
+      r_ = yy + aa;
+      const float mag = fmaxf(fabsf(r_) - tt, 0.f);
+      xo_ = r_ > 0.f ? mag : (r_ < 0.f ? -mag : 0.f);
+      yo_ = xo_ + mm * (xo_ - x0);
+    };
+    one(yv.x, av.x, xv.x, th.x, xn.x, yn.x, rv.x);
+    one(yv.y, av.y, xv.y, th.y, xn.y, yn.y, rv.y);
+    one(yv.z, av.z, xv.z, th.z, xn.z, yn.z, rv.z);
+    one(yv.w, av.w, xv.w, th.w, xn.w, yn.w, rv.w);
+    xo[t] = xn;
+    yo[t] = yn;
+    if (r_out) r_out[t] = rv;
+    if (yob) yob[t] = make_ushort4(f2bf(yn.x), f2bf(yn.y), f2bf(yn.z), f2bf(yn.w));
+    ab = fabsf(yn.x) + fabsf(yn.y) + fabsf(yn.z) + fabsf(yn.w);
+  }
+  if (absp) {
+    __shared__ float red[8];
+    ab = block_sum_256(ab, red);
+    if (threadIdx.x == 0) absp[blockIdx.x] = ab;
+  }
 }
 
 // grid (n / 256, B / rb, G), 256 threads = 4 row lanes x 64 column lanes of 4 columns each.
-__global__ __launch_bounds__(256) void lista_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ gx,
-                                                        const float* __restrict__ y, const float* __restrict__ a,
-                                                        const float* __restrict__ xs, const float* __restrict__ theta,
-                                                        const float* __restrict__ m, float* __restrict__ gr,
-                                                        float* __restrict__ gxs, float* __restrict__ gth_part,
+// a == nullptr: y holds r = y + a (the explicit step saves r from the forward).  dL/dy' = gy (+ gy2)
+// (+ l1c[g] sign(y'): the last layer's L1 term, y' recomputed).  Outputs, each optional: gr (fp32 dr),
+// grb (its bf16 copy), gxs (fp32 dxs); ub = bf16(dr + dxs) for the first layer, whose xs is y itself.
+__global__ __launch_bounds__(256) void lista_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
+                                                        const float* __restrict__ gx, const float* __restrict__ y,
+                                                        const float* __restrict__ a, const float* __restrict__ xs,
+                                                        const float* __restrict__ theta, const float* __restrict__ m,
+                                                        const float* __restrict__ l1c, float* __restrict__ gr,
+                                                        uint16_t* __restrict__ grb, float* __restrict__ gxs,
+                                                        uint16_t* __restrict__ ub, float* __restrict__ gth_part,
                                                         float* __restrict__ gm_part, int B, int n, int rb) {
   __shared__ float4 red4[4][64];
   __shared__ float redm[256];
@@ -55,35 +75,48 @@ __global__ __launch_bounds__(256) void lista_bwd_kernel(const float* __restrict_
   const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
   const int j = blockIdx.x * 256 + cl * 4;
   const float mm = m[g];
+  const float lc = l1c ? l1c[g] : 0.f;
   const float4 th = *reinterpret_cast<const float4*>(theta + (long)g * n + j);
-  float4 gt = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 gt = z4;
   float gmv = 0.f;
   for (int r = rbk * rb + rl; r < (rbk + 1) * rb; r += 4) {
     const long o = ((long)g * B + r) * n + j;
     const float4 gyv = *reinterpret_cast<const float4*>(gy + o);
-    const float4 gxv = gx ? *reinterpret_cast<const float4*>(gx + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 gy2v = gy2 ? *reinterpret_cast<const float4*>(gy2 + o) : z4;
+    const float4 gxv = gx ? *reinterpret_cast<const float4*>(gx + o) : z4;
     const float4 yv = *reinterpret_cast<const float4*>(y + o);
-    const float4 av = *reinterpret_cast<const float4*>(a + o);
+    const float4 av = a ? *reinterpret_cast<const float4*>(a + o) : z4;
     const float4 xv = *reinterpret_cast<const float4*>(xs + o);
     float4 gro, gxo;
-    auto one = [&](float gyy, float gxx, float yy, float aa, float x0, float tt, float& gro_, float& gxo_, float& gtt) {
+    auto one = [&](float gyy, float gyy2, float gxx, float yy, float aa, float x0, float tt, float& gro_, float& gxo_,
+                   float& gtt) {
       const float r_ = yy + aa;
       const float mag = fabsf(r_) - tt;
       const float on = mag > 0.f ? 1.f : 0.f;
       const float sg = r_ > 0.f ? 1.f : (r_ < 0.f ? -1.f : 0.f);
       const float xo_ = sg * fmaxf(mag, 0.f);
-      const float gtot = (1.f + mm) * gyy + gxx;   // dL/dx_
+      float gyt = gyy + gyy2;
+      if (l1c) {
+        const float yo_ = xo_ + mm * (xo_ - x0);
+        gyt += lc * (yo_ > 0.f ? 1.f : (yo_ < 0.f ? -1.f : 0.f));
+      }
+      const float gtot = (1.f + mm) * gyt + gxx;   // dL/dx_
       gro_ = gtot * on * (sg != 0.f ? 1.f : 0.f);  // d x_/d r = 1 where |r| > theta (0 at r = 0)
-      gxo_ = -mm * gyy;
+      gxo_ = -mm * gyt;
       gtt -= gtot * sg * on;                        // d x_/d theta = -sign(r) where |r| > theta
-      gmv += gyy * (xo_ - x0);                      // d y'/d m = x_ - xs
+      gmv += gyt * (xo_ - x0);                      // d y'/d m = x_ - xs
     };
-    one(gyv.x, gxv.x, yv.x, av.x, xv.x, th.x, gro.x, gxo.x, gt.x);
-    one(gyv.y, gxv.y, yv.y, av.y, xv.y, th.y, gro.y, gxo.y, gt.y);
-    one(gyv.z, gxv.z, yv.z, av.z, xv.z, th.z, gro.z, gxo.z, gt.z);
-    one(gyv.w, gxv.w, yv.w, av.w, xv.w, th.w, gro.w, gxo.w, gt.w);
-    *reinterpret_cast<float4*>(gr + o) = gro;
-    *reinterpret_cast<float4*>(gxs + o) = gxo;
+    one(gyv.x, gy2v.x, gxv.x, yv.x, av.x, xv.x, th.x, gro.x, gxo.x, gt.x);
+    one(gyv.y, gy2v.y, gxv.y, yv.y, av.y, xv.y, th.y, gro.y, gxo.y, gt.y);
+    one(gyv.z, gy2v.z, gxv.z, yv.z, av.z, xv.z, th.z, gro.z, gxo.z, gt.z);
+    one(gyv.w, gy2v.w, gxv.w, yv.w, av.w, xv.w, th.w, gro.w, gxo.w, gt.w);
+    if (gr) *reinterpret_cast<float4*>(gr + o) = gro;
+    if (gxs) *reinterpret_cast<float4*>(gxs + o) = gxo;
+    if (grb) *reinterpret_cast<ushort4*>(grb + o) = make_ushort4(f2bf(gro.x), f2bf(gro.y), f2bf(gro.z), f2bf(gro.w));
+    if (ub)
+      *reinterpret_cast<ushort4*>(ub + o) = make_ushort4(f2bf(gro.x + gxo.x), f2bf(gro.y + gxo.y),
+                                                         f2bf(gro.z + gxo.z), f2bf(gro.w + gxo.w));
   }
   red4[rl][cl] = gt;
   redm[threadIdx.x] = gmv;
@@ -194,7 +227,21 @@ int sc_lista_fwd(const float* y, const float* a, const float* xs, const float* t
   hipLaunchKernelGGL(lista_fwd_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, stream,
                      reinterpret_cast<const float4*>(y), reinterpret_cast<const float4*>(a),
                      reinterpret_cast<const float4*>(xs), theta, m, reinterpret_cast<float4*>(xo),
-                     reinterpret_cast<float4*>(yo), B, n, total4);
+                     reinterpret_cast<float4*>(yo), nullptr, nullptr, nullptr, B, n, total4);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+// The explicit step's forward: also r (may be a itself), the bf16 y', and |y'| block sums
+// absp[G][B n / 1024] (needs B n % 1024 == 0).
+int sc_lista_fwd2(const float* y, const float* a, const float* xs, const float* theta, const float* m, float* xo,
+                  float* yo, float* r_out, void* yob, float* absp, int G, int B, int n, hipStream_t stream) {
+  if (n % 4 || G < 1 || B < 1 || (absp && ((long)B * n) % 1024)) return 1;
+  const long total4 = (long)G * B * n / 4;
+  hipLaunchKernelGGL(lista_fwd_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const float4*>(y), reinterpret_cast<const float4*>(a),
+                     reinterpret_cast<const float4*>(xs), theta, m, reinterpret_cast<float4*>(xo),
+                     reinterpret_cast<float4*>(yo), reinterpret_cast<float4*>(r_out),
+                     reinterpret_cast<ushort4*>(yob), absp, B, n, total4);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
@@ -203,8 +250,18 @@ int sc_lista_bwd(const float* gy, const float* gx, const float* y, const float* 
                  const float* theta, const float* m, float* gr, float* gxs, float* gth_part, float* gm_part,
                  int G, int B, int n, int rb, hipStream_t stream) {
   if (n % 256 || rb < 4 || rb % 4 || B % rb || G < 1) return 1;
-  hipLaunchKernelGGL(lista_bwd_kernel, dim3(n / 256, B / rb, G), dim3(256), 0, stream, gy, gx, y, a, xs, theta, m,
-                     gr, gxs, gth_part, gm_part, B, n, rb);
+  hipLaunchKernelGGL(lista_bwd_kernel, dim3(n / 256, B / rb, G), dim3(256), 0, stream, gy, nullptr, gx, y, a, xs,
+                     theta, m, nullptr, gr, nullptr, gxs, nullptr, gth_part, gm_part, B, n, rb);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_lista_bwd2(const float* gy, const float* gy2, const float* gx, const float* y, const float* a, const float* xs,
+                  const float* theta, const float* m, const float* l1c, float* gr, void* grb, float* gxs, void* ub,
+                  float* gth_part, float* gm_part, int G, int B, int n, int rb, hipStream_t stream) {
+  if (n % 256 || rb < 4 || rb % 4 || B % rb || G < 1) return 1;
+  hipLaunchKernelGGL(lista_bwd_kernel, dim3(n / 256, B / rb, G), dim3(256), 0, stream, gy, gy2, gx, y, a, xs,
+                     theta, m, l1c, gr, reinterpret_cast<uint16_t*>(grb), gxs, reinterpret_cast<uint16_t*>(ub),
+                     gth_part, gm_part, B, n, rb);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
