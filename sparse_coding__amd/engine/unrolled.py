@@ -352,44 +352,82 @@ class UnrolledEnsemble:
         l_rec = part.sum(1) / (B * d)
         l_l1 = self.l1 * absp.view(G, -1).sum(1) / B
 
-        # ---- backward
+        # ---- backward (the bf16 code gradients carry -dr, so every weight-gradient term has unit weight:
+        # dW = (-dr)^T (-E), -dE = (-dr) W; the decoder's reconstruction term takes alpha r in bf16)
         alpha = 2.0 / (B * d)
         gc = torch.empty(G, B, n, **f32)
         gemm_ops.matmul_nt(rf, Db, gc, alpha=alpha)  # d l_rec / dc
-        nterm = L + 2  # decoder terms of unit weight: one per layer, and dy_0^T x as two bf16 pieces
-        nslab = 1 + (nterm + 1) // 2
-        slabs = torch.empty(nslab, G, n, d, **f32)
-        gemm_ops.weight_grads([[(cb, rf)]], [slabs[0]], alpha)  # c^T dL/dx_hat
         rb = 64
         gth_part = torch.empty(G, B // rb, n, **f32)
         gm_part = torch.empty(G, B // rb, n // 256, **f32)
-        gW, gth, grho, terms = {}, {}, {}, []
+        gth, grho = {}, {}
+        dterms = [(cb, rf.mul(alpha))]  # decoder (D_hat) terms: c^T dL/dx_hat, then per layer
+        wterms = {}
         gy, gy2, gx, l1c = gc, None, None, (self.l1 / B).float().contiguous()
         for i in reversed(range(L)):
             yb_i, r_i, xs_i, rneg_i = saved[i]
             first = i == 0
-            grb = torch.empty(G, B, n, **bf)
+            ngrb = torch.empty(G, B, n, **bf)
             gr = None if first else torch.empty(G, B, n, **f32)
             gxs = None if first else torch.empty(G, B, n, **f32)
             ub = torch.empty(G, B, n, **bf) if first else None
             _lib.check(_lib.lib().sc_lista_bwd2(p(gy), p(gy2), p(gx), p(r_i), None, p(xs_i), p(ths[i]), p(ms[i]),
-                                                p(l1c), p(gr), p(grb), p(gxs), p(ub), p(gth_part), p(gm_part),
+                                                p(l1c), p(gr), p(ngrb), -1.0, p(gxs), p(ub), p(gth_part), p(gm_part),
                                                 G, B, n, rb, st), "sc_lista_bwd2")
             gth[i] = gth_part.sum(1)
             grho[i] = gm_part.sum((1, 2)) * ((rho[i] >= 0.0) & (rho[i] <= 1.0)).float()
-            gW[i] = torch.empty(G, n, d, **f32)
-            gemm_ops.weight_grads([[(grb, rneg_i)]], [gW[i]], -1.0)  # dW = dr^T E
             ngE = torch.empty(G, B, d, **bf)
-            gemm_ops.matmul_nn(grb, sh[f"layer{i}.W"], ngE, alpha=-1.0)  # -dE = -dr W
+            gemm_ops.matmul_nn(ngrb, sh[f"layer{i}.W"], ngE)  # -dE = -dr W
             t = torch.empty(G, B, n, **(bf if first else f32))
             gemm_ops.matmul_nt(ngE, Db, t)  # dy through P = y D
-            terms.append((yb_i, ngE))
+            wterms[i] = (ngrb, rneg_i)
+            dterms.append((yb_i, ngE))
             if first:
-                terms += [(ub, xb), (t, xb)]  # dy_0 = dr_0 + dxs_0 + t_0 (xs_0 is y_0)
+                dterms += [(ub, xb), (t, xb)]  # dy_0 = dr_0 + dxs_0 + t_0 (xs_0 is y_0)
             gy, gy2, gx, l1c = gr, t, gxs, None
-        for s in range(nslab - 1):  # (an odd term count leaves the last slab one segment)
-            gemm_ops.weight_grads([terms[2 * s:2 * s + 2]], [slabs[1 + s]], 1.0)
+        # the weight gradients last, two problems per launch (one [n, d] problem is half the GPU's
+        # 256x256 tiles), a lone problem split along K; the Adam kernel sums the split slabs
+        probs = [dterms[k:k + 2] for k in range(0, len(dterms), 2)]
+        dsplits = self._wg_splits([len(q) for q in probs], B)
+        slabs = torch.empty(sum(dsplits), G, n, d, **f32)
+        self._wg_launch(probs, dsplits, slabs)
+        order = sorted(wterms, reverse=True)
+        wsplits = self._wg_splits([1] * L, B)
+        gW = {i: torch.empty(wsplits[k], G, n, d, **f32) for k, i in enumerate(order)}
+        self._wg_launch([[wterms[i]] for i in order], wsplits, None, outs=[gW[i] for i in order])
         return slabs, gW, gth, grho, (l_rec + l_l1, l_rec, l_l1, c)
+
+    def _wg_splits(self, nsegs, B):
+        """Split-K factor per weight-gradient problem: problems run in pairs of equal segment count;
+        a lone one is split so its launch still fills the GPU."""
+        from ..ops import gemm as gemm_ops
+
+        G, n, d = self.params["decoder"].shape
+        out, k = [], 0
+        while k < len(nsegs):
+            if k + 1 < len(nsegs) and nsegs[k + 1] == nsegs[k]:
+                out += [1, 1]
+                k += 2
+            else:
+                out.append(gemm_ops.wgrad_split(G, n, d, B * nsegs[k], 1))
+                k += 1
+        return out
+
+    @staticmethod
+    def _wg_launch(probs, splits, slabs, outs=None):
+        from ..ops import gemm as gemm_ops
+
+        k = j = 0
+        while k < len(probs):
+            if splits[k] == 1 and k + 1 < len(probs) and splits[k + 1] == 1 and len(probs[k]) == len(probs[k + 1]):
+                o = [slabs[j], slabs[j + 1]] if outs is None else [outs[k][0], outs[k + 1][0]]
+                gemm_ops.weight_grads([probs[k], probs[k + 1]], o, 1.0)
+                k, j = k + 2, j + 2
+            else:
+                s = splits[k]
+                o = (slabs[j:j + s] if outs is None else outs[k])
+                gemm_ops.weight_grads([probs[k]], [o if s > 1 else o[0]], 1.0, ksplit=s)
+                k, j = k + 1, j + s
 
     def fused_grads(self, x: torch.Tensor):
         """The explicit step's gradients in the autograd path's form (tests): the decoder's through
@@ -400,7 +438,7 @@ class UnrolledEnsemble:
         gh = slabs.sum(0)
         out = {"decoder": gh / nrm - dec * (dec * gh).sum(-1, keepdim=True) / nrm ** 3}
         for i in range(self.n_layers):
-            out[f"layer{i}.W"], out[f"layer{i}.theta"], out[f"layer{i}.rho"] = gW[i], gth[i], grho[i]
+            out[f"layer{i}.W"], out[f"layer{i}.theta"], out[f"layer{i}.rho"] = gW[i].sum(0), gth[i], grho[i]
         return out, losses
 
     @torch.no_grad()
@@ -420,17 +458,26 @@ class UnrolledEnsemble:
                            self.eps, nsplit=slabs.shape[0], gstride=G * n * d)
         for i in range(L):
             k = f"layer{i}.W"
-            adam_ops.adam_rows([dict(p=self.params[k].data, g=gW[i], m=self.m[k], v=self.v[k], shadow=sh[k],
-                                     norms=None, norm=False)], self.lr, self.step_count, b1, b2, self.eps)
+            adam_ops.adam_rows([dict(p=self.params[k].data, g=gW[i][0], m=self.m[k], v=self.v[k], shadow=sh[k],
+                                     norms=None, norm=False)], self.lr, self.step_count, b1, b2, self.eps,
+                               nsplit=gW[i].shape[0], gstride=G * n * d)
+        # the vectors (theta [G, n], rho [G]): torch Adam as multi-tensor ops (a handful of launches)
         bc1 = 1.0 - b1 ** self.step_count
         bc2 = 1.0 - b2 ** self.step_count
-        for i in range(L):
-            for k, g in ((f"layer{i}.theta", gth[i]), (f"layer{i}.rho", grho[i])):
-                pk, m, v = self.params[k], self.m[k], self.v[k]
-                m.mul_(b1).add_(g, alpha=1.0 - b1)
-                v.mul_(b2).addcmul_(g, g, value=1.0 - b2)
-                lr = self.lr.view(-1, *([1] * (pk.dim() - 1)))
-                pk.sub_(lr * (m / bc1) / ((v / bc2).sqrt() + self.eps))
+        keys = [k for i in range(L) for k in (f"layer{i}.theta", f"layer{i}.rho")]
+        gs = [t for i in range(L) for t in (gth[i], grho[i])]
+        ps, ms_, vs = [self.params[k].data for k in keys], [self.m[k] for k in keys], [self.v[k] for k in keys]
+        torch._foreach_mul_(ms_, b1)
+        torch._foreach_add_(ms_, gs, alpha=1.0 - b1)
+        torch._foreach_mul_(vs, b2)
+        torch._foreach_addcmul_(vs, gs, gs, value=1.0 - b2)
+        den = torch._foreach_div(vs, bc2)
+        torch._foreach_sqrt_(den)
+        torch._foreach_add_(den, self.eps)
+        upd = torch._foreach_div(ms_, den)
+        lrs = [self.lr.view(-1, *([1] * (t.dim() - 1))) * (1.0 / bc1) for t in ps]
+        torch._foreach_mul_(upd, [l.expand_as(u) for l, u in zip(lrs, upd)])
+        torch._foreach_sub_(ps, upd)
         return losses
 
     # ------------------------------------------------------------------ export / state

@@ -60,13 +60,13 @@ __global__ __launch_bounds__(256) void lista_fwd_kernel(const float4* __restrict
 // grid (n / 256, B / rb, G), 256 threads = 4 row lanes x 64 column lanes of 4 columns each.
 // a == nullptr: y holds r = y + a (the explicit step saves r from the forward).  dL/dy' = gy (+ gy2)
 // (+ l1c[g] sign(y'): the last layer's L1 term, y' recomputed).  Outputs, each optional: gr (fp32 dr),
-// grb (its bf16 copy), gxs (fp32 dxs); ub = bf16(dr + dxs) for the first layer, whose xs is y itself.
+// grb (bf16 gsign * dr), gxs (fp32 dxs); ub = bf16(dr + dxs) for the first layer, whose xs is y itself.
 __global__ __launch_bounds__(256) void lista_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
                                                         const float* __restrict__ gx, const float* __restrict__ y,
                                                         const float* __restrict__ a, const float* __restrict__ xs,
                                                         const float* __restrict__ theta, const float* __restrict__ m,
                                                         const float* __restrict__ l1c, float* __restrict__ gr,
-                                                        uint16_t* __restrict__ grb, float* __restrict__ gxs,
+                                                        uint16_t* __restrict__ grb, float gsign, float* __restrict__ gxs,
                                                         uint16_t* __restrict__ ub, float* __restrict__ gth_part,
                                                         float* __restrict__ gm_part, int B, int n, int rb) {
   __shared__ float4 red4[4][64];
@@ -113,7 +113,9 @@ __global__ __launch_bounds__(256) void lista_bwd_kernel(const float* __restrict_
     one(gyv.w, gy2v.w, gxv.w, yv.w, av.w, xv.w, th.w, gro.w, gxo.w, gt.w);
     if (gr) *reinterpret_cast<float4*>(gr + o) = gro;
     if (gxs) *reinterpret_cast<float4*>(gxs + o) = gxo;
-    if (grb) *reinterpret_cast<ushort4*>(grb + o) = make_ushort4(f2bf(gro.x), f2bf(gro.y), f2bf(gro.z), f2bf(gro.w));
+    if (grb)
+      *reinterpret_cast<ushort4*>(grb + o) =
+          make_ushort4(f2bf(gsign * gro.x), f2bf(gsign * gro.y), f2bf(gsign * gro.z), f2bf(gsign * gro.w));
     if (ub)
       *reinterpret_cast<ushort4*>(ub + o) = make_ushort4(f2bf(gro.x + gxo.x), f2bf(gro.y + gxo.y),
                                                          f2bf(gro.z + gxo.z), f2bf(gro.w + gxo.w));
@@ -251,16 +253,16 @@ int sc_lista_bwd(const float* gy, const float* gx, const float* y, const float* 
                  int G, int B, int n, int rb, hipStream_t stream) {
   if (n % 256 || rb < 4 || rb % 4 || B % rb || G < 1) return 1;
   hipLaunchKernelGGL(lista_bwd_kernel, dim3(n / 256, B / rb, G), dim3(256), 0, stream, gy, nullptr, gx, y, a, xs,
-                     theta, m, nullptr, gr, nullptr, gxs, nullptr, gth_part, gm_part, B, n, rb);
+                     theta, m, nullptr, gr, nullptr, 1.f, gxs, nullptr, gth_part, gm_part, B, n, rb);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 
 int sc_lista_bwd2(const float* gy, const float* gy2, const float* gx, const float* y, const float* a, const float* xs,
-                  const float* theta, const float* m, const float* l1c, float* gr, void* grb, float* gxs, void* ub,
-                  float* gth_part, float* gm_part, int G, int B, int n, int rb, hipStream_t stream) {
+                  const float* theta, const float* m, const float* l1c, float* gr, void* grb, float gsign, float* gxs,
+                  void* ub, float* gth_part, float* gm_part, int G, int B, int n, int rb, hipStream_t stream) {
   if (n % 256 || rb < 4 || rb % 4 || B % rb || G < 1) return 1;
   hipLaunchKernelGGL(lista_bwd_kernel, dim3(n / 256, B / rb, G), dim3(256), 0, stream, gy, gy2, gx, y, a, xs,
-                     theta, m, l1c, gr, reinterpret_cast<uint16_t*>(grb), gxs, reinterpret_cast<uint16_t*>(ub),
+                     theta, m, l1c, gr, reinterpret_cast<uint16_t*>(grb), gsign, gxs, reinterpret_cast<uint16_t*>(ub),
                      gth_part, gm_part, B, n, rb);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
