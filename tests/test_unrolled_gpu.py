@@ -102,13 +102,18 @@ def test_unrolled_adam_kernel_matches_torch_adam():
         torch.testing.assert_close(eng.params[k].detach(), p[k], rtol=1e-5, atol=1e-6)
 
 
-def test_lista_fused_grads_match_fp32():
+@pytest.mark.parametrize("layers,n,B", [(3, 512, 256), (2, 768, 384), (1, 256, 128)])
+def test_lista_fused_grads_match_fp32(layers, n, B):
     """The explicit (autograd-free) LISTA step's gradients == the engine's fp32 torch path (CPU),
-    every parameter of every model, per-model relative Frobenius error <= 3e-2, losses alike."""
+    every parameter of every model, per-model relative Frobenius error <= 3e-2 (or within 1.5x of the
+    autograd GPU path's own distance, at the small shapes), losses alike (odd and even layer counts:
+    paired and lone weight-gradient problems)."""
     torch.manual_seed(3)
-    d, n, B, G = 256, 512, 256, 3
+    d, G = 256, 3
     sig = FunctionalLISTADenoisingSAE
-    models = [sig.init(d, n, 3, l1) for l1 in (1e-3, 3e-3, 1e-2)]
+    models = [sig.init(d, n, layers, l1) for l1 in (1e-3, 3e-3, 1e-2)]
+    for p_, _ in models:  # off the orthogonal init, where y_0 D reproduces x and the residual is ~0
+        p_["decoder"] = p_["decoder"] + 0.3 * torch.randn_like(p_["decoder"]) / d ** 0.5
     x = torch.randn(B, d)
     hip = UnrolledEnsemble(models, sig, device=DEV)
     ref = UnrolledEnsemble(models, sig, device="cpu")
@@ -119,10 +124,11 @@ def test_lista_fused_grads_match_fp32():
     torch.testing.assert_close(l1h.cpu(), l1r, rtol=2e-2, atol=1e-6)
     assert _rel(ch, cr) < 2e-2
     assert set(gh) == set(gr)
+    ga, _ = hip.grads(x.to(DEV))  # the autograd path on the same bf16 kernels: its distance is the noise floor
     for k in gr:
         for g in range(G):
-            e = _rel(gh[k][g], gr[k][g])
-            assert e <= 3e-2, (k, g, e)
+            e, ea = _rel(gh[k][g], gr[k][g]), _rel(ga[k][g], gr[k][g])
+            assert e <= max(3e-2, 1.5 * ea), (k, g, e, ea)
 
 
 def test_lista_fused_step_tracks_autograd_step():
@@ -154,3 +160,32 @@ def test_lista_fused_step_tracks_autograd_step():
     want = (dec / dec.norm(dim=-1, keepdim=True)).to(torch.bfloat16).float()
     torch.testing.assert_close(fused._sh["decoder"].float(), want, rtol=1e-2, atol=1e-2)
     assert torch.isfinite(out_f["loss"]).all()
+
+
+def test_lista_fused_training_and_resume():
+    """The explicit LISTA step trains (loss falls over 60 steps) and resumes: a state_dict round trip
+    into a fresh engine (bf16 shadows rebuilt from the loaded masters, which the running engine's Adam
+    wrote itself -- the row norm may differ in the last bit) gives the same next step."""
+    torch.manual_seed(8)
+    d, n, B = 256, 512, 256
+    sig = FunctionalLISTADenoisingSAE
+    models = [sig.init(d, n, 2, l1) for l1 in (1e-4, 1e-3)]
+    eng = UnrolledEnsemble(models, sig, lr=3e-3, device=DEV)
+    basis = torch.randn(64, d, device=DEV)
+    data = [(torch.rand(B, 64, device=DEV) ** 4) @ basis for _ in range(8)]
+    first = last = None
+    for t in range(60):
+        out, _ = eng.step_batch(data[t % 8])
+        if t == 0:
+            first = out["l_reconstruction"].clone()
+        last = out["l_reconstruction"]
+    assert (last < 0.5 * first).all(), (first, last)
+    sd = {k: ({kk: vv.clone() for kk, vv in v.items()} if isinstance(v, dict) else v) for k, v in eng.state_dict().items()}
+    other = UnrolledEnsemble([sig.init(d, n, 2, l1) for l1 in (1e-4, 1e-3)], sig, lr=3e-3, device=DEV)
+    other.load_state_dict(sd)
+    a, _ = eng.step_batch(data[0])
+    b, _ = other.step_batch(data[0])
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a["loss"], b["loss"], rtol=1e-4, atol=1e-7)
+    for k in eng.params:
+        torch.testing.assert_close(eng.params[k], other.params[k], rtol=1e-4, atol=1e-6)
