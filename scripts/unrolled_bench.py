@@ -1,5 +1,5 @@
-"""LISTA ensemble step: UnrolledEnsemble (grouped MFMA GEMMs) vs the vmap(grad) FunctionalEnsemble
-on the same GPU (8 models, d=512, n=2048, 3 layers, B=2048)."""
+"""LISTA (or, with --residual, residual-denoising) ensemble step: UnrolledEnsemble (grouped MFMA
+GEMMs) vs the vmap(grad) FunctionalEnsemble on the same GPU (8 models, d=512, n=2048, 3 layers, B=2048)."""
 import json
 import os
 import sys
@@ -12,7 +12,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from sparse_coding__amd.engine.ensemble import FunctionalEnsemble
 from sparse_coding__amd.engine.optim import adam
 from sparse_coding__amd.engine.unrolled import UnrolledEnsemble
-from sparse_coding__amd.models.lista import FunctionalLISTADenoisingSAE as S
+from sparse_coding__amd.models.lista import FunctionalLISTADenoisingSAE, FunctionalResidualDenoisingSAE
+
+S = FunctionalResidualDenoisingSAE if "--residual" in sys.argv else FunctionalLISTADenoisingSAE
 
 
 def timeit(fn, steps=10, warm=3):
@@ -33,10 +35,10 @@ x = torch.randn(B, d, device="cuda")
 eng = UnrolledEnsemble(models, S, device="cuda")
 ms = timeit(lambda: eng.step_batch(x))
 if "--only-unrolled" in sys.argv:
-    print(json.dumps({"unrolled_ms_per_step": round(ms, 3)}))
+    print(json.dumps({"model": S.__name__, "unrolled_ms_per_step": round(ms, 3)}))
     sys.exit(0)
 ens = FunctionalEnsemble(models, S, adam, {"lr": 1e-3}, device="cuda")
 ms_e = timeit(lambda: ens.step_batch(x))
-print(json.dumps({"config": f"LISTA {G} models d={d} n={n} layers={L} B={B}", "unrolled_ms_per_step": round(ms, 3),
+print(json.dumps({"config": f"{'residual-denoising' if S is FunctionalResidualDenoisingSAE else 'LISTA'} {G} models d={d} n={n} layers={L} B={B}", "unrolled_ms_per_step": round(ms, 3),
                   "eager_vmap_ms_per_step": round(ms_e, 3), "speedup": round(ms_e / ms, 2),
                   "unrolled_act_per_s": round(B / ms * 1e3)}))
