@@ -34,11 +34,19 @@ models = [S.init(d, n, L, float(l1), device="cuda") for l1 in torch.logspace(-4,
 x = torch.randn(B, d, device="cuda")
 eng = UnrolledEnsemble(models, S, device="cuda")
 ms = timeit(lambda: eng.step_batch(x))
+
+
+def autograd_step():  # the engine's torch-autograd path over the same kernels (before round 6's explicit step)
+    g, _ = eng.grads(x)
+    eng.apply_grads(g)
+
+
 if "--only-unrolled" in sys.argv:
     print(json.dumps({"model": S.__name__, "unrolled_ms_per_step": round(ms, 3)}))
     sys.exit(0)
+ms_a = timeit(autograd_step)
 ens = FunctionalEnsemble(models, S, adam, {"lr": 1e-3}, device="cuda")
 ms_e = timeit(lambda: ens.step_batch(x))
-print(json.dumps({"config": f"{'residual-denoising' if S is FunctionalResidualDenoisingSAE else 'LISTA'} {G} models d={d} n={n} layers={L} B={B}", "unrolled_ms_per_step": round(ms, 3),
+print(json.dumps({"config": f"{'residual-denoising' if S is FunctionalResidualDenoisingSAE else 'LISTA'} {G} models d={d} n={n} layers={L} B={B}", "unrolled_ms_per_step": round(ms, 3), "autograd_path_ms_per_step": round(ms_a, 3),
                   "eager_vmap_ms_per_step": round(ms_e, 3), "speedup": round(ms_e / ms, 2),
                   "unrolled_act_per_s": round(B / ms * 1e3)}))

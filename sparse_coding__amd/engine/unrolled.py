@@ -5,14 +5,15 @@ Reference: ``autoencoders/residual_denoising_autoencoder.py:9-122`` (LISTA layer
 shrinkage and momentum, https://arxiv.org/pdf/2008.02683.pdf) and ``:125-201`` (residual
 denoising layers), trained by ``FunctionalEnsemble`` = ``vmap(grad(loss))`` per model.
 
-LISTA on the GPU trains through ``UnrolledEnsemble._lista_fused_step``: the forward and a hand-derived
+On the GPU both families train through ``UnrolledEnsemble._fused_step``: the forward and a hand-derived
 backward with no autograd, every product a grouped MFMA GEMM whose epilogue writes the operand the
 next product reads (bf16 residuals, bf16 code gradients, alpha-scaled signs folded in), the
 shrinkage/momentum of each layer one HIP pass each way (``sc_lista_fwd2`` / ``sc_lista_bwd2``: r, the
 bf16 copy of y', the L1 sums, the summed incoming gradients, the first layer's y0 = xs0 gradient), and
 the matrices' Adam the row kernel that also rewrites their bf16 shadows (the decoder's normalised:
-the unit-row Jacobian is applied there).  The autograd path (``grads``) stays for the residual
-family, the CPU and the tests.
+the unit-row Jacobian is applied there); the residual family's ReLU layers likewise
+(``sc_res_fwd`` / ``sc_res_bwd``).  The autograd path (``grads``) stays for the CPU, the tests and
+shapes the kernels do not tile.
 
 Here every model's parameters are stacked on a leading model axis and the loss of all models
 is written once in batched form.  Each layer's matrix products are grouped GEMMs over the
@@ -209,7 +210,7 @@ class UnrolledEnsemble:
         self.step_count = 0
         # bf16 shadows of the matrices for the explicit LISTA step (built on first use, rewritten by
         # its Adam; dropped whenever the parameters change another way)
-        self._mats = ["decoder"] + [f"layer{i}.W" for i in range(self.n_layers)] if self.kind == "lista" else []
+        self._mats = ["decoder"] + [f"layer{i}.W" for i in range(self.n_layers)]
         self._sh = None
 
     # ------------------------------------------------------------------ model
@@ -280,7 +281,7 @@ class UnrolledEnsemble:
 
     def step_batch(self, batch: torch.Tensor, expand_dims: bool = True):
         if self._fused_ok(batch.shape[0]):
-            total, l_rec, l_l1, c = self._lista_fused_step(batch)
+            total, l_rec, l_l1, c = self._fused_step(batch)
         else:
             grads, (total, l_rec, l_l1, c) = self.grads(batch)
             self.apply_grads(grads)
@@ -289,8 +290,8 @@ class UnrolledEnsemble:
     # ------------------------------------------------------------------ explicit LISTA step (GPU)
     def _fused_ok(self, B: int) -> bool:
         G, n, d = self.params["decoder"].shape
-        return (self.kind == "lista" and self.device.type == "cuda" and B % 128 == 0 and n % 256 == 0
-                and d % 256 == 0 and d <= 4096 and (B * n) % 1024 == 0)
+        return (self.device.type == "cuda" and B % 128 == 0 and n % 256 == 0 and d % 256 == 0 and d <= 4096
+                and (B * n) % 1024 == 0 and (self.kind == "lista" or n <= 4096))
 
     def _shadows(self):
         from ..ops import adam as adam_ops
@@ -395,7 +396,10 @@ class UnrolledEnsemble:
         wsplits = self._wg_splits([1] * L, B)
         gW = {i: torch.empty(wsplits[k], G, n, d, **f32) for k, i in enumerate(order)}
         self._wg_launch([[wterms[i]] for i in order], wsplits, None, outs=[gW[i] for i in order])
-        return slabs, gW, gth, grho, (l_rec + l_l1, l_rec, l_l1, c)
+        vec = {}
+        for i in range(L):
+            vec[f"layer{i}.theta"], vec[f"layer{i}.rho"] = gth[i], grho[i]
+        return slabs, gW, vec, (l_rec + l_l1, l_rec, l_l1, c)
 
     def _wg_splits(self, nsegs, B):
         """Split-K factor per weight-gradient problem: problems run in pairs of equal segment count;
@@ -429,23 +433,109 @@ class UnrolledEnsemble:
                 gemm_ops.weight_grads([probs[k]], [o if s > 1 else o[0]], 1.0, ksplit=s)
                 k, j = k + 1, j + s
 
+    @torch.no_grad()
+    def _residual_fused_grads(self, x: torch.Tensor):
+        """The residual-denoising family's step without autograd (reference
+        autoencoders/residual_denoising_autoencoder.py:92-122).  Forward (c_0 = x D^T):
+        h_i = relu(c_i + theta_i), c_{i+1} = h_i W_i^T + c_i, codes c = relu(c_L + b).  Backward
+        (G = dL/dc_{i+1}):  dW_i = G^T h_i,  dh = G W_i,  dc_i = G + dh 1[c_i + theta_i > 0],
+        dtheta_i / db = column sums of the masked terms, dD_hat = dc_0^T x + c^T dL/dx_hat."""
+        from ..ops import _lib
+        from ..ops import gemm as gemm_ops
+
+        G, n, d = self.params["decoder"].shape
+        B, L, dev = int(x.shape[0]), self.n_layers, self.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        bf = dict(device=dev, dtype=torch.bfloat16)
+        sh = self._shadows()
+        Db = sh["decoder"]
+        xb = x.to(dev, torch.bfloat16).contiguous()
+        p, st = _lib.ptr, _lib.stream_handle()
+        ths = [self.params[f"layer{i}.theta"].detach().contiguous() for i in range(L)]
+        bias = self.params["encoder_bias"].detach().contiguous()
+        part = torch.empty(G, (B // 128) * (d // 128), **f32)
+        absp = torch.empty(G * B * n // 1024, **f32)
+
+        def fwd(u, cin, th, cout, hb, fin):
+            _lib.check(_lib.lib().sc_res_fwd(p(u), p(cin), p(th), p(cout), p(hb), p(absp) if fin else None, int(fin),
+                                             G, B, n, st), "sc_res_fwd")
+
+        # ---- forward
+        cs, hbs = [torch.empty(G, B, n, **f32)], [torch.empty(G, B, n, **bf)]
+        gemm_ops.matmul_nt(xb, Db, cs[0])  # c_0 = x D^T
+        if L == 0:
+            c, cb = torch.empty(G, B, n, **f32), torch.empty(G, B, n, **bf)
+            fwd(None, cs[0], bias, c, cb, True)
+        else:
+            fwd(None, cs[0], ths[0], None, hbs[0], False)
+        for i in range(L):
+            u = torch.empty(G, B, n, **f32)
+            gemm_ops.matmul_nt(hbs[i], sh[f"layer{i}.W"], u)  # h_i W_i^T
+            if i + 1 < L:
+                cs.append(torch.empty(G, B, n, **f32))
+                hbs.append(torch.empty(G, B, n, **bf))
+                fwd(u, cs[i], ths[i + 1], cs[i + 1], hbs[i + 1], False)
+            else:
+                c, cb = torch.empty(G, B, n, **f32), torch.empty(G, B, n, **bf)
+                fwd(u, cs[i], bias, c, cb, True)
+        rf = torch.empty(G, B, d, **bf)
+        gemm_ops.decode_residual(cb, Db, xb, rf, part)
+        l_rec = part.sum(1) / (B * d)
+        l_l1 = self.l1 * absp.view(G, -1).sum(1) / B
+
+        # ---- backward
+        alpha = 2.0 / (B * d)
+        gc = torch.empty(G, B, n, **f32)
+        gemm_ops.matmul_nt(rf, Db, gc, alpha=alpha)
+        rb = 64
+        cpart = torch.empty(G, B // rb, n, **f32)
+        vec = {}
+
+        def bwd(gin, gadd, pre, th, l1c, out, outb):
+            _lib.check(_lib.lib().sc_res_bwd(p(gin), p(gadd), p(pre), p(th), p(l1c), p(out), p(outb), p(cpart),
+                                             G, B, n, rb, st), "sc_res_bwd")
+            return cpart.sum(1)
+
+        Gf, Gb = torch.empty(G, B, n, **f32), torch.empty(G, B, n, **bf)
+        vec["encoder_bias"] = bwd(gc, None, c, None, (self.l1 / B).float().contiguous(), Gf, Gb)
+        gW = {}
+        for i in reversed(range(L)):  # (an [n, n] weight gradient is G n^2 / 256^2 >= 256 tiles: no split)
+            gW[i] = torch.empty(1, G, n, n, **f32)
+            gemm_ops.weight_grads([[(Gb, hbs[i])]], [gW[i][0]], 1.0)  # G^T h_i
+            gh = torch.empty(G, B, n, **f32)
+            gemm_ops.matmul_nn(Gb, sh[f"layer{i}.W"], gh)  # G W_i
+            Gf2 = torch.empty(G, B, n, **f32) if i else None
+            Gb2 = torch.empty(G, B, n, **bf)
+            vec[f"layer{i}.theta"] = bwd(Gf, gh, cs[i], ths[i], None, Gf2, Gb2)
+            Gf, Gb = Gf2, Gb2
+        probs = [[(Gb, xb), (cb, rf.mul(alpha))]]  # dc_0^T x + c^T dL/dx_hat
+        dsplits = self._wg_splits([2], B)
+        slabs = torch.empty(dsplits[0], G, n, d, **f32)
+        self._wg_launch(probs, dsplits, slabs)
+        return slabs, gW, vec, (l_rec + l_l1, l_rec, l_l1, c)
+
     def fused_grads(self, x: torch.Tensor):
         """The explicit step's gradients in the autograd path's form (tests): the decoder's through
         the unit-row Jacobian, the split slabs summed."""
-        slabs, gW, gth, grho, losses = self._lista_fused_grads(x)
+        slabs, gW, vec, losses = self._fused_grads(x)
         dec = self.params["decoder"].detach()
         nrm = torch.linalg.vector_norm(dec, dim=-1, keepdim=True).clamp_min(1e-8)
         gh = slabs.sum(0)
         out = {"decoder": gh / nrm - dec * (dec * gh).sum(-1, keepdim=True) / nrm ** 3}
         for i in range(self.n_layers):
-            out[f"layer{i}.W"], out[f"layer{i}.theta"], out[f"layer{i}.rho"] = gW[i].sum(0), gth[i], grho[i]
+            out[f"layer{i}.W"] = gW[i].sum(0)
+        out.update(vec)
         return out, losses
 
     @torch.no_grad()
-    def _lista_fused_step(self, x: torch.Tensor):
+    def _fused_grads(self, x: torch.Tensor):
+        return self._lista_fused_grads(x) if self.kind == "lista" else self._residual_fused_grads(x)
+
+    @torch.no_grad()
+    def _fused_step(self, x: torch.Tensor):
         from ..ops import adam as adam_ops
 
-        slabs, gW, gth, grho, losses = self._lista_fused_grads(x)
+        slabs, gW, vec, losses = self._fused_grads(x)
         G, n, d = self.params["decoder"].shape
         sh = self._sh
         # ---- update: the row-Adam kernel (and the shadows) for the matrices, torch for the vectors
@@ -458,14 +548,16 @@ class UnrolledEnsemble:
                            self.eps, nsplit=slabs.shape[0], gstride=G * n * d)
         for i in range(L):
             k = f"layer{i}.W"
-            adam_ops.adam_rows([dict(p=self.params[k].data, g=gW[i][0], m=self.m[k], v=self.v[k], shadow=sh[k],
+            w = self.params[k]
+            adam_ops.adam_rows([dict(p=w.data, g=gW[i][0], m=self.m[k], v=self.v[k], shadow=sh[k],
                                      norms=None, norm=False)], self.lr, self.step_count, b1, b2, self.eps,
-                               nsplit=gW[i].shape[0], gstride=G * n * d)
-        # the vectors (theta [G, n], rho [G]): torch Adam as multi-tensor ops (a handful of launches)
+                               nsplit=gW[i].shape[0], gstride=w[0].numel() * G)
+        # the vectors (theta [G, n], rho [G], the residual family's encoder bias [G, n]): torch Adam as
+        # multi-tensor ops (a handful of launches)
         bc1 = 1.0 - b1 ** self.step_count
         bc2 = 1.0 - b2 ** self.step_count
-        keys = [k for i in range(L) for k in (f"layer{i}.theta", f"layer{i}.rho")]
-        gs = [t for i in range(L) for t in (gth[i], grho[i])]
+        keys = list(vec)
+        gs = [vec[k] for k in keys]
         ps, ms_, vs = [self.params[k].data for k in keys], [self.m[k] for k in keys], [self.v[k] for k in keys]
         torch._foreach_mul_(ms_, b1)
         torch._foreach_add_(ms_, gs, alpha=1.0 - b1)

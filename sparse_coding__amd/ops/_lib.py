@@ -83,6 +83,10 @@ def signatures():
         "sc_lista_bwd2": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                           c_int, c_void_p],
+        "sc_res_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                       c_void_p],
+        "sc_res_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                       c_int, c_int, c_void_p],
         "sc_synth_codes": [c_void_p, c_void_p, c_long, c_int, C.c_ulonglong, C.c_ulonglong, c_void_p],
         "sc_coef_search": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_float, c_void_p],

@@ -138,6 +138,89 @@ __global__ __launch_bounds__(256) void lista_bwd_kernel(const float* __restrict_
   if (threadIdx.x == 0) gm_part[((long)g * gridDim.y + rbk) * gridDim.x + blockIdx.x] = redm[0];
 }
 
+// Residual-denoising layers, explicit step (reference autoencoders/residual_denoising_autoencoder.py:
+// 92-122: c' = relu(c + theta) W^T + c, codes relu(c_L + b)).  res_fwd: c' = u + c (u = the layer GEMM,
+// absent for the first layer: c' = c), written to cout when given; hb = bf16(relu(c' + th)) with th the
+// NEXT layer's theta; `fin`: th is the encoder bias, cout = relu(c' + b) (the codes), hb their bf16
+// copy and absp the |c| block sums (B n % 1024 == 0).
+__global__ __launch_bounds__(256) void res_fwd_kernel(const float4* __restrict__ u, const float4* __restrict__ c,
+                                                      const float* __restrict__ th, float4* __restrict__ cout,
+                                                      ushort4* __restrict__ hb, float* __restrict__ absp, int fin,
+                                                      int B, int n, long total4) {
+  const long t = (long)blockIdx.x * 256 + threadIdx.x;
+  float ab = 0.f;
+  if (t < total4) {
+    const long e = t * 4;
+    const int g = (int)(e / ((long)B * n));
+    const int j = (int)(e % n);
+    float4 cv = c[t];
+    if (u) {
+      const float4 uv = u[t];
+      cv.x += uv.x; cv.y += uv.y; cv.z += uv.z; cv.w += uv.w;
+    }
+    const float4 tv = *reinterpret_cast<const float4*>(th + (long)g * n + j);
+    const float4 h = make_float4(fmaxf(cv.x + tv.x, 0.f), fmaxf(cv.y + tv.y, 0.f), fmaxf(cv.z + tv.z, 0.f),
+                                 fmaxf(cv.w + tv.w, 0.f));
+    if (fin) {
+      cout[t] = h;
+      ab = h.x + h.y + h.z + h.w;
+    } else if (cout) {
+      cout[t] = cv;
+    }
+    hb[t] = make_ushort4(f2bf(h.x), f2bf(h.y), f2bf(h.z), f2bf(h.w));
+  }
+  if (absp) {
+    __shared__ float red[8];
+    ab = block_sum_256(ab, red);
+    if (threadIdx.x == 0) absp[blockIdx.x] = ab;
+  }
+}
+
+// res_bwd, grid (n / 256, B / rb, G): m = 1[pre + th > 0] (th optional); t = gadd, or gin + l1c[g]
+// without gadd; out = (gadd ? gin : 0) + t m (fp32 optional) and outb = bf16(out); cpart[G][B / rb][n]
+// = column sums of t m (the layer's theta gradient, or with the codes as `pre` the bias gradient).
+__global__ __launch_bounds__(256) void res_bwd_kernel(const float* __restrict__ gin, const float* __restrict__ gadd,
+                                                      const float* __restrict__ pre, const float* __restrict__ th,
+                                                      const float* __restrict__ l1c, float* __restrict__ out,
+                                                      uint16_t* __restrict__ outb, float* __restrict__ cpart, int B,
+                                                      int n, int rb) {
+  __shared__ float4 red4[4][64];
+  const int g = blockIdx.z, rbk = blockIdx.y;
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int j = blockIdx.x * 256 + cl * 4;
+  const float lc = l1c ? l1c[g] : 0.f;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 tv = th ? *reinterpret_cast<const float4*>(th + (long)g * n + j) : z4;
+  float4 cs = z4;
+  for (int r = rbk * rb + rl; r < (rbk + 1) * rb; r += 4) {
+    const long o = ((long)g * B + r) * n + j;
+    const float4 gi = *reinterpret_cast<const float4*>(gin + o);
+    const float4 pv = *reinterpret_cast<const float4*>(pre + o);
+    float4 tt;
+    if (gadd) tt = *reinterpret_cast<const float4*>(gadd + o);
+    else tt = make_float4(gi.x + lc, gi.y + lc, gi.z + lc, gi.w + lc);
+    const float4 mt = make_float4(pv.x + tv.x > 0.f ? tt.x : 0.f, pv.y + tv.y > 0.f ? tt.y : 0.f,
+                                  pv.z + tv.z > 0.f ? tt.z : 0.f, pv.w + tv.w > 0.f ? tt.w : 0.f);
+    float4 ov = mt;
+    if (gadd) {
+      ov.x += gi.x; ov.y += gi.y; ov.z += gi.z; ov.w += gi.w;
+    }
+    if (out) *reinterpret_cast<float4*>(out + o) = ov;
+    *reinterpret_cast<ushort4*>(outb + o) = make_ushort4(f2bf(ov.x), f2bf(ov.y), f2bf(ov.z), f2bf(ov.w));
+    cs.x += mt.x; cs.y += mt.y; cs.z += mt.z; cs.w += mt.w;
+  }
+  red4[rl][cl] = cs;
+  __syncthreads();
+  if (rl == 0) {
+    float4 s = red4[0][cl];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      s.x += red4[k][cl].x; s.y += red4[k][cl].y; s.z += red4[k][cl].z; s.w += red4[k][cl].w;
+    }
+    *reinterpret_cast<float4*>(cpart + ((long)g * gridDim.y + rbk) * n + j) = s;
+  }
+}
+
 __global__ __launch_bounds__(256) void center_rows_kernel(const uint16_t* __restrict__ x, const float* __restrict__ c,
                                                           uint16_t* __restrict__ out, int G, int B, int d) {
   const long t = (long)blockIdx.x * 256 + threadIdx.x;  // one thread per 4 elements of out
@@ -264,6 +347,24 @@ int sc_lista_bwd2(const float* gy, const float* gy2, const float* gx, const floa
   hipLaunchKernelGGL(lista_bwd_kernel, dim3(n / 256, B / rb, G), dim3(256), 0, stream, gy, gy2, gx, y, a, xs,
                      theta, m, l1c, gr, reinterpret_cast<uint16_t*>(grb), gsign, gxs, reinterpret_cast<uint16_t*>(ub),
                      gth_part, gm_part, B, n, rb);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_res_fwd(const float* u, const float* c, const float* th, float* cout, void* hb, float* absp, int fin, int G,
+               int B, int n, hipStream_t stream) {
+  if (n % 4 || G < 1 || B < 1 || (absp && ((long)B * n) % 1024) || (fin && !cout)) return 1;
+  const long total4 = (long)G * B * n / 4;
+  hipLaunchKernelGGL(res_fwd_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, stream,
+                     reinterpret_cast<const float4*>(u), reinterpret_cast<const float4*>(c), th,
+                     reinterpret_cast<float4*>(cout), reinterpret_cast<ushort4*>(hb), absp, fin, B, n, total4);
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
+
+int sc_res_bwd(const float* gin, const float* gadd, const float* pre, const float* th, const float* l1c, float* out,
+               void* outb, float* cpart, int G, int B, int n, int rb, hipStream_t stream) {
+  if (n % 256 || rb < 4 || rb % 4 || B % rb || G < 1) return 1;
+  hipLaunchKernelGGL(res_bwd_kernel, dim3(n / 256, B / rb, G), dim3(256), 0, stream, gin, gadd, pre, th, l1c, out,
+                     reinterpret_cast<uint16_t*>(outb), cpart, B, n, rb);
   return hipGetLastError() == hipSuccess ? 0 : 3;
 }
 

@@ -102,15 +102,16 @@ def test_unrolled_adam_kernel_matches_torch_adam():
         torch.testing.assert_close(eng.params[k].detach(), p[k], rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("sig", [FunctionalLISTADenoisingSAE, FunctionalResidualDenoisingSAE])
 @pytest.mark.parametrize("layers,n,B", [(3, 512, 256), (2, 768, 384), (1, 256, 128)])
-def test_lista_fused_grads_match_fp32(layers, n, B):
-    """The explicit (autograd-free) LISTA step's gradients == the engine's fp32 torch path (CPU),
+def test_lista_fused_grads_match_fp32(layers, n, B, sig):
+    """The explicit (autograd-free) LISTA / residual-denoising step's gradients == the engine's fp32
+    torch path (CPU),
     every parameter of every model, per-model relative Frobenius error <= 3e-2 (or within 1.5x of the
     autograd GPU path's own distance, at the small shapes), losses alike (odd and even layer counts:
     paired and lone weight-gradient problems)."""
     torch.manual_seed(3)
     d, G = 256, 3
-    sig = FunctionalLISTADenoisingSAE
     models = [sig.init(d, n, layers, l1) for l1 in (1e-3, 3e-3, 1e-2)]
     for p_, _ in models:  # off the orthogonal init, where y_0 D reproduces x and the residual is ~0
         p_["decoder"] = p_["decoder"] + 0.3 * torch.randn_like(p_["decoder"]) / d ** 0.5
@@ -131,14 +132,14 @@ def test_lista_fused_grads_match_fp32(layers, n, B):
             assert e <= max(3e-2, 1.5 * ea), (k, g, e, ea)
 
 
-def test_lista_fused_step_tracks_autograd_step():
+@pytest.mark.parametrize("sig", [FunctionalLISTADenoisingSAE, FunctionalResidualDenoisingSAE])
+def test_lista_fused_step_tracks_autograd_step(sig):
     """Three explicit steps (row Adam + bf16 shadows) move every parameter as close to three steps of
     the fp32 CPU path as three steps of the autograd GPU path do (Adam's early steps are sign-like,
     so near-zero gradient entries flip either way); the maintained decoder shadow is the normalised
     decoder."""
     torch.manual_seed(4)
     d, n, B = 256, 512, 256
-    sig = FunctionalLISTADenoisingSAE
     models = [sig.init(d, n, 3, l1) for l1 in (1e-3, 1e-2)]
     fused = UnrolledEnsemble(models, sig, lr=1e-3, device=DEV)
     auto = UnrolledEnsemble(models, sig, lr=1e-3, device=DEV)
