@@ -17,7 +17,7 @@ from sparse_coding__amd.models.lista import FunctionalLISTADenoisingSAE, Functio
 S = FunctionalResidualDenoisingSAE if "--residual" in sys.argv else FunctionalLISTADenoisingSAE
 
 
-def timeit(fn, steps=10, warm=3):
+def timeit(fn, steps=30, warm=5):
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
