@@ -14,6 +14,7 @@ struct Shape {
 };
 using S128 = Shape<2, 2, 4, 4>;
 using S256x128 = Shape<2, 2, 8, 4>;
+using S256x128w8 = Shape<4, 2, 4, 4>;  // 256x128 as eight 64x64 waves (two blocks per CU on BK32 x 3)
 using S256 = Shape<2, 4, 8, 4>;
 // Partial-sum buffers (scalar parts, column parts, row-dot parts, squared-norm
 // parts) are laid out on a 128x128 sub-tile grid whatever the block shape, so the

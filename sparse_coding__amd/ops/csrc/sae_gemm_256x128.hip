@@ -10,6 +10,9 @@ namespace scamd {
 int launch_256x128(int pipe, int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
   // (256x128 on the BK32 rings, two blocks per CU, measured slower in the step: 0.302-0.307 vs
   // 0.296-0.297 ms, profiles/r5/batch3/cfg14.jsonl)
+  // pipe 3: EIGHT waves of 64x64 on the BK32 x 3 ring (72 KB, <= 128 VGPRs: two blocks per CU) -- the
+  // encoder / masked code gradient default (ops/gemm.py _CFG_DEFAULT, profiles/r6/w8/)
+  if (pipe == 3) return launch<S256x128w8, 32, 3, false>(epi, ak, bk, p, nprob, stream);
   if (pipe) return 8;
   return launch<S256x128, 64, 2>(epi, ak, bk, p, nprob, stream);
 }

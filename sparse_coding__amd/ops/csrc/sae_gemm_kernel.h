@@ -145,7 +145,9 @@ __device__ __forceinline__ int stage_at(int row, int byte) {  // 8-byte granule 
   return row * STAGE_ROW + ((((byte >> 4) ^ (row >> 1)) & 7) << 4) + ((((byte >> 3) ^ row) & 1) << 3);
 }
 template <class S>
-constexpr int stage_bytes() { return STAGE_OFF + S::NW * stage_wave<S>(); }
+constexpr int stage_off() { return (2 * S::WGM * S::BN + 2 * S::NW) * 4 <= STAGE_OFF ? STAGE_OFF : 2 * STAGE_OFF; }
+template <class S>
+constexpr int stage_bytes() { return stage_off<S>() + S::NW * stage_wave<S>(); }
 
 template <class S, int EPI, bool AUX_EARLY, bool STAGE = false, bool FSTAGE = false>
 __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)[S::WI][S::WJ],
@@ -163,8 +165,9 @@ __device__ __forceinline__ void sae_epilogue(const GemmParams& p, f32x4_t (&acc)
   const bool p1 = pi != 0;
   const int rowb = m0 + wr * (WI * 16) + (lane & 15);
   const int colb = n0 + wc * (WJ * 16) + 4 * (lane >> 4);
-  static_assert(!STAGE || ((WI == 4 || WI == 8) && WJ == 4 && 2 * S::WGM * BN + 2 * NW <= STAGE_OFF / 4), "stage layout");
-  char* stage = reinterpret_cast<char*>(red) + STAGE_OFF + wid * stage_wave<S>();
+  static_assert(!STAGE || ((WI == 4 || WI == 8) && WJ == 4 && 2 * S::WGM * BN + 2 * NW <= stage_off<S>() / 4),
+                "stage layout");
+  char* stage = reinterpret_cast<char*>(red) + stage_off<S>() + wid * stage_wave<S>();
   // one 4-wide bf16 output fragment (rows rowb + 16 i, columns colb + 16 j .. +3)
   auto put = [&](uint16_t* C, int i, int j, ushort4 h) {
     if constexpr (STAGE) {
@@ -1001,7 +1004,9 @@ __device__ __forceinline__ void gemm_block(const GemmParams& p, const int bid, c
 
 // (the software-pipelined BK32 x 3 loop: three waves per SIMD, so three blocks co-reside per CU)
 template <class S, bool AK, bool BKM, int EPI, int BKT, int NST, bool P32 = false>
-__global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : 1) void sae_gemm_kernel(GemmParams p) {
+// (the eight-wave 256x128 block on BK32 x 3: four waves per SIMD, i.e. two blocks per CU -- the second
+// launch-bounds argument is waves per execution unit)
+__global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : ((S::NW == 8 && S::BN == 128 && NST == 3) ? 4 : 1)) void sae_gemm_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[NST * (S::BM + S::BN) * BKT * 2];
   gemm_block<S, AK, BKM, EPI, BKT, NST, P32>(p, xcd_remap(blockIdx.x, gridDim.x), smem);
 }

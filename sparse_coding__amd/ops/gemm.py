@@ -41,8 +41,14 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 # Round 5 (profiles/r5/batch4/): the same BK32 x 3 ring with the software-pipelined K loop (cfg bit 4:
 # 13 | 16 = 29; the next K-tile's fragments are read while the current tile's MFMAs run, three waves
 # per SIMD kept) -- step median 0.2893 vs 0.2915 ms over 4 alternating runs each on one box.
-_CFG_DEFAULT = {EPI_ENC: 29, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 29,
-                EPI_DC_MASK: 29, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
+# Round 6 (profiles/r6/w8/): 256x128 blocks of EIGHT 64x64 waves on the BK32 x 3 ring (cfg 14 = shape 2 |
+# pipe 3; 72 KB, <= 128 VGPRs: two blocks / sixteen waves per CU) for the encoder and the masked code
+# gradient -- 25 % fewer operand bytes per FLOP than 128x128 at the same per-wave tile: step 0.2873 vs
+# 0.2926 ms (3 alternating runs each, same box; again 0.2869 vs 0.2918 on a second box).  Not for the
+# counting encoder (its epilogue spills at 128 VGPRs: slower), the decoder (slower) or masked launches.
+_CFG_DEFAULT = {EPI_ENC: 14, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 29,
+                EPI_DC_MASK: 14, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
+_CFG_FALLBACK = {14: 29}  # 256x128 eight-wave default -> the 128x128 pipelined BK32 x 3 ring (M % 256 != 0)
 _CFG_OVERRIDE = None
 _CFG_LAYOUT = {}  # (epi, operand layout) -> cfg: overrides _CFG_DEFAULT for that layout only
 
@@ -122,6 +128,11 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
     _need(K1 % TILE_K == 0 and K2 % TILE_K == 0, f"K={K1}+{K2} must be multiples of 64")
     if cfg is None:
         cfg = _CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_LAYOUT.get((epi, layout), _CFG_DEFAULT[epi])
+        if _CFG_OVERRIDE is None and (((cfg & 3) and not shape_fits(cfg, M, N))
+                                      or (cfg in _CFG_FALLBACK and (nactive is not None or nact_k is not None))):
+            # a default whose block does not tile this problem; masked launches keep the 128x128 ring
+            # (their compacted live tiles pack better in its three slots per CU: profiles/r6/w8/)
+            cfg = _CFG_FALLBACK.get(cfg, 1)
     cfg = int(cfg)
     _need((cfg & 3) == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg & 3)} does not tile M={M}, N={N}")
     nprob = len(outs)

@@ -86,7 +86,8 @@ def test_identity_asymmetric():
 
 
 PIPE_CFGS = [1 | 1 << 2, 1 | 2 << 2, 1 | 3 << 2, 3 | 1 << 2, 3 | 2 << 2, 3 | 3 << 2,  # deeper K pipelines
-             1 | 2 << 2 | 16, 1 | 3 << 2 | 16]  # 128x128 BK32 rings, software-pipelined K loop
+             1 | 2 << 2 | 16, 1 | 3 << 2 | 16,  # 128x128 BK32 rings, software-pipelined K loop
+             2 | 3 << 2]  # 256x128 as eight 64x64 waves on BK32 x 3 (the encoder / masked code-gradient default)
 
 
 @pytest.mark.parametrize("cfg", SHAPE_CFGS + PIPE_CFGS)
