@@ -50,7 +50,10 @@ _CFG_DEFAULT = {EPI_ENC: 14, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI
                 EPI_DC_MASK: 14, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
 _CFG_FALLBACK = {14: 29}  # 256x128 eight-wave default -> the 128x128 pipelined BK32 x 3 ring (M % 256 != 0)
 _CFG_OVERRIDE = None
-_CFG_LAYOUT = {}  # (epi, operand layout) -> cfg: overrides _CFG_DEFAULT for that layout only
+# (epi, operand layout) -> cfg: overrides _CFG_DEFAULT for that layout only.  The bf16-out GEMMs of the
+# top-k step (scores x D^T: layout 3; the two-segment dense weight gradient: layout 0) on the eight-wave
+# 256x128 block: config 4 0.988-0.993 vs 1.012-1.015 ms/step (profiles/r6/w8/)
+_CFG_LAYOUT = {(EPI_BF16, 3): 14, (EPI_BF16, 0): 14}
 
 
 def _env_cfgs():
