@@ -82,7 +82,7 @@ int sc_gemm(int epi, int layout, int nprob, int M, int N, int K1, int K2, int G,
   switch (shape) {
     case 3:
       if (!fits<S256>(M, N)) return 6;
-      return launch_big(3, pipe, epi, ak, bk, p, nprob, stream, p32);
+      return launch_big(3, pipe, epi, ak, bk, p, nprob, stream);
     case 2:
       if (!fits<S256x128>(M, N)) return 6;
       return launch_big(2, pipe, epi, ak, bk, p, nprob, stream);

@@ -5,10 +5,9 @@
 
 namespace scamd {
 
-int launch_big(int shape, int pipe, int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream,
-               bool w16) {
-  // (lab) 256x256 as SIXTEEN 64x64 waves on BK32 x 3 (96 KB, one block of 16 waves per CU)
-  if (shape == 3 && w16 && pipe == 3) return launch<Shape<4, 4, 4, 4>, 32, 3, false>(epi, ak, bk, p, nprob, stream);
+int launch_big(int shape, int pipe, int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream) {
+  // (256x256 as sixteen 64x64 waves on BK32 x 3, one block of 16 waves per CU, measured no faster for the
+  // weight gradients and slower for the top-k GEMMs: profiles/r6/w16/, scripts/lab/w16_256x256_r6.patch)
   if (shape == 3) {
     if (pipe == 1) return launch<S256, 32, 4, false>(epi, ak, bk, p, nprob, stream);
     if (pipe == 3) return launch<S256, 32, 3, false>(epi, ak, bk, p, nprob, stream);

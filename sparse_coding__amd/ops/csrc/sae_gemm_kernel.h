@@ -1006,7 +1006,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& p, const int bid, c
 template <class S, bool AK, bool BKM, int EPI, int BKT, int NST, bool P32 = false>
 // (the eight-wave 256x128 block on BK32 x 3: four waves per SIMD, i.e. two blocks per CU -- the second
 // launch-bounds argument is waves per execution unit)
-__global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : (((S::NW == 8 && S::BN == 128) || S::NW == 16) && NST == 3 ? 4 : 1)) void sae_gemm_kernel(GemmParams p) {
+__global__ __launch_bounds__(S::NT, (P32 && NST == 3) ? 3 : ((S::NW == 8 && S::BN == 128 && NST == 3) ? 4 : 1)) void sae_gemm_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[NST * (S::BM + S::BN) * BKT * 2];
   gemm_block<S, AK, BKM, EPI, BKT, NST, P32>(p, xcd_remap(blockIdx.x, gridDim.x), smem);
 }
@@ -1138,8 +1138,7 @@ int launch(int epi, bool ak, bool bk, GemmParams p, int nprob, hipStream_t strea
 
 
 // 256x128 / 256x256 launches (sae_gemm_big.hip)
-int launch_big(int shape, int pipe, int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream,
-               bool w16 = false);
+int launch_big(int shape, int pipe, int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream);
 int launch_256x128(int pipe, int epi, bool ak, bool bk, const GemmParams& p, int nprob, hipStream_t stream);
 
 }  // namespace scamd
