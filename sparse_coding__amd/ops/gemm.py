@@ -135,7 +135,7 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
                                       or (cfg in _CFG_FALLBACK and (nactive is not None or nact_k is not None))):
             # a default whose block does not tile this problem; masked launches keep the 128x128 ring
             # (their compacted live tiles pack better in its three slots per CU: profiles/r6/w8/)
-            cfg = _CFG_FALLBACK.get(cfg, 1)
+            cfg = 0 if epi == EPI_F32 else _CFG_FALLBACK.get(cfg, 1)  # (fp32 out: the automatic shape)
     cfg = int(cfg)
     _need((cfg & 3) == 0 or shape_fits(cfg, M, N), f"block shape {SHAPES.get(cfg & 3)} does not tile M={M}, N={N}")
     nprob = len(outs)
