@@ -42,10 +42,11 @@ TILE_M, TILE_N, TILE_K = 128, 128, 64
 # 13 | 16 = 29; the next K-tile's fragments are read while the current tile's MFMAs run, three waves
 # per SIMD kept) -- step median 0.2893 vs 0.2915 ms over 4 alternating runs each on one box.
 # Round 6 (profiles/r6/w8/): 256x128 blocks of EIGHT 64x64 waves on the BK32 x 3 ring (cfg 14 = shape 2 |
-# pipe 3; 72 KB, <= 128 VGPRs: two blocks / sixteen waves per CU) for the encoder and the masked code
-# gradient -- 25 % fewer operand bytes per FLOP than 128x128 at the same per-wave tile: step 0.2873 vs
+# pipe 3; 72 KB, <= 128 VGPRs: two blocks / sixteen waves per CU) for the encoder and the bitmask code
+# gradient (EPI_DC_MASK) -- 25 % fewer operand bytes per FLOP than 128x128 at the same per-wave tile: step 0.2873 vs
 # 0.2926 ms (3 alternating runs each, same box; again 0.2869 vs 0.2918 on a second box).  Not for the
-# counting encoder (its epilogue spills at 128 VGPRs: slower), the decoder (slower) or masked launches.
+# counting encoder (its epilogue spills at 128 VGPRs: slower), the decoder (slower) or masked-ensemble
+# launches (nactive / nact_k: they fall back to cfg 29 below).
 _CFG_DEFAULT = {EPI_ENC: 14, EPI_DEC: 1, EPI_DC: 1, EPI_F32: 0, EPI_BF16: 0, EPI_ENC_CNT: 29,
                 EPI_DC_MASK: 14, EPI_ENC_ACT: 1, EPI_DC_ACT: 1, EPI_ROWMAX: 1}
 _CFG_FALLBACK = {14: 29}  # 256x128 eight-wave default -> the 128x128 pipelined BK32 x 3 ring (M % 256 != 0)
