@@ -37,6 +37,11 @@ from ..models.lista import (FunctionalLISTADenoisingSAE, FunctionalResidualDenoi
 from ..models.signatures import unit_rows
 
 
+# the unrolled steps' weight gradients keep the automatic block shape (256x256 here: the eight-wave
+# 256x128 layout default of the SAE step measured +1.4 % on LISTA, profiles/r6/wg14/)
+_WG_CFG = 0
+
+
 def _hip_ok(*dims) -> bool:
     return all(int(x) % 128 == 0 for x in dims)
 
@@ -425,12 +430,12 @@ class UnrolledEnsemble:
         while k < len(probs):
             if splits[k] == 1 and k + 1 < len(probs) and splits[k + 1] == 1 and len(probs[k]) == len(probs[k + 1]):
                 o = [slabs[j], slabs[j + 1]] if outs is None else [outs[k][0], outs[k + 1][0]]
-                gemm_ops.weight_grads([probs[k], probs[k + 1]], o, 1.0)
+                gemm_ops.weight_grads([probs[k], probs[k + 1]], o, 1.0, cfg=_WG_CFG)
                 k, j = k + 2, j + 2
             else:
                 s = splits[k]
                 o = (slabs[j:j + s] if outs is None else outs[k])
-                gemm_ops.weight_grads([probs[k]], [o if s > 1 else o[0]], 1.0, ksplit=s)
+                gemm_ops.weight_grads([probs[k]], [o if s > 1 else o[0]], 1.0, ksplit=s, cfg=_WG_CFG)
                 k, j = k + 1, j + s
 
     @torch.no_grad()
@@ -501,7 +506,7 @@ class UnrolledEnsemble:
         gW = {}
         for i in reversed(range(L)):  # (an [n, n] weight gradient is G n^2 / 256^2 >= 256 tiles: no split)
             gW[i] = torch.empty(1, G, n, n, **f32)
-            gemm_ops.weight_grads([[(Gb, hbs[i])]], [gW[i][0]], 1.0)  # G^T h_i
+            gemm_ops.weight_grads([[(Gb, hbs[i])]], [gW[i][0]], 1.0, cfg=_WG_CFG)  # G^T h_i
             gh = torch.empty(G, B, n, **f32)
             gemm_ops.matmul_nn(Gb, sh[f"layer{i}.W"], gh)  # G W_i
             Gf2 = torch.empty(G, B, n, **f32) if i else None

@@ -54,7 +54,9 @@ _CFG_OVERRIDE = None
 # (epi, operand layout) -> cfg: overrides _CFG_DEFAULT for that layout only.  The bf16-out GEMMs of the
 # top-k step (scores x D^T: layout 3; the two-segment dense weight gradient: layout 0) on the eight-wave
 # 256x128 block: config 4 0.988-0.993 vs 1.012-1.015 ms/step (profiles/r6/w8/)
-_CFG_LAYOUT = {(EPI_BF16, 3): 14, (EPI_BF16, 0): 14}
+# The fp32 weight gradients (layout 0) too: headline 0.2822 vs 0.2833 ms median over 5 alternating runs
+# (profiles/r6/wg14/).
+_CFG_LAYOUT = {(EPI_BF16, 3): 14, (EPI_BF16, 0): 14, (EPI_F32, 0): 14}
 
 
 def _env_cfgs():
@@ -133,7 +135,8 @@ def _launch(epi, layout, M, N, K1, K2, G, a_ops, b_ops, outs, alphas, ldc, sc, *
     if cfg is None:
         cfg = _CFG_OVERRIDE if _CFG_OVERRIDE is not None else _CFG_LAYOUT.get((epi, layout), _CFG_DEFAULT[epi])
         if _CFG_OVERRIDE is None and (((cfg & 3) and not shape_fits(cfg, M, N))
-                                      or (cfg in _CFG_FALLBACK and (nactive is not None or nact_k is not None))):
+                                      or (cfg in _CFG_FALLBACK and (nactive is not None or nact_k is not None
+                                                                    or nact_m is not None))):
             # a default whose block does not tile this problem; masked launches keep the 128x128 ring
             # (their compacted live tiles pack better in its three slots per CU: profiles/r6/w8/)
             cfg = 0 if epi == EPI_F32 else _CFG_FALLBACK.get(cfg, 1)  # (fp32 out: the automatic shape)
@@ -317,13 +320,14 @@ def wgrad_split(G, n, d, K, nprob, live=None):
     return s
 
 
-def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None, live_host=None):
+def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None, live_host=None, cfg=None):
     """out_i[g] = alpha * sum_segments A_s[g]^T @ B_s[g]   (reduction over batch rows).
 
     pairs: list (one per problem, 1 or 2 problems) of lists of (A, B) segments
     (1 or 2 segments, summed along K).  A: [G, Bk, n] bf16 (or [Bk, n] shared),
     B: [G, Bk, d] bf16 (or [Bk, d] shared).  outs: [G, n, d] fp32 (or all bf16), or with ``ksplit`` > 1
     [ksplit, G, n, d] partial slabs (their sum is the product; the Adam kernel sums them).
+    ``cfg``: the block configuration (default: the launcher's layout default; split-K picks its own).
     """
     _need(1 <= len(pairs) == len(outs) <= 2, "1 or 2 problems")
     G, n, d = outs[0].shape[-3:]
@@ -354,7 +358,6 @@ def weight_grads(pairs, outs, alpha, ksplit=1, nactive=None, live_host=None):
     _need(odt in (torch.float32, torch.bfloat16), "out must be fp32 or bf16")
     for o in outs:
         _need(o.dtype == odt and tuple(o.shape) == want and o.is_contiguous(), f"out must be {want} {odt}")
-    cfg = None
     if ksplit > 1:
         cfg = 3 if shape_fits(3, n, d) else 1
     # nactive (masked ensembles): gradient rows past a model's live size are zero -- those tiles
